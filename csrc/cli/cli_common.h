@@ -1,0 +1,126 @@
+// Shared command-line handling of bin/RS and bin/CPU-RS (reference CLI: src/main.c:32-167,
+// README.md:29-50). Same short flags; uppercase aliases take their argument (the reference declares
+// them argument-less and segfaults on atoi(NULL)); flags may come in any order;
+// numeric arguments are validated (the reference divides by zero on -s 0).
+#pragma once
+
+#include <getopt.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+
+namespace gfrs_cli {
+
+struct Args {
+  enum Op { kNone, kEncode, kDecode, kMakeConf } op = kNone;
+  int k = 0, n = 0;
+  int grid = 0;     // -p: cap on gridDim.x (0 = uncapped)
+  int streams = 1;  // -s
+  std::string in_file, conf, out;
+  std::string matrix = "vandermonde";
+  std::string mul = "row";
+  int gpus = 0;  // 0 = all visible
+  int threads = 1;
+  long long slice = 16ll << 20;
+  bool cpu_meta = false;
+  bool quiet = false;
+};
+
+inline void usage(const char* prog, bool gpu) {
+  std::printf("Usage:\n");
+  std::printf("[-h]: show usage information\n");
+  std::printf("Encode: [-k|-K nativeBlockNum] [-n|-N totalBlockNum] [-e|-E fileName]\n");
+  std::printf("Decode: [-d|-D] [-k|-K nativeBlockNum] [-n|-N totalBlockNum] \n\t [-i|-I originalFileName] "
+              "[-c|-C config] [-o|-O output]\n");
+  std::printf("For encoding, the -k, -n, and -e options are all necessary.\n");
+  std::printf("For decoding, the -d, -i, and -c options are all necessary.\n");
+  std::printf("If the -o option is not set, the original file name will be chosen as the output file name by "
+              "default.\n");
+  if (gpu) {
+    std::printf("Performance-tuning Options:\n");
+    std::printf("[-p|-P]: set maximum gridDim.x (0 = one block per 4 KiB column group)\n");
+    std::printf("[-s|-S]: set stream number\n");
+  }
+  std::printf("Extensions:\n");
+  std::printf("  --matrix vandermonde|cauchy|sys_vandermonde  coding matrix (default: reference Vandermonde)\n");
+  std::printf("  --cpu-meta              write the 2-line CPU-format METADATA\n");
+  std::printf("  --make-conf             write conf-<n>-<k>-<file> keeping the last k chunks (unit-test.sh)\n");
+  std::printf("  -q                      quiet\n");
+  if (gpu) {
+    std::printf("  --gpus N                number of GPUs (default: all visible)\n");
+    std::printf("  --slice BYTES           column slice per stream step (default 16 MiB)\n");
+  } else {
+    std::printf("  --mul logexp|logexp0|logexp1|logexp2|logexp3|loop|full|double|perm|row\n");
+    std::printf("  --threads T             worker threads (default 1, the reference's single thread)\n");
+  }
+  (void)prog;
+}
+
+inline int to_int(const char* s, const char* what, int lo) {
+  char* end = nullptr;
+  const long v = std::strtol(s ? s : "", &end, 10);
+  if (!s || *end || v < lo) {
+    std::fprintf(stderr, "invalid %s: %s\n", what, s ? s : "(null)");
+    std::exit(2);
+  }
+  return int(v);
+}
+
+inline Args parse(int argc, char** argv, bool gpu) {
+  Args a;
+  static const option longopts[] = {{"matrix", required_argument, nullptr, 1},
+                                    {"cpu-meta", no_argument, nullptr, 2},
+                                    {"gpus", required_argument, nullptr, 3},
+                                    {"slice", required_argument, nullptr, 4},
+                                    {"mul", required_argument, nullptr, 5},
+                                    {"threads", required_argument, nullptr, 6},
+                                    {"make-conf", no_argument, nullptr, 7},
+                                    {"help", no_argument, nullptr, 'h'},
+                                    {nullptr, 0, nullptr, 0}};
+  int c;
+  while ((c = getopt_long(argc, argv, "k:K:n:N:e:E:i:I:c:C:o:O:p:P:s:S:dDhq", longopts, nullptr)) != -1) {
+    switch (c) {
+      case 'k': case 'K': a.k = to_int(optarg, "nativeBlockNum", 1); break;
+      case 'n': case 'N': a.n = to_int(optarg, "totalBlockNum", 1); break;
+      case 'e': case 'E': a.op = a.op == Args::kMakeConf ? a.op : Args::kEncode; a.in_file = optarg; break;
+      case 'd': case 'D': a.op = Args::kDecode; break;
+      case 'i': case 'I': a.in_file = optarg; break;
+      case 'c': case 'C': a.conf = optarg; break;
+      case 'o': case 'O': a.out = optarg; break;
+      case 'p': case 'P': a.grid = to_int(optarg, "grid size", 0); break;
+      case 's': case 'S': a.streams = to_int(optarg, "stream number", 1); break;
+      case 'q': a.quiet = true; break;
+      case 1: a.matrix = optarg; break;
+      case 2: a.cpu_meta = true; break;
+      case 3: a.gpus = to_int(optarg, "GPU count", 1); break;
+      case 4: a.slice = to_int(optarg, "slice bytes", 256); break;
+      case 5: a.mul = optarg; break;
+      case 6: a.threads = to_int(optarg, "thread count", 0); break;
+      case 7: a.op = Args::kMakeConf; break;
+      case 'h': default: usage(argv[0], gpu); std::exit(c == 'h' ? 0 : 2);
+    }
+  }
+  if (a.op == Args::kEncode) {
+    if (a.k <= 0 || a.n <= a.k - 1 || a.in_file.empty() || a.n > 256) {
+      std::fprintf(stderr, "encode needs -k K -n N -e FILE with 1 <= K <= N <= 256\n");
+      std::exit(2);
+    }
+  } else if (a.op == Args::kDecode) {
+    if (a.in_file.empty() || a.conf.empty()) {
+      std::fprintf(stderr, "decode needs -d -i FILE -c CONF\n");
+      std::exit(2);
+    }
+  } else if (a.op == Args::kMakeConf) {
+    if (a.k <= 0 || a.n < a.k || a.in_file.empty()) {
+      std::fprintf(stderr, "--make-conf needs -k K -n N -e FILE\n");
+      std::exit(2);
+    }
+  } else {
+    usage(argv[0], gpu);
+    std::exit(2);
+  }
+  return a;
+}
+
+}  // namespace gfrs_cli

@@ -1,0 +1,164 @@
+// CPU GF(2^8) GEMM with the reference's multiply strategies (see gfrs/cpu_codec.h).
+#include "gfrs/cpu_codec.h"
+
+#include <algorithm>
+#include <array>
+#include <cstring>
+#include <stdexcept>
+#include <thread>
+
+namespace gfrs {
+namespace {
+
+// ---- strategy tables, generated once -------------------------------------------------------
+struct CpuTables {
+  uint8_t exp255[256];   // exp[0..254], exp[255] = exp[0] (variant 1)
+  uint8_t exp509[509];   // two periods (variant 2)
+  uint8_t full[256][256];
+  uint8_t nib_hi[16][256];  // (h << 4) * b
+  uint8_t nib_lo[16][256];  // l * b
+  CpuTables() {
+    for (int i = 0; i < 255; ++i) exp255[i] = kTables.exp[i];
+    exp255[255] = kTables.exp[0];
+    for (int i = 0; i < 509; ++i) exp509[i] = kTables.exp[i % 255];
+    for (int a = 0; a < 256; ++a)
+      for (int b = 0; b < 256; ++b) full[a][b] = mul(uint8_t(a), uint8_t(b));
+    for (int h = 0; h < 16; ++h)
+      for (int b = 0; b < 256; ++b) {
+        nib_hi[h][b] = full[h << 4][b];
+        nib_lo[h][b] = full[h][b];
+      }
+  }
+};
+
+const CpuTables& tables() {
+  static const CpuTables t;
+  return t;
+}
+
+inline uint8_t m_logexp(uint8_t a, uint8_t b) {
+  if (!a || !b) return 0;
+  int s = kTables.log[a] + kTables.log[b];
+  if (s >= 255) s -= 255;
+  return kTables.exp[s];
+}
+inline uint8_t m_mod(uint8_t a, uint8_t b) {
+  if (!a || !b) return 0;
+  return kTables.exp[(kTables.log[a] + kTables.log[b]) % 255];
+}
+inline uint8_t m_fold(uint8_t a, uint8_t b) {
+  if (!a || !b) return 0;
+  const int s = kTables.log[a] + kTables.log[b];
+  return tables().exp255[(s & 255) + (s >> 8)];
+}
+inline uint8_t m_double(uint8_t a, uint8_t b) {
+  if (!a || !b) return 0;
+  return tables().exp509[kTables.log[a] + kTables.log[b]];
+}
+inline uint8_t m_zeroband(uint8_t a, uint8_t b) { return kTables.exp[kTables.log[a] + kTables.log[b]]; }
+inline uint8_t m_full(uint8_t a, uint8_t b) { return tables().full[a][b]; }
+inline uint8_t m_nibble(uint8_t a, uint8_t b) { return tables().nib_hi[a >> 4][b] ^ tables().nib_lo[a & 15][b]; }
+
+// Per-row kernel for one coefficient c over bytes [0, n): out ^= c * in.
+template <CpuMul S>
+void axpy(uint8_t c, const uint8_t* __restrict__ in, uint8_t* __restrict__ out, int64_t n) {
+  if (c == 0) return;
+  if (c == 1) {
+    for (int64_t x = 0; x < n; ++x) out[x] ^= in[x];
+    return;
+  }
+  if constexpr (S == CpuMul::kRow || S == CpuMul::kFull) {
+    const uint8_t* row = tables().full[c];
+    for (int64_t x = 0; x < n; ++x) out[x] ^= row[in[x]];
+  } else if constexpr (S == CpuMul::kPerm) {
+    const PermTable t = perm_for_coeff(c);
+    for (int64_t x = 0; x < n; ++x) out[x] ^= perm_apply(t, in[x]);
+  } else {
+    for (int64_t x = 0; x < n; ++x) out[x] ^= cpu_mul(S, in[x], c);
+  }
+}
+
+template <CpuMul S>
+void gemm_range(const std::vector<const uint8_t*>& in, const std::vector<uint8_t*>& out, const Mat& coeff, int64_t a,
+                int64_t b) {
+  const int k = int(in.size()), m = int(out.size());
+  constexpr int64_t kTile = 32 << 10;  // keep the k input tiles + m outputs L2-resident
+  for (int64_t t = a; t < b; t += kTile) {
+    const int64_t n = std::min(kTile, b - t);
+    for (int i = 0; i < m; ++i) {
+      uint8_t* o = out[i] + t;
+      std::memset(o, 0, size_t(n));
+      for (int j = 0; j < k; ++j) axpy<S>(coeff[size_t(i) * k + j], in[j] + t, o, n);
+    }
+  }
+}
+
+template <CpuMul S>
+void gemm_threads(const std::vector<const uint8_t*>& in, const std::vector<uint8_t*>& out, const Mat& coeff,
+                  int64_t ncols, int threads) {
+  if (threads <= 1 || ncols < (1 << 20)) {
+    gemm_range<S>(in, out, coeff, 0, ncols);
+    return;
+  }
+  std::vector<std::thread> th;
+  const int64_t per = (ncols + threads - 1) / threads;
+  for (int t = 0; t < threads; ++t) {
+    const int64_t a = int64_t(t) * per, b = std::min(ncols, a + per);
+    if (a >= b) break;
+    th.emplace_back([&, a, b] { gemm_range<S>(in, out, coeff, a, b); });
+  }
+  for (auto& x : th) x.join();
+}
+
+}  // namespace
+
+CpuMul parse_cpu_mul(const std::string& s) {
+  static const std::array<const char*, 10> names = {"logexp", "logexp0", "logexp1", "logexp2", "logexp3",
+                                                    "loop",   "full",    "double",  "perm",    "row"};
+  for (size_t i = 0; i < names.size(); ++i)
+    if (s == names[i]) return CpuMul(i);
+  throw std::invalid_argument("unknown CPU multiply strategy: " + s);
+}
+
+const char* cpu_mul_name(CpuMul m) {
+  static const char* names[] = {"logexp", "logexp0", "logexp1", "logexp2", "logexp3",
+                                "loop",   "full",    "double",  "perm",    "row"};
+  return names[int(m)];
+}
+
+uint8_t cpu_mul(CpuMul s, uint8_t a, uint8_t b) {
+  switch (s) {
+    case CpuMul::kLogExp: return m_logexp(a, b);
+    case CpuMul::kLogExpMod: return m_mod(a, b);
+    case CpuMul::kLogExpFold: return m_fold(a, b);
+    case CpuMul::kLogExpDouble: return m_double(a, b);
+    case CpuMul::kZeroBand: return m_zeroband(a, b);
+    case CpuMul::kLoop: return mul_loop(a, b);
+    case CpuMul::kFull: return m_full(a, b);
+    case CpuMul::kNibble: return m_nibble(a, b);
+    case CpuMul::kPerm: return perm_apply(perm_for_coeff(b), a);
+    case CpuMul::kRow: return m_full(a, b);
+  }
+  return 0;
+}
+
+void cpu_gemm(const std::vector<const uint8_t*>& in, const std::vector<uint8_t*>& out, const Mat& coeff,
+              int64_t ncols, CpuMul s, int threads) {
+  const int k = int(in.size()), m = int(out.size());
+  if (coeff.size() != size_t(m) * k) throw std::invalid_argument("cpu_gemm: coeff must be m x k");
+  if (threads <= 0) threads = int(std::max(1u, std::thread::hardware_concurrency()));
+  switch (s) {
+    case CpuMul::kLogExp: return gemm_threads<CpuMul::kLogExp>(in, out, coeff, ncols, threads);
+    case CpuMul::kLogExpMod: return gemm_threads<CpuMul::kLogExpMod>(in, out, coeff, ncols, threads);
+    case CpuMul::kLogExpFold: return gemm_threads<CpuMul::kLogExpFold>(in, out, coeff, ncols, threads);
+    case CpuMul::kLogExpDouble: return gemm_threads<CpuMul::kLogExpDouble>(in, out, coeff, ncols, threads);
+    case CpuMul::kZeroBand: return gemm_threads<CpuMul::kZeroBand>(in, out, coeff, ncols, threads);
+    case CpuMul::kLoop: return gemm_threads<CpuMul::kLoop>(in, out, coeff, ncols, threads);
+    case CpuMul::kFull: return gemm_threads<CpuMul::kFull>(in, out, coeff, ncols, threads);
+    case CpuMul::kNibble: return gemm_threads<CpuMul::kNibble>(in, out, coeff, ncols, threads);
+    case CpuMul::kPerm: return gemm_threads<CpuMul::kPerm>(in, out, coeff, ncols, threads);
+    case CpuMul::kRow: return gemm_threads<CpuMul::kRow>(in, out, coeff, ncols, threads);
+  }
+}
+
+}  // namespace gfrs

@@ -1,0 +1,46 @@
+// File-level encode/decode shared by the GPU CLI (bin/RS), the CPU CLI (bin/CPU-RS) and the Python
+// bindings. The arithmetic backend is a callback, so the same code drives the gfx950 streaming
+// pipeline and the CPU reference codec. Mirrors encode_file/decode_file of the reference
+// (src/encode.cu:301-473, src/decode.cu:236-434; call stacks in SURVEY §3.1-3.2) with its defects
+// fixed: zero-padded tails, 64-bit sizes, singular-pattern detection, row-pivoted inversion,
+// survivor rows passed through instead of re-multiplied by the identity.
+#pragma once
+
+#include <cstdint>
+#include <functional>
+#include <string>
+#include <vector>
+
+#include "gfrs/matrix.h"
+
+namespace gfrs {
+
+using GemmFn = std::function<void(const std::vector<const uint8_t*>& in, const std::vector<uint8_t*>& out,
+                                  const Mat& coeff, int64_t ncols)>;
+
+struct HostAlloc {
+  std::function<uint8_t*(size_t)> alloc;  // e.g. pinned hipHostMalloc for the GPU path
+  std::function<void(uint8_t*)> release;
+};
+HostAlloc default_host_alloc();
+
+struct FileReport {
+  int64_t total_size = 0, chunk_size = 0;
+  int k = 0, p = 0, erased = 0;
+  double ms_read = 0, ms_matrix = 0, ms_compute = 0, ms_write = 0;
+};
+
+// Writes _0_<file> .. _{n-1}_<file> and <file>.METADATA (full matrix format unless `cpu_meta`).
+FileReport encode_file(const std::string& file, int k, int p, MatrixKind kind, const GemmFn& gemm,
+                       const HostAlloc& alloc, bool cpu_meta = false);
+
+// Reads <file>.METADATA and the k chunks named in `conf`, writes `out` (or overwrites `file` when
+// `out` is empty, like the reference, src/decode.cu:410-425). Throws std::runtime_error for an
+// unrecoverable (singular) erasure pattern.
+FileReport decode_file(const std::string& file, const std::string& conf, const std::string& out,
+                       const GemmFn& gemm, const HostAlloc& alloc);
+
+// The reference's src/unit-test.sh: conf keeping the LAST k chunks (erases natives 0..n-k-1).
+std::vector<std::string> worst_case_conf(const std::string& file, int n, int k);
+
+}  // namespace gfrs

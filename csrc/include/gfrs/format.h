@@ -1,0 +1,48 @@
+// On-disk formats shared with the reference:
+//   * chunk files  "_<i>_<name>" next to the input file, natives 0..k-1 then parity k..n-1
+//     (src/encode.cu:434-465). Unlike the reference, a path with directories works: the chunk
+//     lands in the file's directory.
+//   * "<file>.METADATA" text: totalSize \n p k \n then, in the GPU format, the k+p rows of
+//     G = [I; E] as "%d " values (src/encode.cu:61-101). The CPU reference writes only the first
+//     two lines (src/cpu-rs.c:465-476); read_metadata() accepts both and regenerates G from the
+//     reference Vandermonde for the short form.
+//   * decode config: whitespace-separated k chunk names; row index = atoi(basename + 1)
+//     (src/decode.cu:302-318). Conf order defines the row order of the decode system.
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "gfrs/matrix.h"
+
+namespace gfrs {
+
+struct Metadata {
+  int64_t total_size = 0;
+  int p = 0, k = 0;
+  Mat g;                    // (k+p) x k generator
+  bool has_matrix = false;  // false: 2-line CPU format, g regenerated (reference Vandermonde)
+};
+
+std::string chunk_path(const std::string& file, int index);
+std::string metadata_path(const std::string& file);
+int chunk_index(const std::string& name);  // atoi(basename + 1); -1 if malformed
+
+void write_metadata(const std::string& path, int64_t total_size, int p, int k, const Mat& e, bool with_matrix = true);
+Metadata read_metadata(const std::string& path);
+std::vector<std::string> read_conf(const std::string& path);
+void write_conf(const std::string& path, const std::vector<std::string>& names);
+
+// Chunk geometry: C = ceil(total / k) (src/encode.cu:317).
+inline int64_t chunk_size(int64_t total, int k) { return (total + k - 1) / k; }
+
+int64_t file_size(const std::string& path);
+// Reads up to `len` bytes at `offset` into dst; zero-fills what the file does not cover.
+void read_into(const std::string& path, int64_t offset, uint8_t* dst, int64_t len);
+void write_from(const std::string& path, const uint8_t* src, int64_t len);
+// Resolve a chunk name from a conf: as given (relative to the CWD, like the reference), else
+// relative to the directory of `anchor`.
+std::string resolve_chunk(const std::string& name, const std::string& anchor);
+
+}  // namespace gfrs

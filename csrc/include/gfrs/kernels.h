@@ -1,0 +1,52 @@
+// Launch entry points of the gfx950 HIP kernels (csrc/kernels/*.hip). Every launcher is
+// asynchronous on `stream`, performs no allocation and no host synchronisation, so callers may
+// capture it into a hipGraph (cdna_hip_programming.md Guideline 9).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace gfrs {
+
+// ---- GF-GEMM (csrc/kernels/gf_gemm.hip) -------------------------------------------------------
+// desc: device descriptor (gfrs/desc.h) for k inputs and m_pad outputs. Processes byte columns
+// [col0, col0 + ncols). Uses the 16-byte v_perm kernel for the aligned body and a byte kernel for
+// the ragged tail; `force_bytewise` routes everything through the byte kernel (unaligned rows).
+// max_blocks caps grid.x (the reference's -p gridDim knob, src/main.c:74-77); 0 = uncapped.
+hipError_t launch_gf_gemm(const void* desc, int k, int m_pad, int64_t col0, int64_t ncols,
+                          bool force_bytewise, int max_blocks, hipStream_t stream);
+
+// Variant selector for benchmarks/ablation: vec = 16-byte groups per thread (1 or 2).
+hipError_t launch_gf_gemm_variant(const void* desc, int k, int m_pad, int64_t col0, int64_t ncols,
+                                  int vec, int max_blocks, hipStream_t stream);
+
+// ---- Gauss-Jordan inverse (csrc/kernels/gf_invert.hip) ---------------------------------------
+// Inverts `batch` n x n matrices (row-major, contiguous) with row pivoting, one workgroup each,
+// [A|I] resident in LDS. status[b] = 0 ok, 1 singular. n <= 256.
+// If `desc` is non-null, additionally writes the perm tables of rows `sel_rows[0..m)` of each
+// inverse into desc's table block (k = n, m_pad given) — the decode GEMM then runs without a
+// host round-trip. (batch must be 1 in that mode.)
+hipError_t launch_gf_invert(const uint8_t* a, uint8_t* a_inv, int n, int batch, int* status,
+                            void* desc, const int* sel_rows, int m, int m_pad, hipStream_t stream);
+
+// ---- matrix utilities (csrc/kernels/gf_matrix.hip) -------------------------------------------
+// kind: 0 = reference Vandermonde, 1 = Cauchy. Writes the p x k block.
+hipError_t launch_gen_matrix(uint8_t* e, int k, int p, int kind, hipStream_t stream);
+// Build perm tables [k][m_pad] for an m x k coefficient matrix into desc's table block.
+hipError_t launch_perm_tables(const uint8_t* coeff, int m, int k, void* desc, int m_pad,
+                              hipStream_t stream);
+// Deterministic counter-based random bytes (synthetic benchmark input), 16 B per lane stores.
+hipError_t launch_fill_random(uint8_t* dst, int64_t bytes, uint64_t seed, hipStream_t stream);
+// Gather an m x k sub-matrix: out[i][:] = g[rows[i]][:]  (decode system assembly on device).
+hipError_t launch_gather_rows(const uint8_t* g, const int* rows, uint8_t* out, int m, int k,
+                              hipStream_t stream);
+
+// ---- int8-MFMA bit-matrix GF-GEMM (csrc/kernels/gf_mfma.hip) ----------------------------------
+// Same contract as launch_gf_gemm but on matrix cores; requires k % 4 == 0 (see kernel notes).
+hipError_t launch_gf_gemm_mfma(const void* bitmat, const void* desc, int k, int m, int64_t col0,
+                               int64_t ncols, hipStream_t stream);
+size_t mfma_bitmat_bytes(int k, int m);
+hipError_t launch_mfma_bitmat(const uint8_t* coeff, int m, int k, void* bitmat,
+                              hipStream_t stream);
+
+}  // namespace gfrs

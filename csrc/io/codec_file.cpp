@@ -1,0 +1,167 @@
+// File-level codec (see gfrs/codec_file.h).
+#include "gfrs/codec_file.h"
+
+#include <chrono>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <set>
+#include <stdexcept>
+
+#include "gfrs/format.h"
+
+namespace gfrs {
+namespace {
+
+using Clock = std::chrono::steady_clock;
+double ms_since(Clock::time_point t0) { return std::chrono::duration<double, std::milli>(Clock::now() - t0).count(); }
+
+struct Buf {
+  const HostAlloc* a = nullptr;
+  uint8_t* p = nullptr;
+  Buf(const HostAlloc& al, size_t n) : a(&al), p(al.alloc(n ? n : 1)) {
+    if (!p) throw std::runtime_error("host allocation failed");
+  }
+  ~Buf() {
+    if (p) a->release(p);
+  }
+  Buf(const Buf&) = delete;
+  Buf& operator=(const Buf&) = delete;
+};
+
+}  // namespace
+
+HostAlloc default_host_alloc() {
+  return {[](size_t n) -> uint8_t* {
+            void* p = nullptr;
+            if (posix_memalign(&p, 4096, (n + 4095) / 4096 * 4096) != 0) return nullptr;
+            return static_cast<uint8_t*>(p);
+          },
+          [](uint8_t* p) { std::free(p); }};
+}
+
+FileReport encode_file(const std::string& file, int k, int p, MatrixKind kind, const GemmFn& gemm,
+                       const HostAlloc& alloc, bool cpu_meta) {
+  if (k <= 0 || p < 0 || k + p > 256) throw std::invalid_argument("encode: need k >= 1, p >= 0, k + p <= 256");
+  FileReport r;
+  r.k = k;
+  r.p = p;
+  auto t = Clock::now();
+  r.total_size = file_size(file);
+  r.chunk_size = std::max<int64_t>(1, chunk_size(r.total_size, k));
+  const int64_t C = r.chunk_size;
+  Buf data(alloc, size_t(k) * C), parity(alloc, size_t(std::max(p, 1)) * C);
+  read_into(file, 0, data.p, int64_t(k) * C);  // one contiguous read; tail zero-padded
+  r.ms_read = ms_since(t);
+
+  t = Clock::now();
+  const Mat e = p ? encoding_matrix(kind, k, p) : Mat{};
+  r.ms_matrix = ms_since(t);
+
+  t = Clock::now();
+  if (p) {
+    std::vector<const uint8_t*> in(k);
+    std::vector<uint8_t*> out(p);
+    for (int j = 0; j < k; ++j) in[j] = data.p + size_t(j) * C;
+    for (int i = 0; i < p; ++i) out[i] = parity.p + size_t(i) * C;
+    gemm(in, out, e, C);
+  }
+  r.ms_compute = ms_since(t);
+
+  t = Clock::now();
+  for (int i = 0; i < k; ++i) write_from(chunk_path(file, i), data.p + size_t(i) * C, C);
+  for (int i = 0; i < p; ++i) write_from(chunk_path(file, k + i), parity.p + size_t(i) * C, C);
+  write_metadata(metadata_path(file), r.total_size, p, k, e, !cpu_meta);
+  r.ms_write = ms_since(t);
+  return r;
+}
+
+FileReport decode_file(const std::string& file, const std::string& conf, const std::string& out,
+                       const GemmFn& gemm, const HostAlloc& alloc) {
+  FileReport r;
+  auto t = Clock::now();
+  const Metadata md = read_metadata(metadata_path(file));
+  const int k = md.k, n = md.k + md.p;
+  r.k = k;
+  r.p = md.p;
+  r.total_size = md.total_size;
+  r.chunk_size = std::max<int64_t>(1, chunk_size(md.total_size, k));
+  const int64_t C = r.chunk_size;
+
+  std::vector<std::string> names = read_conf(conf);
+  if (int(names.size()) < k)
+    throw std::runtime_error("configuration lists " + std::to_string(names.size()) + " chunks, need k = " +
+                             std::to_string(k));
+  names.resize(k);
+  std::vector<int> rows(k);
+  std::set<int> seen;
+  for (int i = 0; i < k; ++i) {
+    rows[i] = chunk_index(names[i]);
+    if (rows[i] < 0 || rows[i] >= n) throw std::runtime_error("bad chunk name in configuration: " + names[i]);
+    if (!seen.insert(rows[i]).second) throw std::runtime_error("duplicate chunk in configuration: " + names[i]);
+  }
+  Buf surv(alloc, size_t(k) * C);
+  for (int i = 0; i < k; ++i) read_into(resolve_chunk(names[i], file), 0, surv.p + size_t(i) * C, C);
+  r.ms_read = ms_since(t);
+
+  t = Clock::now();
+  Mat dm;
+  if (!decode_matrix(md.g, k, rows, dm))
+    throw std::runtime_error("unrecoverable erasure pattern: the selected rows of the generator are singular");
+  // survivors that are natives pass through; only erased natives are reconstructed
+  std::vector<int> pos_of_native(k, -1);
+  for (int i = 0; i < k; ++i)
+    if (rows[i] < k) pos_of_native[rows[i]] = i;
+  std::vector<int> erased;
+  for (int i = 0; i < k; ++i)
+    if (pos_of_native[i] < 0) erased.push_back(i);
+  r.erased = int(erased.size());
+  r.ms_matrix = ms_since(t);
+
+  t = Clock::now();
+  Buf rec(alloc, size_t(std::max<size_t>(erased.size(), 1)) * C);
+  if (!erased.empty()) {
+    Mat coeff(erased.size() * size_t(k));
+    for (size_t e = 0; e < erased.size(); ++e)
+      std::memcpy(&coeff[e * k], &dm[size_t(erased[e]) * k], size_t(k));
+    std::vector<const uint8_t*> in(k);
+    std::vector<uint8_t*> o(erased.size());
+    for (int j = 0; j < k; ++j) in[j] = surv.p + size_t(j) * C;
+    for (size_t e = 0; e < erased.size(); ++e) o[e] = rec.p + e * C;
+    gemm(in, o, coeff, C);
+  }
+  r.ms_compute = ms_since(t);
+
+  t = Clock::now();
+  const std::string dst = out.empty() ? file : out;
+  FILE* fp = std::fopen(dst.c_str(), "wb");
+  if (!fp) throw std::runtime_error("cannot open output file " + dst);
+  int64_t left = md.total_size;
+  size_t e_idx = 0;
+  for (int i = 0; i < k && left > 0; ++i) {
+    const uint8_t* row;
+    if (pos_of_native[i] >= 0) {
+      row = surv.p + size_t(pos_of_native[i]) * C;
+    } else {
+      row = rec.p + e_idx * C;
+      ++e_idx;
+    }
+    const int64_t w = std::min(C, left);
+    if (std::fwrite(row, 1, size_t(w), fp) != size_t(w)) {
+      std::fclose(fp);
+      throw std::runtime_error("short write to " + dst);
+    }
+    left -= w;
+  }
+  std::fclose(fp);
+  r.ms_write = ms_since(t);
+  return r;
+}
+
+std::vector<std::string> worst_case_conf(const std::string& file, int n, int k) {
+  std::vector<std::string> names;
+  for (int i = n - k; i < n; ++i) names.push_back(chunk_path(file, i));
+  return names;
+}
+
+}  // namespace gfrs

@@ -1,0 +1,155 @@
+// File formats (see gfrs/format.h). 64-bit sizes throughout; tails zero-padded (the reference's GPU
+// encoder leaves padding uninitialised, src/encode.cu:325).
+#include "gfrs/format.h"
+
+#include <sys/stat.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <sstream>
+#include <stdexcept>
+
+namespace gfrs {
+namespace {
+
+void split_path(const std::string& p, std::string& dir, std::string& base) {
+  const size_t s = p.find_last_of('/');
+  if (s == std::string::npos) {
+    dir.clear();
+    base = p;
+  } else {
+    dir = p.substr(0, s + 1);
+    base = p.substr(s + 1);
+  }
+}
+
+bool exists(const std::string& p) {
+  struct stat sb;
+  return ::stat(p.c_str(), &sb) == 0;
+}
+
+}  // namespace
+
+std::string chunk_path(const std::string& file, int index) {
+  std::string dir, base;
+  split_path(file, dir, base);
+  return dir + "_" + std::to_string(index) + "_" + base;
+}
+
+std::string metadata_path(const std::string& file) { return file + ".METADATA"; }
+
+int chunk_index(const std::string& name) {
+  std::string dir, base;
+  split_path(name, dir, base);
+  if (base.size() < 2 || base[0] != '_') return -1;
+  char* end = nullptr;
+  const long v = std::strtol(base.c_str() + 1, &end, 10);
+  if (end == base.c_str() + 1 || v < 0) return -1;
+  return int(v);
+}
+
+void write_metadata(const std::string& path, int64_t total_size, int p, int k, const Mat& e, bool with_matrix) {
+  FILE* fp = std::fopen(path.c_str(), "wb");
+  if (!fp) throw std::runtime_error("cannot open metadata file " + path);
+  std::fprintf(fp, "%lld\n%d %d\n", static_cast<long long>(total_size), p, k);
+  if (with_matrix) {
+    for (int i = 0; i < k; ++i) {
+      for (int j = 0; j < k; ++j) std::fprintf(fp, "%d ", i == j ? 1 : 0);
+      std::fprintf(fp, "\n");
+    }
+    for (int i = 0; i < p; ++i) {
+      for (int j = 0; j < k; ++j) std::fprintf(fp, "%d ", int(e[size_t(i) * k + j]));
+      std::fprintf(fp, "\n");
+    }
+  }
+  std::fclose(fp);
+}
+
+Metadata read_metadata(const std::string& path) {
+  std::ifstream in(path);
+  if (!in) throw std::runtime_error("cannot open metadata file " + path);
+  Metadata md;
+  long long total = 0;
+  if (!(in >> total >> md.p >> md.k)) throw std::runtime_error("malformed metadata " + path);
+  if (md.k <= 0 || md.p < 0 || md.k + md.p > 256 || total < 0)
+    throw std::runtime_error("metadata out of range in " + path);
+  md.total_size = total;
+  const size_t n = size_t(md.k + md.p) * md.k;
+  md.g.resize(n);
+  size_t got = 0;
+  int v;
+  while (got < n && (in >> v)) {
+    if (v < 0 || v > 255) throw std::runtime_error("metadata matrix entry out of range in " + path);
+    md.g[got++] = uint8_t(v);
+  }
+  if (got == n) {
+    md.has_matrix = true;
+  } else if (got == 0) {
+    md.g = generator(vandermonde_ref(md.k, md.p), md.k, md.p);  // CPU-format metadata
+    md.has_matrix = false;
+  } else {
+    throw std::runtime_error("truncated metadata matrix in " + path);
+  }
+  return md;
+}
+
+std::vector<std::string> read_conf(const std::string& path) {
+  std::ifstream in(path);
+  if (!in) throw std::runtime_error("cannot open configuration file " + path);
+  std::vector<std::string> names;
+  std::string s;
+  while (in >> s) names.push_back(s);
+  return names;
+}
+
+void write_conf(const std::string& path, const std::vector<std::string>& names) {
+  std::ofstream out(path);
+  if (!out) throw std::runtime_error("cannot write configuration file " + path);
+  for (const auto& n : names) out << n << "\n";
+}
+
+int64_t file_size(const std::string& path) {
+  struct stat sb;
+  if (::stat(path.c_str(), &sb) != 0) throw std::runtime_error("cannot stat " + path);
+  return int64_t(sb.st_size);
+}
+
+void read_into(const std::string& path, int64_t offset, uint8_t* dst, int64_t len) {
+  FILE* fp = std::fopen(path.c_str(), "rb");
+  if (!fp) throw std::runtime_error("cannot open input file " + path);
+  int64_t got = 0;
+  if (fseeko(fp, offset, SEEK_SET) == 0) {
+    while (got < len) {
+      const size_t r = std::fread(dst + got, 1, size_t(len - got), fp);
+      if (r == 0) break;
+      got += int64_t(r);
+    }
+  }
+  std::fclose(fp);
+  if (got < len) std::memset(dst + got, 0, size_t(len - got));
+}
+
+void write_from(const std::string& path, const uint8_t* src, int64_t len) {
+  FILE* fp = std::fopen(path.c_str(), "wb");
+  if (!fp) throw std::runtime_error("cannot open output file " + path);
+  int64_t put = 0;
+  while (put < len) {
+    const size_t w = std::fwrite(src + put, 1, size_t(len - put), fp);
+    if (w == 0) break;
+    put += int64_t(w);
+  }
+  std::fclose(fp);
+  if (put < len) throw std::runtime_error("short write to " + path);
+}
+
+std::string resolve_chunk(const std::string& name, const std::string& anchor) {
+  if (exists(name) || name.empty() || name[0] == '/') return name;
+  std::string dir, base;
+  split_path(anchor, dir, base);
+  const std::string alt = dir + name;
+  return exists(alt) ? alt : name;
+}
+
+}  // namespace gfrs

@@ -1,0 +1,292 @@
+// GF(2^8) GEMM on gfx950 VALU: out[i][c] = XOR_j coeff[i][j] * in[j][c].
+//
+// Replaces the reference's K1/K2 `matrix_mul` kernels (src/matrix.cu:232-407). What changes and why
+// (SURVEY §2.3, §3.3):
+//   * GF multiply: the reference does 3 dependent LDS lookups per byte product
+//     (gflog[a], gflog[b], gfexp[sum]; src/matrix.cu:105-110). Here every coefficient is a
+//     GF(2)-linear byte map split over bit-chunks [2:0],[5:3],[7:6]; each chunk is ONE
+//     v_perm_b32 byte-select from an 8-byte pool, applied to 4 bytes per instruction. Per 4
+//     byte-products: 3 v_perm + 1.5 v_xor3 — no LDS, no branches. The selectors depend only on
+//     the input bytes and are shared by all outputs of the tile.
+//   * Tables are wave-uniform and live in a device descriptor read with scalar loads; nothing is
+//     copied into LDS per block (the reference re-copies 1.5 KB of LUTs per block and every thread
+//     redundantly re-stores the coefficient and data tiles, src/matrix.cu:250-292).
+//   * 16-byte vector loads/stores per lane (global_load_dwordx4), one-row software prefetch,
+//     no barriers at all (the reference has divergent __syncthreads on ragged tails,
+//     src/matrix.cu:269-322). Ragged byte tails go to a byte kernel instead of the reference's
+//     all-or-nothing `C % 8` switch to its slow byte path (src/matrix.cu:796).
+//   * XCD-aware block mapping: output tiles of the same column block are dealt to one XCD so the
+//     re-read of the input rows by tile > 0 hits that XCD's L2 (cdna_hip_programming.md §5.5 T1).
+//   * Fused survivor copy: decode streams every survivor row once and, when asked, writes it to
+//     its destination row in the same pass (saves a full re-read of the survivors).
+#include <hip/hip_runtime.h>
+
+#include "gfrs/desc.h"
+#include "gfrs/kernels.h"
+
+namespace gfrs {
+namespace {
+
+constexpr int kBlock = 256;
+
+struct Sel {
+  uint32_t s0, s1, s2;
+};
+
+__device__ __forceinline__ Sel make_sel(uint32_t w) {
+  return {w & 0x07070707u, (w >> 3) & 0x07070707u, (w >> 6) & 0x03030303u};
+}
+
+using u32x4 = unsigned int __attribute__((ext_vector_type(4)));
+
+// 3-input XOR in one VALU op: gfx950's v_bitop3_b32 with truth table 0x96 (a ^ b ^ c).
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
+// acc ^= L(x) for one GF(2)-linear byte map L on 4 packed bytes: 3 v_perm_b32 + 2 v_bitop3.
+template <typename P>
+__device__ __forceinline__ uint32_t mac_map(uint32_t acc, P t, const Sel& s) {
+  const uint32_t a = __builtin_amdgcn_perm(t[1], t[0], s.s0);
+  const uint32_t b = __builtin_amdgcn_perm(t[3], t[2], s.s1);
+  const uint32_t c = __builtin_amdgcn_perm(0u, t[4], s.s2);
+  return xor3(xor3(acc, a, b), c, 0u);
+}
+
+// Descriptor words are wave-uniform and read-only for the kernel's lifetime: reading them through
+// the constant address space (4) makes hipcc emit s_load (scalar cache, lgkmcnt) instead of vector
+// loads that would share vmcnt with the data stream and serialise the prefetch.
+template <typename T>
+using cptr = const __attribute__((address_space(4))) T*;
+// Data rows through the global address space (1): global_load/store instead of flat_*.
+template <typename T>
+using gptr = __attribute__((address_space(1))) T*;
+
+struct DescView {
+  cptr<uint64_t> in;
+  cptr<uint64_t> copy;
+  cptr<uint64_t> out;
+  cptr<uint32_t> tab;
+};
+
+inline DescView view(const void* desc, int k, int m_pad) {
+  const DescLayout l = desc_layout(k, m_pad);
+  const char* b = static_cast<const char*>(desc);
+  return {(cptr<uint64_t>)(b + l.in_off), (cptr<uint64_t>)(b + l.copy_off), (cptr<uint64_t>)(b + l.out_off),
+          (cptr<uint32_t>)(b + l.tab_off)};
+}
+
+__device__ __forceinline__ gptr<const u32x4> row_vec(uint64_t base, int64_t off) {
+  return (gptr<const u32x4>)(base + uint64_t(off));
+}
+__device__ __forceinline__ gptr<u32x4> row_vec_w(uint64_t base, int64_t off) {
+  return (gptr<u32x4>)(base + uint64_t(off));
+}
+
+// Block -> (column block, output tile) mapping. Blocks b and b+8 share an XCD under the observed
+// round-robin dispatch; consecutive `local` ids of one XCD sweep the tiles of one column block.
+// Placement only affects speed, never correctness.
+struct TileMap {
+  int tile;
+  int64_t cb0;
+};
+__device__ __forceinline__ TileMap map_block(int ntiles) {
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7;
+  const int local = bid >> 3;
+  return {local % ntiles, int64_t(local / ntiles) * 8 + xcd};
+}
+
+// Vector kernel: each lane owns V consecutive 16-byte groups of every row.
+template <int MT, int V>
+__global__ __launch_bounds__(kBlock) void gf_gemm_vec_kernel(DescView d, int k, int m_pad, int ntiles,
+                                                             int64_t col0, int64_t ngroups, int64_t nblk,
+                                                             int64_t ncb) {
+  const TileMap tm = map_block(ntiles);
+  if (tm.cb0 >= ncb) return;
+  const int i0 = tm.tile * MT;
+  const bool do_copy = (tm.tile == 0);
+
+  for (int64_t cb = tm.cb0; cb < nblk; cb += ncb) {
+    const int64_t g = cb * kBlock + threadIdx.x;
+    if (g >= ngroups) continue;
+    const int64_t off = col0 + g * (16 * V);
+
+    uint32_t acc[MT][4 * V];
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int w = 0; w < 4 * V; ++w) acc[i][w] = 0;
+
+    u32x4 cur[V], nxt[V];
+    {
+      const auto src = row_vec(d.in[0], off);
+#pragma unroll
+      for (int v = 0; v < V; ++v) cur[v] = src[v];
+    }
+    for (int j = 0; j < k; ++j) {
+      if (j + 1 < k) {
+        const auto src = row_vec(d.in[j + 1], off);
+#pragma unroll
+        for (int v = 0; v < V; ++v) nxt[v] = src[v];
+      }
+      if (do_copy) {
+        const uint64_t cp = d.copy[j];
+        if (cp) {
+          const auto dst = row_vec_w(cp, off);
+#pragma unroll
+          for (int v = 0; v < V; ++v) dst[v] = cur[v];
+        }
+      }
+      const auto t = d.tab + (size_t(j) * m_pad + i0) * kPermStride;
+#pragma unroll
+      for (int v = 0; v < V; ++v) {
+        const u32x4 wv = cur[v];
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+          const Sel s = make_sel(wv[w]);
+#pragma unroll
+          for (int i = 0; i < MT; ++i) acc[i][v * 4 + w] = mac_map(acc[i][v * 4 + w], t + i * kPermStride, s);
+        }
+      }
+      if (j + 1 < k) {
+#pragma unroll
+        for (int v = 0; v < V; ++v) cur[v] = nxt[v];
+      }
+    }
+
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+      const uint64_t op = d.out[i0 + i];
+      if (!op) continue;
+      const auto dst = row_vec_w(op, off);
+#pragma unroll
+      for (int v = 0; v < V; ++v)
+        dst[v] = u32x4{acc[i][v * 4 + 0], acc[i][v * 4 + 1], acc[i][v * 4 + 2], acc[i][v * 4 + 3]};
+    }
+  }
+}
+
+// Byte kernel: one lane per byte column; any alignment. Used for ragged tails and unaligned rows.
+template <int MT>
+__global__ __launch_bounds__(kBlock) void gf_gemm_byte_kernel(DescView d, int k, int m_pad, int ntiles,
+                                                              int64_t col0, int64_t ncols, int64_t nblk,
+                                                              int64_t ncb) {
+  const TileMap tm = map_block(ntiles);
+  if (tm.cb0 >= ncb) return;
+  const int i0 = tm.tile * MT;
+  const bool do_copy = (tm.tile == 0);
+  for (int64_t cb = tm.cb0; cb < nblk; cb += ncb) {
+    const int64_t c = cb * kBlock + threadIdx.x;
+    if (c >= ncols) continue;
+    const int64_t off = col0 + c;
+    uint32_t acc[MT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i) acc[i] = 0;
+    for (int j = 0; j < k; ++j) {
+      const uint8_t x = ((gptr<const uint8_t>)d.in[j])[off];
+      if (do_copy) {
+        const uint64_t cp = d.copy[j];
+        if (cp) ((gptr<uint8_t>)cp)[off] = x;
+      }
+      const Sel s = make_sel(x);
+      const auto t = d.tab + (size_t(j) * m_pad + i0) * kPermStride;
+#pragma unroll
+      for (int i = 0; i < MT; ++i) acc[i] = mac_map(acc[i], t + i * kPermStride, s);
+    }
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+      const uint64_t op = d.out[i0 + i];
+      if (op) ((gptr<uint8_t>)op)[off] = static_cast<uint8_t>(acc[i] & 0xFF);
+    }
+  }
+}
+
+struct Grid {
+  int64_t nblk, ncb;
+  unsigned blocks;
+};
+
+inline Grid make_grid(int64_t items, int ntiles, int max_blocks) {
+  Grid g{};
+  g.nblk = (items + kBlock - 1) / kBlock;
+  g.ncb = g.nblk;
+  if (max_blocks > 0 && g.ncb > max_blocks) g.ncb = max_blocks;
+  const int64_t ncb8 = (g.ncb + 7) / 8 * 8;
+  g.blocks = static_cast<unsigned>(ncb8 * ntiles);
+  return g;
+}
+
+template <int MT>
+hipError_t launch_vec(const DescView& d, int k, int m_pad, int64_t col0, int64_t ngroups, int vec, int max_blocks,
+                      hipStream_t stream) {
+  const int ntiles = m_pad / MT;
+  if (ngroups <= 0) return hipSuccess;
+  if (vec == 2) {
+    const Grid g = make_grid(ngroups, ntiles, max_blocks);
+    gf_gemm_vec_kernel<MT, 2><<<g.blocks, kBlock, 0, stream>>>(d, k, m_pad, ntiles, col0, ngroups, g.nblk, g.ncb);
+  } else {
+    const Grid g = make_grid(ngroups, ntiles, max_blocks);
+    gf_gemm_vec_kernel<MT, 1><<<g.blocks, kBlock, 0, stream>>>(d, k, m_pad, ntiles, col0, ngroups, g.nblk, g.ncb);
+  }
+  return hipGetLastError();
+}
+
+template <int MT>
+hipError_t launch_byte(const DescView& d, int k, int m_pad, int64_t col0, int64_t ncols, int max_blocks,
+                       hipStream_t stream) {
+  if (ncols <= 0) return hipSuccess;
+  const int ntiles = m_pad / MT;
+  const Grid g = make_grid(ncols, ntiles, max_blocks);
+  gf_gemm_byte_kernel<MT><<<g.blocks, kBlock, 0, stream>>>(d, k, m_pad, ntiles, col0, ncols, g.nblk, g.ncb);
+  return hipGetLastError();
+}
+
+template <typename F>
+hipError_t dispatch_tile(int m_pad, F&& f) {
+  const int t = tile_for(m_pad);
+  switch (t) {
+    case 1: return f(std::integral_constant<int, 1>{});
+    case 2: return f(std::integral_constant<int, 2>{});
+    case 4: return f(std::integral_constant<int, 4>{});
+    case 8: return f(std::integral_constant<int, 8>{});
+    default: return f(std::integral_constant<int, 16>{});
+  }
+}
+
+hipError_t run(const void* desc, int k, int m_pad, int64_t col0, int64_t ncols, bool bytewise, int vec,
+               int max_blocks, hipStream_t stream) {
+  if (k <= 0 || m_pad <= 0 || ncols <= 0) return hipSuccess;
+  if (m_pad % tile_for(m_pad) != 0) return hipErrorInvalidValue;
+  const DescView d = view(desc, k, m_pad);
+  return dispatch_tile(m_pad, [&](auto mt) -> hipError_t {
+    constexpr int MT = decltype(mt)::value;
+    if (bytewise || (col0 & 15)) return launch_byte<MT>(d, k, m_pad, col0, ncols, max_blocks, stream);
+    const int64_t n16 = ncols / 16;
+    const int64_t nmain = (vec == 2) ? n16 / 2 : n16;
+    hipError_t e = launch_vec<MT>(d, k, m_pad, col0, nmain, vec, max_blocks, stream);
+    if (e != hipSuccess) return e;
+    int64_t done = nmain * 16 * vec;
+    if (vec == 2 && (n16 & 1)) {
+      e = launch_vec<MT>(d, k, m_pad, col0 + done, 1, 1, max_blocks, stream);
+      if (e != hipSuccess) return e;
+      done += 16;
+    }
+    return launch_byte<MT>(d, k, m_pad, col0 + done, ncols - done, max_blocks, stream);
+  });
+}
+
+}  // namespace
+
+hipError_t launch_gf_gemm(const void* desc, int k, int m_pad, int64_t col0, int64_t ncols, bool force_bytewise,
+                          int max_blocks, hipStream_t stream) {
+  return run(desc, k, m_pad, col0, ncols, force_bytewise, 1, max_blocks, stream);
+}
+
+hipError_t launch_gf_gemm_variant(const void* desc, int k, int m_pad, int64_t col0, int64_t ncols, int vec,
+                                  int max_blocks, hipStream_t stream) {
+  if (vec == 0) return run(desc, k, m_pad, col0, ncols, true, 1, max_blocks, stream);
+  return run(desc, k, m_pad, col0, ncols, false, vec, max_blocks, stream);
+}
+
+}  // namespace gfrs

@@ -1,0 +1,89 @@
+// _cpu extension: CPU reference codec, GF(2^8) scalar ops, formats, file-level codec.
+#include "bind_common.h"
+#include "gfrs/cpu_codec.h"
+#include "gfrs/format.h"
+
+PYBIND11_MODULE(_cpu, m) {
+  using namespace gfrs;
+  using namespace gfrs_py;
+  m.doc() = "gpu_rscode_amd CPU reference codec (C++)";
+  bind_common(m);
+
+  m.def("tables", [] {
+    py::dict d;
+    d["exp"] = py::bytes(reinterpret_cast<const char*>(kTables.exp), kExpLen);
+    d["log"] = std::vector<int>(kTables.log, kTables.log + 256);
+    d["inv"] = py::bytes(reinterpret_cast<const char*>(kTables.inv), 256);
+    return d;
+  });
+  m.def("mul", [](int a, int b) { return int(mul(uint8_t(a), uint8_t(b))); });
+  m.def("div", [](int a, int b) { return int(div(uint8_t(a), uint8_t(b))); });
+  m.def("pow_ref", [](int a, unsigned e) { return int(pow_ref(uint8_t(a), e)); });
+  m.def("mul_strategy", [](const std::string& s, int a, int b) { return int(cpu_mul(parse_cpu_mul(s), uint8_t(a), uint8_t(b))); });
+  m.def(
+      "gemm",
+      [](const std::vector<uint64_t>& in, const std::vector<uint64_t>& out, const py::bytes& coeff, int64_t ncols,
+         const std::string& strategy, int threads) {
+        const Mat c = to_mat(coeff);
+        const CpuMul s = parse_cpu_mul(strategy);
+        auto ip = ptrs<const uint8_t*>(in);
+        auto op = ptrs<uint8_t*>(out);
+        py::gil_scoped_release nogil;
+        cpu_gemm(ip, op, c, ncols, s, threads);
+      },
+      py::arg("in_ptrs"), py::arg("out_ptrs"), py::arg("coeff"), py::arg("ncols"), py::arg("strategy") = "row",
+      py::arg("threads") = 1);
+
+  auto gemm_fn = [](const std::string& strategy, int threads) -> GemmFn {
+    const CpuMul s = parse_cpu_mul(strategy);
+    return [s, threads](const std::vector<const uint8_t*>& in, const std::vector<uint8_t*>& out, const Mat& coeff,
+                        int64_t ncols) { cpu_gemm(in, out, coeff, ncols, s, threads); };
+  };
+  m.def(
+      "encode_file",
+      [gemm_fn](const std::string& file, int k, int p, const std::string& matrix, bool cpu_meta,
+                const std::string& strategy, int threads) {
+        const GemmFn g = gemm_fn(strategy, threads);
+        FileReport r;
+        {
+          py::gil_scoped_release nogil;
+          r = encode_file(file, k, p, parse_matrix_kind(matrix), g, default_host_alloc(), cpu_meta);
+        }
+        return report(r);
+      },
+      py::arg("file"), py::arg("k"), py::arg("p"), py::arg("matrix") = "vandermonde", py::arg("cpu_meta") = false,
+      py::arg("strategy") = "row", py::arg("threads") = 1);
+  m.def(
+      "decode_file",
+      [gemm_fn](const std::string& file, const std::string& conf, const std::string& out, const std::string& strategy,
+                int threads) {
+        const GemmFn g = gemm_fn(strategy, threads);
+        FileReport r;
+        {
+          py::gil_scoped_release nogil;
+          r = decode_file(file, conf, out, g, default_host_alloc());
+        }
+        return report(r);
+      },
+      py::arg("file"), py::arg("conf"), py::arg("out") = "", py::arg("strategy") = "row", py::arg("threads") = 1);
+
+  m.def("chunk_path", &chunk_path);
+  m.def("chunk_index", &chunk_index);
+  m.def("metadata_path", &metadata_path);
+  m.def("read_conf", &read_conf);
+  m.def("write_conf", &write_conf);
+  m.def("worst_case_conf", &worst_case_conf);
+  m.def("write_metadata", [](const std::string& path, int64_t total, int p, int k, const py::bytes& e, bool full) {
+    write_metadata(path, total, p, k, to_mat(e), full);
+  });
+  m.def("read_metadata", [](const std::string& path) {
+    const Metadata md = read_metadata(path);
+    py::dict d;
+    d["total_size"] = md.total_size;
+    d["p"] = md.p;
+    d["k"] = md.k;
+    d["g"] = from_mat(md.g);
+    d["has_matrix"] = md.has_matrix;
+    return d;
+  });
+}

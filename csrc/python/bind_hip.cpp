@@ -1,0 +1,168 @@
+// _hip extension: gfx950 kernels and the device runtime. Device pointers and hipStream_t are passed
+// as integers (torch tensors' data_ptr() and torch.cuda.current_stream().cuda_stream), so the
+// extension has no libtorch build dependency and shares the process' single HIP runtime.
+#include <hip/hip_runtime.h>
+
+#include <stdexcept>
+
+#include "bind_common.h"
+#include "gfrs/kernels.h"
+#include "gfrs/pipeline.h"
+
+namespace {
+
+void check(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+hipStream_t as_stream(uint64_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+py::dict stats_dict(const gfrs::PipelineStats& s) {
+  py::dict d;
+  d["ms_setup"] = s.ms_setup;
+  d["ms_stream"] = s.ms_stream;
+  d["ms_teardown"] = s.ms_teardown;
+  d["ms_total"] = s.ms_total;
+  d["bytes_h2d"] = s.bytes_h2d;
+  d["bytes_d2h"] = s.bytes_d2h;
+  d["slices"] = s.slices;
+  return d;
+}
+
+gfrs::HostAlloc pinned_alloc() {
+  return {[](size_t n) -> uint8_t* {
+            void* p = nullptr;
+            if (hipHostMalloc(&p, n, hipHostMallocDefault) != hipSuccess) return nullptr;
+            return static_cast<uint8_t*>(p);
+          },
+          [](uint8_t* p) { (void)hipHostFree(p); }};
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_hip, m) {
+  using namespace gfrs;
+  using namespace gfrs_py;
+  m.doc() = "gpu_rscode_amd gfx950 HIP kernels and runtime";
+  bind_common(m);
+
+  m.def("device_count", [] {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+  });
+  m.def(
+      "gemm",
+      [](uint64_t desc, int k, int m_pad, int64_t col0, int64_t ncols, bool bytewise, int max_blocks, uint64_t stream) {
+        check(launch_gf_gemm(reinterpret_cast<const void*>(desc), k, m_pad, col0, ncols, bytewise, max_blocks,
+                             as_stream(stream)),
+              "gf_gemm");
+      },
+      py::arg("desc"), py::arg("k"), py::arg("m_pad"), py::arg("col0"), py::arg("ncols"), py::arg("bytewise") = false,
+      py::arg("max_blocks") = 0, py::arg("stream") = 0);
+  m.def(
+      "gemm_variant",
+      [](uint64_t desc, int k, int m_pad, int64_t col0, int64_t ncols, int vec, int max_blocks, uint64_t stream) {
+        check(launch_gf_gemm_variant(reinterpret_cast<const void*>(desc), k, m_pad, col0, ncols, vec, max_blocks,
+                                     as_stream(stream)),
+              "gf_gemm_variant");
+      },
+      py::arg("desc"), py::arg("k"), py::arg("m_pad"), py::arg("col0"), py::arg("ncols"), py::arg("vec"),
+      py::arg("max_blocks") = 0, py::arg("stream") = 0);
+  m.def(
+      "invert",
+      [](uint64_t a, uint64_t a_inv, int n, int batch, uint64_t status, uint64_t desc, uint64_t sel_rows, int mm,
+         int m_pad, uint64_t stream) {
+        check(launch_gf_invert(reinterpret_cast<const uint8_t*>(a), reinterpret_cast<uint8_t*>(a_inv), n, batch,
+                               reinterpret_cast<int*>(status), reinterpret_cast<void*>(desc),
+                               reinterpret_cast<const int*>(sel_rows), mm, m_pad, as_stream(stream)),
+              "gf_invert");
+      },
+      py::arg("a"), py::arg("a_inv"), py::arg("n"), py::arg("batch") = 1, py::arg("status") = 0, py::arg("desc") = 0,
+      py::arg("sel_rows") = 0, py::arg("m") = 0, py::arg("m_pad") = 0, py::arg("stream") = 0);
+  m.def("gen_matrix", [](uint64_t e, int k, int p, int kind, uint64_t stream) {
+    check(launch_gen_matrix(reinterpret_cast<uint8_t*>(e), k, p, kind, as_stream(stream)), "gen_matrix");
+  });
+  m.def("perm_tables", [](uint64_t coeff, int mm, int k, uint64_t desc, int m_pad, uint64_t stream) {
+    check(launch_perm_tables(reinterpret_cast<const uint8_t*>(coeff), mm, k, reinterpret_cast<void*>(desc), m_pad,
+                             as_stream(stream)),
+          "perm_tables");
+  });
+  m.def("fill_random", [](uint64_t dst, int64_t bytes, uint64_t seed, uint64_t stream) {
+    check(launch_fill_random(reinterpret_cast<uint8_t*>(dst), bytes, seed, as_stream(stream)), "fill_random");
+  });
+  m.def("gather_rows", [](uint64_t g, uint64_t rows, uint64_t out, int mm, int k, uint64_t stream) {
+    check(launch_gather_rows(reinterpret_cast<const uint8_t*>(g), reinterpret_cast<const int*>(rows),
+                             reinterpret_cast<uint8_t*>(out), mm, k, as_stream(stream)),
+          "gather_rows");
+  });
+
+  m.def(
+      "gemm_host",
+      [](const std::vector<int>& devices, const std::vector<uint64_t>& in, const std::vector<uint64_t>& out,
+         const py::bytes& coeff, int64_t ncols, int streams, int64_t slice, int max_blocks, bool bytewise) {
+        PipelineOptions opt;
+        opt.streams = streams;
+        opt.slice_bytes = slice;
+        opt.max_blocks = max_blocks;
+        opt.bytewise = bytewise;
+        const Mat c = to_mat(coeff);
+        auto ip = ptrs<const uint8_t*>(in);
+        auto op = ptrs<uint8_t*>(out);
+        std::vector<PipelineStats> st;
+        double wall = 0;
+        hipError_t e;
+        {
+          py::gil_scoped_release nogil;
+          e = gemm_host_multi(devices, ip, op, c, ncols, opt, &st, &wall);
+        }
+        check(e, "gemm_host");
+        py::dict d;
+        d["wall_ms"] = wall;
+        py::list per;
+        for (const auto& s : st) per.append(stats_dict(s));
+        d["devices"] = per;
+        return d;
+      },
+      py::arg("devices"), py::arg("in_ptrs"), py::arg("out_ptrs"), py::arg("coeff"), py::arg("ncols"),
+      py::arg("streams") = 2, py::arg("slice") = 16 << 20, py::arg("max_blocks") = 0, py::arg("bytewise") = false);
+
+  auto gpu_gemm = [](const std::vector<int>& devices, int streams, int64_t slice, int max_blocks) -> GemmFn {
+    return [=](const std::vector<const uint8_t*>& in, const std::vector<uint8_t*>& out, const Mat& coeff,
+               int64_t ncols) {
+      PipelineOptions opt;
+      opt.streams = streams;
+      opt.slice_bytes = slice;
+      opt.max_blocks = max_blocks;
+      check(gemm_host_multi(devices, in, out, coeff, ncols, opt, nullptr, nullptr), "GPU pipeline");
+    };
+  };
+  m.def(
+      "encode_file",
+      [gpu_gemm](const std::string& file, int k, int p, const std::string& matrix, bool cpu_meta,
+                 const std::vector<int>& devices, int streams, int64_t slice, int max_blocks) {
+        const GemmFn g = gpu_gemm(devices, streams, slice, max_blocks);
+        FileReport r;
+        {
+          py::gil_scoped_release nogil;
+          r = encode_file(file, k, p, parse_matrix_kind(matrix), g, pinned_alloc(), cpu_meta);
+        }
+        return report(r);
+      },
+      py::arg("file"), py::arg("k"), py::arg("p"), py::arg("matrix") = "vandermonde", py::arg("cpu_meta") = false,
+      py::arg("devices") = std::vector<int>{0}, py::arg("streams") = 2, py::arg("slice") = 16 << 20,
+      py::arg("max_blocks") = 0);
+  m.def(
+      "decode_file",
+      [gpu_gemm](const std::string& file, const std::string& conf, const std::string& out,
+                 const std::vector<int>& devices, int streams, int64_t slice, int max_blocks) {
+        const GemmFn g = gpu_gemm(devices, streams, slice, max_blocks);
+        FileReport r;
+        {
+          py::gil_scoped_release nogil;
+          r = decode_file(file, conf, out, g, pinned_alloc());
+        }
+        return report(r);
+      },
+      py::arg("file"), py::arg("conf"), py::arg("out") = "", py::arg("devices") = std::vector<int>{0},
+      py::arg("streams") = 2, py::arg("slice") = 16 << 20, py::arg("max_blocks") = 0);
+}

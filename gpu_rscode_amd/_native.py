@@ -1,0 +1,47 @@
+"""Loading of the native extension modules.
+
+``torch`` is imported before ``_hip`` is loaded so the extension binds to the HIP runtime torch
+already mapped (both carry soname ``libamdhip64.so.7``): one runtime per process, pointers and
+streams interchangeable. On a machine with a GPU the HIP module is mandatory — :func:`hip` raises
+instead of silently falling back to a slower path.
+"""
+from __future__ import annotations
+
+import importlib
+import os
+
+import torch  # noqa: F401  (must precede the _hip import, see module docstring)
+
+from . import _build
+
+_mods: dict[str, object] = {}
+
+
+def _load(name: str, target: str):
+    if name in _mods:
+        return _mods[name]
+    so = _build.artifact(f"_{name}.so")
+    if os.environ.get("GPURS_NO_BUILD") != "1":
+        # incremental: a no-op when the .so is newer than every source
+        try:
+            _build.build(target)
+        except RuntimeError:
+            if not so.exists():
+                raise
+    mod = importlib.import_module(f"gpu_rscode_amd._{name}")
+    _mods[name] = mod
+    return mod
+
+
+def cpu():
+    """The C++ CPU codec module (always available; built with g++)."""
+    return _load("cpu", "cpu")
+
+
+def hip():
+    """The gfx950 HIP module. Raises if it cannot be built or loaded."""
+    return _load("hip", "hip")
+
+
+def gpu_available() -> bool:
+    return torch.cuda.is_available() and torch.cuda.device_count() > 0

@@ -1,0 +1,238 @@
+"""Reed-Solomon erasure codec — the framework's "model".
+
+A systematic (k, n) code over GF(2^8): generator ``G = [I_k; E]`` with ``E`` (p x k, p = n - k)
+from the reference Vandermonde (default, bit-compatible with ``src/matrix.cu:752-759``) or an MDS
+construction. Encode is one GF-GEMM ``parity = E . data``; decode inverts the k x k rows of G that
+survived and applies only the rows for erased natives, copying surviving natives in the same pass
+(the reference multiplies the full k x k inverse, ``src/matrix.cu:838-905``).
+
+Tensors: chunk rows are uint8 byte rows, either a 2-D ``[rows, C]`` tensor (use
+:func:`alloc_rows` to get 256-byte-pitched storage so every row is 16-byte aligned even for odd C)
+or a list of 1-D tensors. CUDA tensors run the gfx950 kernels; CPU tensors run the C++ codec.
+"""
+from __future__ import annotations
+
+from typing import Sequence
+
+import numpy as np
+import torch
+
+from .. import gf
+from .._native import cpu
+from ..ops.gemm import GemmPlan, _rows
+from ..ops.inverse import invert_into_plan
+from ..ops.matrix import decode_matrix, encoding_matrix
+
+PITCH = 256
+
+
+def alloc_rows(rows: int, ncols: int, device="cuda", fill: int | None = None) -> torch.Tensor:
+    """A [rows, ncols] uint8 view over storage whose row pitch is a multiple of 256 bytes."""
+    pitch = max(PITCH, (ncols + PITCH - 1) // PITCH * PITCH)
+    base = torch.empty(rows * pitch, dtype=torch.uint8, device=device)
+    if fill is not None:
+        base.fill_(fill)
+    return base.as_strided((rows, ncols), (pitch, 1))
+
+
+class UnrecoverableError(gf.SingularMatrixError):
+    """The surviving chunks do not determine the data (singular decode system)."""
+
+
+class ReedSolomon:
+    """(k, n) Reed-Solomon codec.
+
+    Args:
+        k: native (data) chunks. n: total chunks (k + parity).
+        matrix: ``"vandermonde"`` (reference, not MDS — SURVEY §2.2), ``"cauchy"`` or
+            ``"sys_vandermonde"`` (both MDS).
+        field: ``"gf256"`` (bytes are GF(2^8) symbols) or ``"gf16"`` (the design doc's GF(16)
+            method: each byte is two GF(2^4) symbols; needs n <= 16).
+        cpu_strategy / cpu_threads: multiply strategy and threads of the C++ CPU path.
+    """
+
+    def __init__(self, k: int, n: int, matrix: str = "vandermonde", field: str = "gf256",
+                 cpu_strategy: str = "row", cpu_threads: int = 1):
+        if not (1 <= k <= n):
+            raise ValueError("need 1 <= k <= n")
+        self.k, self.n, self.p = k, n, n - k
+        self.matrix, self.field = matrix, field
+        self.cpu_strategy, self.cpu_threads = cpu_strategy, cpu_threads
+        if field == "gf256":
+            if n > 256:
+                raise ValueError("GF(2^8) codes need n <= 256")
+            self.gf = gf.GF256
+            self.E = encoding_matrix(matrix, k, self.p)
+        elif field == "gf16":
+            if n > 16:
+                raise ValueError("GF(16) codes need n <= 16")
+            self.gf = gf.field(4)
+            self.E = self.gf.encoding_matrix(matrix, k, self.p).astype(np.uint8)
+        else:
+            raise ValueError(f"unknown field {field!r}")
+        self.G = np.vstack([np.eye(k, dtype=np.uint8), self.E]).astype(np.uint8)
+        self._plans: dict = {}
+        self._dm: dict = {}
+
+    # ---- helpers -----------------------------------------------------------------------------
+    def _maps(self, coeff: np.ndarray) -> np.ndarray | None:
+        if self.field == "gf256":
+            return None
+        m, k = coeff.shape
+        return np.stack([np.stack([gf.byte_map_gf16_nibbles(int(coeff[i, j])) for j in range(k)]) for i in range(m)])
+
+    def _plan(self, key, inputs, outputs, coeff, copies=None) -> GemmPlan:
+        plan = self._plans.get(key)
+        if plan is None:
+            maps = self._maps(coeff)
+            plan = GemmPlan(inputs, outputs, None if maps is not None else coeff, maps=maps, copies=copies)
+            if len(self._plans) > 64:
+                self._plans.clear()
+            self._plans[key] = plan
+        return plan
+
+    @staticmethod
+    def _key(tag, *row_lists):
+        return (tag,) + tuple(tuple((int(r.data_ptr()), r.numel()) if r is not None else None for r in rl)
+                              for rl in row_lists)
+
+    def _cpu_gemm(self, coeff: np.ndarray, ins: list[torch.Tensor], outs: list[torch.Tensor]) -> None:
+        ncols = min(r.numel() for r in ins + outs)
+        if self.field == "gf256":
+            cpu().gemm([int(r.data_ptr()) for r in ins], [int(r.data_ptr()) for r in outs],
+                       np.ascontiguousarray(coeff, dtype=np.uint8).tobytes(), ncols, self.cpu_strategy,
+                       self.cpu_threads)
+        else:
+            maps = self._maps(coeff)
+            for i, o in enumerate(outs):
+                acc = np.zeros(ncols, dtype=np.uint8)
+                for j, x in enumerate(ins):
+                    acc ^= maps[i, j][x[:ncols].numpy()]
+                o[:ncols].copy_(torch.from_numpy(acc))
+
+    # ---- encode ------------------------------------------------------------------------------
+    def encode(self, data, parity=None, stream: torch.cuda.Stream | None = None):
+        """parity = E . data. ``data``: [k, C] tensor or k rows. Returns the parity rows."""
+        ins = _rows(data)
+        if len(ins) != self.k:
+            raise ValueError(f"expected {self.k} data rows, got {len(ins)}")
+        ncols = min(r.numel() for r in ins)
+        if parity is None:
+            parity = alloc_rows(self.p, ncols, ins[0].device)
+        outs = _rows(parity)
+        if self.p == 0:
+            return parity
+        if ins[0].device.type == "cuda":
+            self._plan(self._key("enc", ins, outs), ins, outs, self.E).run(stream)
+        else:
+            self._cpu_gemm(self.E, ins, outs)
+        return parity
+
+    # ---- decode ------------------------------------------------------------------------------
+    def decode_matrix(self, rows: Sequence[int]) -> np.ndarray:
+        rows = tuple(int(r) for r in rows)
+        dm = self._dm.get(rows)
+        if dm is None:
+            if len(rows) != self.k or len(set(rows)) != self.k or min(rows) < 0 or max(rows) >= self.n:
+                raise ValueError(f"need {self.k} distinct chunk ids in [0, {self.n})")
+            try:
+                if self.field == "gf256":
+                    dm = decode_matrix(self.G, rows)
+                else:
+                    dm = self.gf.decode_matrix(self.G, rows).astype(np.uint8)
+            except gf.SingularMatrixError as e:
+                raise UnrecoverableError(str(e)) from None
+            self._dm[rows] = dm
+        return dm
+
+    def is_recoverable(self, rows: Sequence[int]) -> bool:
+        try:
+            self.decode_matrix(rows)
+            return True
+        except UnrecoverableError:
+            return False
+
+    def decode(self, survivors, rows: Sequence[int], out=None, stream: torch.cuda.Stream | None = None,
+               device_invert: bool = False):
+        """Reconstruct the k native rows from k surviving chunks.
+
+        Args:
+            survivors: [k, C] tensor or k rows, chunk ``rows[j]`` in position j (the reference's conf
+                order, ``src/decode.cu:302-318``).
+            rows: the chunk ids (0..n-1) of the survivors.
+            out: optional [k, C] destination for the natives.
+            device_invert: invert on the GPU (``gf_invert`` kernel writing the GEMM tables directly);
+                a singular pattern then yields zeros and a nonzero ``self.last_status`` instead of an
+                exception (checked lazily, no host sync on the hot path).
+        """
+        ins = _rows(survivors)
+        rows = [int(r) for r in rows]
+        if len(ins) != self.k or len(rows) != self.k:
+            raise ValueError(f"need exactly k={self.k} survivors")
+        ncols = min(r.numel() for r in ins)
+        dev = ins[0].device
+        if out is None:
+            out = alloc_rows(self.k, ncols, dev)
+        outs = _rows(out)
+        pos = {r: j for j, r in enumerate(rows)}
+        erased = [i for i in range(self.k) if i not in pos]
+        copies = [outs[r] if r < self.k else None for r in rows]
+        if dev.type != "cuda":
+            for j, r in enumerate(rows):
+                if r < self.k:
+                    outs[r][:ncols].copy_(ins[j][:ncols])
+            if erased:
+                dm = self.decode_matrix(rows)
+                self._cpu_gemm(dm[erased], ins, [outs[i] for i in erased])
+            return out
+        if not erased:  # pure copy: one fused pass with a single dummy output row would waste work
+            for j, r in enumerate(rows):
+                outs[r][:ncols].copy_(ins[j][:ncols], non_blocking=True)
+            return out
+        key = self._key(("dec", tuple(rows), device_invert), ins, outs)
+        if device_invert and self.field == "gf256":
+            plan = self._plans.get(key)
+            if plan is None:
+                plan = GemmPlan(ins, [outs[i] for i in erased], copies=copies, device_tables=True)
+                self._plans[key] = plan
+                plan.a_dev = torch.from_numpy(self.G[rows].copy()).to(dev)
+                plan.status = torch.zeros(1, dtype=torch.int32, device=dev)
+            invert_into_plan(plan.a_dev, plan, erased, status=plan.status, stream=stream)
+            self.last_status = plan.status
+        else:
+            dm = self.decode_matrix(rows)
+            plan = self._plan(key, ins, [outs[i] for i in erased], dm[erased], copies=copies)
+        plan.run(stream)
+        return out
+
+    def reconstruct(self, stripe, erased: Sequence[int], survivors: Sequence[int] | None = None,
+                    stream: torch.cuda.Stream | None = None):
+        """In-place repair of an n-row stripe: rewrite rows ``erased`` (natives and/or parity) from k
+        surviving rows. One GEMM: rows = G[erased] . inv(G[survivors]) . survivors."""
+        rows_all = _rows(stripe)
+        if len(rows_all) != self.n:
+            raise ValueError(f"stripe must have n={self.n} rows")
+        erased = sorted(set(int(e) for e in erased))
+        if survivors is None:
+            survivors = [i for i in range(self.n) if i not in erased][: self.k]
+        survivors = [int(s) for s in survivors]
+        if len(survivors) < self.k:
+            raise UnrecoverableError(f"only {len(survivors)} survivors, need k={self.k}")
+        if not erased:
+            return stripe
+        dm = self.decode_matrix(survivors)
+        coeff = self.gf.matmul(self.G[erased], dm).astype(np.uint8)
+        ins = [rows_all[s] for s in survivors]
+        outs = [rows_all[e] for e in erased]
+        if ins[0].device.type == "cuda":
+            self._plan(self._key(("rep", tuple(survivors), tuple(erased)), ins, outs), ins, outs, coeff).run(stream)
+        else:
+            self._cpu_gemm(coeff, ins, outs)
+        return stripe
+
+    def verify(self, data, parity) -> bool:
+        """True when ``parity`` is the encoding of ``data`` (recomputes and compares)."""
+        ins = _rows(data)
+        ref = self.encode(ins)
+        got = _rows(parity)
+        return all(torch.equal(a[: b.numel()], b[: a.numel()]) for a, b in zip(_rows(ref), got))

@@ -1,0 +1,233 @@
+"""GF-GEMM tensor op on gfx950: ``out[i] = XOR_j L_ij(in[j])`` over byte rows.
+
+``L_ij`` is any GF(2)-linear byte map — multiplication by a GF(2^8) coefficient (the reference's
+only case, ``src/matrix.cu:232-407``), or the nibble-wise GF(2^4) "GF(16) method" of
+``doc/design.tex:190-209``. The kernel (``csrc/kernels/gf_gemm.hip``) reads a device descriptor of
+row pointers + per-map v_perm tables; :class:`GemmPlan` builds and caches that descriptor so a
+repeated encode/decode is one kernel launch.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Sequence
+
+import numpy as np
+import torch
+
+from .. import gf
+from .._native import hip
+
+MAX_TILE = 16
+
+
+def tile_for(m: int) -> int:
+    t = 1
+    while t < m and t < MAX_TILE:
+        t <<= 1
+    return t
+
+
+def pad_m(m: int) -> int:
+    t = tile_for(m)
+    return (m + t - 1) // t * t
+
+
+@dataclass(frozen=True)
+class DescLayout:
+    in_off: int
+    copy_off: int
+    out_off: int
+    tab_off: int
+    bytes: int
+
+
+def desc_layout(k: int, m_pad: int) -> DescLayout:
+    """Mirror of ``gfrs::desc_layout`` (``csrc/include/gfrs/desc.h``); a test pins the two equal."""
+    in_off = 16
+    copy_off = in_off + 8 * k
+    out_off = copy_off + 8 * k
+    tab_off = (out_off + 8 * m_pad + 31) // 32 * 32
+    return DescLayout(in_off, copy_off, out_off, tab_off, tab_off + 32 * k * m_pad)
+
+
+def perm_tables_from_coeff(coeff: np.ndarray) -> np.ndarray:
+    """(m, k) GF(2^8) coefficients -> (m, k, 8) uint32 v_perm records."""
+    coeff = np.asarray(coeff, dtype=np.uint8)
+    cache: dict[int, np.ndarray] = {}
+    m, k = coeff.shape
+    out = np.zeros((m, k, 8), dtype=np.uint32)
+    for i in range(m):
+        for j in range(k):
+            c = int(coeff[i, j])
+            if c not in cache:
+                cache[c] = gf.perm_record(gf.byte_map_gf256(c))
+            out[i, j] = cache[c]
+    return out
+
+
+def perm_tables_from_maps(maps: np.ndarray) -> np.ndarray:
+    """(m, k, 256) linear byte maps -> (m, k, 8) uint32 v_perm records."""
+    maps = np.asarray(maps, dtype=np.uint8)
+    m, k, _ = maps.shape
+    out = np.zeros((m, k, 8), dtype=np.uint32)
+    for i in range(m):
+        for j in range(k):
+            out[i, j] = gf.perm_record(maps[i, j])
+    return out
+
+
+def build_desc(in_ptrs: Sequence[int], out_ptrs: Sequence[int], copy_ptrs: Sequence[int] | None,
+               tables: np.ndarray | None) -> np.ndarray:
+    """Descriptor bytes for k inputs, m outputs; ``tables`` is (m, k, 8) uint32 or None (zeros)."""
+    k, m = len(in_ptrs), len(out_ptrs)
+    if not (1 <= k <= 256 and 1 <= m <= 256):
+        raise ValueError("GF-GEMM supports 1 <= k, m <= 256")
+    mp = pad_m(m)
+    lay = desc_layout(k, mp)
+    d = np.zeros(lay.bytes, dtype=np.uint8)
+    d[0:16] = np.frombuffer(np.array([k, m, mp, 0], dtype="<i4").tobytes(), dtype=np.uint8)
+    d[lay.in_off : lay.in_off + 8 * k] = np.frombuffer(np.array(in_ptrs, dtype="<u8").tobytes(), dtype=np.uint8)
+    if copy_ptrs is not None:
+        if len(copy_ptrs) != k:
+            raise ValueError("copy_ptrs must have k entries")
+        d[lay.copy_off : lay.copy_off + 8 * k] = np.frombuffer(
+            np.array([p or 0 for p in copy_ptrs], dtype="<u8").tobytes(), dtype=np.uint8)
+    outs = list(out_ptrs) + [0] * (mp - m)
+    d[lay.out_off : lay.out_off + 8 * mp] = np.frombuffer(np.array(outs, dtype="<u8").tobytes(), dtype=np.uint8)
+    if tables is not None:
+        t = np.zeros((k, mp, 8), dtype="<u4")
+        t[:, :m, :] = np.transpose(np.asarray(tables, dtype=np.uint32), (1, 0, 2))
+        d[lay.tab_off :] = np.frombuffer(t.tobytes(), dtype=np.uint8)
+    return d
+
+
+def _rows(x) -> list[torch.Tensor]:
+    if isinstance(x, torch.Tensor):
+        if x.dim() == 1:
+            return [x]
+        if x.dim() != 2:
+            raise ValueError("expected a 2-D [rows, bytes] tensor or a list of 1-D tensors")
+        return [x[i] for i in range(x.shape[0])]
+    return list(x)
+
+
+def _check_rows(rows: list[torch.Tensor], what: str, device: torch.device | None) -> torch.device:
+    for r in rows:
+        if r.dtype != torch.uint8:
+            raise TypeError(f"{what} rows must be uint8, got {r.dtype}")
+        if r.dim() != 1 or (r.numel() > 1 and r.stride(0) != 1):
+            raise ValueError(f"{what} rows must be contiguous 1-D byte rows")
+        if device is None:
+            device = r.device
+        elif r.device != device:
+            raise ValueError(f"all rows must live on one device ({device} vs {r.device})")
+    return device
+
+
+class GemmPlan:
+    """A reusable device GF-GEMM.
+
+    Args:
+        inputs: k input byte rows (2-D uint8 tensor or list of 1-D tensors) on one GPU.
+        outputs: m output byte rows on the same GPU.
+        coeff: (m, k) GF(2^8) coefficients; or
+        maps: (m, k, 256) GF(2)-linear byte maps (e.g. :func:`gf.byte_map_gf16_nibbles`); or neither
+            with ``device_tables=True`` (tables are written later on device, e.g. by
+            :func:`gpu_rscode_amd.ops.inverse.invert_into_plan`).
+        copies: optional k destination rows (or None entries): input j is copied there in the same
+            pass (the fused survivor copy of decode).
+    """
+
+    def __init__(self, inputs, outputs, coeff=None, *, maps=None, copies=None, device_tables: bool = False):
+        self.inputs = _rows(inputs)
+        self.outputs = _rows(outputs)
+        self.copies = None if copies is None else [c for c in copies]
+        dev = _check_rows(self.inputs, "input", None)
+        dev = _check_rows(self.outputs, "output", dev)
+        if self.copies is not None:
+            if len(self.copies) != len(self.inputs):
+                raise ValueError("copies must have one entry per input row")
+            dev = _check_rows([c for c in self.copies if c is not None], "copy", dev)
+        if dev.type != "cuda":
+            raise ValueError("GemmPlan runs on a GPU; use the CPU codec for host tensors")
+        self.device = dev
+        self.k, self.m = len(self.inputs), len(self.outputs)
+        self.m_pad = pad_m(self.m)
+        lens = [r.numel() for r in self.inputs + self.outputs + [c for c in (self.copies or []) if c is not None]]
+        self.ncols = min(lens) if lens else 0
+        if coeff is not None:
+            tables = perm_tables_from_coeff(np.asarray(coeff).reshape(self.m, self.k))
+        elif maps is not None:
+            tables = perm_tables_from_maps(maps)
+        elif device_tables:
+            tables = None
+        else:
+            raise ValueError("need coeff, maps or device_tables=True")
+        ptr = lambda t: int(t.data_ptr())  # noqa: E731
+        self.bytewise = any(ptr(r) % 16 for r in self.inputs + self.outputs) or any(
+            c is not None and ptr(c) % 16 for c in (self.copies or []))
+        host = build_desc([ptr(r) for r in self.inputs], [ptr(r) for r in self.outputs],
+                          None if self.copies is None else [ptr(c) if c is not None else 0 for c in self.copies],
+                          tables)
+        self.desc = torch.from_numpy(host).to(self.device)
+        self.layout = desc_layout(self.k, self.m_pad)
+        self._mark_ready()
+
+    def _mark_ready(self) -> None:
+        # descriptor writes are ordered on the current stream; launches on other streams wait on this
+        self._ready = torch.cuda.Event()
+        self._ready.record(torch.cuda.current_stream(self.device))
+
+    def set_coeff(self, coeff, stream: torch.cuda.Stream | None = None) -> None:
+        """Replace the coefficient tables (host-built, async H2D on ``stream``)."""
+        tables = perm_tables_from_coeff(np.asarray(coeff).reshape(self.m, self.k))
+        t = np.zeros((self.k, self.m_pad, 8), dtype="<u4")
+        t[:, : self.m, :] = np.transpose(tables, (1, 0, 2))
+        src = torch.from_numpy(np.frombuffer(t.tobytes(), dtype=np.uint8).copy())
+        with torch.cuda.stream(stream) if stream is not None else _null():
+            self.desc[self.layout.tab_off :].copy_(src, non_blocking=False)
+            self._mark_ready()
+
+    def table_view(self) -> torch.Tensor:
+        """Device view of the table block (k, m_pad, 8) int32 words."""
+        return self.desc[self.layout.tab_off :].view(torch.int32).view(self.k, self.m_pad, 8)
+
+    def run(self, stream: torch.cuda.Stream | None = None, col0: int = 0, ncols: int | None = None,
+            max_blocks: int = 0, vec: int = 1) -> None:
+        """Launch asynchronously on ``stream`` (default: the current stream)."""
+        ncols = self.ncols - col0 if ncols is None else ncols
+        if col0 < 0 or ncols < 0 or col0 + ncols > self.ncols:
+            raise ValueError(f"column range [{col0}, {col0 + ncols}) outside rows of {self.ncols} bytes")
+        st = stream or torch.cuda.current_stream(self.device)
+        if self._ready is not None:
+            st.wait_event(self._ready)
+            self._ready = None
+        if stream is not None:
+            self.desc.record_stream(stream)
+        s = st.cuda_stream
+        h = hip()
+        if self.bytewise or vec == 0:
+            h.gemm(int(self.desc.data_ptr()), self.k, self.m_pad, col0, ncols, True, max_blocks, s)
+        elif vec == 1:
+            h.gemm(int(self.desc.data_ptr()), self.k, self.m_pad, col0, ncols, False, max_blocks, s)
+        else:
+            h.gemm_variant(int(self.desc.data_ptr()), self.k, self.m_pad, col0, ncols, vec, max_blocks, s)
+
+
+class _null:
+    def __enter__(self):
+        return None
+
+    def __exit__(self, *a):
+        return False
+
+
+def gf_gemm(coeff, inputs, outputs=None, *, maps=None, copies=None, stream=None) -> torch.Tensor:
+    """One-shot GF-GEMM. Returns the output tensor (allocated as [m, C] when ``outputs`` is None)."""
+    ins = _rows(inputs)
+    m = (np.asarray(coeff).shape[0] if coeff is not None else np.asarray(maps).shape[0])
+    if outputs is None:
+        c = min(r.numel() for r in ins)
+        outputs = torch.empty((m, c), dtype=torch.uint8, device=ins[0].device)
+    GemmPlan(ins, outputs, coeff, maps=maps, copies=copies).run(stream)
+    return outputs
