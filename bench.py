@@ -53,7 +53,10 @@ def parse():
     ap.add_argument("--n", type=int, default=14)
     ap.add_argument("--bytes", type=int, default=1 << 30, help="input bytes per GPU")
     ap.add_argument("--erasures", type=int, default=4)
-    ap.add_argument("--vec", type=int, default=1, help="16-byte groups per lane (ablation)")
+    ap.add_argument("--vec", type=int, default=None, help="kernel variant: 16-byte groups per lane (ablation)")
+    ap.add_argument("--pf", type=int, default=2, help="kernel variant: rows in flight (with --vec)")
+    ap.add_argument("--nt", action="store_true", help="kernel variant: non-temporal (with --vec)")
+    ap.add_argument("--no-overlap", action="store_true", help="invert on the main stream (no side stream)")
     ap.add_argument("--gather", action="store_true", help="gather parity to rank 0 every step (RCCL)")
     ap.add_argument("--e2e", action="store_true", help="also time the pinned host->device->host pipeline")
     ap.add_argument("--streams", type=int, default=4)
@@ -117,13 +120,23 @@ def main():
 
     h = hip()
     stream = torch.cuda.current_stream(dev)
+    side = torch.cuda.Stream(dev)  # decode-system inversion overlaps the encode GEMM
+    inv_done = torch.cuda.Event()
+    kv = dict(vec=a.vec, pf=a.pf, nt=a.nt)
 
     def step(i: int):
-        enc.run(vec=a.vec)
         plan = dec[i % len(dec)]
+        inv_stream = stream if a.no_overlap else side
+        if not a.no_overlap:
+            side.wait_stream(stream)  # the previous step's decode has consumed this plan's tables
         h.invert(plan.a_dev.data_ptr(), 0, k, 1, plan.status.data_ptr(), plan.desc.data_ptr(),
-                 plan.sel.data_ptr(), plan.m, plan.m_pad, stream.cuda_stream)
-        plan.run(vec=a.vec)
+                 plan.sel.data_ptr(), plan.m, plan.m_pad, inv_stream.cuda_stream)
+        if not a.no_overlap:
+            inv_done.record(side)
+        enc.run(**kv)
+        if not a.no_overlap:
+            stream.wait_event(inv_done)
+        plan.run(**kv)
         if a.gather and world > 1:
             flat = parity.as_strided((p * parity.stride(0),), (1,))
             dist.gather(flat, gathered if rank == 0 else None, dst=0)

@@ -16,9 +16,10 @@ namespace gfrs {
 hipError_t launch_gf_gemm(const void* desc, int k, int m_pad, int64_t col0, int64_t ncols,
                           bool force_bytewise, int max_blocks, hipStream_t stream);
 
-// Variant selector for benchmarks/ablation: vec = 16-byte groups per thread (1 or 2).
+// Variant selector for benchmarks/ablation: vec = 16-byte groups per lane (0 = byte kernel),
+// pf = input rows kept in flight per lane, nt = non-temporal loads/stores.
 hipError_t launch_gf_gemm_variant(const void* desc, int k, int m_pad, int64_t col0, int64_t ncols,
-                                  int vec, int max_blocks, hipStream_t stream);
+                                  int vec, int pf, bool nt, int max_blocks, hipStream_t stream);
 
 // ---- Gauss-Jordan inverse (csrc/kernels/gf_invert.hip) ---------------------------------------
 // Inverts `batch` n x n matrices (row-major, contiguous) with row pivoting, one workgroup each,

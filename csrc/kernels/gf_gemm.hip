@@ -97,11 +97,46 @@ __device__ __forceinline__ TileMap map_block(int ntiles) {
   return {local % ntiles, int64_t(local / ntiles) * 8 + xcd};
 }
 
-// Vector kernel: each lane owns V consecutive 16-byte groups of every row.
-template <int MT, int V>
+template <bool NT>
+__device__ __forceinline__ u32x4 ld16(gptr<const u32x4> p) {
+  if constexpr (NT) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+template <bool NT>
+__device__ __forceinline__ void st16(gptr<u32x4> p, u32x4 v) {
+  if constexpr (NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+
+// Byte-granular GEMM of `nbytes` columns starting at `off` for one lane (ragged tail).
+template <int MT>
+__device__ void tail_bytes(const DescView& d, int k, int m_pad, int i0, bool do_copy, int64_t off, int nbytes) {
+  for (int b = 0; b < nbytes; ++b) {
+    uint32_t acc[MT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i) acc[i] = 0;
+    for (int j = 0; j < k; ++j) {
+      const uint8_t x = ((gptr<const uint8_t>)d.in[j])[off + b];
+      if (do_copy && d.copy[j]) ((gptr<uint8_t>)d.copy[j])[off + b] = x;
+      const Sel s = make_sel(x);
+      const auto t = d.tab + (size_t(j) * m_pad + i0) * kPermStride;
+#pragma unroll
+      for (int i = 0; i < MT; ++i) acc[i] = mac_map(acc[i], t + i * kPermStride, s);
+    }
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+      if (d.out[i0 + i]) ((gptr<uint8_t>)d.out[i0 + i])[off + b] = uint8_t(acc[i]);
+  }
+}
+
+// Vector kernel: each lane owns V consecutive 16-byte groups of every row and keeps PF input rows
+// in flight (a static register ring: the ring slot of row j is j % PF, resolved at compile time by
+// unrolling the row loop PF-fold). Lane `ngroups` (one past the last full group) also processes the
+// < 16*V ragged tail bytes, so no second launch is needed for odd chunk sizes.
+template <int MT, int V, int PF, bool NT>
 __global__ __launch_bounds__(kBlock) void gf_gemm_vec_kernel(DescView d, int k, int m_pad, int ntiles,
                                                              int64_t col0, int64_t ngroups, int64_t nblk,
-                                                             int64_t ncb) {
+                                                             int64_t ncb, int tail) {
   const TileMap tm = map_block(ntiles);
   if (tm.cb0 >= ncb) return;
   const int i0 = tm.tile * MT;
@@ -109,7 +144,10 @@ __global__ __launch_bounds__(kBlock) void gf_gemm_vec_kernel(DescView d, int k, 
 
   for (int64_t cb = tm.cb0; cb < nblk; cb += ncb) {
     const int64_t g = cb * kBlock + threadIdx.x;
-    if (g >= ngroups) continue;
+    if (g >= ngroups) {
+      if (g == ngroups && tail > 0) tail_bytes<MT>(d, k, m_pad, i0, do_copy, col0 + g * (16 * V), tail);
+      continue;
+    }
     const int64_t off = col0 + g * (16 * V);
 
     uint32_t acc[MT][4 * V];
@@ -118,40 +156,47 @@ __global__ __launch_bounds__(kBlock) void gf_gemm_vec_kernel(DescView d, int k, 
 #pragma unroll
       for (int w = 0; w < 4 * V; ++w) acc[i][w] = 0;
 
-    u32x4 cur[V], nxt[V];
-    {
-      const auto src = row_vec(d.in[0], off);
+    u32x4 ring[PF][V];
 #pragma unroll
-      for (int v = 0; v < V; ++v) cur[v] = src[v];
-    }
-    for (int j = 0; j < k; ++j) {
-      if (j + 1 < k) {
-        const auto src = row_vec(d.in[j + 1], off);
+    for (int u = 0; u < PF; ++u)
+      if (u < k) {
+        const auto src = row_vec(d.in[u], off);
 #pragma unroll
-        for (int v = 0; v < V; ++v) nxt[v] = src[v];
+        for (int v = 0; v < V; ++v) ring[u][v] = ld16<NT>(src + v);
       }
-      if (do_copy) {
-        const uint64_t cp = d.copy[j];
-        if (cp) {
-          const auto dst = row_vec_w(cp, off);
+
+    for (int j0 = 0; j0 < k; j0 += PF) {
 #pragma unroll
-          for (int v = 0; v < V; ++v) dst[v] = cur[v];
+      for (int u = 0; u < PF; ++u) {
+        const int j = j0 + u;
+        if (j < k) {
+          u32x4 x[V];
+#pragma unroll
+          for (int v = 0; v < V; ++v) x[v] = ring[u][v];
+          if (j + PF < k) {
+            const auto src = row_vec(d.in[j + PF], off);
+#pragma unroll
+            for (int v = 0; v < V; ++v) ring[u][v] = ld16<NT>(src + v);
+          }
+          if (do_copy) {
+            const uint64_t cp = d.copy[j];
+            if (cp) {
+              const auto dst = row_vec_w(cp, off);
+#pragma unroll
+              for (int v = 0; v < V; ++v) st16<NT>(dst + v, x[v]);
+            }
+          }
+          const auto t = d.tab + (size_t(j) * m_pad + i0) * kPermStride;
+#pragma unroll
+          for (int v = 0; v < V; ++v) {
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+              const Sel s = make_sel(x[v][w]);
+#pragma unroll
+              for (int i = 0; i < MT; ++i) acc[i][v * 4 + w] = mac_map(acc[i][v * 4 + w], t + i * kPermStride, s);
+            }
+          }
         }
-      }
-      const auto t = d.tab + (size_t(j) * m_pad + i0) * kPermStride;
-#pragma unroll
-      for (int v = 0; v < V; ++v) {
-        const u32x4 wv = cur[v];
-#pragma unroll
-        for (int w = 0; w < 4; ++w) {
-          const Sel s = make_sel(wv[w]);
-#pragma unroll
-          for (int i = 0; i < MT; ++i) acc[i][v * 4 + w] = mac_map(acc[i][v * 4 + w], t + i * kPermStride, s);
-        }
-      }
-      if (j + 1 < k) {
-#pragma unroll
-        for (int v = 0; v < V; ++v) cur[v] = nxt[v];
       }
     }
 
@@ -162,7 +207,7 @@ __global__ __launch_bounds__(kBlock) void gf_gemm_vec_kernel(DescView d, int k, 
       const auto dst = row_vec_w(op, off);
 #pragma unroll
       for (int v = 0; v < V; ++v)
-        dst[v] = u32x4{acc[i][v * 4 + 0], acc[i][v * 4 + 1], acc[i][v * 4 + 2], acc[i][v * 4 + 3]};
+        st16<NT>(dst + v, u32x4{acc[i][v * 4 + 0], acc[i][v * 4 + 1], acc[i][v * 4 + 2], acc[i][v * 4 + 3]});
     }
   }
 }
@@ -217,18 +262,15 @@ inline Grid make_grid(int64_t items, int ntiles, int max_blocks) {
   return g;
 }
 
-template <int MT>
-hipError_t launch_vec(const DescView& d, int k, int m_pad, int64_t col0, int64_t ngroups, int vec, int max_blocks,
-                      hipStream_t stream) {
+template <int MT, int V, int PF, bool NT>
+hipError_t launch_vec_cfg(const DescView& d, int k, int m_pad, int64_t col0, int64_t ngroups, int tail, int max_blocks,
+                          hipStream_t stream) {
   const int ntiles = m_pad / MT;
-  if (ngroups <= 0) return hipSuccess;
-  if (vec == 2) {
-    const Grid g = make_grid(ngroups, ntiles, max_blocks);
-    gf_gemm_vec_kernel<MT, 2><<<g.blocks, kBlock, 0, stream>>>(d, k, m_pad, ntiles, col0, ngroups, g.nblk, g.ncb);
-  } else {
-    const Grid g = make_grid(ngroups, ntiles, max_blocks);
-    gf_gemm_vec_kernel<MT, 1><<<g.blocks, kBlock, 0, stream>>>(d, k, m_pad, ntiles, col0, ngroups, g.nblk, g.ncb);
-  }
+  // one extra lane past the last group handles the ragged tail
+  const Grid g = make_grid(ngroups + (tail > 0 ? 1 : 0), ntiles, max_blocks);
+  if (g.nblk == 0) return hipSuccess;
+  gf_gemm_vec_kernel<MT, V, PF, NT>
+      <<<g.blocks, kBlock, 0, stream>>>(d, k, m_pad, ntiles, col0, ngroups, g.nblk, g.ncb, tail);
   return hipGetLastError();
 }
 
@@ -254,7 +296,43 @@ hipError_t dispatch_tile(int m_pad, F&& f) {
   }
 }
 
-hipError_t run(const void* desc, int k, int m_pad, int64_t col0, int64_t ncols, bool bytewise, int vec,
+// Kernel configuration (V = 16-byte groups per lane, PF = rows in flight, NT = non-temporal).
+struct Cfg {
+  int vec = 1, pf = 2;
+  bool nt = false;
+};
+
+template <int MT>
+hipError_t launch_vec(const DescView& d, int k, int m_pad, int64_t col0, int64_t ncols, Cfg c, int max_blocks,
+                      hipStream_t stream) {
+  const int gbytes = 16 * c.vec;
+  const int64_t ngroups = ncols / gbytes;
+  const int tail = int(ncols - ngroups * gbytes);
+#define GFRS_CFG(V, PF, NT)                                                                             \
+  if (c.vec == V && c.pf == PF && c.nt == NT)                                                           \
+    return launch_vec_cfg<MT, V, PF, NT>(d, k, m_pad, col0, ngroups, tail, max_blocks, stream);
+  GFRS_CFG(1, 1, false)
+  GFRS_CFG(1, 2, false)
+  GFRS_CFG(1, 4, false)
+  GFRS_CFG(1, 2, true)
+  GFRS_CFG(1, 4, true)
+  GFRS_CFG(2, 1, false)
+  GFRS_CFG(2, 2, false)
+  GFRS_CFG(2, 2, true)
+#undef GFRS_CFG
+  return hipErrorInvalidValue;
+}
+
+// Default configuration per output tile (chosen by scripts/kbench.py on MI355X; see profiles/).
+Cfg default_cfg(int mt) {
+  Cfg c;
+  c.vec = 1;
+  c.pf = mt <= 4 ? 4 : 2;
+  c.nt = false;
+  return c;
+}
+
+hipError_t run(const void* desc, int k, int m_pad, int64_t col0, int64_t ncols, bool bytewise, const Cfg* cfg,
                int max_blocks, hipStream_t stream) {
   if (k <= 0 || m_pad <= 0 || ncols <= 0) return hipSuccess;
   if (m_pad % tile_for(m_pad) != 0) return hipErrorInvalidValue;
@@ -262,17 +340,7 @@ hipError_t run(const void* desc, int k, int m_pad, int64_t col0, int64_t ncols, 
   return dispatch_tile(m_pad, [&](auto mt) -> hipError_t {
     constexpr int MT = decltype(mt)::value;
     if (bytewise || (col0 & 15)) return launch_byte<MT>(d, k, m_pad, col0, ncols, max_blocks, stream);
-    const int64_t n16 = ncols / 16;
-    const int64_t nmain = (vec == 2) ? n16 / 2 : n16;
-    hipError_t e = launch_vec<MT>(d, k, m_pad, col0, nmain, vec, max_blocks, stream);
-    if (e != hipSuccess) return e;
-    int64_t done = nmain * 16 * vec;
-    if (vec == 2 && (n16 & 1)) {
-      e = launch_vec<MT>(d, k, m_pad, col0 + done, 1, 1, max_blocks, stream);
-      if (e != hipSuccess) return e;
-      done += 16;
-    }
-    return launch_byte<MT>(d, k, m_pad, col0 + done, ncols - done, max_blocks, stream);
+    return launch_vec<MT>(d, k, m_pad, col0, ncols, cfg ? *cfg : default_cfg(MT), max_blocks, stream);
   });
 }
 
@@ -280,13 +348,17 @@ hipError_t run(const void* desc, int k, int m_pad, int64_t col0, int64_t ncols, 
 
 hipError_t launch_gf_gemm(const void* desc, int k, int m_pad, int64_t col0, int64_t ncols, bool force_bytewise,
                           int max_blocks, hipStream_t stream) {
-  return run(desc, k, m_pad, col0, ncols, force_bytewise, 1, max_blocks, stream);
+  return run(desc, k, m_pad, col0, ncols, force_bytewise, nullptr, max_blocks, stream);
 }
 
-hipError_t launch_gf_gemm_variant(const void* desc, int k, int m_pad, int64_t col0, int64_t ncols, int vec,
-                                  int max_blocks, hipStream_t stream) {
-  if (vec == 0) return run(desc, k, m_pad, col0, ncols, true, 1, max_blocks, stream);
-  return run(desc, k, m_pad, col0, ncols, false, vec, max_blocks, stream);
+hipError_t launch_gf_gemm_variant(const void* desc, int k, int m_pad, int64_t col0, int64_t ncols, int vec, int pf,
+                                  bool nt, int max_blocks, hipStream_t stream) {
+  if (vec == 0) return run(desc, k, m_pad, col0, ncols, true, nullptr, max_blocks, stream);
+  Cfg c;
+  c.vec = vec;
+  c.pf = pf;
+  c.nt = nt;
+  return run(desc, k, m_pad, col0, ncols, false, &c, max_blocks, stream);
 }
 
 }  // namespace gfrs

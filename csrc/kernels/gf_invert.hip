@@ -24,7 +24,6 @@ namespace {
 
 __constant__ Tables d_gf_tables = make_tables();
 
-constexpr int kInvBlock = 256;
 
 __device__ __forceinline__ uint8_t dmul_log(const uint8_t* exp_s, int la, int lb) { return exp_s[la + lb]; }
 
@@ -64,6 +63,9 @@ __device__ void perm_record(const uint8_t* exp_s, const uint16_t* log_s, uint8_t
   rec[5] = rec[6] = rec[7] = 0;
 }
 
+// One wave (64 lanes) for n <= 64: the per-column barriers are then single-wave s_barriers and
+// the k=10 decode system inverts in a few microseconds; 256 lanes for wide stripes.
+template <int kInvBlock>
 __global__ __launch_bounds__(kInvBlock) void gf_invert_kernel(const uint8_t* __restrict__ a,
                                                               uint8_t* __restrict__ a_inv, int n,
                                                               int* __restrict__ status, uint32_t* __restrict__ tab,
@@ -154,16 +156,20 @@ hipError_t launch_gf_invert(const uint8_t* a, uint8_t* a_inv, int n, int batch, 
   if (n <= 0 || n > 256 || batch <= 0) return hipErrorInvalidValue;
   if (desc && (batch != 1 || !sel_rows || m <= 0 || m > m_pad)) return hipErrorInvalidValue;
   const size_t lds = 2064 + 2 * size_t(n) * n;
+  uint32_t* tab = nullptr;
+  if (desc) tab = reinterpret_cast<uint32_t*>(static_cast<char*>(desc) + desc_layout(n, m_pad).tab_off);
+  if (n <= 64) {
+    gf_invert_kernel<64><<<batch, 64, lds, stream>>>(a, a_inv, n, status, tab, sel_rows, m, m_pad);
+    return hipGetLastError();
+  }
   static bool attr_set = false;  // >64 KiB of dynamic LDS must be opted into once per process
   if (lds > 65536 && !attr_set) {
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gf_invert_kernel),
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gf_invert_kernel<256>),
                                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (e != hipSuccess) return e;
     attr_set = true;
   }
-  uint32_t* tab = nullptr;
-  if (desc) tab = reinterpret_cast<uint32_t*>(static_cast<char*>(desc) + desc_layout(n, m_pad).tab_off);
-  gf_invert_kernel<<<batch, kInvBlock, lds, stream>>>(a, a_inv, n, status, tab, sel_rows, m, m_pad);
+  gf_invert_kernel<256><<<batch, 256, lds, stream>>>(a, a_inv, n, status, tab, sel_rows, m, m_pad);
   return hipGetLastError();
 }
 

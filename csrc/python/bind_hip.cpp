@@ -61,13 +61,14 @@ PYBIND11_MODULE(_hip, m) {
       py::arg("max_blocks") = 0, py::arg("stream") = 0);
   m.def(
       "gemm_variant",
-      [](uint64_t desc, int k, int m_pad, int64_t col0, int64_t ncols, int vec, int max_blocks, uint64_t stream) {
-        check(launch_gf_gemm_variant(reinterpret_cast<const void*>(desc), k, m_pad, col0, ncols, vec, max_blocks,
-                                     as_stream(stream)),
+      [](uint64_t desc, int k, int m_pad, int64_t col0, int64_t ncols, int vec, int pf, bool nt, int max_blocks,
+         uint64_t stream) {
+        check(launch_gf_gemm_variant(reinterpret_cast<const void*>(desc), k, m_pad, col0, ncols, vec, pf, nt,
+                                     max_blocks, as_stream(stream)),
               "gf_gemm_variant");
       },
       py::arg("desc"), py::arg("k"), py::arg("m_pad"), py::arg("col0"), py::arg("ncols"), py::arg("vec"),
-      py::arg("max_blocks") = 0, py::arg("stream") = 0);
+      py::arg("pf") = 2, py::arg("nt") = false, py::arg("max_blocks") = 0, py::arg("stream") = 0);
   m.def(
       "invert",
       [](uint64_t a, uint64_t a_inv, int n, int batch, uint64_t status, uint64_t desc, uint64_t sel_rows, int mm,

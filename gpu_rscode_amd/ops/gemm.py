@@ -193,8 +193,12 @@ class GemmPlan:
         return self.desc[self.layout.tab_off :].view(torch.int32).view(self.k, self.m_pad, 8)
 
     def run(self, stream: torch.cuda.Stream | None = None, col0: int = 0, ncols: int | None = None,
-            max_blocks: int = 0, vec: int = 1) -> None:
-        """Launch asynchronously on ``stream`` (default: the current stream)."""
+            max_blocks: int = 0, vec: int | None = None, pf: int = 2, nt: bool = False) -> None:
+        """Launch asynchronously on ``stream`` (default: the current stream).
+
+        ``vec``/``pf``/``nt`` select an explicit kernel variant (ablation; ``vec=0`` = byte kernel);
+        by default the tuned configuration for the output tile is used.
+        """
         ncols = self.ncols - col0 if ncols is None else ncols
         if col0 < 0 or ncols < 0 or col0 + ncols > self.ncols:
             raise ValueError(f"column range [{col0}, {col0 + ncols}) outside rows of {self.ncols} bytes")
@@ -206,12 +210,12 @@ class GemmPlan:
             self.desc.record_stream(stream)
         s = st.cuda_stream
         h = hip()
-        if self.bytewise or vec == 0:
+        if self.bytewise:
             h.gemm(int(self.desc.data_ptr()), self.k, self.m_pad, col0, ncols, True, max_blocks, s)
-        elif vec == 1:
+        elif vec is None:
             h.gemm(int(self.desc.data_ptr()), self.k, self.m_pad, col0, ncols, False, max_blocks, s)
         else:
-            h.gemm_variant(int(self.desc.data_ptr()), self.k, self.m_pad, col0, ncols, vec, max_blocks, s)
+            h.gemm_variant(int(self.desc.data_ptr()), self.k, self.m_pad, col0, ncols, vec, pf, nt, max_blocks, s)
 
 
 class _null:

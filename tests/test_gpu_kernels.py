@@ -42,15 +42,16 @@ def test_gemm_matches_oracle(k, m, ncols):
     assert np.array_equal(out.cpu().numpy(), want)
 
 
-@pytest.mark.parametrize("vec", [0, 1, 2])
-def test_gemm_variants_agree(vec):
+@pytest.mark.parametrize("vec,pf,nt", [(0, 1, False), (1, 1, False), (1, 2, False), (1, 4, False), (1, 2, True),
+                                       (1, 4, True), (2, 1, False), (2, 2, False), (2, 2, True)])
+def test_gemm_variants_agree(vec, pf, nt):
     _native_loaded()
-    k, m, ncols = 10, 4, 300001
+    k, m, ncols = 10, 4, 300001 + 16 * vec
     rng = np.random.default_rng(7)
     coeff = rng.integers(0, 256, size=(m, k), dtype=np.uint8)
     host, dev = _rand_rows(k, ncols, 3)
     out = alloc_rows(m, ncols, "cuda", fill=0)
-    GemmPlan(dev, out, coeff).run(vec=vec)
+    GemmPlan(dev, out, coeff).run(vec=vec, pf=pf, nt=nt)
     torch.cuda.synchronize()
     assert np.array_equal(out.cpu().numpy(), GF256.gemm(coeff, host))
 
