@@ -323,12 +323,15 @@ hipError_t launch_vec(const DescView& d, int k, int m_pad, int64_t col0, int64_t
   return hipErrorInvalidValue;
 }
 
-// Default configuration per output tile (chosen by scripts/kbench.py on MI355X; see profiles/).
+// Default configuration per output tile, chosen by scripts/kbench.py on MI355X
+// (profiles/r01_kbench/kbench.json): non-temporal streaming with two rows in flight wins on every
+// HBM-bound shape (k=10 encode 5.6 TB/s, 4-erasure decode 5.8 TB/s); the VALU-bound wide tile
+// (MT = 16) prefers two 16-byte groups per lane to amortise the per-row table moves.
 Cfg default_cfg(int mt) {
   Cfg c;
-  c.vec = 1;
-  c.pf = mt <= 4 ? 4 : 2;
-  c.nt = false;
+  c.vec = mt >= 16 ? 2 : 1;
+  c.pf = 2;
+  c.nt = true;
   return c;
 }
 

@@ -1,0 +1,264 @@
+"""C++ CPU reference codec, descriptors, file formats and CLIs (CPU only).
+
+Parity fixture: tests/fixtures/golden_parity.json holds SHA-256 digests of the chunk files the
+reference's own CPU codec (src/cpu-rs.c, compiled with gcc in /tmp — never in this repo) wrote
+for deterministic inputs; our encoder must reproduce them bit for bit (BASELINE config #1).
+"""
+import hashlib
+import itertools
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+import torch
+
+from gpu_rscode_amd import ReedSolomon, gf
+from gpu_rscode_amd.gf import GF256
+from gpu_rscode_amd._native import cpu
+from gpu_rscode_amd._build import binary
+from gpu_rscode_amd.ops.gemm import build_desc, desc_layout, pad_m, perm_tables_from_coeff
+from gpu_rscode_amd.utils import fileformat as ff
+
+FIX = os.path.join(os.path.dirname(__file__), "fixtures", "golden_parity.json")
+STRATEGIES = ["logexp", "logexp0", "logexp1", "logexp2", "logexp3", "loop", "full", "double", "perm", "row"]
+
+
+def golden_input(n: int) -> bytes:
+    out = bytearray()
+    i = 0
+    while len(out) < n:
+        out += hashlib.sha256(b"gpu_rscode_amd-golden" + i.to_bytes(8, "little")).digest()
+        i += 1
+    return bytes(out[:n])
+
+
+def sha(path):
+    with open(path, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
+
+
+# ---- descriptors -------------------------------------------------------------------------------
+@pytest.mark.parametrize("k,m", [(1, 1), (4, 2), (10, 4), (10, 3), (16, 4), (128, 32), (7, 17), (255, 1)])
+def test_desc_layout_python_equals_native(k, m):
+    mp = pad_m(m)
+    assert cpu().pad_m(m) == mp
+    lay = desc_layout(k, mp)
+    nat = cpu().desc_layout(k, mp)
+    assert (lay.in_off, lay.copy_off, lay.out_off, lay.tab_off, lay.bytes) == (
+        nat["in_off"], nat["copy_off"], nat["out_off"], nat["tab_off"], nat["bytes"])
+
+
+def test_build_desc_python_equals_native():
+    k, m = 10, 3
+    coeff = np.random.default_rng(0).integers(0, 256, size=(m, k), dtype=np.uint8)
+    ins = [0x1000 * (j + 1) for j in range(k)]
+    outs = [0x900000 + 0x100 * i for i in range(m)]
+    copies = [0x77770000 + j if j % 3 == 0 else 0 for j in range(k)]
+    py = build_desc(ins, outs, copies, perm_tables_from_coeff(coeff))
+    nat = np.frombuffer(cpu().build_desc(k, m, ins, copies, outs, coeff.tobytes()), dtype=np.uint8)
+    assert np.array_equal(py, nat)
+
+
+# ---- multiply strategies (the reference's nine CPU programs) -----------------------------------
+@pytest.mark.parametrize("strategy", STRATEGIES)
+def test_every_strategy_matches_oracle(strategy):
+    rng = np.random.default_rng(hash(strategy) % 2**32)
+    for a, b in rng.integers(0, 256, size=(400, 2)).tolist() + [(0, 0), (0, 7), (7, 0), (255, 255), (1, 1)]:
+        assert cpu().mul_strategy(strategy, a, b) == int(GF256.mul(a, b)), (strategy, a, b)
+
+
+@pytest.mark.parametrize("strategy", STRATEGIES)
+@pytest.mark.parametrize("k,m,ncols", [(4, 2, 1000), (10, 4, 4099), (3, 3, 1)])
+def test_cpu_gemm_matches_oracle(strategy, k, m, ncols):
+    rng = np.random.default_rng(k * m + ncols)
+    coeff = rng.integers(0, 256, size=(m, k), dtype=np.uint8)
+    data = rng.integers(0, 256, size=(k, ncols), dtype=np.uint8)
+    out = np.zeros((m, ncols), dtype=np.uint8)
+    cpu().gemm([data[j].ctypes.data for j in range(k)], [out[i].ctypes.data for i in range(m)], coeff.tobytes(),
+               ncols, strategy, 1)
+    assert np.array_equal(out, GF256.gemm(coeff, data))
+
+
+def test_cpu_gemm_multithreaded():
+    k, m, ncols = 10, 4, 3 << 20
+    rng = np.random.default_rng(5)
+    coeff = rng.integers(0, 256, size=(m, k), dtype=np.uint8)
+    data = rng.integers(0, 256, size=(k, ncols), dtype=np.uint8)
+    out = np.zeros((m, ncols), dtype=np.uint8)
+    cpu().gemm([data[j].ctypes.data for j in range(k)], [out[i].ctypes.data for i in range(m)], coeff.tobytes(),
+               ncols, "row", 4)
+    assert np.array_equal(out, GF256.gemm(coeff, data))
+
+
+# ---- host matrix algebra -----------------------------------------------------------------------
+@pytest.mark.parametrize("kind", ["vandermonde", "cauchy", "sys_vandermonde"])
+def test_native_encoding_matrix_equals_oracle(kind):
+    for k, p in [(4, 2), (10, 4), (16, 4), (128, 32)]:
+        nat = np.frombuffer(cpu().encoding_matrix(kind, k, p), dtype=np.uint8).reshape(p, k)
+        assert np.array_equal(nat, GF256.encoding_matrix(kind, k, p)), (kind, k, p)
+
+
+def test_native_invert_and_singular():
+    g = GF256.generator(GF256.vandermonde_ref(10, 4))
+    for rows in [(0, 1, 2, 3, 4, 5, 6, 10, 11, 12), (4, 5, 6, 7, 8, 9, 10, 11, 12, 13)]:
+        nat = np.frombuffer(cpu().decode_matrix(g.tobytes(), 10, list(rows)), dtype=np.uint8).reshape(10, 10)
+        assert np.array_equal(nat, GF256.invert(g[list(rows)]))
+    for bad in GF256.singular_patterns(g, 10):
+        assert cpu().decode_matrix(g.tobytes(), 10, list(bad)) is None
+
+
+# ---- model on CPU tensors ----------------------------------------------------------------------
+@pytest.mark.parametrize("matrix", ["vandermonde", "cauchy"])
+def test_reed_solomon_cpu_all_erasure_subsets_k4_n6(matrix):
+    k, n = 4, 6
+    rs = ReedSolomon(k, n, matrix=matrix)
+    data = torch.from_numpy(np.random.default_rng(1).integers(0, 256, size=(k, 3001), dtype=np.uint8))
+    parity = rs.encode(data)
+    assert np.array_equal(parity.numpy(), GF256.gemm(rs.E, data.numpy()))
+    stripe = [data[i] for i in range(k)] + [parity[i] for i in range(n - k)]
+    for rows in itertools.combinations(range(n), k):
+        out = rs.decode([stripe[r].clone() for r in rows], rows)
+        assert torch.equal(out, data), rows
+
+
+def test_reed_solomon_cpu_reconstruct_mixed():
+    k, n = 10, 14
+    rs = ReedSolomon(k, n)
+    data = torch.from_numpy(np.random.default_rng(2).integers(0, 256, size=(k, 999), dtype=np.uint8))
+    parity = rs.encode(data)
+    full = torch.cat([data, parity])
+    broken = full.clone()
+    erased = [1, 7, 11, 13]
+    broken[erased] = 0
+    rs.reconstruct(broken, erased)
+    assert torch.equal(broken, full)
+
+
+def test_reed_solomon_unrecoverable_pattern_raises():
+    from gpu_rscode_amd import UnrecoverableError
+
+    rs = ReedSolomon(10, 14)
+    bad = GF256.singular_patterns(rs.G, 10)[0]
+    assert not rs.is_recoverable(bad)
+    with pytest.raises(UnrecoverableError):
+        rs.decode_matrix(bad)
+
+
+def test_reed_solomon_gf16_cpu_roundtrip():
+    rs = ReedSolomon(4, 6, field="gf16")
+    data = torch.from_numpy(np.random.default_rng(3).integers(0, 256, size=(4, 777), dtype=np.uint8))
+    parity = rs.encode(data)
+    stripe = [data[i] for i in range(4)] + [parity[i] for i in range(2)]
+    for rows in itertools.combinations(range(6), 4):
+        assert torch.equal(rs.decode([stripe[r] for r in rows], rows), data)
+
+
+# ---- file formats ------------------------------------------------------------------------------
+def test_chunk_names_and_index():
+    assert ff.chunk_path("f.bin", 3) == "_3_f.bin" == cpu().chunk_path("f.bin", 3)
+    assert ff.chunk_path("a/b/f.bin", 12) == "a/b/_12_f.bin" == cpu().chunk_path("a/b/f.bin", 12)
+    assert ff.chunk_index("_12_f.bin") == 12 == cpu().chunk_index("x/_12_f.bin")
+    assert ff.chunk_index("f.bin") == -1 == cpu().chunk_index("f.bin")
+
+
+def test_metadata_roundtrip_both_formats(tmp_path):
+    e = GF256.vandermonde_ref(4, 2)
+    p = str(tmp_path / "m.METADATA")
+    ff.write_metadata(p, 12345, 2, 4, e)
+    md = ff.read_metadata(p)
+    assert md.has_matrix and md.total_size == 12345 and np.array_equal(md.e, e)
+    nat = cpu().read_metadata(p)
+    assert nat["has_matrix"] and np.array_equal(np.frombuffer(nat["g"], np.uint8).reshape(6, 4), md.g)
+    text = open(p).read().splitlines()
+    assert text[:3] == ["12345", "2 4", "1 0 0 0 "]  # reference write_metadata layout
+    ff.write_metadata(p, 99, 2, 4, None, with_matrix=False)  # cpu-rs.c 2-line form
+    md = ff.read_metadata(p)
+    assert not md.has_matrix and np.array_equal(md.e, e)
+
+
+def test_worst_case_conf_matches_unit_test_sh():
+    assert ff.worst_case_conf("f", 6, 4) == ["_2_f", "_3_f", "_4_f", "_5_f"]
+    assert cpu().worst_case_conf("f", 6, 4) == ff.worst_case_conf("f", 6, 4)
+
+
+# ---- file-level codec --------------------------------------------------------------------------
+@pytest.mark.parametrize("case", ["4,6,1000003", "10,14,1000003", "8,11,65536"])
+def test_golden_parity_equals_reference_cpu_rs(tmp_path, case):
+    k, n, size = map(int, case.split(","))
+    golden = json.load(open(FIX))["cases"][case]
+    f = tmp_path / "in.bin"
+    f.write_bytes(golden_input(size))
+    cpu().encode_file(str(f), k, n - k)
+    for i in range(n):
+        assert sha(tmp_path / f"_{i}_in.bin") == golden[str(i)], f"chunk {i}"
+
+
+def test_file_roundtrip_every_erasure_subset_k4_n6(tmp_path):
+    k, n = 4, 6
+    f = tmp_path / "f.bin"
+    payload = os.urandom(100_003)
+    f.write_bytes(payload)
+    cpu().encode_file(str(f), k, n - k)
+    for rows in itertools.combinations(range(n), k):
+        conf = tmp_path / "conf"
+        ff.write_conf(str(conf), [ff.chunk_path(str(f), r) for r in rows])
+        out = tmp_path / "out.bin"
+        cpu().decode_file(str(f), str(conf), str(out))
+        assert out.read_bytes() == payload, rows
+
+
+def test_file_decode_singular_pattern_errors(tmp_path):
+    f = tmp_path / "f.bin"
+    f.write_bytes(os.urandom(5000))
+    cpu().encode_file(str(f), 10, 4)
+    g = GF256.generator(GF256.vandermonde_ref(10, 4))
+    bad = GF256.singular_patterns(g, 10)[0]
+    conf = tmp_path / "conf"
+    ff.write_conf(str(conf), [ff.chunk_path(str(f), r) for r in bad])
+    with pytest.raises(RuntimeError, match="unrecoverable"):
+        cpu().decode_file(str(f), str(conf), str(tmp_path / "o"))
+
+
+def test_file_decode_accepts_cpu_metadata(tmp_path):
+    f = tmp_path / "f.bin"
+    payload = os.urandom(7777)
+    f.write_bytes(payload)
+    cpu().encode_file(str(f), 4, 2, cpu_meta=True)
+    assert len(open(str(f) + ".METADATA").read().split()) == 3
+    conf = tmp_path / "c"
+    ff.write_conf(str(conf), ff.worst_case_conf(str(f), 6, 4))
+    cpu().decode_file(str(f), str(conf), str(tmp_path / "o"))
+    assert (tmp_path / "o").read_bytes() == payload
+
+
+# ---- CLI ---------------------------------------------------------------------------------------
+def run(cmd, cwd):
+    return subprocess.run(cmd, cwd=cwd, capture_output=True, text=True, timeout=120)
+
+
+def test_cpu_rs_cli_roundtrip_reference_flags(tmp_path):
+    exe = str(binary("CPU-RS"))
+    payload = os.urandom(1 << 20)
+    (tmp_path / "f.bin").write_bytes(payload)
+    r = run([exe, "-K", "4", "-N", "6", "-E", "f.bin"], tmp_path)  # uppercase aliases take arguments
+    assert r.returncode == 0, r.stderr
+    r = run([exe, "-k", "4", "-n", "6", "-e", "f.bin", "--make-conf"], tmp_path)
+    assert r.returncode == 0 and (tmp_path / "conf-6-4-f.bin").exists()
+    r = run([exe, "-d", "-i", "f.bin", "-c", "conf-6-4-f.bin", "-o", "out.bin"], tmp_path)
+    assert r.returncode == 0, r.stderr
+    assert (tmp_path / "out.bin").read_bytes() == payload
+    # without -o the decoder overwrites the input file (reference behaviour, src/decode.cu:410-425)
+    (tmp_path / "f.bin").write_bytes(b"garbage")
+    r = run([exe, "-d", "-i", "f.bin", "-c", "conf-6-4-f.bin"], tmp_path)
+    assert r.returncode == 0 and (tmp_path / "f.bin").read_bytes() == payload
+
+
+def test_cpu_rs_cli_validation(tmp_path):
+    exe = str(binary("CPU-RS"))
+    assert run([exe, "-h"], tmp_path).returncode == 0
+    assert run([exe], tmp_path).returncode != 0
+    assert run([exe, "-k", "0", "-n", "4", "-e", "x"], tmp_path).returncode != 0
+    assert run([exe, "-d", "-i", "x"], tmp_path).returncode != 0
+    assert run([exe, "-k", "4", "-n", "6", "-e", "missing.bin"], tmp_path).returncode == 1

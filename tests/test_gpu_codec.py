@@ -1,0 +1,160 @@
+"""End-to-end codec on the GPU: ReedSolomon model, host streaming pipeline, file codec, bin/RS."""
+import itertools
+import os
+import subprocess
+
+import numpy as np
+import pytest
+import torch
+
+from gpu_rscode_amd import ReedSolomon, alloc_rows
+from gpu_rscode_amd.gf import GF256
+from gpu_rscode_amd._build import binary
+from gpu_rscode_amd._native import cpu, hip
+from gpu_rscode_amd.utils import fileformat as ff
+
+pytestmark = pytest.mark.gpu
+
+
+def _data(k, C, seed=0):
+    host = np.random.default_rng(seed).integers(0, 256, size=(k, C), dtype=np.uint8)
+    dev = alloc_rows(k, C, "cuda")
+    dev.copy_(torch.from_numpy(host))
+    return host, dev
+
+
+@pytest.mark.parametrize("matrix", ["vandermonde", "cauchy", "sys_vandermonde"])
+def test_all_erasure_subsets_k4_n6(matrix):
+    rs = ReedSolomon(4, 6, matrix=matrix)
+    host, data = _data(4, 65537)
+    parity = rs.encode(data)
+    stripe = [data[i] for i in range(4)] + [parity[i] for i in range(2)]
+    for rows in itertools.combinations(range(6), 4):
+        for dev_inv in (False, True):
+            out = rs.decode([stripe[r] for r in rows], rows, device_invert=dev_inv)
+            torch.cuda.synchronize()
+            assert np.array_equal(out.cpu().numpy(), host), (rows, dev_inv)
+
+
+def test_k10_n14_odd_chunk_random_patterns():
+    k, n = 10, 14
+    rs = ReedSolomon(k, n)
+    C = 1_000_003
+    host, data = _data(k, C, 1)
+    parity = rs.encode(data)
+    torch.cuda.synchronize()
+    assert np.array_equal(parity.cpu().numpy(), GF256.gemm(rs.E, host))
+    stripe = [data[i] for i in range(k)] + [parity[i] for i in range(n - k)]
+    rng = np.random.default_rng(2)
+    tested = 0
+    while tested < 12:
+        erased = set(rng.choice(n, size=4, replace=False).tolist())
+        rows = [r for r in range(n) if r not in erased]
+        if not rs.is_recoverable(rows):
+            continue
+        out = rs.decode([stripe[r] for r in rows], rows, device_invert=bool(tested % 2))
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy(), host), sorted(erased)
+        tested += 1
+
+
+def test_device_invert_flags_singular_pattern():
+    rs = ReedSolomon(10, 14)
+    host, data = _data(10, 4096)
+    parity = rs.encode(data)
+    stripe = [data[i] for i in range(10)] + [parity[i] for i in range(4)]
+    bad = GF256.singular_patterns(rs.G, 10)[0]
+    rs.decode([stripe[r] for r in bad], bad, device_invert=True)
+    torch.cuda.synchronize()
+    assert int(rs.last_status.item()) == 1
+
+
+def test_reconstruct_natives_and_parity_in_place():
+    k, n = 12, 16
+    rs = ReedSolomon(k, n, matrix="cauchy")
+    C = 300_001
+    host, data = _data(k, C, 3)
+    stripe = alloc_rows(n, C, "cuda")
+    stripe[:k].copy_(data)
+    rs.encode([stripe[i] for i in range(k)], [stripe[i] for i in range(k, n)])
+    want = stripe.clone()
+    erased = [0, 5, 13, 15]
+    stripe[erased] = 0
+    rs.reconstruct(stripe, erased)
+    torch.cuda.synchronize()
+    assert torch.equal(stripe, want)
+
+
+def test_gf16_field_on_gpu():
+    rs = ReedSolomon(6, 9, field="gf16")
+    host, data = _data(6, 10007, 4)
+    parity = rs.encode(data)
+    stripe = [data[i] for i in range(6)] + [parity[i] for i in range(3)]
+    cpu_par = rs.encode(torch.from_numpy(host))
+    assert np.array_equal(parity.cpu().numpy(), cpu_par.numpy())
+    for rows in [(3, 4, 5, 6, 7, 8), (0, 2, 4, 6, 7, 8)]:
+        out = rs.decode([stripe[r] for r in rows], rows)
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy(), host)
+
+
+def test_wide_stripe_k128_n160():
+    k, n = 128, 160
+    rs = ReedSolomon(k, n, matrix="cauchy")
+    C = 40_003
+    host, data = _data(k, C, 5)
+    parity = rs.encode(data)
+    torch.cuda.synchronize()
+    assert np.array_equal(parity.cpu().numpy(), GF256.gemm(rs.E, host))
+    stripe = [data[i] for i in range(k)] + [parity[i] for i in range(n - k)]
+    rows = list(range(32, 160))  # lose the first 32 natives
+    out = rs.decode([stripe[r] for r in rows], rows, device_invert=True)
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), host)
+
+
+@pytest.mark.parametrize("streams,slice_", [(1, 1 << 20), (2, 1 << 20), (4, 3 << 18), (3, 256)])
+def test_host_pipeline_streams(streams, slice_):
+    k, p, C = 10, 4, 3_000_017
+    rng = np.random.default_rng(streams)
+    host = torch.from_numpy(rng.integers(0, 256, size=(k, C), dtype=np.uint8)).pin_memory()
+    par = torch.zeros((p, C), dtype=torch.uint8).pin_memory()
+    e = GF256.vandermonde_ref(k, p)
+    res = hip().gemm_host([0], [host[j].data_ptr() for j in range(k)], [par[i].data_ptr() for i in range(p)],
+                          e.tobytes(), C, streams, slice_, 0, False)
+    assert res["devices"][0]["bytes_h2d"] == k * C
+    assert np.array_equal(par.numpy(), GF256.gemm(e, host.numpy()))
+
+
+def test_file_codec_gpu_and_cross_compat_with_cpu(tmp_path):
+    f = tmp_path / "f.bin"
+    payload = os.urandom(2_000_003)
+    f.write_bytes(payload)
+    hip().encode_file(str(f), 10, 4, "vandermonde", False, [0], 2, 1 << 20, 0)
+    parity_gpu = [(tmp_path / f"_{i}_f.bin").read_bytes() for i in range(14)]
+    g2 = tmp_path / "g"
+    g2.mkdir()
+    (g2 / "f.bin").write_bytes(payload)
+    cpu().encode_file(str(g2 / "f.bin"), 10, 4)
+    assert parity_gpu == [(g2 / f"_{i}_f.bin").read_bytes() for i in range(14)]
+    conf = tmp_path / "conf"
+    ff.write_conf(str(conf), [ff.chunk_path(str(f), r) for r in (0, 2, 3, 5, 6, 8, 10, 11, 12, 13)])
+    hip().decode_file(str(f), str(conf), str(tmp_path / "o_gpu"), [0], 3, 1 << 19, 0)
+    cpu().decode_file(str(f), str(conf), str(tmp_path / "o_cpu"))
+    assert (tmp_path / "o_gpu").read_bytes() == payload == (tmp_path / "o_cpu").read_bytes()
+
+
+def test_rs_cli_reference_flags(tmp_path):
+    exe = str(binary("RS"))
+    payload = os.urandom(3_333_333)
+    (tmp_path / "f.bin").write_bytes(payload)
+    r = subprocess.run([exe, "-k", "4", "-n", "6", "-e", "f.bin", "-s", "2", "-p", "64"], cwd=tmp_path,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert "Total GPU encoding time" in r.stdout
+    subprocess.run([exe, "-k", "4", "-n", "6", "-e", "f.bin", "--make-conf"], cwd=tmp_path, check=True,
+                   capture_output=True, timeout=60)
+    r = subprocess.run([exe, "-d", "-i", "f.bin", "-c", "conf-6-4-f.bin", "-o", "out.bin", "-s", "4"], cwd=tmp_path,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert (tmp_path / "out.bin").read_bytes() == payload
