@@ -133,7 +133,20 @@ __global__ __launch_bounds__(B) void gf_invert_kernel(const uint8_t* __restrict_
 #pragma unroll
       for (int q = 0; q < 5; ++q) t[q] = T[r * 8 + q];
       if ((t[0] | t[1] | t[2] | t[3] | t[4]) == 0) continue;  // factor 0: row already clear
-      for (int w = sub; w < PW; w += TPR) M[r * PW + w] ^= apply4(t, M[c * PW + w]);
+      // batches of 8 dwords: all LDS reads issued before the writes (r != c, so no aliasing),
+      // which the compiler cannot prove on its own and would otherwise serialise per dword
+      int w = sub;
+      for (; w + 7 * TPR < PW; w += 8 * TPR) {
+        uint32_t pv[8], rv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          pv[u] = M[c * PW + w + u * TPR];
+          rv[u] = M[r * PW + w + u * TPR];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) M[r * PW + w + u * TPR] = rv[u] ^ apply4(t, pv[u]);
+      }
+      for (; w < PW; w += TPR) M[r * PW + w] ^= apply4(t, M[c * PW + w]);
     }
     __syncthreads();
   }

@@ -1,0 +1,60 @@
+"""Python CLI: single-process (CPU backend) and torchrun --dist mode over gloo (world size 2)."""
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+from gpu_rscode_amd.utils import fileformat as ff
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _py(args, cwd, env=None):
+    e = dict(os.environ, PYTHONPATH=ROOT, **(env or {}))
+    return subprocess.run([sys.executable, "-m", "gpu_rscode_amd", *args], cwd=cwd, capture_output=True, text=True,
+                          timeout=300, env=e)
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_python_cli_cpu_roundtrip(tmp_path):
+    payload = os.urandom(123_457)
+    (tmp_path / "f.bin").write_bytes(payload)
+    r = _py(["-k", "4", "-n", "6", "-e", "f.bin", "--backend", "cpu", "--matrix", "cauchy"], tmp_path)
+    assert r.returncode == 0, r.stderr
+    ff.write_conf(str(tmp_path / "conf"), ["_0_f.bin", "_3_f.bin", "_4_f.bin", "_5_f.bin"])
+    r = _py(["-d", "-i", "f.bin", "-c", "conf", "-o", "o.bin", "--backend", "cpu"], tmp_path)
+    assert r.returncode == 0, r.stderr
+    assert (tmp_path / "o.bin").read_bytes() == payload
+
+
+@pytest.mark.parametrize("gather", ["rccl", "none"])
+def test_torchrun_dist_cli_matches_single_process(tmp_path, gather):
+    payload = os.urandom(3 * 4096 * 10 + 999)
+    d1, d2 = tmp_path / "dist", tmp_path / "single"
+    d1.mkdir()
+    d2.mkdir()
+    (d1 / "f.bin").write_bytes(payload)
+    (d2 / "f.bin").write_bytes(payload)
+    env = dict(os.environ, PYTHONPATH=ROOT, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    base = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+            "--master-addr=127.0.0.1", f"--master-port={_port()}", "-m", "gpu_rscode_amd", "--dist", "--gather", gather]
+    r = subprocess.run(base + ["-k", "10", "-n", "14", "-e", "f.bin"], cwd=d1, capture_output=True, text=True,
+                       timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    r = _py(["-k", "10", "-n", "14", "-e", "f.bin", "--backend", "cpu"], d2)
+    assert r.returncode == 0, r.stderr
+    for i in range(14):
+        assert (d1 / f"_{i}_f.bin").read_bytes() == (d2 / f"_{i}_f.bin").read_bytes(), i
+    ff.write_conf(str(d1 / "conf"), [f"_{i}_f.bin" for i in (1, 2, 3, 5, 6, 8, 10, 11, 12, 13)])
+    base[6] = f"--master-port={_port()}"
+    r = subprocess.run(base + ["-d", "-i", "f.bin", "-c", "conf", "-o", "o.bin"], cwd=d1, capture_output=True,
+                       text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert (d1 / "o.bin").read_bytes() == payload
