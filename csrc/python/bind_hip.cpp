@@ -80,6 +80,17 @@ PYBIND11_MODULE(_hip, m) {
       },
       py::arg("a"), py::arg("a_inv"), py::arg("n"), py::arg("batch") = 1, py::arg("status") = 0, py::arg("desc") = 0,
       py::arg("sel_rows") = 0, py::arg("m") = 0, py::arg("m_pad") = 0, py::arg("stream") = 0);
+  m.def("mfma_bitmat_bytes", &mfma_bitmat_bytes);
+  m.def("mfma_bitmat", [](uint64_t coeff, int mm, int k, uint64_t bitmat, uint64_t stream) {
+    check(launch_mfma_bitmat(reinterpret_cast<const uint8_t*>(coeff), mm, k, reinterpret_cast<void*>(bitmat),
+                             as_stream(stream)),
+          "mfma_bitmat");
+  });
+  m.def("gemm_mfma", [](uint64_t bitmat, uint64_t desc, int k, int mm, int64_t col0, int64_t ncols, uint64_t stream) {
+    check(launch_gf_gemm_mfma(reinterpret_cast<const void*>(bitmat), reinterpret_cast<const void*>(desc), k, mm, col0,
+                              ncols, as_stream(stream)),
+          "gf_gemm_mfma");
+  });
   m.def("gen_matrix", [](uint64_t e, int k, int p, int kind, uint64_t stream) {
     check(launch_gen_matrix(reinterpret_cast<uint8_t*>(e), k, p, kind, as_stream(stream)), "gen_matrix");
   });

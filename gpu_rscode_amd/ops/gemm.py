@@ -138,7 +138,8 @@ class GemmPlan:
             pass (the fused survivor copy of decode).
     """
 
-    def __init__(self, inputs, outputs, coeff=None, *, maps=None, copies=None, device_tables: bool = False):
+    def __init__(self, inputs, outputs, coeff=None, *, maps=None, copies=None, device_tables: bool = False,
+                 engine: str = "valu"):
         self.inputs = _rows(inputs)
         self.outputs = _rows(outputs)
         self.copies = None if copies is None else [c for c in copies]
@@ -171,6 +172,22 @@ class GemmPlan:
                           tables)
         self.desc = torch.from_numpy(host).to(self.device)
         self.layout = desc_layout(self.k, self.m_pad)
+        self.engine = engine
+        self.bitmat = None
+        if engine == "mfma":
+            # int8-MFMA bit-matrix path (csrc/kernels/gf_mfma.hip): GF(2^8) coefficients only, no
+            # fused copies, 4-byte aligned rows; the < 512-column remainder uses the v_perm tables.
+            if coeff is None or self.copies is not None or self.bytewise:
+                raise ValueError("engine='mfma' needs coeff=, no copies and aligned rows")
+            c = torch.from_numpy(np.ascontiguousarray(np.asarray(coeff, dtype=np.uint8).reshape(self.m, self.k)))
+            c = c.to(self.device)
+            h = hip()
+            self.bitmat = torch.empty(h.mfma_bitmat_bytes(self.k, self.m), dtype=torch.uint8, device=self.device)
+            h.mfma_bitmat(c.data_ptr(), self.m, self.k, self.bitmat.data_ptr(),
+                          torch.cuda.current_stream(self.device).cuda_stream)
+            self._coeff_dev = c
+        elif engine != "valu":
+            raise ValueError(f"unknown engine {engine!r}")
         self._mark_ready()
 
     def _mark_ready(self) -> None:
@@ -210,7 +227,9 @@ class GemmPlan:
             self.desc.record_stream(stream)
         s = st.cuda_stream
         h = hip()
-        if self.bytewise:
+        if self.engine == "mfma":
+            h.gemm_mfma(int(self.bitmat.data_ptr()), int(self.desc.data_ptr()), self.k, self.m, col0, ncols, s)
+        elif self.bytewise:
             h.gemm(int(self.desc.data_ptr()), self.k, self.m_pad, col0, ncols, True, max_blocks, s)
         elif vec is None:
             h.gemm(int(self.desc.data_ptr()), self.k, self.m_pad, col0, ncols, False, max_blocks, s)

@@ -22,7 +22,7 @@ from gpu_rscode_amd.models import alloc_rows  # noqa: E402
 from gpu_rscode_amd.ops import GemmPlan, fill_random_, gf_invert  # noqa: E402
 
 VARIANTS = [None, (1, 1, False), (1, 2, False), (1, 4, False), (1, 2, True), (1, 4, True), (2, 1, False),
-            (2, 2, False), (2, 2, True)]
+            (2, 2, False), (2, 2, True), "mfma"]
 
 
 def timed(fn, reps):
@@ -46,9 +46,10 @@ def make_case(name, k, m, ncopy, total_bytes):
         copies = [dst[j] if j < ncopy else None for j in range(k)]
     coeff = np.random.default_rng(k + m).integers(1, 256, size=(m, k), dtype=np.uint8)
     plan = GemmPlan(data, out, coeff, copies=copies)
+    mplan = GemmPlan(data, out, coeff, engine="mfma") if not ncopy else None
     traffic = (k + m + ncopy) * C
-    return {"name": name, "k": k, "m": m, "copies": ncopy, "C": C, "plan": plan, "traffic": traffic,
-            "keep": (data, out, copies)}
+    return {"name": name, "k": k, "m": m, "copies": ncopy, "C": C, "plan": plan, "mplan": mplan,
+            "traffic": traffic, "keep": (data, out, copies)}
 
 
 def main():
@@ -74,17 +75,25 @@ def main():
         times = {str(v): [] for v in VARIANTS}
         for _ in range(a.rounds):
             for v in VARIANTS:
+                if v == "mfma":
+                    if c["mplan"] is None:
+                        continue
+                    c["mplan"].run()
+                    times[str(v)].append(timed(lambda: c["mplan"].run(), a.reps))
+                    continue
                 kw = {} if v is None else dict(vec=v[0], pf=v[1], nt=v[2])
                 c["plan"].run(**kw)  # warm
                 times[str(v)].append(timed(lambda: c["plan"].run(**kw), a.reps))
         out = {}
         for v, ts in times.items():
+            if not ts:
+                continue
             med = float(np.median(ts))
             out[v] = {"us_median": round(med, 2), "us_min": round(min(ts), 2),
                       "TBps": round(c["traffic"] / med / 1e6, 3),
                       "input_GBps": round(c["k"] * c["C"] / med / 1e3, 1)}
         res["cases"][c["name"]] = {"k": c["k"], "m": c["m"], "copies": c["copies"], "C": c["C"], "variants": out}
-        del c["plan"], c["keep"]
+        del c["plan"], c["keep"], c["mplan"]
         torch.cuda.empty_cache()
 
     for n in (10, 16, 128, 255):
