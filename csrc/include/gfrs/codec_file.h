@@ -27,6 +27,7 @@ HostAlloc default_host_alloc();
 struct FileReport {
   int64_t total_size = 0, chunk_size = 0;
   int k = 0, p = 0, erased = 0;
+  int rejected = 0;  // chunks skipped because their CRC-32 did not match METADATA
   double ms_read = 0, ms_matrix = 0, ms_compute = 0, ms_write = 0;
 };
 

@@ -23,13 +23,20 @@ struct Metadata {
   int p = 0, k = 0;
   Mat g;                    // (k+p) x k generator
   bool has_matrix = false;  // false: 2-line CPU format, g regenerated (reference Vandermonde)
+  std::vector<uint32_t> crc;  // optional per-chunk CRC-32 (n entries) — extension, see below
 };
+
+// Extension (failure detection): after the matrix rows the GPU-format METADATA may
+// carry a line "crc32 <c_0> ... <c_{n-1}>" (hex). The reference's reader stops after the matrix
+// (src/decode.cu:272-281) and ignores it, so files stay readable by the reference.
+uint32_t crc32(const uint8_t* data, int64_t len, uint32_t crc = 0);
 
 std::string chunk_path(const std::string& file, int index);
 std::string metadata_path(const std::string& file);
 int chunk_index(const std::string& name);  // atoi(basename + 1); -1 if malformed
 
-void write_metadata(const std::string& path, int64_t total_size, int p, int k, const Mat& e, bool with_matrix = true);
+void write_metadata(const std::string& path, int64_t total_size, int p, int k, const Mat& e, bool with_matrix = true,
+                    const std::vector<uint32_t>& crc = {});
 Metadata read_metadata(const std::string& path);
 std::vector<std::string> read_conf(const std::string& path);
 void write_conf(const std::string& path, const std::vector<std::string>& names);

@@ -6,6 +6,7 @@
 #include <cstring>
 #include <memory>
 #include <set>
+#include <thread>
 #include <stdexcept>
 
 #include "gfrs/format.h"
@@ -69,9 +70,20 @@ FileReport encode_file(const std::string& file, int k, int p, MatrixKind kind, c
   r.ms_compute = ms_since(t);
 
   t = Clock::now();
+  std::vector<uint32_t> crc;
+  if (!cpu_meta) {  // per-chunk CRC-32 (METADATA extension): lets decode reject corrupted chunks
+    crc.resize(size_t(k + p));
+    std::vector<std::thread> th;
+    for (int i = 0; i < k + p; ++i)
+      th.emplace_back([&, i] {
+        const uint8_t* row = i < k ? data.p + size_t(i) * C : parity.p + size_t(i - k) * C;
+        crc[size_t(i)] = crc32(row, C);
+      });
+    for (auto& x : th) x.join();
+  }
   for (int i = 0; i < k; ++i) write_from(chunk_path(file, i), data.p + size_t(i) * C, C);
   for (int i = 0; i < p; ++i) write_from(chunk_path(file, k + i), parity.p + size_t(i) * C, C);
-  write_metadata(metadata_path(file), r.total_size, p, k, e, !cpu_meta);
+  write_metadata(metadata_path(file), r.total_size, p, k, e, !cpu_meta, crc);
   r.ms_write = ms_since(t);
   return r;
 }
@@ -88,20 +100,84 @@ FileReport decode_file(const std::string& file, const std::string& conf, const s
   r.chunk_size = std::max<int64_t>(1, chunk_size(md.total_size, k));
   const int64_t C = r.chunk_size;
 
-  std::vector<std::string> names = read_conf(conf);
+  // The reference uses exactly the first k names (src/decode.cu:302-318). Here the conf may list
+  // more: chunks that are missing or fail their METADATA CRC-32 are skipped, and the first
+  // recoverable k-subset (in conf order) is used — the "aggressive read" the reference's design
+  // notes list as future work (doc/design.tex:529).
+  const std::vector<std::string> names = read_conf(conf);
   if (int(names.size()) < k)
     throw std::runtime_error("configuration lists " + std::to_string(names.size()) + " chunks, need k = " +
                              std::to_string(k));
-  names.resize(k);
-  std::vector<int> rows(k);
+  std::vector<int> cand_idx;
+  std::vector<std::string> cand_path;
   std::set<int> seen;
-  for (int i = 0; i < k; ++i) {
-    rows[i] = chunk_index(names[i]);
-    if (rows[i] < 0 || rows[i] >= n) throw std::runtime_error("bad chunk name in configuration: " + names[i]);
-    if (!seen.insert(rows[i]).second) throw std::runtime_error("duplicate chunk in configuration: " + names[i]);
+  for (const auto& nm : names) {
+    const int idx = chunk_index(nm);
+    if (idx < 0 || idx >= n) throw std::runtime_error("bad chunk name in configuration: " + nm);
+    if (!seen.insert(idx).second) throw std::runtime_error("duplicate chunk in configuration: " + nm);
+    cand_idx.push_back(idx);
+    cand_path.push_back(resolve_chunk(nm, file));
   }
   Buf surv(alloc, size_t(k) * C);
-  for (int i = 0; i < k; ++i) read_into(resolve_chunk(names[i], file), 0, surv.p + size_t(i) * C, C);
+  std::vector<int> rows;
+  std::vector<std::vector<uint8_t>> spare;  // verified chunks beyond the first k (rarely needed)
+  auto row_ok = [&](int ci, uint8_t* dst) -> bool {
+    try {
+      if (file_size(cand_path[size_t(ci)]) < C && md.total_size > 0) return false;
+      read_into(cand_path[size_t(ci)], 0, dst, C);
+    } catch (const std::exception&) {
+      return false;  // missing chunk
+    }
+    if (!md.crc.empty() && crc32(dst, C) != md.crc[size_t(cand_idx[size_t(ci)])]) {
+      ++r.rejected;
+      return false;
+    }
+    return true;
+  };
+  // fill k slots in conf order, then search for a recoverable subset among the verified chunks
+  std::vector<int> verified;
+  for (int ci = 0; ci < int(cand_idx.size()); ++ci) {
+    if (int(verified.size()) < k) {
+      if (row_ok(ci, surv.p + size_t(verified.size()) * C)) verified.push_back(ci);
+    } else {
+      std::vector<uint8_t> tmp(static_cast<size_t>(C));
+      if (row_ok(ci, tmp.data())) {
+        verified.push_back(ci);
+        spare.push_back(std::move(tmp));
+      }
+    }
+  }
+  if (int(verified.size()) < k)
+    throw std::runtime_error("only " + std::to_string(verified.size()) + " intact chunks available, need k = " +
+                             std::to_string(k));
+  std::vector<int> pick(k);
+  for (int i = 0; i < k; ++i) pick[i] = i;  // positions into `verified`
+  auto rows_of = [&](const std::vector<int>& pk) {
+    std::vector<int> rr(k);
+    for (int i = 0; i < k; ++i) rr[i] = cand_idx[size_t(verified[size_t(pk[i])])];
+    return rr;
+  };
+  Mat probe;
+  bool found = decode_matrix(md.g, k, rows_of(pick), probe);
+  for (long tries = 0; !found && tries < 100000; ++tries) {  // next k-combination of the verified set
+    int i = k - 1;
+    const int V = int(verified.size());
+    while (i >= 0 && pick[i] == V - k + i) --i;
+    if (i < 0) break;
+    ++pick[i];
+    for (int j = i + 1; j < k; ++j) pick[j] = pick[j - 1] + 1;
+    found = decode_matrix(md.g, k, rows_of(pick), probe);
+  }
+  if (!found)
+    throw std::runtime_error("unrecoverable erasure pattern: the selected rows of the generator are singular");
+  // gather the chosen rows into the first k slots of `surv` (slot order = pick order)
+  for (int i = 0; i < k; ++i) {
+    const int pos = pick[i];
+    if (pos == i) continue;
+    const uint8_t* src = pos < k ? surv.p + size_t(pos) * C : spare[size_t(pos - k)].data();
+    std::memcpy(surv.p + size_t(i) * C, src, size_t(C));  // pick is increasing: slot i <= pos, no clobber of later picks
+  }
+  rows = rows_of(pick);
   r.ms_read = ms_since(t);
 
   t = Clock::now();

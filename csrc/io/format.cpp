@@ -50,7 +50,36 @@ int chunk_index(const std::string& name) {
   return int(v);
 }
 
-void write_metadata(const std::string& path, int64_t total_size, int p, int k, const Mat& e, bool with_matrix) {
+uint32_t crc32(const uint8_t* data, int64_t len, uint32_t crc) {
+  // slicing-by-8 CRC-32 (IEEE 802.3, reflected 0xEDB88320)
+  static uint32_t t[8][256];
+  static bool init = [] {
+    for (uint32_t i = 0; i < 256; ++i) {
+      uint32_t c = i;
+      for (int b = 0; b < 8; ++b) c = (c >> 1) ^ (0xEDB88320u & (0u - (c & 1u)));
+      t[0][i] = c;
+    }
+    for (uint32_t i = 0; i < 256; ++i)
+      for (int s = 1; s < 8; ++s) t[s][i] = (t[s - 1][i] >> 8) ^ t[0][t[s - 1][i] & 0xFF];
+    return true;
+  }();
+  (void)init;
+  crc = ~crc;
+  int64_t i = 0;
+  for (; i + 8 <= len; i += 8) {
+    uint32_t lo, hi;
+    std::memcpy(&lo, data + i, 4);
+    std::memcpy(&hi, data + i + 4, 4);
+    lo ^= crc;
+    crc = t[7][lo & 0xFF] ^ t[6][(lo >> 8) & 0xFF] ^ t[5][(lo >> 16) & 0xFF] ^ t[4][lo >> 24] ^ t[3][hi & 0xFF] ^
+          t[2][(hi >> 8) & 0xFF] ^ t[1][(hi >> 16) & 0xFF] ^ t[0][hi >> 24];
+  }
+  for (; i < len; ++i) crc = (crc >> 8) ^ t[0][(crc ^ data[i]) & 0xFF];
+  return ~crc;
+}
+
+void write_metadata(const std::string& path, int64_t total_size, int p, int k, const Mat& e, bool with_matrix,
+                    const std::vector<uint32_t>& crc) {
   FILE* fp = std::fopen(path.c_str(), "wb");
   if (!fp) throw std::runtime_error("cannot open metadata file " + path);
   std::fprintf(fp, "%lld\n%d %d\n", static_cast<long long>(total_size), p, k);
@@ -61,6 +90,11 @@ void write_metadata(const std::string& path, int64_t total_size, int p, int k, c
     }
     for (int i = 0; i < p; ++i) {
       for (int j = 0; j < k; ++j) std::fprintf(fp, "%d ", int(e[size_t(i) * k + j]));
+      std::fprintf(fp, "\n");
+    }
+    if (!crc.empty()) {
+      std::fprintf(fp, "crc32");
+      for (uint32_t c : crc) std::fprintf(fp, " %08x", c);
       std::fprintf(fp, "\n");
     }
   }
@@ -86,6 +120,12 @@ Metadata read_metadata(const std::string& path) {
   }
   if (got == n) {
     md.has_matrix = true;
+    std::string tag;
+    if (in >> tag && tag == "crc32") {
+      std::string h;
+      for (int i = 0; i < md.k + md.p && (in >> h); ++i) md.crc.push_back(uint32_t(std::stoul(h, nullptr, 16)));
+      if (int(md.crc.size()) != md.k + md.p) md.crc.clear();
+    }
   } else if (got == 0) {
     md.g = generator(vandermonde_ref(md.k, md.p), md.k, md.p);  // CPU-format metadata
     md.has_matrix = false;

@@ -38,6 +38,7 @@ inline py::dict report(const gfrs::FileReport& r) {
   d["k"] = r.k;
   d["p"] = r.p;
   d["erased"] = r.erased;
+  d["rejected"] = r.rejected;
   d["ms_read"] = r.ms_read;
   d["ms_matrix"] = r.ms_matrix;
   d["ms_compute"] = r.ms_compute;

@@ -49,6 +49,7 @@ class Metadata:
     k: int
     g: np.ndarray  # (k+p) x k
     has_matrix: bool
+    crc: list | None = None  # per-chunk CRC-32 (METADATA extension line "crc32 ...")
 
     @property
     def n(self) -> int:
@@ -59,13 +60,16 @@ class Metadata:
         return self.g[self.k :]
 
 
-def write_metadata(path: str, total_size: int, p: int, k: int, e: np.ndarray | None, with_matrix: bool = True) -> None:
+def write_metadata(path: str, total_size: int, p: int, k: int, e: np.ndarray | None, with_matrix: bool = True,
+                   crc=None) -> None:
     lines = [f"{total_size}\n", f"{p} {k}\n"]
     if with_matrix:
         for i in range(k):
             lines.append("".join("1 " if i == j else "0 " for j in range(k)) + "\n")
         for i in range(p):
             lines.append("".join(f"{int(v)} " for v in np.asarray(e)[i]) + "\n")
+        if crc:
+            lines.append("crc32" + "".join(f" {int(c):08x}" for c in crc) + "\n")
     with open(path, "w") as f:
         f.writelines(lines)
 
@@ -88,7 +92,11 @@ def read_metadata(path: str) -> Metadata:
     g = np.array([int(v) for v in vals[:need]], dtype=np.int64)
     if g.min() < 0 or g.max() > 255:
         raise ValueError(f"metadata matrix entry out of range in {path}")
-    return Metadata(total, p, k, g.astype(np.uint8).reshape(k + p, k), True)
+    crc = None
+    rest = vals[need:]
+    if rest and rest[0] == "crc32" and len(rest) >= 1 + k + p:
+        crc = [int(h, 16) for h in rest[1 : 1 + k + p]]
+    return Metadata(total, p, k, g.astype(np.uint8).reshape(k + p, k), True, crc)
 
 
 def read_conf(path: str) -> list[str]:

@@ -262,3 +262,38 @@ def test_cpu_rs_cli_validation(tmp_path):
     assert run([exe, "-k", "0", "-n", "4", "-e", "x"], tmp_path).returncode != 0
     assert run([exe, "-d", "-i", "x"], tmp_path).returncode != 0
     assert run([exe, "-k", "4", "-n", "6", "-e", "missing.bin"], tmp_path).returncode == 1
+
+
+# ---- failure detection: checksums and aggressive read -----------------------------------------
+def test_metadata_crc_extension_and_corruption_detection(tmp_path):
+    import zlib
+
+    f = tmp_path / "f.bin"
+    payload = os.urandom(60_001)
+    f.write_bytes(payload)
+    cpu().encode_file(str(f), 4, 3)
+    md = ff.read_metadata(str(f) + ".METADATA")
+    assert md.crc is not None and len(md.crc) == 7
+    for i in range(7):
+        assert md.crc[i] == zlib.crc32((tmp_path / f"_{i}_f.bin").read_bytes())
+    # corrupt native 1; list all chunks: decoder must skip it and still rebuild the file
+    bad = bytearray((tmp_path / "_1_f.bin").read_bytes())
+    bad[100] ^= 0xFF
+    (tmp_path / "_1_f.bin").write_bytes(bytes(bad))
+    ff.write_conf(str(tmp_path / "conf"), [ff.chunk_path(str(f), i) for i in range(7)])
+    r = cpu().decode_file(str(f), str(tmp_path / "conf"), str(tmp_path / "o"))
+    assert r["rejected"] == 1 and (tmp_path / "o").read_bytes() == payload
+
+
+def test_aggressive_read_skips_missing_and_singular_subsets(tmp_path):
+    f = tmp_path / "f.bin"
+    payload = os.urandom(33_333)
+    f.write_bytes(payload)
+    cpu().encode_file(str(f), 10, 4)
+    g = GF256.generator(GF256.vandermonde_ref(10, 4))
+    bad = list(GF256.singular_patterns(g, 10)[0])  # a singular first-k subset ...
+    rest = [r for r in range(14) if r not in bad]
+    os.remove(tmp_path / f"_{rest[0]}_f.bin")  # ... plus one missing chunk listed after it
+    ff.write_conf(str(tmp_path / "conf"), [ff.chunk_path(str(f), r) for r in bad + rest])
+    cpu().decode_file(str(f), str(tmp_path / "conf"), str(tmp_path / "o"))
+    assert (tmp_path / "o").read_bytes() == payload
