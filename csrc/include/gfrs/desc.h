@@ -8,7 +8,7 @@
 // buffer, src/encode.cu:389-398, src/decode.cu:149-170).
 //
 // Layout (all offsets from the descriptor base, 32-byte aligned records):
-//   [0,  16)              header {k, m, m_pad, flags}
+//   [0,  16)              header {k, m, m_pad, batch}
 //   [16, 16+8k)           in_ptr[k]      (uint64 device addresses)
 //   [.., +8k)             copy_ptr[k]    (0 = no copy)
 //   [.., +8*m_pad)        out_ptr[m_pad] (0 = padding row, never stored)
@@ -26,7 +26,7 @@ struct DescHeader {
   int32_t k;
   int32_t m;
   int32_t m_pad;
-  int32_t flags;
+  int32_t batch;
 };
 
 struct DescLayout {
@@ -35,12 +35,14 @@ struct DescLayout {
 
 constexpr size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
-constexpr DescLayout desc_layout(int k, int m_pad) {
+// `batch` stripes share one table block; stripe b's pointers are in[b*k + j], copy[b*k + j],
+// out[b*m_pad + i] (batched small-object encode/decode in one launch).
+constexpr DescLayout desc_layout(int k, int m_pad, int batch = 1) {
   DescLayout l{};
   l.in_off = sizeof(DescHeader);
-  l.copy_off = l.in_off + 8 * size_t(k);
-  l.out_off = l.copy_off + 8 * size_t(k);
-  l.tab_off = align_up(l.out_off + 8 * size_t(m_pad), 32);
+  l.copy_off = l.in_off + 8 * size_t(k) * size_t(batch);
+  l.out_off = l.copy_off + 8 * size_t(k) * size_t(batch);
+  l.tab_off = align_up(l.out_off + 8 * size_t(m_pad) * size_t(batch), 32);
   l.bytes = l.tab_off + sizeof(PermTable) * size_t(k) * size_t(m_pad);
   return l;
 }

@@ -23,7 +23,7 @@ inline std::vector<uint8_t> build_desc(int k, int m, const std::vector<uint64_t>
   const int m_pad = pad_m(m);
   const DescLayout l = desc_layout(k, m_pad);
   std::vector<uint8_t> d(l.bytes, 0);
-  DescHeader h{k, m, m_pad, 0};
+  DescHeader h{k, m, m_pad, 1};
   std::memcpy(d.data(), &h, sizeof(h));
   std::memcpy(d.data() + l.in_off, in.data(), 8 * size_t(k));
   if (!copy.empty()) std::memcpy(d.data() + l.copy_off, copy.data(), 8 * size_t(k));

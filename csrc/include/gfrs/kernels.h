@@ -16,6 +16,11 @@ namespace gfrs {
 hipError_t launch_gf_gemm(const void* desc, int k, int m_pad, int64_t col0, int64_t ncols,
                           bool force_bytewise, int max_blocks, hipStream_t stream);
 
+// Batched form: `batch` stripes of identical shape share the coefficient tables (small-object
+// serving: one launch for many objects). desc built with desc_layout(k, m_pad, batch).
+hipError_t launch_gf_gemm_batched(const void* desc, int k, int m_pad, int batch, int64_t col0, int64_t ncols,
+                                  bool force_bytewise, hipStream_t stream);
+
 // Variant selector for benchmarks/ablation: vec = 16-byte groups per lane (0 = byte kernel),
 // pf = input rows kept in flight per lane, nt = non-temporal loads/stores.
 hipError_t launch_gf_gemm_variant(const void* desc, int k, int m_pad, int64_t col0, int64_t ncols,
@@ -47,6 +52,14 @@ hipError_t launch_gather_rows(const uint8_t* g, const int* rows, uint8_t* out, i
 hipError_t launch_gf_gemm_mfma(const void* bitmat, const void* desc, int k, int m, int64_t col0,
                                int64_t ncols, hipStream_t stream);
 size_t mfma_bitmat_bytes(int k, int m);
+
+// ---- FP4 (e2m1) block-scaled MFMA bit-matrix GF-GEMM (csrc/kernels/gf_mfma_fp4.hip) ------------
+// Rows must be 2-byte aligned; whole 256-column chunks run on the matrix cores, the remainder on
+// the v_perm kernel (desc must carry the perm tables too).
+hipError_t launch_gf_gemm_fp4(const void* bitmat, const void* desc, int k, int m, int64_t col0,
+                              int64_t ncols, hipStream_t stream);
+size_t fp4_bitmat_bytes(int k, int m);
+hipError_t launch_fp4_bitmat(const uint8_t* coeff, int m, int k, void* bitmat, hipStream_t stream);
 hipError_t launch_mfma_bitmat(const uint8_t* coeff, int m, int k, void* bitmat,
                               hipStream_t stream);
 

@@ -69,8 +69,8 @@ struct DescView {
   cptr<uint32_t> tab;
 };
 
-inline DescView view(const void* desc, int k, int m_pad) {
-  const DescLayout l = desc_layout(k, m_pad);
+inline DescView view(const void* desc, int k, int m_pad, int batch = 1) {
+  const DescLayout l = desc_layout(k, m_pad, batch);
   const char* b = static_cast<const char*>(desc);
   return {(cptr<uint64_t>)(b + l.in_off), (cptr<uint64_t>)(b + l.copy_off), (cptr<uint64_t>)(b + l.out_off),
           (cptr<uint32_t>)(b + l.tab_off)};
@@ -133,10 +133,20 @@ __device__ void tail_bytes(const DescView& d, int k, int m_pad, int i0, bool do_
 // in flight (a static register ring: the ring slot of row j is j % PF, resolved at compile time by
 // unrolling the row loop PF-fold). Lane `ngroups` (one past the last full group) also processes the
 // < 16*V ragged tail bytes, so no second launch is needed for odd chunk sizes.
+// Stripe b of a batched descriptor (blockIdx.y): its own row pointers, the shared table block.
+__device__ __forceinline__ DescView stripe(DescView d, int k, int m_pad) {
+  const int b = blockIdx.y;
+  d.in += size_t(b) * k;
+  d.copy += size_t(b) * k;
+  d.out += size_t(b) * m_pad;
+  return d;
+}
+
 template <int MT, int V, int PF, bool NT>
 __global__ __launch_bounds__(kBlock) void gf_gemm_vec_kernel(DescView d, int k, int m_pad, int ntiles,
                                                              int64_t col0, int64_t ngroups, int64_t nblk,
                                                              int64_t ncb, int tail) {
+  d = stripe(d, k, m_pad);
   const TileMap tm = map_block(ntiles);
   if (tm.cb0 >= ncb) return;
   const int i0 = tm.tile * MT;
@@ -217,6 +227,7 @@ template <int MT>
 __global__ __launch_bounds__(kBlock) void gf_gemm_byte_kernel(DescView d, int k, int m_pad, int ntiles,
                                                               int64_t col0, int64_t ncols, int64_t nblk,
                                                               int64_t ncb) {
+  d = stripe(d, k, m_pad);
   const TileMap tm = map_block(ntiles);
   if (tm.cb0 >= ncb) return;
   const int i0 = tm.tile * MT;
@@ -263,24 +274,25 @@ inline Grid make_grid(int64_t items, int ntiles, int max_blocks) {
 }
 
 template <int MT, int V, int PF, bool NT>
-hipError_t launch_vec_cfg(const DescView& d, int k, int m_pad, int64_t col0, int64_t ngroups, int tail, int max_blocks,
-                          hipStream_t stream) {
+hipError_t launch_vec_cfg(const DescView& d, int k, int m_pad, int batch, int64_t col0, int64_t ngroups, int tail,
+                          int max_blocks, hipStream_t stream) {
   const int ntiles = m_pad / MT;
   // one extra lane past the last group handles the ragged tail
   const Grid g = make_grid(ngroups + (tail > 0 ? 1 : 0), ntiles, max_blocks);
   if (g.nblk == 0) return hipSuccess;
   gf_gemm_vec_kernel<MT, V, PF, NT>
-      <<<g.blocks, kBlock, 0, stream>>>(d, k, m_pad, ntiles, col0, ngroups, g.nblk, g.ncb, tail);
+      <<<dim3(g.blocks, batch), kBlock, 0, stream>>>(d, k, m_pad, ntiles, col0, ngroups, g.nblk, g.ncb, tail);
   return hipGetLastError();
 }
 
 template <int MT>
-hipError_t launch_byte(const DescView& d, int k, int m_pad, int64_t col0, int64_t ncols, int max_blocks,
+hipError_t launch_byte(const DescView& d, int k, int m_pad, int batch, int64_t col0, int64_t ncols, int max_blocks,
                        hipStream_t stream) {
   if (ncols <= 0) return hipSuccess;
   const int ntiles = m_pad / MT;
   const Grid g = make_grid(ncols, ntiles, max_blocks);
-  gf_gemm_byte_kernel<MT><<<g.blocks, kBlock, 0, stream>>>(d, k, m_pad, ntiles, col0, ncols, g.nblk, g.ncb);
+  gf_gemm_byte_kernel<MT>
+      <<<dim3(g.blocks, batch), kBlock, 0, stream>>>(d, k, m_pad, ntiles, col0, ncols, g.nblk, g.ncb);
   return hipGetLastError();
 }
 
@@ -303,14 +315,14 @@ struct Cfg {
 };
 
 template <int MT>
-hipError_t launch_vec(const DescView& d, int k, int m_pad, int64_t col0, int64_t ncols, Cfg c, int max_blocks,
-                      hipStream_t stream) {
+hipError_t launch_vec(const DescView& d, int k, int m_pad, int batch, int64_t col0, int64_t ncols, Cfg c,
+                      int max_blocks, hipStream_t stream) {
   const int gbytes = 16 * c.vec;
   const int64_t ngroups = ncols / gbytes;
   const int tail = int(ncols - ngroups * gbytes);
 #define GFRS_CFG(V, PF, NT)                                                                             \
   if (c.vec == V && c.pf == PF && c.nt == NT)                                                           \
-    return launch_vec_cfg<MT, V, PF, NT>(d, k, m_pad, col0, ngroups, tail, max_blocks, stream);
+    return launch_vec_cfg<MT, V, PF, NT>(d, k, m_pad, batch, col0, ngroups, tail, max_blocks, stream);
   GFRS_CFG(1, 1, false)
   GFRS_CFG(1, 2, false)
   GFRS_CFG(1, 4, false)
@@ -335,15 +347,15 @@ Cfg default_cfg(int mt) {
   return c;
 }
 
-hipError_t run(const void* desc, int k, int m_pad, int64_t col0, int64_t ncols, bool bytewise, const Cfg* cfg,
-               int max_blocks, hipStream_t stream) {
-  if (k <= 0 || m_pad <= 0 || ncols <= 0) return hipSuccess;
-  if (m_pad % tile_for(m_pad) != 0) return hipErrorInvalidValue;
-  const DescView d = view(desc, k, m_pad);
+hipError_t run(const void* desc, int k, int m_pad, int batch, int64_t col0, int64_t ncols, bool bytewise,
+               const Cfg* cfg, int max_blocks, hipStream_t stream) {
+  if (k <= 0 || m_pad <= 0 || ncols <= 0 || batch <= 0) return batch < 0 ? hipErrorInvalidValue : hipSuccess;
+  if (m_pad % tile_for(m_pad) != 0 || batch > 65535) return hipErrorInvalidValue;
+  const DescView d = view(desc, k, m_pad, batch);
   return dispatch_tile(m_pad, [&](auto mt) -> hipError_t {
     constexpr int MT = decltype(mt)::value;
-    if (bytewise || (col0 & 15)) return launch_byte<MT>(d, k, m_pad, col0, ncols, max_blocks, stream);
-    return launch_vec<MT>(d, k, m_pad, col0, ncols, cfg ? *cfg : default_cfg(MT), max_blocks, stream);
+    if (bytewise || (col0 & 15)) return launch_byte<MT>(d, k, m_pad, batch, col0, ncols, max_blocks, stream);
+    return launch_vec<MT>(d, k, m_pad, batch, col0, ncols, cfg ? *cfg : default_cfg(MT), max_blocks, stream);
   });
 }
 
@@ -351,17 +363,22 @@ hipError_t run(const void* desc, int k, int m_pad, int64_t col0, int64_t ncols, 
 
 hipError_t launch_gf_gemm(const void* desc, int k, int m_pad, int64_t col0, int64_t ncols, bool force_bytewise,
                           int max_blocks, hipStream_t stream) {
-  return run(desc, k, m_pad, col0, ncols, force_bytewise, nullptr, max_blocks, stream);
+  return run(desc, k, m_pad, 1, col0, ncols, force_bytewise, nullptr, max_blocks, stream);
+}
+
+hipError_t launch_gf_gemm_batched(const void* desc, int k, int m_pad, int batch, int64_t col0, int64_t ncols,
+                                  bool force_bytewise, hipStream_t stream) {
+  return run(desc, k, m_pad, batch, col0, ncols, force_bytewise, nullptr, 0, stream);
 }
 
 hipError_t launch_gf_gemm_variant(const void* desc, int k, int m_pad, int64_t col0, int64_t ncols, int vec, int pf,
                                   bool nt, int max_blocks, hipStream_t stream) {
-  if (vec == 0) return run(desc, k, m_pad, col0, ncols, true, nullptr, max_blocks, stream);
+  if (vec == 0) return run(desc, k, m_pad, 1, col0, ncols, true, nullptr, max_blocks, stream);
   Cfg c;
   c.vec = vec;
   c.pf = pf;
   c.nt = nt;
-  return run(desc, k, m_pad, col0, ncols, false, &c, max_blocks, stream);
+  return run(desc, k, m_pad, 1, col0, ncols, false, &c, max_blocks, stream);
 }
 
 }  // namespace gfrs

@@ -1,0 +1,257 @@
+// GF(2^8) GEMM on gfx950 matrix cores, FP4 (e2m1) form of the GF(2) bit-matrix product.
+//
+// Same algebra as gf_mfma.hip (out_bits = A . in_bits mod 2 over the (8m x 8k) bit-matrix), but on
+// `v_mfma_scale_f32_32x32x64_f8f6f4` with FP4 operands: {0, 1.0} are exact e2m1 codes (0x0, 0x2),
+// the f32 accumulator holds the exact integer count (<= 8k <= 2048), and its parity is the GF(2)
+// result. Why FP4 and not i8 (measured, profiles/r01_pmc):
+//   * rate: the scaled FP4 MFMA does 64 K per 32 cycles — twice the i8 32x32x32 rate;
+//   * size: an A fragment is 32 nibbles (16 B) per lane, so the k=128, p=32 coefficient bit-matrix
+//     is 128 KiB and ALL of its M-tiles fit in one CU's LDS: each input byte is loaded and
+//     bit-expanded once per block instead of once per M-group (the i8 kernel re-expanded every
+//     byte 4x and was VALU-bound: 87 VALU per 8 MFMA, PMC in profiles/).
+// Per wave and K-step (8 input rows = 64 K bits): 2 N-tiles (64 interleaved columns: tile t holds
+// columns 2c + t, so one ushort load / store serves both), MG M-tiles (MG <= 8) from LDS,
+// 2 x MG MFMAs. Input bytes are expanded to 8 FP4 nibbles with one v_perm of a 4-entry pool
+// {0x00,0x02,0x20,0x22} indexed by the byte's 2-bit chunks.
+// Output bits are placed on MFMA rows exactly as in gf_mfma.hip so every lane owns whole bytes.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "gfrs/desc.h"
+#include "gfrs/kernels.h"
+
+namespace gfrs {
+namespace {
+
+using i32x8 = int __attribute__((ext_vector_type(8)));
+using i32x4 = int __attribute__((ext_vector_type(4)));
+using f32x16 = float __attribute__((ext_vector_type(16)));
+template <typename T>
+using cptr = const __attribute__((address_space(4))) T*;
+template <typename T>
+using gptr = __attribute__((address_space(1))) T*;
+
+constexpr int kNTW = 2;        // N-tiles per wave (64 columns)
+constexpr int kBlockCols = 256;  // 4 waves x 64 columns
+constexpr int kPF = 4;         // K-steps of input kept in flight
+constexpr int kMaxLdsKiB = 144;
+
+__constant__ Tables d_tab = make_tables();
+
+__device__ __forceinline__ uint8_t dmul(uint8_t a, uint8_t b) { return d_tab.exp[d_tab.log[a] + d_tab.log[b]]; }
+__host__ __device__ constexpr int out_row_of(int r) { return 2 * ((r >> 2) & 1) + (r >> 4); }
+__host__ __device__ constexpr int out_bit_of(int r) { return ((r >> 3) & 1) * 4 + (r & 3); }
+
+// bitmat layout: [group][mt < MG][kstep][lane][16 bytes]; element j = nibble j of the 16 bytes.
+__global__ void fp4_bitmat_kernel(const uint8_t* __restrict__ coeff, int m, int k, int ksteps, int mg, int groups,
+                                  uint8_t* __restrict__ bitmat) {
+  const int64_t total = int64_t(groups) * mg * ksteps * 64 * 16;
+  for (int64_t idx = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; idx < total;
+       idx += int64_t(gridDim.x) * blockDim.x) {
+    const int q = int(idx & 15);
+    const int lane = int((idx >> 4) & 63);
+    int64_t rest = idx >> 10;
+    const int s = int(rest % ksteps);
+    rest /= ksteps;
+    const int mt = int(rest % mg);
+    const int g = int(rest / mg);
+    const int r = lane & 31, h = lane >> 5;
+    const int orow = 4 * (g * mg + mt) + out_row_of(r);
+    const int obit = out_bit_of(r);
+    uint8_t v = 0;
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      const int j = 2 * q + half;
+      const int irow = 8 * s + 4 * h + (j >> 3);
+      const int ibit = j & 7;
+      if (orow < m && irow < k && ((dmul(coeff[size_t(orow) * k + irow], uint8_t(1u << ibit)) >> obit) & 1))
+        v |= uint8_t(0x2u << (4 * half));
+    }
+    bitmat[idx] = v;
+  }
+}
+
+// 8 bits of x -> 8 FP4 nibbles (bit b -> nibble b = 0x2 if set).
+__device__ __forceinline__ int expand_fp4(uint32_t x) {
+  const uint32_t sel = (((x & 0x33u) * 0x1001u) | ((x & 0xCCu) * 0x40040u)) & 0x03030303u;
+  return int(__builtin_amdgcn_perm(0u, 0x22200200u, sel));
+}
+
+__device__ __forceinline__ uint32_t parity(float v) { return uint32_t(v) & 1u; }
+
+// Output byte u (0/1) of one accumulator tile (regs 8u .. 8u+7).
+__device__ __forceinline__ uint32_t pack_byte(const f32x16& acc, int u) {
+  uint32_t v = 0;
+#pragma unroll
+  for (int q = 0; q < 2; ++q)
+#pragma unroll
+    for (int low = 0; low < 4; ++low) v |= parity(acc[4 * (2 * u + q) + low]) << (q * 4 + low);
+  return v;
+}
+
+template <int MG>
+__global__ __launch_bounds__(256, 1) void gf_gemm_fp4_kernel(cptr<uint64_t> in, cptr<uint64_t> out,
+                                                             const i32x4* __restrict__ bitmat, int k, int m,
+                                                             int ksteps, int groups, int64_t col0, int64_t nchunks,
+                                                             int64_t chunk_slots) {
+  extern __shared__ __attribute__((aligned(16))) i32x4 afrag[];  // [MG][ksteps][64]
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7;
+  const int local = bid >> 3;
+  const int g = local % groups;
+  const int64_t slot = int64_t(local / groups) * 8 + xcd;
+  if (slot >= chunk_slots) return;
+
+  const i32x4* src = bitmat + size_t(g) * MG * ksteps * 64;
+  for (int i = threadIdx.x; i < MG * ksteps * 64; i += 256) afrag[i] = src[i];
+  __syncthreads();
+
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 31, h = lane >> 5;
+  const int scale = 0x7F7F7F7F;  // E8M0 1.0 for every block of 32
+  for (int64_t chunk = slot; chunk < nchunks; chunk += chunk_slots) {
+    const int64_t colw = col0 + chunk * kBlockCols + wave * 64 + 2 * c;  // this lane's 2 columns
+    f32x16 acc[MG][kNTW];
+#pragma unroll
+    for (int mt = 0; mt < MG; ++mt)
+#pragma unroll
+      for (int t = 0; t < kNTW; ++t) acc[mt][t] = (f32x16)(0.0f);
+
+    // register ring: ring[u][i] = ushort (2 columns) of input row 8s + 4h + i for K-step s = u mod PF
+    uint32_t ring[kPF][4];
+#pragma unroll
+    for (int u = 0; u < kPF; ++u)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = 8 * u + 4 * h + i;
+        ring[u][i] = (u < ksteps && row < k) ? uint32_t(*(gptr<const uint16_t>)(in[row] + colw)) : 0u;
+      }
+    for (int s0 = 0; s0 < ksteps; s0 += kPF) {
+#pragma unroll
+      for (int u = 0; u < kPF; ++u) {
+        const int s = s0 + u;
+        if (s < ksteps) {
+          uint32_t x[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) x[i] = ring[u][i];
+          if (s + kPF < ksteps) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const int row = 8 * (s + kPF) + 4 * h + i;
+              ring[u][i] = row < k ? uint32_t(*(gptr<const uint16_t>)(in[row] + colw)) : 0u;
+            }
+          }
+          i32x8 b[kNTW];
+#pragma unroll
+          for (int t = 0; t < kNTW; ++t) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) b[t][i] = expand_fp4((x[i] >> (8 * t)) & 0xFFu);
+#pragma unroll
+            for (int i = 4; i < 8; ++i) b[t][i] = 0;
+          }
+#pragma unroll
+          for (int mt = 0; mt < MG; ++mt) {
+            const i32x4 a4 = afrag[(mt * ksteps + s) * 64 + lane];
+            const i32x8 a = {a4[0], a4[1], a4[2], a4[3], 0, 0, 0, 0};
+#pragma unroll
+            for (int t = 0; t < kNTW; ++t)
+              acc[mt][t] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b[t], acc[mt][t], 4, 4, 0, scale, 0,
+                                                                          scale);
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int mt = 0; mt < MG; ++mt)
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int row = 4 * (g * MG + mt) + 2 * h + u;
+        if (row >= m) continue;
+        const uint64_t op = out[row];
+        if (!op) continue;
+        const uint32_t w = pack_byte(acc[mt][0], u) | (pack_byte(acc[mt][1], u) << 8);
+        *(gptr<uint16_t>)(op + colw) = uint16_t(w);
+      }
+  }
+}
+
+struct Fp4Geometry {
+  int ksteps, mtiles, mg, groups;
+  size_t lds;
+};
+
+Fp4Geometry geometry(int k, int m) {
+  Fp4Geometry g{};
+  g.ksteps = (k + 7) / 8;
+  g.mtiles = (m + 3) / 4;
+  // MG = M-tiles per block: next power of two >= mtiles (<= 8, the accumulator budget), halved
+  // until the block's A slice fits the LDS
+  g.mg = 1;
+  while (g.mg < g.mtiles && g.mg < 8) g.mg <<= 1;
+  while (g.mg > 1 && g.mg * g.ksteps > kMaxLdsKiB) g.mg >>= 1;
+  g.groups = (g.mtiles + g.mg - 1) / g.mg;
+  g.lds = size_t(g.mg) * g.ksteps * 64 * 16;
+  return g;
+}
+
+template <int MG>
+hipError_t launch_fp4(const Fp4Geometry& geo, cptr<uint64_t> in, cptr<uint64_t> out, const void* bitmat, int k, int m,
+                      int64_t col0, int64_t nchunks, hipStream_t stream) {
+  static bool attr_set = false;
+  if (!attr_set) {
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gf_gemm_fp4_kernel<MG>),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  // one block per CU in total (the LDS holds the whole A slice), chunk slots a multiple of 8
+  int64_t slots = std::max<int64_t>(8, (256 / geo.groups) / 8 * 8);
+  slots = std::min<int64_t>(slots, (nchunks + 7) / 8 * 8);
+  const unsigned blocks = unsigned(slots * geo.groups);
+  gf_gemm_fp4_kernel<MG><<<blocks, 256, geo.lds, stream>>>(in, out, static_cast<const i32x4*>(bitmat), k, m,
+                                                           geo.ksteps, geo.groups, col0, nchunks, slots);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+size_t fp4_bitmat_bytes(int k, int m) {
+  const Fp4Geometry g = geometry(k, m);
+  return size_t(g.groups) * g.mg * g.ksteps * 64 * 16;
+}
+
+hipError_t launch_fp4_bitmat(const uint8_t* coeff, int m, int k, void* bitmat, hipStream_t stream) {
+  if (m <= 0 || k <= 0 || m > 256 || k > 256) return hipErrorInvalidValue;
+  const Fp4Geometry g = geometry(k, m);
+  const int64_t total = int64_t(fp4_bitmat_bytes(k, m));
+  const int blocks = int(std::min<int64_t>((total + 255) / 256, 4096));
+  fp4_bitmat_kernel<<<blocks, 256, 0, stream>>>(coeff, m, k, g.ksteps, g.mg, g.groups, static_cast<uint8_t*>(bitmat));
+  return hipGetLastError();
+}
+
+hipError_t launch_gf_gemm_fp4(const void* bitmat, const void* desc, int k, int m, int64_t col0, int64_t ncols,
+                              hipStream_t stream) {
+  if (k <= 0 || m <= 0 || ncols < 0 || (col0 & 1)) return hipErrorInvalidValue;
+  const int m_pad = pad_m(m);
+  const DescLayout l = desc_layout(k, m_pad);
+  const char* b = static_cast<const char*>(desc);
+  const Fp4Geometry geo = geometry(k, m);
+  const int64_t nchunks = ncols / kBlockCols;
+  if (nchunks > 0) {
+    const auto in = (cptr<uint64_t>)(b + l.in_off);
+    const auto out = (cptr<uint64_t>)(b + l.out_off);
+    hipError_t e;
+    switch (geo.mg) {
+      case 8: e = launch_fp4<8>(geo, in, out, bitmat, k, m, col0, nchunks, stream); break;
+      case 4: e = launch_fp4<4>(geo, in, out, bitmat, k, m, col0, nchunks, stream); break;
+      case 2: e = launch_fp4<2>(geo, in, out, bitmat, k, m, col0, nchunks, stream); break;
+      default: e = launch_fp4<1>(geo, in, out, bitmat, k, m, col0, nchunks, stream); break;
+    }
+    if (e != hipSuccess) return e;
+  }
+  const int64_t done = nchunks * kBlockCols;
+  if (done < ncols) return launch_gf_gemm(desc, k, m_pad, col0 + done, ncols - done, false, 0, stream);
+  return hipSuccess;
+}
+
+}  // namespace gfrs

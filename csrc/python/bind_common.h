@@ -50,8 +50,8 @@ inline py::dict report(const gfrs::FileReport& r) {
 inline void bind_common(py::module_& m) {
   m.def("pad_m", &gfrs::pad_m);
   m.def("tile_for", &gfrs::tile_for);
-  m.def("desc_layout", [](int k, int m_pad) {
-    const gfrs::DescLayout l = gfrs::desc_layout(k, m_pad);
+  m.def("desc_layout", [](int k, int m_pad, int batch) {
+    const gfrs::DescLayout l = gfrs::desc_layout(k, m_pad, batch);
     py::dict d;
     d["in_off"] = l.in_off;
     d["copy_off"] = l.copy_off;
@@ -59,7 +59,7 @@ inline void bind_common(py::module_& m) {
     d["tab_off"] = l.tab_off;
     d["bytes"] = l.bytes;
     return d;
-  });
+  }, py::arg("k"), py::arg("m_pad"), py::arg("batch") = 1);
   m.def(
       "build_desc",
       [](int k, int mm, const std::vector<uint64_t>& in, const std::vector<uint64_t>& copy,

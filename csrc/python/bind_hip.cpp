@@ -60,6 +60,15 @@ PYBIND11_MODULE(_hip, m) {
       py::arg("desc"), py::arg("k"), py::arg("m_pad"), py::arg("col0"), py::arg("ncols"), py::arg("bytewise") = false,
       py::arg("max_blocks") = 0, py::arg("stream") = 0);
   m.def(
+      "gemm_batched",
+      [](uint64_t desc, int k, int m_pad, int batch, int64_t col0, int64_t ncols, bool bytewise, uint64_t stream) {
+        check(launch_gf_gemm_batched(reinterpret_cast<const void*>(desc), k, m_pad, batch, col0, ncols, bytewise,
+                                     as_stream(stream)),
+              "gf_gemm_batched");
+      },
+      py::arg("desc"), py::arg("k"), py::arg("m_pad"), py::arg("batch"), py::arg("col0"), py::arg("ncols"),
+      py::arg("bytewise") = false, py::arg("stream") = 0);
+  m.def(
       "gemm_variant",
       [](uint64_t desc, int k, int m_pad, int64_t col0, int64_t ncols, int vec, int pf, bool nt, int max_blocks,
          uint64_t stream) {
@@ -90,6 +99,17 @@ PYBIND11_MODULE(_hip, m) {
     check(launch_gf_gemm_mfma(reinterpret_cast<const void*>(bitmat), reinterpret_cast<const void*>(desc), k, mm, col0,
                               ncols, as_stream(stream)),
           "gf_gemm_mfma");
+  });
+  m.def("fp4_bitmat_bytes", &fp4_bitmat_bytes);
+  m.def("fp4_bitmat", [](uint64_t coeff, int mm, int k, uint64_t bitmat, uint64_t stream) {
+    check(launch_fp4_bitmat(reinterpret_cast<const uint8_t*>(coeff), mm, k, reinterpret_cast<void*>(bitmat),
+                            as_stream(stream)),
+          "fp4_bitmat");
+  });
+  m.def("gemm_fp4", [](uint64_t bitmat, uint64_t desc, int k, int mm, int64_t col0, int64_t ncols, uint64_t stream) {
+    check(launch_gf_gemm_fp4(reinterpret_cast<const void*>(bitmat), reinterpret_cast<const void*>(desc), k, mm, col0,
+                             ncols, as_stream(stream)),
+          "gf_gemm_fp4");
   });
   m.def("gen_matrix", [](uint64_t e, int k, int p, int kind, uint64_t stream) {
     check(launch_gen_matrix(reinterpret_cast<uint8_t*>(e), k, p, kind, as_stream(stream)), "gen_matrix");

@@ -41,12 +41,12 @@ class DescLayout:
     bytes: int
 
 
-def desc_layout(k: int, m_pad: int) -> DescLayout:
+def desc_layout(k: int, m_pad: int, batch: int = 1) -> DescLayout:
     """Mirror of ``gfrs::desc_layout`` (``csrc/include/gfrs/desc.h``); a test pins the two equal."""
     in_off = 16
-    copy_off = in_off + 8 * k
-    out_off = copy_off + 8 * k
-    tab_off = (out_off + 8 * m_pad + 31) // 32 * 32
+    copy_off = in_off + 8 * k * batch
+    out_off = copy_off + 8 * k * batch
+    tab_off = (out_off + 8 * m_pad * batch + 31) // 32 * 32
     return DescLayout(in_off, copy_off, out_off, tab_off, tab_off + 32 * k * m_pad)
 
 
@@ -77,28 +77,44 @@ def perm_tables_from_maps(maps: np.ndarray) -> np.ndarray:
 
 
 def build_desc(in_ptrs: Sequence[int], out_ptrs: Sequence[int], copy_ptrs: Sequence[int] | None,
-               tables: np.ndarray | None) -> np.ndarray:
-    """Descriptor bytes for k inputs, m outputs; ``tables`` is (m, k, 8) uint32 or None (zeros)."""
-    k, m = len(in_ptrs), len(out_ptrs)
+               tables: np.ndarray | None, batch: int = 1) -> np.ndarray:
+    """Descriptor bytes for ``batch`` stripes of k inputs and m outputs each (pointer lists are
+    stripe-major: ``batch * k`` / ``batch * m``); ``tables`` is (m, k, 8) uint32 or None (zeros)."""
+    if len(in_ptrs) % batch or len(out_ptrs) % batch:
+        raise ValueError("pointer lists must hold batch * k / batch * m entries")
+    k, m = len(in_ptrs) // batch, len(out_ptrs) // batch
     if not (1 <= k <= 256 and 1 <= m <= 256):
         raise ValueError("GF-GEMM supports 1 <= k, m <= 256")
     mp = pad_m(m)
-    lay = desc_layout(k, mp)
+    lay = desc_layout(k, mp, batch)
     d = np.zeros(lay.bytes, dtype=np.uint8)
-    d[0:16] = np.frombuffer(np.array([k, m, mp, 0], dtype="<i4").tobytes(), dtype=np.uint8)
-    d[lay.in_off : lay.in_off + 8 * k] = np.frombuffer(np.array(in_ptrs, dtype="<u8").tobytes(), dtype=np.uint8)
+    d[0:16] = np.frombuffer(np.array([k, m, mp, batch], dtype="<i4").tobytes(), dtype=np.uint8)
+    d[lay.in_off : lay.in_off + 8 * k * batch] = np.frombuffer(np.array(in_ptrs, dtype="<u8").tobytes(),
+                                                               dtype=np.uint8)
     if copy_ptrs is not None:
-        if len(copy_ptrs) != k:
-            raise ValueError("copy_ptrs must have k entries")
-        d[lay.copy_off : lay.copy_off + 8 * k] = np.frombuffer(
+        if len(copy_ptrs) != k * batch:
+            raise ValueError("copy_ptrs must have batch * k entries")
+        d[lay.copy_off : lay.copy_off + 8 * k * batch] = np.frombuffer(
             np.array([p or 0 for p in copy_ptrs], dtype="<u8").tobytes(), dtype=np.uint8)
-    outs = list(out_ptrs) + [0] * (mp - m)
-    d[lay.out_off : lay.out_off + 8 * mp] = np.frombuffer(np.array(outs, dtype="<u8").tobytes(), dtype=np.uint8)
+    outs = []
+    for b in range(batch):
+        outs += list(out_ptrs[b * m : (b + 1) * m]) + [0] * (mp - m)
+    d[lay.out_off : lay.out_off + 8 * mp * batch] = np.frombuffer(np.array(outs, dtype="<u8").tobytes(),
+                                                                  dtype=np.uint8)
     if tables is not None:
         t = np.zeros((k, mp, 8), dtype="<u4")
         t[:, :m, :] = np.transpose(np.asarray(tables, dtype=np.uint32), (1, 0, 2))
         d[lay.tab_off :] = np.frombuffer(t.tobytes(), dtype=np.uint8)
     return d
+
+
+def _batched_rows(x) -> list[list[torch.Tensor]] | None:
+    """[B, rows, C] tensor or list of per-stripe row lists -> list of stripes; None if not batched."""
+    if isinstance(x, torch.Tensor):
+        return [_rows(x[b]) for b in range(x.shape[0])] if x.dim() == 3 else None
+    if isinstance(x, (list, tuple)) and x and isinstance(x[0], (list, tuple)):
+        return [list(s) for s in x]
+    return None
 
 
 def _rows(x) -> list[torch.Tensor]:
@@ -140,6 +156,19 @@ class GemmPlan:
 
     def __init__(self, inputs, outputs, coeff=None, *, maps=None, copies=None, device_tables: bool = False,
                  engine: str = "valu"):
+        bi, bo = _batched_rows(inputs), _batched_rows(outputs)
+        if (bi is None) != (bo is None):
+            raise ValueError("inputs and outputs must both be batched ([B, rows, C]) or both not")
+        self.batch = 1
+        if bi is not None:
+            # batched: B stripes of identical shape, one launch (grid.y = stripe)
+            if len(bi) != len(bo) or len(bi) < 1 or len(bi) > 65535:
+                raise ValueError("batched plan needs 1..65535 stripes in inputs and outputs")
+            if copies is not None or engine != "valu":
+                raise ValueError("batched plans support neither fused copies nor engine='mfma'")
+            self.batch = len(bi)
+            self._stripes_in, self._stripes_out = bi, bo
+            inputs, outputs = bi[0], bo[0]
         self.inputs = _rows(inputs)
         self.outputs = _rows(outputs)
         self.copies = None if copies is None else [c for c in copies]
@@ -154,7 +183,14 @@ class GemmPlan:
         self.device = dev
         self.k, self.m = len(self.inputs), len(self.outputs)
         self.m_pad = pad_m(self.m)
-        lens = [r.numel() for r in self.inputs + self.outputs + [c for c in (self.copies or []) if c is not None]]
+        all_in = [r for st in self._stripes_in for r in st] if self.batch > 1 else self.inputs
+        all_out = [r for st in self._stripes_out for r in st] if self.batch > 1 else self.outputs
+        if self.batch > 1:
+            _check_rows(all_in, "input", dev)
+            _check_rows(all_out, "output", dev)
+            if any(len(st) != self.k for st in self._stripes_in) or any(len(st) != self.m for st in self._stripes_out):
+                raise ValueError("every stripe needs the same number of input / output rows")
+        lens = [r.numel() for r in all_in + all_out + [c for c in (self.copies or []) if c is not None]]
         self.ncols = min(lens) if lens else 0
         if coeff is not None:
             tables = perm_tables_from_coeff(np.asarray(coeff).reshape(self.m, self.k))
@@ -165,26 +201,29 @@ class GemmPlan:
         else:
             raise ValueError("need coeff, maps or device_tables=True")
         ptr = lambda t: int(t.data_ptr())  # noqa: E731
-        self.bytewise = any(ptr(r) % 16 for r in self.inputs + self.outputs) or any(
+        self.bytewise = any(ptr(r) % 16 for r in all_in + all_out) or any(
             c is not None and ptr(c) % 16 for c in (self.copies or []))
-        host = build_desc([ptr(r) for r in self.inputs], [ptr(r) for r in self.outputs],
+        host = build_desc([ptr(r) for r in all_in], [ptr(r) for r in all_out],
                           None if self.copies is None else [ptr(c) if c is not None else 0 for c in self.copies],
-                          tables)
+                          tables, self.batch)
         self.desc = torch.from_numpy(host).to(self.device)
-        self.layout = desc_layout(self.k, self.m_pad)
+        self.layout = desc_layout(self.k, self.m_pad, self.batch)
         self.engine = engine
         self.bitmat = None
-        if engine == "mfma":
-            # int8-MFMA bit-matrix path (csrc/kernels/gf_mfma.hip): GF(2^8) coefficients only, no
-            # fused copies, 4-byte aligned rows; the < 512-column remainder uses the v_perm tables.
+        if engine in ("mfma", "mfma_i8"):
+            # matrix-core GF(2) bit-matrix paths: "mfma" = FP4 block-scaled MFMA
+            # (csrc/kernels/gf_mfma_fp4.hip), "mfma_i8" = int8 MFMA (csrc/kernels/gf_mfma.hip).
+            # GF(2^8) coefficients only, no fused copies, aligned rows; the column remainder of a
+            # chunk runs on the v_perm tables that the descriptor also carries.
             if coeff is None or self.copies is not None or self.bytewise:
-                raise ValueError("engine='mfma' needs coeff=, no copies and aligned rows")
+                raise ValueError(f"engine={engine!r} needs coeff=, no copies and aligned rows")
             c = torch.from_numpy(np.ascontiguousarray(np.asarray(coeff, dtype=np.uint8).reshape(self.m, self.k)))
             c = c.to(self.device)
             h = hip()
-            self.bitmat = torch.empty(h.mfma_bitmat_bytes(self.k, self.m), dtype=torch.uint8, device=self.device)
-            h.mfma_bitmat(c.data_ptr(), self.m, self.k, self.bitmat.data_ptr(),
-                          torch.cuda.current_stream(self.device).cuda_stream)
+            sz = h.fp4_bitmat_bytes(self.k, self.m) if engine == "mfma" else h.mfma_bitmat_bytes(self.k, self.m)
+            self.bitmat = torch.empty(sz, dtype=torch.uint8, device=self.device)
+            build = h.fp4_bitmat if engine == "mfma" else h.mfma_bitmat
+            build(c.data_ptr(), self.m, self.k, self.bitmat.data_ptr(), torch.cuda.current_stream(self.device).cuda_stream)
             self._coeff_dev = c
         elif engine != "valu":
             raise ValueError(f"unknown engine {engine!r}")
@@ -227,7 +266,13 @@ class GemmPlan:
             self.desc.record_stream(stream)
         s = st.cuda_stream
         h = hip()
-        if self.engine == "mfma":
+        if self.batch > 1:
+            if vec is not None:
+                raise ValueError("kernel variants are not selectable on batched plans")
+            h.gemm_batched(int(self.desc.data_ptr()), self.k, self.m_pad, self.batch, col0, ncols, self.bytewise, s)
+        elif self.engine == "mfma":
+            h.gemm_fp4(int(self.bitmat.data_ptr()), int(self.desc.data_ptr()), self.k, self.m, col0, ncols, s)
+        elif self.engine == "mfma_i8":
             h.gemm_mfma(int(self.bitmat.data_ptr()), int(self.desc.data_ptr()), self.k, self.m, col0, ncols, s)
         elif self.bytewise:
             h.gemm(int(self.desc.data_ptr()), self.k, self.m_pad, col0, ncols, True, max_blocks, s)

@@ -22,7 +22,7 @@ from gpu_rscode_amd.models import alloc_rows  # noqa: E402
 from gpu_rscode_amd.ops import GemmPlan, fill_random_, gf_invert  # noqa: E402
 
 VARIANTS = [None, (1, 1, False), (1, 2, False), (1, 4, False), (1, 2, True), (1, 4, True), (2, 1, False),
-            (2, 2, False), (2, 2, True), "mfma"]
+            (2, 2, False), (2, 2, True), "mfma", "mfma_i8"]
 
 
 def timed(fn, reps):
@@ -46,7 +46,7 @@ def make_case(name, k, m, ncopy, total_bytes):
         copies = [dst[j] if j < ncopy else None for j in range(k)]
     coeff = np.random.default_rng(k + m).integers(1, 256, size=(m, k), dtype=np.uint8)
     plan = GemmPlan(data, out, coeff, copies=copies)
-    mplan = GemmPlan(data, out, coeff, engine="mfma") if not ncopy else None
+    mplan = {e: GemmPlan(data, out, coeff, engine=e) for e in ("mfma", "mfma_i8")} if not ncopy else None
     traffic = (k + m + ncopy) * C
     return {"name": name, "k": k, "m": m, "copies": ncopy, "C": C, "plan": plan, "mplan": mplan,
             "traffic": traffic, "keep": (data, out, copies)}
@@ -75,11 +75,12 @@ def main():
         times = {str(v): [] for v in VARIANTS}
         for _ in range(a.rounds):
             for v in VARIANTS:
-                if v == "mfma":
+                if v in ("mfma", "mfma_i8"):
                     if c["mplan"] is None:
                         continue
-                    c["mplan"].run()
-                    times[str(v)].append(timed(lambda: c["mplan"].run(), a.reps))
+                    pl = c["mplan"][v]
+                    pl.run()
+                    times[str(v)].append(timed(lambda: pl.run(), a.reps))
                     continue
                 kw = {} if v is None else dict(vec=v[0], pf=v[1], nt=v[2])
                 c["plan"].run(**kw)  # warm

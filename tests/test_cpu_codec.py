@@ -40,12 +40,13 @@ def sha(path):
 
 
 # ---- descriptors -------------------------------------------------------------------------------
-@pytest.mark.parametrize("k,m", [(1, 1), (4, 2), (10, 4), (10, 3), (16, 4), (128, 32), (7, 17), (255, 1)])
-def test_desc_layout_python_equals_native(k, m):
+@pytest.mark.parametrize("k,m,batch", [(1, 1, 1), (4, 2, 1), (10, 4, 1), (10, 3, 7), (16, 4, 1), (128, 32, 1),
+                                       (7, 17, 3), (255, 1, 1), (10, 4, 1000)])
+def test_desc_layout_python_equals_native(k, m, batch):
     mp = pad_m(m)
     assert cpu().pad_m(m) == mp
-    lay = desc_layout(k, mp)
-    nat = cpu().desc_layout(k, mp)
+    lay = desc_layout(k, mp, batch)
+    nat = cpu().desc_layout(k, mp, batch)
     assert (lay.in_off, lay.copy_off, lay.out_off, lay.tab_off, lay.bytes) == (
         nat["in_off"], nat["copy_off"], nat["out_off"], nat["tab_off"], nat["bytes"])
 
