@@ -128,6 +128,64 @@ class ReedSolomon:
             self._cpu_gemm(self.E, ins, outs)
         return parity
 
+    def encode_batch(self, data: torch.Tensor, parity: torch.Tensor | None = None,
+                     stream: torch.cuda.Stream | None = None) -> torch.Tensor:
+        """Encode B same-size stripes in ONE launch: ``data`` [B, k, C] -> parity [B, p, C].
+
+        For small objects (KiB..MiB) a per-stripe launch is dominated by launch overhead; the
+        batched descriptor (grid.y = stripe) amortises it (serving path)."""
+        if data.dim() != 3 or data.shape[1] != self.k:
+            raise ValueError(f"expected [B, {self.k}, C]")
+        B, _, C = data.shape
+        if parity is None:
+            pitch = max(PITCH, (C + PITCH - 1) // PITCH * PITCH)
+            base = torch.empty(B * self.p * pitch, dtype=torch.uint8, device=data.device)
+            parity = base.as_strided((B, self.p, C), (self.p * pitch, pitch, 1))
+        if self.p == 0:
+            return parity
+        if data.device.type != "cuda":
+            for b in range(B):
+                self.encode(data[b], parity[b])
+            return parity
+        key = ("encb", int(data.data_ptr()), tuple(data.stride()), tuple(data.shape), int(parity.data_ptr()))
+        plan = self._plans.get(key)
+        if plan is None:
+            maps = self._maps(self.E)
+            plan = GemmPlan(data, parity, None if maps is not None else self.E, maps=maps)
+            self._plans[key] = plan
+        plan.run(stream)
+        return parity
+
+    def decode_batch(self, survivors: torch.Tensor, rows: Sequence[int], out: torch.Tensor | None = None,
+                     stream: torch.cuda.Stream | None = None) -> torch.Tensor:
+        """Rebuild the erased natives of B stripes that lost the same chunks (one launch):
+        ``survivors`` [B, k, C] (chunk ids ``rows``) -> ``out`` [B, k, C] natives."""
+        rows = [int(r) for r in rows]
+        B, k, C = survivors.shape
+        if k != self.k:
+            raise ValueError(f"expected [B, {self.k}, C]")
+        if out is None:
+            pitch = max(PITCH, (C + PITCH - 1) // PITCH * PITCH)
+            base = torch.empty(B * self.k * pitch, dtype=torch.uint8, device=survivors.device)
+            out = base.as_strided((B, self.k, C), (self.k * pitch, pitch, 1))
+        pos = {r: j for j, r in enumerate(rows)}
+        for r, j in pos.items():
+            if r < self.k:
+                out[:, r].copy_(survivors[:, j])
+        erased = [i for i in range(self.k) if i not in pos]
+        if not erased:
+            return out
+        dm = self.decode_matrix(rows)[erased]
+        if survivors.device.type != "cuda":
+            for b in range(B):
+                self._cpu_gemm(dm, _rows(survivors[b]), [out[b, i] for i in erased])
+            return out
+        outs = [[out[b, i] for i in erased] for b in range(B)]
+        ins = [[survivors[b, j] for j in range(self.k)] for b in range(B)]
+        maps = self._maps(dm)
+        GemmPlan(ins, outs, None if maps is not None else dm, maps=maps).run(stream)
+        return out
+
     # ---- decode ------------------------------------------------------------------------------
     def decode_matrix(self, rows: Sequence[int]) -> np.ndarray:
         rows = tuple(int(r) for r in rows)

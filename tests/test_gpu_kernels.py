@@ -208,3 +208,24 @@ def test_mfma_bitmatrix_gemm_matches_oracle(k, m, ncols, engine):
     GemmPlan(dev, out, coeff, engine=engine).run()
     torch.cuda.synchronize()
     assert np.array_equal(out.cpu().numpy(), GF256.gemm(coeff, host))
+
+
+@pytest.mark.parametrize("batch,k,m,ncols", [(3, 10, 4, 4099), (64, 4, 2, 1 << 14), (5, 16, 20, 777), (2, 1, 1, 16)])
+def test_batched_gemm_matches_oracle(batch, k, m, ncols):
+    _native_loaded()
+    rng = np.random.default_rng(batch * 100 + k)
+    coeff = rng.integers(0, 256, size=(m, k), dtype=np.uint8)
+    host = rng.integers(0, 256, size=(batch, k, ncols), dtype=np.uint8)
+    pitch = (ncols + 255) // 256 * 256
+    dbase = torch.zeros(batch * k * pitch, dtype=torch.uint8, device="cuda")
+    data = dbase.as_strided((batch, k, ncols), (k * pitch, pitch, 1))
+    data.copy_(torch.from_numpy(host))
+    obase = torch.full((batch * m * pitch,), 0xEE, dtype=torch.uint8, device="cuda")
+    out = obase.as_strided((batch, m, ncols), (m * pitch, pitch, 1))
+    plan = GemmPlan(data, out, coeff)
+    assert plan.batch == batch
+    plan.run()
+    torch.cuda.synchronize()
+    got = out.cpu().numpy()
+    for b in range(batch):
+        assert np.array_equal(got[b], GF256.gemm(coeff, host[b])), b
