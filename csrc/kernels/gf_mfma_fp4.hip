@@ -34,8 +34,7 @@ using gptr = __attribute__((address_space(1))) T*;
 
 constexpr int kNTW = 2;        // N-tiles per wave (64 columns)
 constexpr int kBlockCols = 256;  // 4 waves x 64 columns
-constexpr int kPF = 4;         // K-steps of input kept in flight
-constexpr int kMaxLdsKiB = 144;
+constexpr int kMaxLdsKiB = 142;  // A slice; + 2 KiB row pointers + 4 waves x 8 x 512 B rings <= 160 KiB
 
 __constant__ Tables d_tab = make_tables();
 
@@ -90,84 +89,127 @@ __device__ __forceinline__ uint32_t pack_byte(const f32x16& acc, int u) {
   return v;
 }
 
+// Per-wave input ring in LDS filled by LDS-DMA (global_load_lds, 4 B per lane): the loads of the
+// next kRing-1 K-steps stay in flight across chunk boundaries without costing VGPRs, which the
+// one-wave-per-SIMD MFMA loop needs to cover HBM latency. Each wave owns its ring (no barriers):
+// a slot = 8 input rows x the wave's 64 columns = 512 B, written by two 256-B DMA instructions
+// (lane l -> row 4*half + l/16, columns 4*(l%16)..+3). The ring reads are inline asm so the
+// compiler does not order them behind every outstanding DMA (vmcnt(0)); the explicit counted
+// `s_waitcnt vmcnt(2*(kRing-1))` retires exactly the slot about to be read.
+constexpr int kRing = 8;
+constexpr int kSlotBytes = 512;
+using lds_u8 = __attribute__((address_space(3))) uint8_t;
+
 template <int MG>
 __global__ __launch_bounds__(256, 1) void gf_gemm_fp4_kernel(cptr<uint64_t> in, cptr<uint64_t> out,
                                                              const i32x4* __restrict__ bitmat, int k, int m,
                                                              int ksteps, int groups, int64_t col0, int64_t nchunks,
                                                              int64_t chunk_slots) {
-  extern __shared__ __attribute__((aligned(16))) i32x4 afrag[];  // [MG][ksteps][64]
+  // LDS: A [MG][ksteps][64] x 16 B | row pointers [k] x 8 B (padded to 2 KiB) | rings [4][kRing][512]
+  extern __shared__ __attribute__((aligned(16))) i32x4 afrag[];
   const int bid = blockIdx.x;
   const int xcd = bid & 7;
   const int local = bid >> 3;
   const int g = local % groups;
-  const int64_t slot = int64_t(local / groups) * 8 + xcd;
-  if (slot >= chunk_slots) return;
+  const int64_t slot0 = int64_t(local / groups) * 8 + xcd;
+  if (slot0 >= chunk_slots) return;
 
+  const size_t a_bytes = size_t(MG) * ksteps * 1024;
+  uint64_t* rowptr = reinterpret_cast<uint64_t*>(reinterpret_cast<uint8_t*>(afrag) + a_bytes);
+  uint64_t* outptr = rowptr + 256 - 4 * MG;  // this group's 4*MG output rows (k <= 256 - 4*MG)
   const i32x4* src = bitmat + size_t(g) * MG * ksteps * 64;
   for (int i = threadIdx.x; i < MG * ksteps * 64; i += 256) afrag[i] = src[i];
+  for (int i = threadIdx.x; i < k; i += 256) rowptr[i] = in[i];
+  for (int i = threadIdx.x; i < 4 * MG; i += 256) {
+    const int row = 4 * g * MG + i;
+    outptr[i] = row < m ? out[row] : 0;
+  }
   __syncthreads();
 
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 31, h = lane >> 5;
+  lds_u8* ring = (lds_u8*)(reinterpret_cast<uint8_t*>(afrag) + a_bytes + 2048 + size_t(wave) * kRing * kSlotBytes);
+  const uint32_t ring_addr = uint32_t(reinterpret_cast<uintptr_t>(ring));
   const int scale = 0x7F7F7F7F;  // E8M0 1.0 for every block of 32
-  for (int64_t chunk = slot; chunk < nchunks; chunk += chunk_slots) {
-    const int64_t colw = col0 + chunk * kBlockCols + wave * 64 + 2 * c;  // this lane's 2 columns
-    f32x16 acc[MG][kNTW];
+  const int my_chunks = int((nchunks - slot0 + chunk_slots - 1) / chunk_slots);
+
+  // DMA cursor (odometer over my chunks x K-steps)
+  int a_chunk = 0, a_s = 0, a_slot = 0;
+  auto dma_next = [&]() {
+    if (a_chunk >= my_chunks) return;
+    const int64_t colbase = col0 + (slot0 + int64_t(a_chunk) * chunk_slots) * kBlockCols + wave * 64 + 4 * (lane & 15);
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      int row = 8 * a_s + 4 * half + (lane >> 4);
+      row = row < k ? row : k - 1;  // rows >= k are masked to zero at expansion time
+      const auto gsrc = (gptr<const void>)(rowptr[row] + colbase);
+      __builtin_amdgcn_global_load_lds(gsrc, ring + a_slot * kSlotBytes + 256 * half, 4, 0, 0);
+    }
+    if (++a_s == ksteps) {
+      a_s = 0;
+      ++a_chunk;
+    }
+    a_slot = a_slot + 1 == kRing ? 0 : a_slot + 1;
+  };
+  for (int i = 0; i < kRing - 1; ++i) dma_next();
+
+  int r_slot = 0;
+  f32x16 acc[MG][kNTW];
+  for (int ci = 0; ci < my_chunks; ++ci) {
 #pragma unroll
     for (int mt = 0; mt < MG; ++mt)
 #pragma unroll
       for (int t = 0; t < kNTW; ++t) acc[mt][t] = (f32x16)(0.0f);
-
-    // register ring: ring[u][i] = ushort (2 columns) of input row 8s + 4h + i for K-step s = u mod PF
-    uint32_t ring[kPF][4];
-#pragma unroll
-    for (int u = 0; u < kPF; ++u)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int row = 8 * u + 4 * h + i;
-        ring[u][i] = (u < ksteps && row < k) ? uint32_t(*(gptr<const uint16_t>)(in[row] + colw)) : 0u;
+    for (int s = 0; s < ksteps; ++s) {
+      if (a_chunk < my_chunks) {
+        dma_next();
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (kRing - 1)) : "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
-    for (int s0 = 0; s0 < ksteps; s0 += kPF) {
+      // 4 ring reads (rows 4h+i, this lane's 2 columns) + their wait, invisible to the compiler's
+      // LDS-DMA alias tracking
+      const uint32_t addr = ring_addr + uint32_t(r_slot * kSlotBytes + 256 * h + 2 * c);
+      uint32_t x0, x1, x2, x3;
+      asm volatile(
+          "ds_read_u16 %0, %4\n\t"
+          "ds_read_u16 %1, %4 offset:64\n\t"
+          "ds_read_u16 %2, %4 offset:128\n\t"
+          "ds_read_u16 %3, %4 offset:192\n\t"
+          "s_waitcnt lgkmcnt(0)"
+          : "=&v"(x0), "=&v"(x1), "=&v"(x2), "=&v"(x3)
+          : "v"(addr)
+          : "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      r_slot = r_slot + 1 == kRing ? 0 : r_slot + 1;
+      const int rbase = 8 * s + 4 * h;
+      const uint32_t xs[4] = {rbase < k ? x0 : 0u, rbase + 1 < k ? x1 : 0u, rbase + 2 < k ? x2 : 0u,
+                              rbase + 3 < k ? x3 : 0u};
+      i32x8 b[kNTW];
 #pragma unroll
-      for (int u = 0; u < kPF; ++u) {
-        const int s = s0 + u;
-        if (s < ksteps) {
-          uint32_t x[4];
+      for (int t = 0; t < kNTW; ++t) {
 #pragma unroll
-          for (int i = 0; i < 4; ++i) x[i] = ring[u][i];
-          if (s + kPF < ksteps) {
+        for (int i = 0; i < 4; ++i) b[t][i] = expand_fp4((xs[i] >> (8 * t)) & 0xFFu);
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              const int row = 8 * (s + kPF) + 4 * h + i;
-              ring[u][i] = row < k ? uint32_t(*(gptr<const uint16_t>)(in[row] + colw)) : 0u;
-            }
-          }
-          i32x8 b[kNTW];
+        for (int i = 4; i < 8; ++i) b[t][i] = 0;
+      }
+      i32x4 a4[MG];  // issue every A read of the K-step first; the MFMAs then wait on them in order
 #pragma unroll
-          for (int t = 0; t < kNTW; ++t) {
+      for (int mt = 0; mt < MG; ++mt) a4[mt] = afrag[(mt * ksteps + s) * 64 + lane];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) b[t][i] = expand_fp4((x[i] >> (8 * t)) & 0xFFu);
+      for (int mt = 0; mt < MG; ++mt) {
+        const i32x8 a = {a4[mt][0], a4[mt][1], a4[mt][2], a4[mt][3], 0, 0, 0, 0};
 #pragma unroll
-            for (int i = 4; i < 8; ++i) b[t][i] = 0;
-          }
-#pragma unroll
-          for (int mt = 0; mt < MG; ++mt) {
-            const i32x4 a4 = afrag[(mt * ksteps + s) * 64 + lane];
-            const i32x8 a = {a4[0], a4[1], a4[2], a4[3], 0, 0, 0, 0};
-#pragma unroll
-            for (int t = 0; t < kNTW; ++t)
-              acc[mt][t] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b[t], acc[mt][t], 4, 4, 0, scale, 0,
-                                                                          scale);
-          }
-        }
+        for (int t = 0; t < kNTW; ++t)
+          acc[mt][t] =
+              __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b[t], acc[mt][t], 4, 4, 0, scale, 0, scale);
       }
     }
+    const int64_t colw = col0 + (slot0 + int64_t(ci) * chunk_slots) * kBlockCols + wave * 64 + 2 * c;
 #pragma unroll
     for (int mt = 0; mt < MG; ++mt)
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
-        const int row = 4 * (g * MG + mt) + 2 * h + u;
-        if (row >= m) continue;
-        const uint64_t op = out[row];
+        const uint64_t op = outptr[4 * mt + 2 * h + u];  // LDS: no vmcnt wait in the epilogue
         if (!op) continue;
         const uint32_t w = pack_byte(acc[mt][0], u) | (pack_byte(acc[mt][1], u) << 8);
         *(gptr<uint16_t>)(op + colw) = uint16_t(w);
@@ -180,17 +222,17 @@ struct Fp4Geometry {
   size_t lds;
 };
 
-Fp4Geometry geometry(int k, int m) {
+Fp4Geometry geometry(int k, int m, int mg_cap) {
   Fp4Geometry g{};
   g.ksteps = (k + 7) / 8;
   g.mtiles = (m + 3) / 4;
   // MG = M-tiles per block: next power of two >= mtiles (<= 8, the accumulator budget), halved
   // until the block's A slice fits the LDS
   g.mg = 1;
-  while (g.mg < g.mtiles && g.mg < 8) g.mg <<= 1;
+  while (g.mg < g.mtiles && g.mg < mg_cap) g.mg <<= 1;
   while (g.mg > 1 && g.mg * g.ksteps > kMaxLdsKiB) g.mg >>= 1;
   g.groups = (g.mtiles + g.mg - 1) / g.mg;
-  g.lds = size_t(g.mg) * g.ksteps * 64 * 16;
+  g.lds = size_t(g.mg) * g.ksteps * 64 * 16 + 2048 + 4 * 8 * 512;
   return g;
 }
 
@@ -215,27 +257,29 @@ hipError_t launch_fp4(const Fp4Geometry& geo, cptr<uint64_t> in, cptr<uint64_t> 
 
 }  // namespace
 
-size_t fp4_bitmat_bytes(int k, int m) {
-  const Fp4Geometry g = geometry(k, m);
+size_t fp4_bitmat_bytes(int k, int m, int mg_cap) {
+  const Fp4Geometry g = geometry(k, m, mg_cap);
   return size_t(g.groups) * g.mg * g.ksteps * 64 * 16;
 }
 
-hipError_t launch_fp4_bitmat(const uint8_t* coeff, int m, int k, void* bitmat, hipStream_t stream) {
-  if (m <= 0 || k <= 0 || m > 256 || k > 256) return hipErrorInvalidValue;
-  const Fp4Geometry g = geometry(k, m);
-  const int64_t total = int64_t(fp4_bitmat_bytes(k, m));
+hipError_t launch_fp4_bitmat(const uint8_t* coeff, int m, int k, void* bitmat, int mg_cap, hipStream_t stream) {
+  if (m <= 0 || k <= 0 || m > 256 || k > 256 || mg_cap < 1) return hipErrorInvalidValue;
+  const Fp4Geometry g = geometry(k, m, mg_cap);
+  if (k > 256 - 4 * g.mg) return hipErrorInvalidValue;  // row-pointer block shares 2 KiB with out ptrs
+  const int64_t total = int64_t(fp4_bitmat_bytes(k, m, mg_cap));
   const int blocks = int(std::min<int64_t>((total + 255) / 256, 4096));
   fp4_bitmat_kernel<<<blocks, 256, 0, stream>>>(coeff, m, k, g.ksteps, g.mg, g.groups, static_cast<uint8_t*>(bitmat));
   return hipGetLastError();
 }
 
 hipError_t launch_gf_gemm_fp4(const void* bitmat, const void* desc, int k, int m, int64_t col0, int64_t ncols,
-                              hipStream_t stream) {
-  if (k <= 0 || m <= 0 || ncols < 0 || (col0 & 1)) return hipErrorInvalidValue;
+                              int mg_cap, hipStream_t stream) {
+  if (k <= 0 || m <= 0 || ncols < 0 || (col0 & 1) || mg_cap < 1) return hipErrorInvalidValue;
   const int m_pad = pad_m(m);
   const DescLayout l = desc_layout(k, m_pad);
   const char* b = static_cast<const char*>(desc);
-  const Fp4Geometry geo = geometry(k, m);
+  const Fp4Geometry geo = geometry(k, m, mg_cap);
+  if (k > 256 - 4 * geo.mg) return hipErrorInvalidValue;
   const int64_t nchunks = ncols / kBlockCols;
   if (nchunks > 0) {
     const auto in = (cptr<uint64_t>)(b + l.in_off);

@@ -101,14 +101,15 @@ PYBIND11_MODULE(_hip, m) {
           "gf_gemm_mfma");
   });
   m.def("fp4_bitmat_bytes", &fp4_bitmat_bytes);
-  m.def("fp4_bitmat", [](uint64_t coeff, int mm, int k, uint64_t bitmat, uint64_t stream) {
-    check(launch_fp4_bitmat(reinterpret_cast<const uint8_t*>(coeff), mm, k, reinterpret_cast<void*>(bitmat),
+  m.def("fp4_bitmat", [](uint64_t coeff, int mm, int k, uint64_t bitmat, int mg_cap, uint64_t stream) {
+    check(launch_fp4_bitmat(reinterpret_cast<const uint8_t*>(coeff), mm, k, reinterpret_cast<void*>(bitmat), mg_cap,
                             as_stream(stream)),
           "fp4_bitmat");
   });
-  m.def("gemm_fp4", [](uint64_t bitmat, uint64_t desc, int k, int mm, int64_t col0, int64_t ncols, uint64_t stream) {
+  m.def("gemm_fp4", [](uint64_t bitmat, uint64_t desc, int k, int mm, int64_t col0, int64_t ncols, int mg_cap,
+                       uint64_t stream) {
     check(launch_gf_gemm_fp4(reinterpret_cast<const void*>(bitmat), reinterpret_cast<const void*>(desc), k, mm, col0,
-                             ncols, as_stream(stream)),
+                             ncols, mg_cap, as_stream(stream)),
           "gf_gemm_fp4");
   });
   m.def("gen_matrix", [](uint64_t e, int k, int p, int kind, uint64_t stream) {

@@ -155,7 +155,7 @@ class GemmPlan:
     """
 
     def __init__(self, inputs, outputs, coeff=None, *, maps=None, copies=None, device_tables: bool = False,
-                 engine: str = "valu"):
+                 engine: str = "valu", mfma_mg: int = 8):
         bi, bo = _batched_rows(inputs), _batched_rows(outputs)
         if (bi is None) != (bo is None):
             raise ValueError("inputs and outputs must both be batched ([B, rows, C]) or both not")
@@ -220,10 +220,15 @@ class GemmPlan:
             c = torch.from_numpy(np.ascontiguousarray(np.asarray(coeff, dtype=np.uint8).reshape(self.m, self.k)))
             c = c.to(self.device)
             h = hip()
-            sz = h.fp4_bitmat_bytes(self.k, self.m) if engine == "mfma" else h.mfma_bitmat_bytes(self.k, self.m)
-            self.bitmat = torch.empty(sz, dtype=torch.uint8, device=self.device)
-            build = h.fp4_bitmat if engine == "mfma" else h.mfma_bitmat
-            build(c.data_ptr(), self.m, self.k, self.bitmat.data_ptr(), torch.cuda.current_stream(self.device).cuda_stream)
+            st = torch.cuda.current_stream(self.device).cuda_stream
+            self.mfma_mg = mfma_mg
+            if engine == "mfma":
+                self.bitmat = torch.empty(h.fp4_bitmat_bytes(self.k, self.m, mfma_mg), dtype=torch.uint8,
+                                          device=self.device)
+                h.fp4_bitmat(c.data_ptr(), self.m, self.k, self.bitmat.data_ptr(), mfma_mg, st)
+            else:
+                self.bitmat = torch.empty(h.mfma_bitmat_bytes(self.k, self.m), dtype=torch.uint8, device=self.device)
+                h.mfma_bitmat(c.data_ptr(), self.m, self.k, self.bitmat.data_ptr(), st)
             self._coeff_dev = c
         elif engine != "valu":
             raise ValueError(f"unknown engine {engine!r}")
@@ -271,7 +276,8 @@ class GemmPlan:
                 raise ValueError("kernel variants are not selectable on batched plans")
             h.gemm_batched(int(self.desc.data_ptr()), self.k, self.m_pad, self.batch, col0, ncols, self.bytewise, s)
         elif self.engine == "mfma":
-            h.gemm_fp4(int(self.bitmat.data_ptr()), int(self.desc.data_ptr()), self.k, self.m, col0, ncols, s)
+            h.gemm_fp4(int(self.bitmat.data_ptr()), int(self.desc.data_ptr()), self.k, self.m, col0, ncols,
+                       self.mfma_mg, s)
         elif self.engine == "mfma_i8":
             h.gemm_mfma(int(self.bitmat.data_ptr()), int(self.desc.data_ptr()), self.k, self.m, col0, ncols, s)
         elif self.bytewise:

@@ -22,7 +22,7 @@ from gpu_rscode_amd.models import alloc_rows  # noqa: E402
 from gpu_rscode_amd.ops import GemmPlan, fill_random_, gf_invert  # noqa: E402
 
 VARIANTS = [None, (1, 1, False), (1, 2, False), (1, 4, False), (1, 2, True), (1, 4, True), (2, 1, False),
-            (2, 2, False), (2, 2, True), "mfma", "mfma_i8"]
+            (2, 2, False), (2, 2, True), "mfma", "mfma_mg4", "mfma_mg2", "mfma_i8"]
 
 
 def timed(fn, reps):
@@ -46,7 +46,12 @@ def make_case(name, k, m, ncopy, total_bytes):
         copies = [dst[j] if j < ncopy else None for j in range(k)]
     coeff = np.random.default_rng(k + m).integers(1, 256, size=(m, k), dtype=np.uint8)
     plan = GemmPlan(data, out, coeff, copies=copies)
-    mplan = {e: GemmPlan(data, out, coeff, engine=e) for e in ("mfma", "mfma_i8")} if not ncopy else None
+    mplan = None
+    if not ncopy:
+        mplan = {"mfma": GemmPlan(data, out, coeff, engine="mfma"),
+                 "mfma_mg4": GemmPlan(data, out, coeff, engine="mfma", mfma_mg=4),
+                 "mfma_mg2": GemmPlan(data, out, coeff, engine="mfma", mfma_mg=2),
+                 "mfma_i8": GemmPlan(data, out, coeff, engine="mfma_i8")}
     traffic = (k + m + ncopy) * C
     return {"name": name, "k": k, "m": m, "copies": ncopy, "C": C, "plan": plan, "mplan": mplan,
             "traffic": traffic, "keep": (data, out, copies)}
@@ -75,7 +80,7 @@ def main():
         times = {str(v): [] for v in VARIANTS}
         for _ in range(a.rounds):
             for v in VARIANTS:
-                if v in ("mfma", "mfma_i8"):
+                if isinstance(v, str):
                     if c["mplan"] is None:
                         continue
                     pl = c["mplan"][v]
