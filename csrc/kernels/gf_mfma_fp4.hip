@@ -34,7 +34,7 @@ using gptr = __attribute__((address_space(1))) T*;
 
 constexpr int kNTW = 2;        // N-tiles per wave (64 columns)
 constexpr int kBlockCols = 256;  // 4 waves x 64 columns
-constexpr int kMaxLdsKiB = 142;  // A slice; + 2 KiB row pointers + 4 waves x 8 x 512 B rings <= 160 KiB
+constexpr int kMaxLdsKiB = 141;  // A slice; + 2.25 KiB row/out pointers + 4 waves x 8 x 512 B rings <= 160 KiB
 
 __constant__ Tables d_tab = make_tables();
 
@@ -105,7 +105,7 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4_kernel(cptr<uint64_t> in, 
                                                              const i32x4* __restrict__ bitmat, int k, int m,
                                                              int ksteps, int groups, int64_t col0, int64_t nchunks,
                                                              int64_t chunk_slots) {
-  // LDS: A [MG][ksteps][64] x 16 B | row pointers [k] x 8 B (padded to 2 KiB) | rings [4][kRing][512]
+  // LDS: A [MG][ksteps][64] x 16 B | row pointers [256] | out pointers [32] | rings [4][kRing][512]
   extern __shared__ __attribute__((aligned(16))) i32x4 afrag[];
   const int bid = blockIdx.x;
   const int xcd = bid & 7;
@@ -116,7 +116,7 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4_kernel(cptr<uint64_t> in, 
 
   const size_t a_bytes = size_t(MG) * ksteps * 1024;
   uint64_t* rowptr = reinterpret_cast<uint64_t*>(reinterpret_cast<uint8_t*>(afrag) + a_bytes);
-  uint64_t* outptr = rowptr + 256 - 4 * MG;  // this group's 4*MG output rows (k <= 256 - 4*MG)
+  uint64_t* outptr = rowptr + 256;  // this group's 4*MG output rows
   const i32x4* src = bitmat + size_t(g) * MG * ksteps * 64;
   for (int i = threadIdx.x; i < MG * ksteps * 64; i += 256) afrag[i] = src[i];
   for (int i = threadIdx.x; i < k; i += 256) rowptr[i] = in[i];
@@ -127,7 +127,7 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4_kernel(cptr<uint64_t> in, 
   __syncthreads();
 
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 31, h = lane >> 5;
-  lds_u8* ring = (lds_u8*)(reinterpret_cast<uint8_t*>(afrag) + a_bytes + 2048 + size_t(wave) * kRing * kSlotBytes);
+  lds_u8* ring = (lds_u8*)(reinterpret_cast<uint8_t*>(afrag) + a_bytes + 2304 + size_t(wave) * kRing * kSlotBytes);
   const uint32_t ring_addr = uint32_t(reinterpret_cast<uintptr_t>(ring));
   const int scale = 0x7F7F7F7F;  // E8M0 1.0 for every block of 32
   const int my_chunks = int((nchunks - slot0 + chunk_slots - 1) / chunk_slots);
@@ -232,7 +232,7 @@ Fp4Geometry geometry(int k, int m, int mg_cap) {
   while (g.mg < g.mtiles && g.mg < mg_cap) g.mg <<= 1;
   while (g.mg > 1 && g.mg * g.ksteps > kMaxLdsKiB) g.mg >>= 1;
   g.groups = (g.mtiles + g.mg - 1) / g.mg;
-  g.lds = size_t(g.mg) * g.ksteps * 64 * 16 + 2048 + 4 * 8 * 512;
+  g.lds = size_t(g.mg) * g.ksteps * 64 * 16 + 2304 + 4 * 8 * 512;
   return g;
 }
 
@@ -265,7 +265,6 @@ size_t fp4_bitmat_bytes(int k, int m, int mg_cap) {
 hipError_t launch_fp4_bitmat(const uint8_t* coeff, int m, int k, void* bitmat, int mg_cap, hipStream_t stream) {
   if (m <= 0 || k <= 0 || m > 256 || k > 256 || mg_cap < 1) return hipErrorInvalidValue;
   const Fp4Geometry g = geometry(k, m, mg_cap);
-  if (k > 256 - 4 * g.mg) return hipErrorInvalidValue;  // row-pointer block shares 2 KiB with out ptrs
   const int64_t total = int64_t(fp4_bitmat_bytes(k, m, mg_cap));
   const int blocks = int(std::min<int64_t>((total + 255) / 256, 4096));
   fp4_bitmat_kernel<<<blocks, 256, 0, stream>>>(coeff, m, k, g.ksteps, g.mg, g.groups, static_cast<uint8_t*>(bitmat));
@@ -279,7 +278,6 @@ hipError_t launch_gf_gemm_fp4(const void* bitmat, const void* desc, int k, int m
   const DescLayout l = desc_layout(k, m_pad);
   const char* b = static_cast<const char*>(desc);
   const Fp4Geometry geo = geometry(k, m, mg_cap);
-  if (k > 256 - 4 * geo.mg) return hipErrorInvalidValue;
   const int64_t nchunks = ncols / kBlockCols;
   if (nchunks > 0) {
     const auto in = (cptr<uint64_t>)(b + l.in_off);
