@@ -38,8 +38,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from gpu_rscode_amd import gf  # noqa: E402
 from gpu_rscode_amd.models import alloc_rows  # noqa: E402
 from gpu_rscode_amd.ops import GemmPlan, fill_random_, invert_into_plan  # noqa: E402
-from gpu_rscode_amd.ops.gemm import pad_m  # noqa: E402
-from gpu_rscode_amd._native import hip  # noqa: E402
+from gpu_rscode_amd._native import cpu, hip  # noqa: E402
 
 BASELINE_GBPS = 2 * 1_096_310_784 / 1.72168 / 1e9  # 1.2736 GB/s
 
@@ -49,10 +48,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--k", type=int, default=10)
-    ap.add_argument("--n", type=int, default=14)
-    ap.add_argument("--bytes", type=int, default=1 << 30, help="input bytes per GPU")
-    ap.add_argument("--erasures", type=int, default=4)
+    ap.add_argument("--k", type=int, default=None)
+    ap.add_argument("--n", type=int, default=None)
+    ap.add_argument("--bytes", type=int, default=None, help="input bytes per GPU")
+    ap.add_argument("--erasures", type=int, default=None)
     ap.add_argument("--vec", type=int, default=None, help="kernel variant: 16-byte groups per lane (ablation)")
     ap.add_argument("--pf", type=int, default=2, help="kernel variant: rows in flight (with --vec)")
     ap.add_argument("--nt", action="store_true", help="kernel variant: non-temporal (with --vec)")
@@ -60,7 +59,26 @@ def parse():
     ap.add_argument("--gather", action="store_true", help="gather parity to rank 0 every step (RCCL)")
     ap.add_argument("--e2e", action="store_true", help="also time the pinned host->device->host pipeline")
     ap.add_argument("--streams", type=int, default=4)
-    return ap.parse_args()
+    ap.add_argument("--preset", default="k10n14", choices=sorted(PRESETS),
+                    help="BASELINE.json config: k10n14 (headline, #2/#3), k16n20_8g (#4 per GPU), k128n160 (#5), "
+                         "k4n6 (the reference's published shape)")
+    ap.add_argument("--engine", default="valu", choices=["valu", "mfma"], help="encode GEMM engine")
+    ap.add_argument("--graph", action="store_true", help="replay each step from a captured hipGraph")
+    a = ap.parse_args()
+    pr = PRESETS[a.preset]
+    for key, val in pr.items():
+        if getattr(a, key) is None:
+            setattr(a, key, val)
+    return a
+
+
+# BASELINE.json configs (per-GPU shapes; scaling is weak: every GPU runs one of these)
+PRESETS = {
+    "k10n14": dict(k=10, n=14, bytes=1 << 30, erasures=4),
+    "k16n20_8g": dict(k=16, n=20, bytes=8 << 30, erasures=4),
+    "k128n160": dict(k=128, n=160, bytes=1 << 30, erasures=32),
+    "k4n6": dict(k=4, n=6, bytes=1_096_310_784, erasures=2),
+}
 
 
 def main():
@@ -86,7 +104,7 @@ def main():
     while len(pool) < 16:
         erased = sorted(rng.choice(n, size=a.erasures, replace=False).tolist())
         rows = [r for r in range(n) if r not in erased]
-        if gf.GF256.is_invertible(g[rows]) and any(e < k for e in erased):
+        if any(e < k for e in erased) and cpu().decode_matrix(g.tobytes(), k, rows) is not None:
             pool.append(rows)
     e_dev = torch.from_numpy(e_host.copy()).to(dev)
     pool_dev = torch.tensor(pool, dtype=torch.int32, device=dev)
@@ -101,7 +119,7 @@ def main():
     parity = alloc_rows(p, C, dev)
     out = alloc_rows(k, C, dev)
 
-    enc = GemmPlan(data, parity, e_mat)
+    enc = GemmPlan(data, parity, e_mat, engine=a.engine)
     stripe = [data[i] for i in range(k)] + [parity[i] for i in range(p)]
     dec = []
     for rows in pool:
@@ -115,6 +133,8 @@ def main():
         plan.status = torch.zeros(1, dtype=torch.int32, device=dev)
         dec.append(plan)
     gathered = None
+    if a.graph and a.gather:
+        raise SystemExit("--graph and --gather are exclusive")
     if a.gather and world > 1 and rank == 0:
         gathered = [torch.empty_like(parity.as_strided((p * parity.stride(0),), (1,))) for _ in range(world)]
 
@@ -141,15 +161,27 @@ def main():
             flat = parity.as_strided((p * parity.stride(0),), (1,))
             dist.gather(flat, gathered if rank == 0 else None, dst=0)
 
-    for i in range(a.warmup):
+    for i in range(max(a.warmup, len(dec) if a.graph else 0)):
         step(i)
     torch.cuda.synchronize()
+    if a.graph:
+        # one captured graph per decode pattern: encode GEMM, side-stream inversion, decode GEMM
+        graphs = []
+        for i in range(len(dec)):
+            gph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gph, stream=stream):
+                step(i)
+            graphs.append(gph)
+        torch.cuda.synchronize()
+        run_step = lambda i: graphs[i % len(graphs)].replay()  # noqa: E731
+    else:
+        run_step = step
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(a.steps):
-        step(i)
+        run_step(i)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -174,8 +206,11 @@ def main():
     ms = elapsed / a.steps * 1e3
     bytes_per_step = 2 * k * C * world  # encoded input + decoded output, all ranks
     gbps = bytes_per_step / (ms / 1e3) / 1e9
+    metric = "encode+decode throughput (GB/s) at k=10,n=14 on 1 GiB; 1/2/4/8-GPU scaling"
+    if a.preset != "k10n14":
+        metric = f"encode+decode throughput (GB/s) at k={k},n={n} on {a.bytes / 2**30:.3g} GiB per GPU"
     rec = {
-        "metric": "encode+decode throughput (GB/s) at k=10,n=14 on 1 GiB; 1/2/4/8-GPU scaling",
+        "metric": metric,
         "value": round(gbps, 3),
         "unit": "GB/s",
         "n_gpus": world,
@@ -191,7 +226,7 @@ def main():
                    "global_batch": f"{a.bytes} B per GPU ({k} x {C} B chunks)", "seq_len": C,
                    "parallelism": f"dp{world} (stripe-sharded, RCCL broadcast of E)",
                    "erasures": a.erasures, "decode_invert": "device Gauss-Jordan per step",
-                   "gather": bool(a.gather)},
+                   "gather": bool(a.gather), "engine": a.engine, "graph": bool(a.graph), "preset": a.preset},
         "verified": ok,
         "baseline": {"gbps": round(BASELINE_GBPS, 4), "source": "k=8,n=11 1.1 GB Tesla C2050 (nearest published)"},
     }
