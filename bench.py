@@ -139,7 +139,8 @@ def main():
         gathered = [torch.empty_like(parity.as_strided((p * parity.stride(0),), (1,))) for _ in range(world)]
 
     h = hip()
-    stream = torch.cuda.current_stream(dev)
+    stream = torch.cuda.Stream(dev)  # a non-default stream (hipGraph capture needs one)
+    torch.cuda.set_stream(stream)
     side = torch.cuda.Stream(dev)  # decode-system inversion overlaps the encode GEMM
     inv_done = torch.cuda.Event()
     kv = dict(vec=a.vec, pf=a.pf, nt=a.nt)
