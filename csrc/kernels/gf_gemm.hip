@@ -188,12 +188,12 @@ __global__ __launch_bounds__(kBlock) void gf_gemm_vec_kernel(DescView d, int k, 
       }
 
     // Rows are consumed in pairs when PF is even: the six lookups of a pair fold into three
-    // v_bitop3 XORs (1.5 per coefficient instead of 2) — the VALU-bound wide tiles gain ~9%.
+    // v_bitop3 XORs (1.5 per coefficient instead of 2). Pairs only for MT <= 8: at MT = 16 the
+    // second row's live selectors/tables cost a wave per SIMD and the VALU-bound wide tile got
+    // slower (profiles/r01_kbench3).
+    constexpr bool kPairs = (PF % 2 == 0) && MT <= 8;
     for (int j0 = 0; j0 < k; j0 += PF) {
 #pragma unroll
-      // (pairs only for MT <= 8: at MT = 16 the second row's live selectors/tables cost a wave
-      // per SIMD and the VALU-bound wide tile got slower — profiles/r01_kbench3)
-      constexpr bool kPairs = (PF % 2 == 0) && MT <= 8;
       for (int u = 0; u < PF; u += (kPairs ? 2 : 1)) {
         const int j = j0 + u;
         if (kPairs && j + 1 < k) {
