@@ -57,9 +57,10 @@ size_t mfma_bitmat_bytes(int k, int m);
 // Rows must be 2-byte aligned; whole 256-column chunks run on the matrix cores, the remainder on
 // the v_perm kernel (desc must carry the perm tables too).
 // mg_cap bounds the M-tiles (4 output rows each) one block keeps in LDS/accumulators; the bitmat
-// must be built with the same cap.
+// must be built with the same cap. in_stride != 0 promises input row j == input row 0 + j*in_stride
+// (rows of one allocation): DMA addresses are then computed instead of read from a pointer table.
 hipError_t launch_gf_gemm_fp4(const void* bitmat, const void* desc, int k, int m, int64_t col0,
-                              int64_t ncols, int mg_cap, hipStream_t stream);
+                              int64_t ncols, int mg_cap, int64_t in_stride, hipStream_t stream);
 size_t fp4_bitmat_bytes(int k, int m, int mg_cap);
 hipError_t launch_fp4_bitmat(const uint8_t* coeff, int m, int k, void* bitmat, int mg_cap, hipStream_t stream);
 hipError_t launch_mfma_bitmat(const uint8_t* coeff, int m, int k, void* bitmat,

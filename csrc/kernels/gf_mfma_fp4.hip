@@ -34,7 +34,7 @@ using gptr = __attribute__((address_space(1))) T*;
 
 constexpr int kNTW = 2;        // N-tiles per wave (64 columns)
 constexpr int kBlockCols = 256;  // 4 waves x 64 columns
-constexpr int kMaxLdsKiB = 141;  // A slice; + 2.25 KiB row/out pointers + 4 waves x 8 x 512 B rings <= 160 KiB
+constexpr int kMaxLdsKiB = 139;  // A slice; + 2.25 KiB row/out pointers + 4 waves x 9 x 512 B rings <= 160 KiB
 
 __constant__ Tables d_tab = make_tables();
 
@@ -42,7 +42,8 @@ __device__ __forceinline__ uint8_t dmul(uint8_t a, uint8_t b) { return d_tab.exp
 __host__ __device__ constexpr int out_row_of(int r) { return 2 * ((r >> 2) & 1) + (r >> 4); }
 __host__ __device__ constexpr int out_bit_of(int r) { return ((r >> 3) & 1) * 4 + (r & 3); }
 
-// bitmat layout: [group][mt < MG][kstep][lane][16 bytes]; element j = nibble j of the 16 bytes.
+// bitmat layout: [group][kstep][mt < MG][lane][16 bytes]; element j = nibble j of the 16 bytes (one
+// K-step's MG fragments are contiguous, so the kernel reads them with immediate LDS offsets).
 __global__ void fp4_bitmat_kernel(const uint8_t* __restrict__ coeff, int m, int k, int ksteps, int mg, int groups,
                                   uint8_t* __restrict__ bitmat) {
   const int64_t total = int64_t(groups) * mg * ksteps * 64 * 16;
@@ -51,10 +52,10 @@ __global__ void fp4_bitmat_kernel(const uint8_t* __restrict__ coeff, int m, int 
     const int q = int(idx & 15);
     const int lane = int((idx >> 4) & 63);
     int64_t rest = idx >> 10;
-    const int s = int(rest % ksteps);
-    rest /= ksteps;
     const int mt = int(rest % mg);
-    const int g = int(rest / mg);
+    rest /= mg;
+    const int s = int(rest % ksteps);
+    const int g = int(rest / ksteps);
     const int r = lane & 31, h = lane >> 5;
     const int orow = 4 * (g * mg + mt) + out_row_of(r);
     const int obit = out_bit_of(r);
@@ -93,19 +94,32 @@ __device__ __forceinline__ uint32_t pack_byte(const f32x16& acc, int u) {
 // next kRing-1 K-steps stay in flight across chunk boundaries without costing VGPRs, which the
 // one-wave-per-SIMD MFMA loop needs to cover HBM latency. Each wave owns its ring (no barriers):
 // a slot = 8 input rows x the wave's 64 columns = 512 B, written by two 256-B DMA instructions
-// (lane l -> row 4*half + l/16, columns 4*(l%16)..+3). The ring reads are inline asm so the
-// compiler does not order them behind every outstanding DMA (vmcnt(0)); the explicit counted
-// `s_waitcnt vmcnt(2*(kRing-1))` retires exactly the slot about to be read.
+// (lane l -> row 4*half + l/16, columns 4*(l%16)..+3).
+//
+// The K loop is software-pipelined by hand: while the 2 x MG MFMAs of step g run, the ring bytes
+// and the MG A fragments of step g+1 (and, for scattered input rows, the row pointers of the next
+// DMA) are already being read from LDS. Those reads are inline asm, retired by one explicit
+// `s_waitcnt lgkmcnt(0)` at the end of the step, and "tied" to their destination registers by
+// empty asm statements so no use can be scheduled above the wait; the compiler's own alias
+// tracking would otherwise put a vmcnt(0)/lgkmcnt(0) in front of every read.
 constexpr int kRing = 8;
 constexpr int kSlotBytes = 512;
 using lds_u8 = __attribute__((address_space(3))) uint8_t;
 
-template <int MG>
+__device__ __forceinline__ void lgkm_wait() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+template <typename T>
+__device__ __forceinline__ void tie(T& v) {
+  asm volatile("" : "+v"(v));
+}
+
+// UNI: input row j lives at in[0] + j * in_stride (rows from one allocation, the usual case), so
+// DMA addresses are pure VALU arithmetic; otherwise the row pointers come from an LDS table.
+template <int MG, bool UNI>
 __global__ __launch_bounds__(256, 1) void gf_gemm_fp4_kernel(cptr<uint64_t> in, cptr<uint64_t> out,
                                                              const i32x4* __restrict__ bitmat, int k, int m,
                                                              int ksteps, int groups, int64_t col0, int64_t nchunks,
-                                                             int64_t chunk_slots) {
-  // LDS: A [MG][ksteps][64] x 16 B | row pointers [256] | out pointers [32] | rings [4][kRing][512]
+                                                             int64_t chunk_slots, int64_t in_stride) {
+  // LDS: A [ksteps][MG][64] x 16 B | row pointers [256] | out pointers [32] | rings [4][kRing+1][512]
   extern __shared__ __attribute__((aligned(16))) i32x4 afrag[];
   const int bid = blockIdx.x;
   const int xcd = bid & 7;
@@ -119,7 +133,8 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4_kernel(cptr<uint64_t> in, 
   uint64_t* outptr = rowptr + 256;  // this group's 4*MG output rows
   const i32x4* src = bitmat + size_t(g) * MG * ksteps * 64;
   for (int i = threadIdx.x; i < MG * ksteps * 64; i += 256) afrag[i] = src[i];
-  for (int i = threadIdx.x; i < k; i += 256) rowptr[i] = in[i];
+  if (!UNI)
+    for (int i = threadIdx.x; i < k; i += 256) rowptr[i] = in[i];
   for (int i = threadIdx.x; i < 4 * MG; i += 256) {
     const int row = 4 * g * MG + i;
     outptr[i] = row < m ? out[row] : 0;
@@ -127,63 +142,114 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4_kernel(cptr<uint64_t> in, 
   __syncthreads();
 
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 31, h = lane >> 5;
-  lds_u8* ring = (lds_u8*)(reinterpret_cast<uint8_t*>(afrag) + a_bytes + 2304 + size_t(wave) * kRing * kSlotBytes);
-  const uint32_t ring_addr = uint32_t(reinterpret_cast<uintptr_t>(ring));
+  const uint32_t lds0 = uint32_t(reinterpret_cast<uintptr_t>((lds_u8*)afrag));
+  const uint32_t a_addr = lds0 + 16u * lane;
+  const uint32_t rowptr_addr = lds0 + uint32_t(a_bytes);
+  lds_u8* ring =
+      (lds_u8*)(reinterpret_cast<uint8_t*>(afrag) + a_bytes + 2304 + size_t(wave) * (kRing + 1) * kSlotBytes);
+  const uint32_t ring_addr = uint32_t(reinterpret_cast<uintptr_t>(ring)) + uint32_t(256 * h + 2 * c);
   const int scale = 0x7F7F7F7F;  // E8M0 1.0 for every block of 32
   const int my_chunks = int((nchunks - slot0 + chunk_slots - 1) / chunk_slots);
+  const int total = my_chunks * ksteps;
+  if (total <= 0) return;
+  const uint64_t in0 = UNI ? in[0] : 0;
 
-  // DMA cursor (odometer over my chunks x K-steps)
-  int a_chunk = 0, a_s = 0, a_slot = 0;
-  auto dma_next = [&]() {
-    if (a_chunk >= my_chunks) return;
-    const int64_t colbase = col0 + (slot0 + int64_t(a_chunk) * chunk_slots) * kBlockCols + wave * 64 + 4 * (lane & 15);
-#pragma unroll
-    for (int half = 0; half < 2; ++half) {
-      int row = 8 * a_s + 4 * half + (lane >> 4);
-      row = row < k ? row : k - 1;  // rows >= k are masked to zero at expansion time
-      const auto gsrc = (gptr<const void>)(rowptr[row] + colbase);
-      __builtin_amdgcn_global_load_lds(gsrc, ring + a_slot * kSlotBytes + 256 * half, 4, 0, 0);
-    }
-    if (++a_s == ksteps) {
-      a_s = 0;
-      ++a_chunk;
-    }
-    a_slot = a_slot + 1 == kRing ? 0 : a_slot + 1;
+  // DMA cursor (odometer over my chunks x K-steps) and, off the UNI path, the row pointers of the
+  // cursor's step. Past the last step the cursor keeps issuing "dummy" DMAs (a valid source, the
+  // wave's spare slot kRing as destination) so the number in flight — and with it every counted
+  // vmcnt below — stays the same and the K loop has no branches.
+  int d_chunk = 0, d_s = 0, d_slot = 0;
+  uint64_t pn0 = 0, pn1 = 0;
+  auto row_of = [&](int half) {
+    const int r = 8 * d_s + 4 * half + (lane >> 4);
+    return r < k ? r : k - 1;  // rows >= k are masked to zero at expansion time
   };
-  for (int i = 0; i < kRing - 1; ++i) dma_next();
+  auto ptr_sync = [&]() {
+    pn0 = rowptr[row_of(0)];
+    pn1 = rowptr[row_of(1)];
+  };
+  auto ptr_async = [&]() {
+    asm volatile("ds_read_b64 %0, %2\n\tds_read_b64 %1, %3"
+                 : "=&v"(pn0), "=&v"(pn1)
+                 : "v"(rowptr_addr + 8u * row_of(0)), "v"(rowptr_addr + 8u * row_of(1))
+                 : "memory");
+  };
+  auto dma_issue = [&]() {
+    const bool live = d_chunk < my_chunks;
+    const int64_t col = col0 + (slot0 + int64_t(live ? d_chunk : 0) * chunk_slots) * kBlockCols + wave * 64 +
+                        4 * (lane & 15);
+    uint64_t s0, s1;
+    if constexpr (UNI) {
+      s0 = in0 + uint64_t(int64_t(row_of(0)) * in_stride + col);
+      s1 = in0 + uint64_t(int64_t(row_of(1)) * in_stride + col);
+    } else {
+      s0 = pn0 + uint64_t(col);
+      s1 = pn1 + uint64_t(col);
+    }
+    lds_u8* dst = ring + (live ? d_slot : kRing) * kSlotBytes;
+    __builtin_amdgcn_global_load_lds((gptr<const void>)s0, dst, 4, 0, 0);
+    __builtin_amdgcn_global_load_lds((gptr<const void>)s1, dst + 256, 4, 0, 0);
+    const bool wrap = d_s + 1 == ksteps;
+    d_s = live ? (wrap ? 0 : d_s + 1) : d_s;
+    d_chunk += (live && wrap) ? 1 : 0;
+    d_slot = live ? (d_slot + 1 == kRing ? 0 : d_slot + 1) : d_slot;
+  };
+  auto read_x = [&](uint32_t (&x)[4], int slot) {
+    asm volatile(
+        "ds_read_u16 %0, %4\n\t"
+        "ds_read_u16 %1, %4 offset:64\n\t"
+        "ds_read_u16 %2, %4 offset:128\n\t"
+        "ds_read_u16 %3, %4 offset:192"
+        : "=&v"(x[0]), "=&v"(x[1]), "=&v"(x[2]), "=&v"(x[3])
+        : "v"(ring_addr + uint32_t(slot * kSlotBytes))
+        : "memory");
+  };
+  auto read_a = [&](i32x4 (&a)[MG], int s) {
+    const uint32_t base = a_addr + uint32_t(s) * (MG * 1024u);
+#pragma unroll
+    for (int mt = 0; mt < MG; ++mt)
+      asm volatile("ds_read_b128 %0, %1 offset:%2" : "=&v"(a[mt]) : "v"(base), "n"(mt * 1024) : "memory");
+  };
+
+  // prologue: kRing-1 steps in flight, step 0's operands in registers
+  for (int i = 0; i < kRing - 1; ++i) {
+    if (!UNI) ptr_sync();
+    dma_issue();
+  }
+  if (!UNI) ptr_sync();
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (kRing - 2)) : "memory");
+  uint32_t xc[4], xn[4];
+  i32x4 ac[MG], an[MG];
+  read_x(xc, 0);
+  read_a(ac, 0);
+  lgkm_wait();
+#pragma unroll
+  for (int i = 0; i < 4; ++i) tie(xc[i]);
+#pragma unroll
+  for (int mt = 0; mt < MG; ++mt) tie(ac[mt]);
 
   int r_slot = 0;
-  f32x16 acc[MG][kNTW];
   for (int ci = 0; ci < my_chunks; ++ci) {
+    f32x16 acc[MG][kNTW];
 #pragma unroll
     for (int mt = 0; mt < MG; ++mt)
 #pragma unroll
       for (int t = 0; t < kNTW; ++t) acc[mt][t] = (f32x16)(0.0f);
     for (int s = 0; s < ksteps; ++s) {
-      if (a_chunk < my_chunks) {
-        dma_next();
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (kRing - 1)) : "memory");
-      } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      // 4 ring reads (rows 4h+i, this lane's 2 columns) + their wait, invisible to the compiler's
-      // LDS-DMA alias tracking
-      const uint32_t addr = ring_addr + uint32_t(r_slot * kSlotBytes + 256 * h + 2 * c);
-      uint32_t x0, x1, x2, x3;
-      asm volatile(
-          "ds_read_u16 %0, %4\n\t"
-          "ds_read_u16 %1, %4 offset:64\n\t"
-          "ds_read_u16 %2, %4 offset:128\n\t"
-          "ds_read_u16 %3, %4 offset:192\n\t"
-          "s_waitcnt lgkmcnt(0)"
-          : "=&v"(x0), "=&v"(x1), "=&v"(x2), "=&v"(x3)
-          : "v"(addr)
-          : "memory");
+      // (1) the DMA kRing-1 steps ahead; (2) step s+1's ring bytes and A fragments (its slot is
+      // the oldest of the kRing-1 pairs in flight); (3) this step's expansion + MFMAs; (4) retire
+      // the reads of (2). Reads past the last step hit valid LDS and are discarded.
+      dma_issue();
+      if (!UNI) ptr_async();
+      const int slot1 = r_slot + 1 == kRing ? 0 : r_slot + 1;
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (kRing - 2)) : "memory");
+      read_x(xn, slot1);
+      read_a(an, s + 1 == ksteps ? 0 : s + 1);
       __builtin_amdgcn_sched_barrier(0);
-      r_slot = r_slot + 1 == kRing ? 0 : r_slot + 1;
+
       const int rbase = 8 * s + 4 * h;
-      const uint32_t xs[4] = {rbase < k ? x0 : 0u, rbase + 1 < k ? x1 : 0u, rbase + 2 < k ? x2 : 0u,
-                              rbase + 3 < k ? x3 : 0u};
+      const uint32_t xs[4] = {rbase < k ? xc[0] : 0u, rbase + 1 < k ? xc[1] : 0u, rbase + 2 < k ? xc[2] : 0u,
+                              rbase + 3 < k ? xc[3] : 0u};
       i32x8 b[kNTW];
 #pragma unroll
       for (int t = 0; t < kNTW; ++t) {
@@ -192,16 +258,30 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4_kernel(cptr<uint64_t> in, 
 #pragma unroll
         for (int i = 4; i < 8; ++i) b[t][i] = 0;
       }
-      i32x4 a4[MG];  // issue every A read of the K-step first; the MFMAs then wait on them in order
-#pragma unroll
-      for (int mt = 0; mt < MG; ++mt) a4[mt] = afrag[(mt * ksteps + s) * 64 + lane];
 #pragma unroll
       for (int mt = 0; mt < MG; ++mt) {
-        const i32x8 a = {a4[mt][0], a4[mt][1], a4[mt][2], a4[mt][3], 0, 0, 0, 0};
+        const i32x8 a = {ac[mt][0], ac[mt][1], ac[mt][2], ac[mt][3], 0, 0, 0, 0};
 #pragma unroll
         for (int t = 0; t < kNTW; ++t)
           acc[mt][t] =
               __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b[t], acc[mt][t], 4, 4, 0, scale, 0, scale);
+      }
+      r_slot = slot1;
+      __builtin_amdgcn_sched_barrier(0);
+      lgkm_wait();
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        tie(xn[i]);
+        xc[i] = xn[i];
+      }
+#pragma unroll
+      for (int mt = 0; mt < MG; ++mt) {
+        tie(an[mt]);
+        ac[mt] = an[mt];
+      }
+      if (!UNI) {
+        tie(pn0);
+        tie(pn1);
       }
     }
     const int64_t colw = col0 + (slot0 + int64_t(ci) * chunk_slots) * kBlockCols + wave * 64 + 2 * c;
@@ -209,12 +289,13 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4_kernel(cptr<uint64_t> in, 
     for (int mt = 0; mt < MG; ++mt)
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
-        const uint64_t op = outptr[4 * mt + 2 * h + u];  // LDS: no vmcnt wait in the epilogue
+        const uint64_t op = outptr[4 * mt + 2 * h + u];
         if (!op) continue;
         const uint32_t w = pack_byte(acc[mt][0], u) | (pack_byte(acc[mt][1], u) << 8);
         *(gptr<uint16_t>)(op + colw) = uint16_t(w);
       }
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA (dummy or not) outlives the wave
 }
 
 struct Fp4Geometry {
@@ -232,16 +313,16 @@ Fp4Geometry geometry(int k, int m, int mg_cap) {
   while (g.mg < g.mtiles && g.mg < mg_cap) g.mg <<= 1;
   while (g.mg > 1 && g.mg * g.ksteps > kMaxLdsKiB) g.mg >>= 1;
   g.groups = (g.mtiles + g.mg - 1) / g.mg;
-  g.lds = size_t(g.mg) * g.ksteps * 64 * 16 + 2304 + 4 * 8 * 512;
+  g.lds = size_t(g.mg) * g.ksteps * 64 * 16 + 2304 + 4 * (kRing + 1) * kSlotBytes;
   return g;
 }
 
-template <int MG>
+template <int MG, bool UNI>
 hipError_t launch_fp4(const Fp4Geometry& geo, cptr<uint64_t> in, cptr<uint64_t> out, const void* bitmat, int k, int m,
-                      int64_t col0, int64_t nchunks, hipStream_t stream) {
+                      int64_t col0, int64_t nchunks, int64_t in_stride, hipStream_t stream) {
   static bool attr_set = false;
   if (!attr_set) {
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gf_gemm_fp4_kernel<MG>),
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gf_gemm_fp4_kernel<MG, UNI>),
                                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (e != hipSuccess) return e;
     attr_set = true;
@@ -250,9 +331,17 @@ hipError_t launch_fp4(const Fp4Geometry& geo, cptr<uint64_t> in, cptr<uint64_t> 
   int64_t slots = std::max<int64_t>(8, (256 / geo.groups) / 8 * 8);
   slots = std::min<int64_t>(slots, (nchunks + 7) / 8 * 8);
   const unsigned blocks = unsigned(slots * geo.groups);
-  gf_gemm_fp4_kernel<MG><<<blocks, 256, geo.lds, stream>>>(in, out, static_cast<const i32x4*>(bitmat), k, m,
-                                                           geo.ksteps, geo.groups, col0, nchunks, slots);
+  gf_gemm_fp4_kernel<MG, UNI><<<blocks, 256, geo.lds, stream>>>(in, out, static_cast<const i32x4*>(bitmat), k, m,
+                                                                geo.ksteps, geo.groups, col0, nchunks, slots,
+                                                                in_stride);
   return hipGetLastError();
+}
+
+template <int MG>
+hipError_t launch_fp4_any(const Fp4Geometry& geo, cptr<uint64_t> in, cptr<uint64_t> out, const void* bitmat, int k,
+                          int m, int64_t col0, int64_t nchunks, int64_t in_stride, hipStream_t stream) {
+  return in_stride ? launch_fp4<MG, true>(geo, in, out, bitmat, k, m, col0, nchunks, in_stride, stream)
+                   : launch_fp4<MG, false>(geo, in, out, bitmat, k, m, col0, nchunks, 0, stream);
 }
 
 }  // namespace
@@ -272,7 +361,7 @@ hipError_t launch_fp4_bitmat(const uint8_t* coeff, int m, int k, void* bitmat, i
 }
 
 hipError_t launch_gf_gemm_fp4(const void* bitmat, const void* desc, int k, int m, int64_t col0, int64_t ncols,
-                              int mg_cap, hipStream_t stream) {
+                              int mg_cap, int64_t in_stride, hipStream_t stream) {
   if (k <= 0 || m <= 0 || ncols < 0 || (col0 & 1) || mg_cap < 1) return hipErrorInvalidValue;
   const int m_pad = pad_m(m);
   const DescLayout l = desc_layout(k, m_pad);
@@ -284,10 +373,10 @@ hipError_t launch_gf_gemm_fp4(const void* bitmat, const void* desc, int k, int m
     const auto out = (cptr<uint64_t>)(b + l.out_off);
     hipError_t e;
     switch (geo.mg) {
-      case 8: e = launch_fp4<8>(geo, in, out, bitmat, k, m, col0, nchunks, stream); break;
-      case 4: e = launch_fp4<4>(geo, in, out, bitmat, k, m, col0, nchunks, stream); break;
-      case 2: e = launch_fp4<2>(geo, in, out, bitmat, k, m, col0, nchunks, stream); break;
-      default: e = launch_fp4<1>(geo, in, out, bitmat, k, m, col0, nchunks, stream); break;
+      case 8: e = launch_fp4_any<8>(geo, in, out, bitmat, k, m, col0, nchunks, in_stride, stream); break;
+      case 4: e = launch_fp4_any<4>(geo, in, out, bitmat, k, m, col0, nchunks, in_stride, stream); break;
+      case 2: e = launch_fp4_any<2>(geo, in, out, bitmat, k, m, col0, nchunks, in_stride, stream); break;
+      default: e = launch_fp4_any<1>(geo, in, out, bitmat, k, m, col0, nchunks, in_stride, stream); break;
     }
     if (e != hipSuccess) return e;
   }

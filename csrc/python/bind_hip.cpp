@@ -107,9 +107,9 @@ PYBIND11_MODULE(_hip, m) {
           "fp4_bitmat");
   });
   m.def("gemm_fp4", [](uint64_t bitmat, uint64_t desc, int k, int mm, int64_t col0, int64_t ncols, int mg_cap,
-                       uint64_t stream) {
+                       int64_t in_stride, uint64_t stream) {
     check(launch_gf_gemm_fp4(reinterpret_cast<const void*>(bitmat), reinterpret_cast<const void*>(desc), k, mm, col0,
-                             ncols, mg_cap, as_stream(stream)),
+                             ncols, mg_cap, in_stride, as_stream(stream)),
           "gf_gemm_fp4");
   });
   m.def("gen_matrix", [](uint64_t e, int k, int p, int kind, uint64_t stream) {

@@ -222,6 +222,11 @@ class GemmPlan:
             h = hip()
             st = torch.cuda.current_stream(self.device).cuda_stream
             self.mfma_mg = mfma_mg
+            # equally spaced input rows (one allocation): the FP4 kernel computes DMA addresses
+            ptrs = [ptr(r) for r in self.inputs]
+            stride = ptrs[1] - ptrs[0] if self.k > 1 else 1
+            uniform = stride != 0 and all(p - ptrs[0] == j * stride for j, p in enumerate(ptrs))
+            self.in_stride = stride if uniform else 0
             if engine == "mfma":
                 self.bitmat = torch.empty(h.fp4_bitmat_bytes(self.k, self.m, mfma_mg), dtype=torch.uint8,
                                           device=self.device)
@@ -277,7 +282,7 @@ class GemmPlan:
             h.gemm_batched(int(self.desc.data_ptr()), self.k, self.m_pad, self.batch, col0, ncols, self.bytewise, s)
         elif self.engine == "mfma":
             h.gemm_fp4(int(self.bitmat.data_ptr()), int(self.desc.data_ptr()), self.k, self.m, col0, ncols,
-                       self.mfma_mg, s)
+                       self.mfma_mg, self.in_stride, s)
         elif self.engine == "mfma_i8":
             h.gemm_mfma(int(self.bitmat.data_ptr()), int(self.desc.data_ptr()), self.k, self.m, col0, ncols, s)
         elif self.bytewise:

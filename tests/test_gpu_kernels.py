@@ -195,7 +195,7 @@ def test_gen_matrix_device(kind):
         assert np.array_equal(got, GF256.encoding_matrix(kind, k, p)), (k, p)
 
 
-@pytest.mark.parametrize("engine", ["mfma", "mfma_mg2", "mfma_i8"])
+@pytest.mark.parametrize("engine", ["mfma", "mfma_mg2", "mfma_scattered", "mfma_i8"])
 @pytest.mark.parametrize("k,m,ncols", [(128, 32, 512 * 40 + 123), (16, 4, 512 * 9), (10, 4, 512 * 7 + 5),
                                         (4, 2, 100), (32, 20, 512 * 3 + 64), (255, 1, 1024), (8, 9, 4096 + 512),
                                         (256, 40, 2048 + 2), (200, 56, 768)])
@@ -206,7 +206,21 @@ def test_mfma_bitmatrix_gemm_matches_oracle(k, m, ncols, engine):
     host, dev = _rand_rows(k, ncols, k * m)
     out = alloc_rows(m, ncols, "cuda", fill=0x5A)
     kw = dict(engine="mfma", mfma_mg=2) if engine == "mfma_mg2" else dict(engine=engine)
-    GemmPlan(dev, out, coeff, **kw).run()
+    inputs = dev
+    if engine == "mfma_scattered":
+        # separately allocated rows in a shuffled order: the FP4 kernel's pointer-table path
+        kw = dict(engine="mfma")
+        order = np.random.default_rng(k).permutation(k)
+        rows = [None] * k
+        for j in order:
+            rows[j] = dev[j].clone()
+        inputs = rows
+    plan = GemmPlan(inputs, out, coeff, **kw)
+    if engine == "mfma_scattered" and k > 2:
+        assert plan.in_stride == 0
+    elif engine in ("mfma", "mfma_mg2"):
+        assert plan.in_stride != 0
+    plan.run()
     torch.cuda.synchronize()
     assert np.array_equal(out.cpu().numpy(), GF256.gemm(coeff, host))
 
