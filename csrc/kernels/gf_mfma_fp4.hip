@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "gfrs/desc.h"
 #include "gfrs/kernels.h"
@@ -34,7 +35,7 @@ using gptr = __attribute__((address_space(1))) T*;
 
 constexpr int kNTW = 2;        // N-tiles per wave (64 columns)
 constexpr int kBlockCols = 256;  // 4 waves x 64 columns
-constexpr int kMaxLdsKiB = 139;  // A slice; + 2.25 KiB row/out pointers + 4 waves x 9 x 512 B rings <= 160 KiB
+constexpr int kMaxLdsKiB = 137;  // A slice; + 2.25 KiB row/out pointers + 4 waves x 5 x 1 KiB rings <= 160 KiB
 
 __constant__ Tables d_tab = make_tables();
 
@@ -90,20 +91,21 @@ __device__ __forceinline__ uint32_t pack_byte(const f32x16& acc, int u) {
   return v;
 }
 
-// Per-wave input ring in LDS filled by LDS-DMA (global_load_lds, 4 B per lane): the loads of the
-// next kRing-1 K-steps stay in flight across chunk boundaries without costing VGPRs, which the
-// one-wave-per-SIMD MFMA loop needs to cover HBM latency. Each wave owns its ring (no barriers):
-// a slot = 8 input rows x the wave's 64 columns = 512 B, written by two 256-B DMA instructions
-// (lane l -> row 4*half + l/16, columns 4*(l%16)..+3).
+// Per-wave input ring in LDS filled by LDS-DMA: a slot holds one K-PAIR (16 input rows x the
+// wave's 64 columns = 1 KiB, row r at byte 64r) and is written by ONE `global_load_lds_dwordx4`
+// (lane l -> row l/4, columns 16*(l%4)..+15): an LDS-DMA costs ~60-180 issue cycles whatever its
+// width (MI355X_MICROARCH.md, constants table), so the widest form and two K-steps per DMA. The
+// loads of the next kRing-1 pairs (kRing = 6..32, as deep as the LDS left over by the A slice
+// allows) stay in flight across chunk boundaries without costing VGPRs. Each wave owns its ring
+// (no barriers); a slot's bytes are ordered for the wave's own ds_reads by its counted vmcnt.
 //
 // The K loop is software-pipelined by hand: while the 2 x MG MFMAs of step g run, the ring bytes
-// and the MG A fragments of step g+1 (and, for scattered input rows, the row pointers of the next
+// and the MG A fragments of step g+1 (and, for scattered input rows, the row pointer of the next
 // DMA) are already being read from LDS. Those reads are inline asm, retired by one explicit
 // `s_waitcnt lgkmcnt(0)` at the end of the step, and "tied" to their destination registers by
 // empty asm statements so no use can be scheduled above the wait; the compiler's own alias
 // tracking would otherwise put a vmcnt(0)/lgkmcnt(0) in front of every read.
-constexpr int kRing = 8;
-constexpr int kSlotBytes = 512;
+constexpr int kSlotBytes = 1024;
 using lds_u8 = __attribute__((address_space(3))) uint8_t;
 
 __device__ __forceinline__ void lgkm_wait() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
@@ -114,12 +116,13 @@ __device__ __forceinline__ void tie(T& v) {
 
 // UNI: input row j lives at in[0] + j * in_stride (rows from one allocation, the usual case), so
 // DMA addresses are pure VALU arithmetic; otherwise the row pointers come from an LDS table.
-template <int MG, bool UNI>
+// ksteps is even (the bitmat pads a zero K-step when ceil(k/8) is odd).
+template <int MG, bool UNI, int kRing>
 __global__ __launch_bounds__(256, 1) void gf_gemm_fp4_kernel(cptr<uint64_t> in, cptr<uint64_t> out,
                                                              const i32x4* __restrict__ bitmat, int k, int m,
                                                              int ksteps, int groups, int64_t col0, int64_t nchunks,
                                                              int64_t chunk_slots, int64_t in_stride) {
-  // LDS: A [ksteps][MG][64] x 16 B | row pointers [256] | out pointers [32] | rings [4][kRing+1][512]
+  // LDS: A [ksteps][MG][64] x 16 B | row pointers [256] | out pointers [32] | rings [4][kRing+1][1 KiB]
   extern __shared__ __attribute__((aligned(16))) i32x4 afrag[];
   const int bid = blockIdx.x;
   const int xcd = bid & 7;
@@ -145,63 +148,55 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4_kernel(cptr<uint64_t> in, 
   const uint32_t lds0 = uint32_t(reinterpret_cast<uintptr_t>((lds_u8*)afrag));
   const uint32_t a_addr = lds0 + 16u * lane;
   const uint32_t rowptr_addr = lds0 + uint32_t(a_bytes);
+  const uint32_t optr_addr = rowptr_addr + 2048u + 16u * h;  // outptr[2h + u] of M-tile 0
   lds_u8* ring =
       (lds_u8*)(reinterpret_cast<uint8_t*>(afrag) + a_bytes + 2304 + size_t(wave) * (kRing + 1) * kSlotBytes);
   const uint32_t ring_addr = uint32_t(reinterpret_cast<uintptr_t>(ring)) + uint32_t(256 * h + 2 * c);
   const int scale = 0x7F7F7F7F;  // E8M0 1.0 for every block of 32
   const int my_chunks = int((nchunks - slot0 + chunk_slots - 1) / chunk_slots);
-  const int total = my_chunks * ksteps;
-  if (total <= 0) return;
+  const int kpairs = ksteps >> 1;
+  if (my_chunks <= 0) return;
   const uint64_t in0 = UNI ? in[0] : 0;
+  const int drow = lane >> 2;                // this lane's row within a DMA'd pair
+  const int dcol = wave * 64 + 16 * (lane & 3);
 
-  // DMA cursor (odometer over my chunks x K-steps) and, off the UNI path, the row pointers of the
-  // cursor's step. Past the last step the cursor keeps issuing "dummy" DMAs (a valid source, the
+  // DMA cursor (odometer over my chunks x K-pairs) and, off the UNI path, the row pointer of the
+  // cursor's pair. Past the last pair the cursor keeps issuing "dummy" DMAs (a valid source, the
   // wave's spare slot kRing as destination) so the number in flight — and with it every counted
   // vmcnt below — stays the same and the K loop has no branches.
-  int d_chunk = 0, d_s = 0, d_slot = 0;
-  uint64_t pn0 = 0, pn1 = 0;
-  auto row_of = [&](int half) {
-    const int r = 8 * d_s + 4 * half + (lane >> 4);
+  int d_chunk = 0, d_p = 0, d_slot = 0;
+  uint64_t pn = 0;
+  auto row_of = [&]() __attribute__((always_inline)) {
+    const int r = 16 * d_p + drow;
     return r < k ? r : k - 1;  // rows >= k are masked to zero at expansion time
   };
-  auto ptr_sync = [&]() {
-    pn0 = rowptr[row_of(0)];
-    pn1 = rowptr[row_of(1)];
+  auto ptr_sync = [&]() __attribute__((always_inline)) { pn = rowptr[row_of()]; };
+  auto ptr_async = [&]() __attribute__((always_inline)) {
+    asm volatile("ds_read_b64 %0, %1" : "=&v"(pn) : "v"(rowptr_addr + 8u * row_of()) : "memory");
   };
-  auto ptr_async = [&]() {
-    asm volatile("ds_read_b64 %0, %2\n\tds_read_b64 %1, %3"
-                 : "=&v"(pn0), "=&v"(pn1)
-                 : "v"(rowptr_addr + 8u * row_of(0)), "v"(rowptr_addr + 8u * row_of(1))
-                 : "memory");
-  };
-  auto dma_issue = [&]() {
+  auto dma_issue = [&]() __attribute__((always_inline)) {
     const bool live = d_chunk < my_chunks;
-    const int64_t col = col0 + (slot0 + int64_t(live ? d_chunk : 0) * chunk_slots) * kBlockCols + wave * 64 +
-                        4 * (lane & 15);
-    uint64_t s0, s1;
-    if constexpr (UNI) {
-      s0 = in0 + uint64_t(int64_t(row_of(0)) * in_stride + col);
-      s1 = in0 + uint64_t(int64_t(row_of(1)) * in_stride + col);
-    } else {
-      s0 = pn0 + uint64_t(col);
-      s1 = pn1 + uint64_t(col);
-    }
-    lds_u8* dst = ring + (live ? d_slot : kRing) * kSlotBytes;
-    __builtin_amdgcn_global_load_lds((gptr<const void>)s0, dst, 4, 0, 0);
-    __builtin_amdgcn_global_load_lds((gptr<const void>)s1, dst + 256, 4, 0, 0);
-    const bool wrap = d_s + 1 == ksteps;
-    d_s = live ? (wrap ? 0 : d_s + 1) : d_s;
+    const int64_t col = col0 + (slot0 + int64_t(live ? d_chunk : 0) * chunk_slots) * kBlockCols + dcol;
+    uint64_t sa;
+    if constexpr (UNI)
+      sa = in0 + uint64_t(int64_t(row_of()) * in_stride + col);
+    else
+      sa = pn + uint64_t(col);
+    __builtin_amdgcn_global_load_lds((gptr<const void>)sa, ring + (live ? d_slot : kRing) * kSlotBytes, 16, 0, 0);
+    const bool wrap = d_p + 1 == kpairs;
+    d_p = live ? (wrap ? 0 : d_p + 1) : d_p;
     d_chunk += (live && wrap) ? 1 : 0;
     d_slot = live ? (d_slot + 1 == kRing ? 0 : d_slot + 1) : d_slot;
   };
-  auto read_x = [&](uint32_t (&x)[4], int slot) {
+  // the 4 bytes (rows 4h+i of the step, this lane's column pair) of K-step half `hs` of a slot
+  auto read_x = [&](uint32_t (&x)[4], int slot, int hs) {
     asm volatile(
         "ds_read_u16 %0, %4\n\t"
         "ds_read_u16 %1, %4 offset:64\n\t"
         "ds_read_u16 %2, %4 offset:128\n\t"
         "ds_read_u16 %3, %4 offset:192"
         : "=&v"(x[0]), "=&v"(x[1]), "=&v"(x[2]), "=&v"(x[3])
-        : "v"(ring_addr + uint32_t(slot * kSlotBytes))
+        : "v"(ring_addr + uint32_t(slot * kSlotBytes + 512 * hs))
         : "memory");
   };
   auto read_a = [&](i32x4 (&a)[MG], int s) {
@@ -211,101 +206,152 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4_kernel(cptr<uint64_t> in, 
       asm volatile("ds_read_b128 %0, %1 offset:%2" : "=&v"(a[mt]) : "v"(base), "n"(mt * 1024) : "memory");
   };
 
-  // prologue: kRing-1 steps in flight, step 0's operands in registers
+  // B operand of K-step t from its 4 raw ring words (rows 8t+4h+i; rows >= k masked to zero)
+  auto expand = [&](i32x4 (&bo)[kNTW], const uint32_t (&x)[4], int t) __attribute__((always_inline)) {
+    const int rbase = 8 * t + 4 * h;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t xi = rbase + i < k ? x[i] : 0u;
+#pragma unroll
+      for (int tt = 0; tt < kNTW; ++tt) bo[tt][i] = expand_fp4((xi >> (8 * tt)) & 0xFFu);
+    }
+  };
+
+  // prologue: kRing-1 pairs in flight; B(0), A(0) and the raw bytes of step 1 in registers
   for (int i = 0; i < kRing - 1; ++i) {
     if (!UNI) ptr_sync();
     dma_issue();
   }
   if (!UNI) ptr_sync();
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (kRing - 2)) : "memory");
-  uint32_t xc[4], xn[4];
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kRing - 2) : "memory");
+  uint32_t x0[4], x1[4], x2[4];  // raw bytes: x1 = step s+1 (in registers), x2 = step s+2 (in flight)
   i32x4 ac[MG], an[MG];
-  read_x(xc, 0);
+  i32x4 bc[kNTW], bn[kNTW];
+  read_x(x0, 0, 0);
+  read_x(x1, 0, 1);
   read_a(ac, 0);
   lgkm_wait();
 #pragma unroll
-  for (int i = 0; i < 4; ++i) tie(xc[i]);
+  for (int i = 0; i < 4; ++i) {
+    tie(x0[i]);
+    tie(x1[i]);
+  }
 #pragma unroll
   for (int mt = 0; mt < MG; ++mt) tie(ac[mt]);
+  expand(bc, x0, 0);
 
-  int r_slot = 0;
-  for (int ci = 0; ci < my_chunks; ++ci) {
-    f32x16 acc[MG][kNTW];
+  f32x16 acc[MG][kNTW];
+  // one K-step s: its 2 x MG MFMAs with the B operand of step s+1 expanded in between (VALU
+  // co-issues under the MFMA pipe; the first step of a chunk starts from the inline constant 0 —
+  // no zeroing pass, no zero copy kept live); then retire the LDS reads of A(s+1) and the raw
+  // bytes of step s+2, issued by the caller before the step
+  auto step = [&](int s, auto first_tag) __attribute__((always_inline)) {
+    constexpr bool kFirst = decltype(first_tag)::value;
+    __builtin_amdgcn_sched_barrier(0);
+    const int s1 = s + 1 == ksteps ? 0 : s + 1;
 #pragma unroll
-    for (int mt = 0; mt < MG; ++mt)
-#pragma unroll
-      for (int t = 0; t < kNTW; ++t) acc[mt][t] = (f32x16)(0.0f);
-    for (int s = 0; s < ksteps; ++s) {
-      // (1) the DMA kRing-1 steps ahead; (2) step s+1's ring bytes and A fragments (its slot is
-      // the oldest of the kRing-1 pairs in flight); (3) this step's expansion + MFMAs; (4) retire
-      // the reads of (2). Reads past the last step hit valid LDS and are discarded.
-      dma_issue();
-      if (!UNI) ptr_async();
-      const int slot1 = r_slot + 1 == kRing ? 0 : r_slot + 1;
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (kRing - 2)) : "memory");
-      read_x(xn, slot1);
-      read_a(an, s + 1 == ksteps ? 0 : s + 1);
-      __builtin_amdgcn_sched_barrier(0);
-
-      const int rbase = 8 * s + 4 * h;
-      const uint32_t xs[4] = {rbase < k ? xc[0] : 0u, rbase + 1 < k ? xc[1] : 0u, rbase + 2 < k ? xc[2] : 0u,
-                              rbase + 3 < k ? xc[3] : 0u};
-      i32x8 b[kNTW];
+    for (int mt = 0; mt < MG; ++mt) {
+      const i32x8 a = {ac[mt][0], ac[mt][1], ac[mt][2], ac[mt][3], 0, 0, 0, 0};
 #pragma unroll
       for (int t = 0; t < kNTW; ++t) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) b[t][i] = expand_fp4((xs[i] >> (8 * t)) & 0xFFu);
-#pragma unroll
-        for (int i = 4; i < 8; ++i) b[t][i] = 0;
-      }
-#pragma unroll
-      for (int mt = 0; mt < MG; ++mt) {
-        const i32x8 a = {ac[mt][0], ac[mt][1], ac[mt][2], ac[mt][3], 0, 0, 0, 0};
-#pragma unroll
-        for (int t = 0; t < kNTW; ++t)
-          acc[mt][t] =
-              __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b[t], acc[mt][t], 4, 4, 0, scale, 0, scale);
-      }
-      r_slot = slot1;
-      __builtin_amdgcn_sched_barrier(0);
-      lgkm_wait();
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        tie(xn[i]);
-        xc[i] = xn[i];
-      }
-#pragma unroll
-      for (int mt = 0; mt < MG; ++mt) {
-        tie(an[mt]);
-        ac[mt] = an[mt];
-      }
-      if (!UNI) {
-        tie(pn0);
-        tie(pn1);
+        const i32x8 bb = {bc[t][0], bc[t][1], bc[t][2], bc[t][3], 0, 0, 0, 0};
+        acc[mt][t] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, bb, kFirst ? (f32x16)(0.0f) : acc[mt][t], 4,
+                                                                      4, 0, scale, 0, scale);
       }
     }
+    expand(bn, x1, s1);
+    // interleave: one MFMA, then a quarter of the next step's expansion (~6 VALU per byte)
+#pragma unroll
+    for (int i = 0; i < 2 * MG; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+      __builtin_amdgcn_sched_group_barrier(0x002, (8 * 8 + 2 * MG - 1) / (2 * MG), 0);  // VALU
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    lgkm_wait();
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      tie(x2[i]);
+      x1[i] = x2[i];
+    }
+#pragma unroll
+    for (int mt = 0; mt < MG; ++mt) {
+      tie(an[mt]);
+      ac[mt] = an[mt];
+    }
+#pragma unroll
+    for (int t = 0; t < kNTW; ++t) bc[t] = bn[t];
+  };
+  using first_t = std::integral_constant<bool, true>;
+  using rest_t = std::integral_constant<bool, false>;
+
+  int r_slot = 0;
+  // the chunk's output: 2 bytes per lane per (M-tile, byte row), one tile at a time, straight
+  // from the last MFMAs' accumulators (inside the last K-pair, so acc never leaves the AGPRs
+  // through a loop-exit copy)
+  auto store_chunk = [&](int ci) __attribute__((always_inline)) {
     const int64_t colw = col0 + (slot0 + int64_t(ci) * chunk_slots) * kBlockCols + wave * 64 + 2 * c;
 #pragma unroll
     for (int mt = 0; mt < MG; ++mt)
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
-        const uint64_t op = outptr[4 * mt + 2 * h + u];
-        if (!op) continue;
-        const uint32_t w = pack_byte(acc[mt][0], u) | (pack_byte(acc[mt][1], u) << 8);
-        *(gptr<uint16_t>)(op + colw) = uint16_t(w);
+        // output row pointer by a 32-bit LDS address + immediate (a C++ read of outptr[] would be
+        // hoisted out of the chunk loop as 2*MG live 64-bit flat addresses)
+        uint64_t op;
+        asm volatile("ds_read_b64 %0, %1 offset:%2\n\ts_waitcnt lgkmcnt(0)"
+                     : "=v"(op)
+                     : "v"(optr_addr), "n"(8 * (4 * mt + u))
+                     : "memory");
+        if (op) {
+          const uint32_t w = pack_byte(acc[mt][0], u) | (pack_byte(acc[mt][1], u) << 8);
+          *(gptr<uint16_t>)(op + colw) = uint16_t(w);
+        }
+        __builtin_amdgcn_sched_barrier(0);
       }
+  };
+
+  // one K-pair (slot r_slot): (1) the DMA kRing-1 pairs ahead; (2) wait for the next slot (the
+  // oldest pair in flight) and, under the even step's MFMAs, read the next pair's even-step bytes
+  // and A(s0+1); (3) under the odd step's MFMAs, the next pair's odd-step bytes and A(s0+2).
+  // Reads past the last step hit valid LDS and are discarded.
+  auto pair = [&](int sp, int ci, auto first_tag, auto last_tag) __attribute__((always_inline)) {
+    dma_issue();
+    if (!UNI) ptr_async();
+    const int s0 = 2 * sp;
+    const int slot1 = r_slot + 1 == kRing ? 0 : r_slot + 1;
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kRing - 2) : "memory");
+    read_x(x2, slot1, 0);
+    read_a(an, s0 + 1);
+    step(s0, first_tag);
+    if (!UNI) tie(pn);
+    read_x(x2, slot1, 1);
+    read_a(an, s0 + 2 == ksteps ? 0 : s0 + 2);
+    step(s0 + 1, rest_t{});
+    r_slot = slot1;
+    if constexpr (decltype(last_tag)::value) store_chunk(ci);
+  };
+
+  for (int ci = 0; ci < my_chunks; ++ci) {
+    if (kpairs == 1) {
+      pair(0, ci, first_t{}, first_t{});
+    } else {
+      pair(0, ci, first_t{}, rest_t{});
+      for (int sp = 1; sp < kpairs - 1; ++sp) pair(sp, ci, rest_t{}, rest_t{});
+      pair(kpairs - 1, ci, rest_t{}, first_t{});
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA (dummy or not) outlives the wave
 }
 
 struct Fp4Geometry {
   int ksteps, mtiles, mg, groups;
-  size_t lds;
+  size_t fixed;  // LDS bytes before the rings: A slice + row/out pointers
 };
+
+constexpr size_t ring_lds(int r) { return 4 * size_t(r + 1) * kSlotBytes; }
 
 Fp4Geometry geometry(int k, int m, int mg_cap) {
   Fp4Geometry g{};
-  g.ksteps = (k + 7) / 8;
+  g.ksteps = ((k + 15) / 16) * 2;  // K-pairs: one 1-KiB DMA slot = 2 K-steps
   g.mtiles = (m + 3) / 4;
   // MG = M-tiles per block: next power of two >= mtiles (<= 8, the accumulator budget), halved
   // until the block's A slice fits the LDS
@@ -313,35 +359,91 @@ Fp4Geometry geometry(int k, int m, int mg_cap) {
   while (g.mg < g.mtiles && g.mg < mg_cap) g.mg <<= 1;
   while (g.mg > 1 && g.mg * g.ksteps > kMaxLdsKiB) g.mg >>= 1;
   g.groups = (g.mtiles + g.mg - 1) / g.mg;
-  g.lds = size_t(g.mg) * g.ksteps * 64 * 16 + 2304 + 4 * (kRing + 1) * kSlotBytes;
+  g.fixed = size_t(g.mg) * g.ksteps * 64 * 16 + 2304;
   return g;
 }
 
-template <int MG, bool UNI>
-hipError_t launch_fp4(const Fp4Geometry& geo, cptr<uint64_t> in, cptr<uint64_t> out, const void* bitmat, int k, int m,
-                      int64_t col0, int64_t nchunks, int64_t in_stride, hipStream_t stream) {
-  static bool attr_set = false;
-  if (!attr_set) {
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gf_gemm_fp4_kernel<MG, UNI>),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    if (e != hipSuccess) return e;
-    attr_set = true;
+int cu_count() {
+  static int n = 0;
+  if (!n) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
   }
-  // one block per CU in total (the LDS holds the whole A slice), chunk slots a multiple of 8
-  int64_t slots = std::max<int64_t>(8, (256 / geo.groups) / 8 * 8);
+  return n;
+}
+
+template <int MG, bool UNI, int R>
+const void* fp4_fn() {
+  static const void* fn = [] {
+    const void* f = reinterpret_cast<const void*>(&gf_gemm_fp4_kernel<MG, UNI, R>);
+    (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    return f;
+  }();
+  return fn;
+}
+
+// co-resident blocks per CU of the ring-depth-R kernel (LDS and VGPR bound); 0 if it does not fit
+template <int MG, bool UNI, int R>
+int fp4_occupancy(size_t fixed) {
+  const size_t lds = fixed + ring_lds(R);
+  if (lds > 160 * 1024) return 0;
+  int occ = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fp4_fn<MG, UNI, R>(), 256, lds) != hipSuccess) return 0;
+  return occ;
+}
+
+template <int MG, bool UNI, int R>
+hipError_t launch_fp4(const Fp4Geometry& geo, int occ, cptr<uint64_t> in, cptr<uint64_t> out, const void* bitmat,
+                      int k, int m, int64_t col0, int64_t nchunks, int64_t in_stride, hipStream_t stream) {
+  // a persistent grid: as many blocks as are co-resident, chunk slots a multiple of 8 so each
+  // slot stays on one XCD
+  const size_t lds = geo.fixed + ring_lds(R);
+  (void)fp4_fn<MG, UNI, R>();
+  int64_t slots = std::max<int64_t>(8, (int64_t(cu_count()) * occ / geo.groups) / 8 * 8);
   slots = std::min<int64_t>(slots, (nchunks + 7) / 8 * 8);
   const unsigned blocks = unsigned(slots * geo.groups);
-  gf_gemm_fp4_kernel<MG, UNI><<<blocks, 256, geo.lds, stream>>>(in, out, static_cast<const i32x4*>(bitmat), k, m,
-                                                                geo.ksteps, geo.groups, col0, nchunks, slots,
-                                                                in_stride);
+  gf_gemm_fp4_kernel<MG, UNI, R><<<blocks, 256, lds, stream>>>(in, out, static_cast<const i32x4*>(bitmat), k,
+                                                                   m, geo.ksteps, geo.groups, col0, nchunks, slots,
+                                                                   in_stride);
   return hipGetLastError();
+}
+
+template <int MG, bool UNI>
+hipError_t launch_fp4_ring(const Fp4Geometry& geo, cptr<uint64_t> in, cptr<uint64_t> out, const void* bitmat, int k,
+                           int m, int64_t col0, int64_t nchunks, int64_t in_stride, hipStream_t stream) {
+  // ring depth: the most waves per SIMD first (up to 4: they hide each other's LDS/MFMA
+  // latencies), then the deepest ring (bytes in flight) at that occupancy. Cached per A size.
+  static int choice[161][2];  // [fixed KiB] -> {ring, occupancy}
+  int (&ch)[2] = choice[std::min<size_t>(geo.fixed / 1024, 160)];
+  if (!ch[0]) {
+    const int rings[6] = {32, 16, 12, 8, 6, 4};
+    const int occs[6] = {fp4_occupancy<MG, UNI, 32>(geo.fixed), fp4_occupancy<MG, UNI, 16>(geo.fixed),
+                         fp4_occupancy<MG, UNI, 12>(geo.fixed), fp4_occupancy<MG, UNI, 8>(geo.fixed),
+                         fp4_occupancy<MG, UNI, 6>(geo.fixed), fp4_occupancy<MG, UNI, 4>(geo.fixed)};
+    int best = -1;
+    for (int i = 0; i < 6; ++i)
+      if (occs[i] > 0 && (best < 0 || std::min(occs[i], 4) > std::min(occs[best], 4))) best = i;
+    if (best < 0) return hipErrorInvalidConfiguration;
+    ch[0] = rings[best];
+    ch[1] = occs[best];
+  }
+  const int occ = ch[1];
+  switch (ch[0]) {
+    case 32: return launch_fp4<MG, UNI, 32>(geo, occ, in, out, bitmat, k, m, col0, nchunks, in_stride, stream);
+    case 16: return launch_fp4<MG, UNI, 16>(geo, occ, in, out, bitmat, k, m, col0, nchunks, in_stride, stream);
+    case 12: return launch_fp4<MG, UNI, 12>(geo, occ, in, out, bitmat, k, m, col0, nchunks, in_stride, stream);
+    case 8: return launch_fp4<MG, UNI, 8>(geo, occ, in, out, bitmat, k, m, col0, nchunks, in_stride, stream);
+    case 6: return launch_fp4<MG, UNI, 6>(geo, occ, in, out, bitmat, k, m, col0, nchunks, in_stride, stream);
+    default: return launch_fp4<MG, UNI, 4>(geo, occ, in, out, bitmat, k, m, col0, nchunks, in_stride, stream);
+  }
 }
 
 template <int MG>
 hipError_t launch_fp4_any(const Fp4Geometry& geo, cptr<uint64_t> in, cptr<uint64_t> out, const void* bitmat, int k,
                           int m, int64_t col0, int64_t nchunks, int64_t in_stride, hipStream_t stream) {
-  return in_stride ? launch_fp4<MG, true>(geo, in, out, bitmat, k, m, col0, nchunks, in_stride, stream)
-                   : launch_fp4<MG, false>(geo, in, out, bitmat, k, m, col0, nchunks, 0, stream);
+  return in_stride ? launch_fp4_ring<MG, true>(geo, in, out, bitmat, k, m, col0, nchunks, in_stride, stream)
+                   : launch_fp4_ring<MG, false>(geo, in, out, bitmat, k, m, col0, nchunks, 0, stream);
 }
 
 }  // namespace

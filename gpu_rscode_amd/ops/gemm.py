@@ -155,7 +155,7 @@ class GemmPlan:
     """
 
     def __init__(self, inputs, outputs, coeff=None, *, maps=None, copies=None, device_tables: bool = False,
-                 engine: str = "valu", mfma_mg: int = 8):
+                 engine: str = "auto", mfma_mg: int = 8):
         bi, bo = _batched_rows(inputs), _batched_rows(outputs)
         if (bi is None) != (bo is None):
             raise ValueError("inputs and outputs must both be batched ([B, rows, C]) or both not")
@@ -164,7 +164,7 @@ class GemmPlan:
             # batched: B stripes of identical shape, one launch (grid.y = stripe)
             if len(bi) != len(bo) or len(bi) < 1 or len(bi) > 65535:
                 raise ValueError("batched plan needs 1..65535 stripes in inputs and outputs")
-            if copies is not None or engine != "valu":
+            if copies is not None or engine not in ("valu", "auto"):
                 raise ValueError("batched plans support neither fused copies nor engine='mfma'")
             self.batch = len(bi)
             self._stripes_in, self._stripes_out = bi, bo
@@ -208,6 +208,9 @@ class GemmPlan:
                           tables, self.batch)
         self.desc = torch.from_numpy(host).to(self.device)
         self.layout = desc_layout(self.k, self.m_pad, self.batch)
+        if engine == "auto":
+            engine = _auto_engine(self.k, self.m, coeff is not None and maps is None, self.copies is None,
+                                  self.bytewise, self.batch)
         self.engine = engine
         self.bitmat = None
         if engine in ("mfma", "mfma_i8"):
@@ -217,27 +220,33 @@ class GemmPlan:
             # chunk runs on the v_perm tables that the descriptor also carries.
             if coeff is None or self.copies is not None or self.bytewise:
                 raise ValueError(f"engine={engine!r} needs coeff=, no copies and aligned rows")
-            c = torch.from_numpy(np.ascontiguousarray(np.asarray(coeff, dtype=np.uint8).reshape(self.m, self.k)))
-            c = c.to(self.device)
-            h = hip()
-            st = torch.cuda.current_stream(self.device).cuda_stream
             self.mfma_mg = mfma_mg
             # equally spaced input rows (one allocation): the FP4 kernel computes DMA addresses
             ptrs = [ptr(r) for r in self.inputs]
             stride = ptrs[1] - ptrs[0] if self.k > 1 else 1
             uniform = stride != 0 and all(p - ptrs[0] == j * stride for j, p in enumerate(ptrs))
             self.in_stride = stride if uniform else 0
-            if engine == "mfma":
-                self.bitmat = torch.empty(h.fp4_bitmat_bytes(self.k, self.m, mfma_mg), dtype=torch.uint8,
-                                          device=self.device)
-                h.fp4_bitmat(c.data_ptr(), self.m, self.k, self.bitmat.data_ptr(), mfma_mg, st)
-            else:
-                self.bitmat = torch.empty(h.mfma_bitmat_bytes(self.k, self.m), dtype=torch.uint8, device=self.device)
-                h.mfma_bitmat(c.data_ptr(), self.m, self.k, self.bitmat.data_ptr(), st)
-            self._coeff_dev = c
+            self._build_bitmat(coeff)
         elif engine != "valu":
             raise ValueError(f"unknown engine {engine!r}")
         self._mark_ready()
+
+    def _build_bitmat(self, coeff) -> None:
+        """Bit-matrix operand of the matrix-core engines, built on device from the m x k coefficients."""
+        c = torch.from_numpy(np.ascontiguousarray(np.asarray(coeff, dtype=np.uint8).reshape(self.m, self.k)))
+        c = c.to(self.device)
+        h = hip()
+        st = torch.cuda.current_stream(self.device).cuda_stream
+        if self.engine == "mfma":
+            if self.bitmat is None:
+                self.bitmat = torch.empty(h.fp4_bitmat_bytes(self.k, self.m, self.mfma_mg), dtype=torch.uint8,
+                                          device=self.device)
+            h.fp4_bitmat(c.data_ptr(), self.m, self.k, self.bitmat.data_ptr(), self.mfma_mg, st)
+        else:
+            if self.bitmat is None:
+                self.bitmat = torch.empty(h.mfma_bitmat_bytes(self.k, self.m), dtype=torch.uint8, device=self.device)
+            h.mfma_bitmat(c.data_ptr(), self.m, self.k, self.bitmat.data_ptr(), st)
+        self._coeff_dev = c
 
     def _mark_ready(self) -> None:
         # descriptor writes are ordered on the current stream; launches on other streams wait on this
@@ -252,6 +261,8 @@ class GemmPlan:
         src = torch.from_numpy(np.frombuffer(t.tobytes(), dtype=np.uint8).copy())
         with torch.cuda.stream(stream) if stream is not None else _null():
             self.desc[self.layout.tab_off :].copy_(src, non_blocking=False)
+            if self.bitmat is not None:
+                self._build_bitmat(coeff)
             self._mark_ready()
 
     def table_view(self) -> torch.Tensor:
@@ -262,8 +273,9 @@ class GemmPlan:
             max_blocks: int = 0, vec: int | None = None, pf: int = 2, nt: bool = False) -> None:
         """Launch asynchronously on ``stream`` (default: the current stream).
 
-        ``vec``/``pf``/``nt`` select an explicit kernel variant (ablation; ``vec=0`` = byte kernel);
-        by default the tuned configuration for the output tile is used.
+        ``vec``/``pf``/``nt`` select an explicit v_perm kernel variant (ablation; ``vec=0`` = byte
+        kernel; this bypasses a matrix-core engine); by default the plan's engine runs with the tuned
+        configuration for the output tile.
         """
         ncols = self.ncols - col0 if ncols is None else ncols
         if col0 < 0 or ncols < 0 or col0 + ncols > self.ncols:
@@ -280,10 +292,10 @@ class GemmPlan:
             if vec is not None:
                 raise ValueError("kernel variants are not selectable on batched plans")
             h.gemm_batched(int(self.desc.data_ptr()), self.k, self.m_pad, self.batch, col0, ncols, self.bytewise, s)
-        elif self.engine == "mfma":
+        elif self.engine == "mfma" and vec is None and col0 % 2 == 0:
             h.gemm_fp4(int(self.bitmat.data_ptr()), int(self.desc.data_ptr()), self.k, self.m, col0, ncols,
                        self.mfma_mg, self.in_stride, s)
-        elif self.engine == "mfma_i8":
+        elif self.engine == "mfma_i8" and vec is None and col0 % 2 == 0:
             h.gemm_mfma(int(self.bitmat.data_ptr()), int(self.desc.data_ptr()), self.k, self.m, col0, ncols, s)
         elif self.bytewise:
             h.gemm(int(self.desc.data_ptr()), self.k, self.m_pad, col0, ncols, True, max_blocks, s)
@@ -291,6 +303,18 @@ class GemmPlan:
             h.gemm(int(self.desc.data_ptr()), self.k, self.m_pad, col0, ncols, False, max_blocks, s)
         else:
             h.gemm_variant(int(self.desc.data_ptr()), self.k, self.m_pad, col0, ncols, vec, pf, nt, max_blocks, s)
+
+
+# wide stripes go to the FP4 matrix-core kernel: measured on MI355X (profiles/r01_kbench5) it wins
+# from k*m ~ 2k coefficients (k=128, p=32: 1.10 ms vs 1.45 ms per GiB); narrow codes stay on the
+# v_perm kernel, which is at the HBM roofline there (k=10, p=4: 0.27 ms vs 0.87 ms).
+_MFMA_MIN_K, _MFMA_MIN_M = 64, 16
+
+
+def _auto_engine(k: int, m: int, have_coeff: bool, no_copies: bool, bytewise: bool, batch: int) -> str:
+    if have_coeff and no_copies and not bytewise and batch == 1 and k >= _MFMA_MIN_K and m >= _MFMA_MIN_M:
+        return "mfma"
+    return "valu"
 
 
 class _null:

@@ -45,7 +45,7 @@ def make_case(name, k, m, ncopy, total_bytes):
         dst = alloc_rows(ncopy, C, "cuda")
         copies = [dst[j] if j < ncopy else None for j in range(k)]
     coeff = np.random.default_rng(k + m).integers(1, 256, size=(m, k), dtype=np.uint8)
-    plan = GemmPlan(data, out, coeff, copies=copies)
+    plan = GemmPlan(data, out, coeff, copies=copies, engine="valu")
     mplan = None
     if not ncopy:
         mplan = {"mfma": GemmPlan(data, out, coeff, engine="mfma"),

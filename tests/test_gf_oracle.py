@@ -133,3 +133,13 @@ def test_gf16_nibble_maps_are_linear():
         assert gf.is_linear(gf.byte_map_gf16_nibbles(c))
         rec = gf.perm_record(gf.byte_map_gf16_nibbles(c))
         assert np.array_equal(gf.perm_apply(rec, np.arange(256)), gf.byte_map_gf16_nibbles(c))
+
+
+def test_auto_engine_policy():
+    from gpu_rscode_amd.ops.gemm import _auto_engine
+    assert _auto_engine(128, 32, True, True, False, 1) == "mfma"
+    assert _auto_engine(10, 4, True, True, False, 1) == "valu"  # narrow: v_perm is at the HBM roofline
+    assert _auto_engine(128, 32, True, False, False, 1) == "valu"  # fused survivor copies
+    assert _auto_engine(128, 32, False, True, False, 1) == "valu"  # device-written tables / GF(16) maps
+    assert _auto_engine(128, 32, True, True, True, 1) == "valu"  # unaligned rows
+    assert _auto_engine(128, 32, True, True, False, 4) == "valu"  # batched stripes

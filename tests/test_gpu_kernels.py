@@ -244,3 +244,23 @@ def test_batched_gemm_matches_oracle(batch, k, m, ncols):
     got = out.cpu().numpy()
     for b in range(batch):
         assert np.array_equal(got[b], GF256.gemm(coeff, host[b])), b
+
+
+def test_auto_engine_wide_stripe_uses_matrix_cores_and_matches():
+    _native_loaded()
+    k, m, ncols = 96, 24, 256 * 37 + 77
+    rng = np.random.default_rng(5)
+    coeff = rng.integers(0, 256, size=(m, k), dtype=np.uint8)
+    host, dev = _rand_rows(k, ncols, 3)
+    out = alloc_rows(m, ncols, "cuda", fill=0x11)
+    plan = GemmPlan(dev, out, coeff)
+    assert plan.engine == "mfma"
+    plan.run()
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), GF256.gemm(coeff, host))
+    coeff2 = rng.integers(0, 256, size=(m, k), dtype=np.uint8)
+    plan.set_coeff(coeff2)  # rebuilds the bit-matrix too
+    plan.run()
+    plan.run(col0=1, ncols=ncols - 1)  # odd column start: v_perm fallback on the same plan
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), GF256.gemm(coeff2, host))
