@@ -25,6 +25,10 @@ struct Args {
   long long slice = 16ll << 20;
   bool cpu_meta = false;
   bool quiet = false;
+  long long window = -1;  // --window: stream in column windows of this many bytes (0 = auto)
+  bool resume = true;     // --no-resume: ignore a <target>.PROGRESS checkpoint
+  bool sync = true;       // --no-sync: skip fdatasync before each checkpoint
+  bool streaming() const { return window >= 0; }
 };
 
 inline void usage(const char* prog, bool gpu) {
@@ -46,6 +50,10 @@ inline void usage(const char* prog, bool gpu) {
   std::printf("  --matrix vandermonde|cauchy|sys_vandermonde  coding matrix (default: reference Vandermonde)\n");
   std::printf("  --cpu-meta              write the 2-line CPU-format METADATA\n");
   std::printf("  --make-conf             write conf-<n>-<k>-<file> keeping the last k chunks (unit-test.sh)\n");
+  std::printf("  --window BYTES          bounded-memory streaming codec: column windows of BYTES per chunk\n");
+  std::printf("                          (0 = auto), checkpointed to <target>.PROGRESS and resumable\n");
+  std::printf("  --no-resume             with --window: start over even if a checkpoint matches\n");
+  std::printf("  --no-sync               with --window: do not fdatasync before each checkpoint\n");
   std::printf("  -q                      quiet\n");
   if (gpu) {
     std::printf("  --gpus N                number of GPUs (default: all visible)\n");
@@ -67,6 +75,16 @@ inline int to_int(const char* s, const char* what, int lo) {
   return int(v);
 }
 
+inline long long to_ll(const char* s, const char* what, long long lo) {
+  char* end = nullptr;
+  const long long v = std::strtoll(s ? s : "", &end, 10);
+  if (!s || *end || v < lo) {
+    std::fprintf(stderr, "invalid %s: %s\n", what, s ? s : "(null)");
+    std::exit(2);
+  }
+  return v;
+}
+
 inline Args parse(int argc, char** argv, bool gpu) {
   Args a;
   static const option longopts[] = {{"matrix", required_argument, nullptr, 1},
@@ -76,6 +94,9 @@ inline Args parse(int argc, char** argv, bool gpu) {
                                     {"mul", required_argument, nullptr, 5},
                                     {"threads", required_argument, nullptr, 6},
                                     {"make-conf", no_argument, nullptr, 7},
+                                    {"window", required_argument, nullptr, 8},
+                                    {"no-resume", no_argument, nullptr, 9},
+                                    {"no-sync", no_argument, nullptr, 10},
                                     {"help", no_argument, nullptr, 'h'},
                                     {nullptr, 0, nullptr, 0}};
   int c;
@@ -98,6 +119,9 @@ inline Args parse(int argc, char** argv, bool gpu) {
       case 5: a.mul = optarg; break;
       case 6: a.threads = to_int(optarg, "thread count", 0); break;
       case 7: a.op = Args::kMakeConf; break;
+      case 8: a.window = to_ll(optarg, "window bytes", 0); break;
+      case 9: a.resume = false; break;
+      case 10: a.sync = false; break;
       case 'h': default: usage(argv[0], gpu); std::exit(c == 'h' ? 0 : 2);
     }
   }

@@ -7,6 +7,7 @@
 #include "gfrs/codec_file.h"
 #include "gfrs/cpu_codec.h"
 #include "gfrs/format.h"
+#include "gfrs/stream_codec.h"
 
 int main(int argc, char** argv) {
   using namespace gfrs;
@@ -20,15 +21,27 @@ int main(int argc, char** argv) {
       write_conf(name, worst_case_conf(a.in_file, a.n, a.k));
       if (!a.quiet) std::printf("wrote %s\n", name.c_str());
     } else if (a.op == gfrs_cli::Args::kEncode) {
-      const FileReport r = encode_file(a.in_file, a.k, a.n - a.k, parse_matrix_kind(a.matrix), gemm,
-                                       default_host_alloc(), a.cpu_meta);
+      StreamOptions so;
+      so.window = a.window;
+      so.resume = a.resume;
+      so.durable = a.sync;
+      const FileReport r = a.streaming() ? encode_file_stream(a.in_file, a.k, a.n - a.k, parse_matrix_kind(a.matrix),
+                                                              gemm, default_host_alloc(), so, a.cpu_meta)
+                                         : encode_file(a.in_file, a.k, a.n - a.k, parse_matrix_kind(a.matrix), gemm,
+                                                       default_host_alloc(), a.cpu_meta);
       if (!a.quiet) {
         std::printf("Total CPU encoding time: %fms\n", r.ms_matrix + r.ms_compute);
         std::printf("CPU encoding bandwidth: %.3f MB/s (strategy %s, %d thread(s))\n",
                     r.total_size / 1048576.0 / ((r.ms_matrix + r.ms_compute) / 1e3), cpu_mul_name(strat), a.threads);
       }
     } else {
-      const FileReport r = decode_file(a.in_file, a.conf, a.out, gemm, default_host_alloc());
+      StreamOptions so;
+      so.window = a.window;
+      so.resume = a.resume;
+      so.durable = a.sync;
+      const FileReport r = a.streaming()
+                               ? decode_file_stream(a.in_file, a.conf, a.out, gemm, default_host_alloc(), so)
+                               : decode_file(a.in_file, a.conf, a.out, gemm, default_host_alloc());
       if (!a.quiet) {
         std::printf("Total CPU decoding time: %fms\n", r.ms_matrix + r.ms_compute);
         std::printf("CPU decoding bandwidth: %.3f MB/s (%d erased native chunk(s))\n",

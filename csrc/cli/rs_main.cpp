@@ -13,6 +13,7 @@
 #include "gfrs/codec_file.h"
 #include "gfrs/format.h"
 #include "gfrs/pipeline.h"
+#include "gfrs/stream_codec.h"
 
 namespace {
 
@@ -66,9 +67,23 @@ int main(int argc, char** argv) {
         std::printf("Total GPU %s time using multiple devices: %fms\n", verb, wall);
       }
     };
-    const FileReport r = enc ? encode_file(a.in_file, a.k, a.n - a.k, parse_matrix_kind(a.matrix), gemm,
-                                           pinned_alloc(), a.cpu_meta)
-                             : decode_file(a.in_file, a.conf, a.out, gemm, pinned_alloc());
+    FileReport r;
+    if (a.streaming()) {
+      StreamOptions so;
+      so.window = a.window;
+      so.resume = a.resume;
+      so.durable = a.sync;
+      const StreamReport sr = enc ? encode_file_stream(a.in_file, a.k, a.n - a.k, parse_matrix_kind(a.matrix),
+                                                       gemm, pinned_alloc(), so, a.cpu_meta)
+                                  : decode_file_stream(a.in_file, a.conf, a.out, gemm, pinned_alloc(), so);
+      if (!a.quiet)
+        std::printf("Streamed %d window(s) of %lld bytes per chunk (resumed at %lld)\n", sr.windows,
+                    static_cast<long long>(sr.window), static_cast<long long>(sr.resumed_from));
+      r = sr;
+    } else {
+      r = enc ? encode_file(a.in_file, a.k, a.n - a.k, parse_matrix_kind(a.matrix), gemm, pinned_alloc(), a.cpu_meta)
+              : decode_file(a.in_file, a.conf, a.out, gemm, pinned_alloc());
+    }
     if (!a.quiet)
       std::printf("GPU %s bandwidth: %.3f MB/s (%lld bytes, k=%d, p=%d, %d GPU(s), %d stream(s))\n", verb,
                   r.total_size / 1048576.0 / (r.ms_compute / 1e3), static_cast<long long>(r.total_size), r.k, r.p,

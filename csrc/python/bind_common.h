@@ -9,6 +9,7 @@
 #include <vector>
 
 #include "gfrs/codec_file.h"
+#include "gfrs/stream_codec.h"
 #include "gfrs/host_desc.h"
 #include "gfrs/matrix.h"
 
@@ -44,6 +45,24 @@ inline py::dict report(const gfrs::FileReport& r) {
   d["ms_compute"] = r.ms_compute;
   d["ms_write"] = r.ms_write;
   return d;
+}
+
+inline py::dict stream_report(const gfrs::StreamReport& r) {
+  py::dict d = report(r);
+  d["window"] = r.window;
+  d["windows"] = r.windows;
+  d["resumed_from"] = r.resumed_from;
+  d["complete"] = r.complete;
+  return d;
+}
+
+inline gfrs::StreamOptions stream_options(int64_t window, bool resume, bool durable, int stop_after) {
+  gfrs::StreamOptions o;
+  o.window = window;
+  o.resume = resume;
+  o.durable = durable;
+  o.stop_after = stop_after;
+  return o;
 }
 
 // Bindings common to both modules: descriptors and matrix algebra.

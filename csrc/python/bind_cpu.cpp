@@ -67,6 +67,39 @@ PYBIND11_MODULE(_cpu, m) {
       },
       py::arg("file"), py::arg("conf"), py::arg("out") = "", py::arg("strategy") = "row", py::arg("threads") = 1);
 
+  m.def(
+      "encode_file_stream",
+      [gemm_fn](const std::string& file, int k, int p, const std::string& matrix, bool cpu_meta,
+                const std::string& strategy, int threads, int64_t window, bool resume, bool durable, int stop_after) {
+        const GemmFn g = gemm_fn(strategy, threads);
+        StreamReport r;
+        {
+          py::gil_scoped_release nogil;
+          r = encode_file_stream(file, k, p, parse_matrix_kind(matrix), g, default_host_alloc(),
+                                 stream_options(window, resume, durable, stop_after), cpu_meta);
+        }
+        return stream_report(r);
+      },
+      py::arg("file"), py::arg("k"), py::arg("p"), py::arg("matrix") = "vandermonde", py::arg("cpu_meta") = false,
+      py::arg("strategy") = "row", py::arg("threads") = 1, py::arg("window") = 0, py::arg("resume") = true,
+      py::arg("durable") = true, py::arg("stop_after") = -1);
+  m.def(
+      "decode_file_stream",
+      [gemm_fn](const std::string& file, const std::string& conf, const std::string& out, const std::string& strategy,
+                int threads, int64_t window, bool resume, bool durable, int stop_after) {
+        const GemmFn g = gemm_fn(strategy, threads);
+        StreamReport r;
+        {
+          py::gil_scoped_release nogil;
+          r = decode_file_stream(file, conf, out, g, default_host_alloc(),
+                                 stream_options(window, resume, durable, stop_after));
+        }
+        return stream_report(r);
+      },
+      py::arg("file"), py::arg("conf"), py::arg("out") = "", py::arg("strategy") = "row", py::arg("threads") = 1,
+      py::arg("window") = 0, py::arg("resume") = true, py::arg("durable") = true, py::arg("stop_after") = -1);
+  m.def("progress_path", &progress_path);
+
   m.def("chunk_path", &chunk_path);
   m.def("chunk_index", &chunk_index);
   m.def("metadata_path", &metadata_path);

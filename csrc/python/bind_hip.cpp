@@ -198,4 +198,38 @@ PYBIND11_MODULE(_hip, m) {
       },
       py::arg("file"), py::arg("conf"), py::arg("out") = "", py::arg("devices") = std::vector<int>{0},
       py::arg("streams") = 2, py::arg("slice") = 16 << 20, py::arg("max_blocks") = 0);
+  m.def(
+      "encode_file_stream",
+      [gpu_gemm](const std::string& file, int k, int p, const std::string& matrix, bool cpu_meta,
+                 const std::vector<int>& devices, int streams, int64_t slice, int max_blocks, int64_t window,
+                 bool resume, bool durable, int stop_after) {
+        const GemmFn g = gpu_gemm(devices, streams, slice, max_blocks);
+        StreamReport r;
+        {
+          py::gil_scoped_release nogil;
+          r = encode_file_stream(file, k, p, parse_matrix_kind(matrix), g, pinned_alloc(),
+                                 stream_options(window, resume, durable, stop_after), cpu_meta);
+        }
+        return stream_report(r);
+      },
+      py::arg("file"), py::arg("k"), py::arg("p"), py::arg("matrix") = "vandermonde", py::arg("cpu_meta") = false,
+      py::arg("devices") = std::vector<int>{0}, py::arg("streams") = 2, py::arg("slice") = 16 << 20,
+      py::arg("max_blocks") = 0, py::arg("window") = 0, py::arg("resume") = true, py::arg("durable") = true,
+      py::arg("stop_after") = -1);
+  m.def(
+      "decode_file_stream",
+      [gpu_gemm](const std::string& file, const std::string& conf, const std::string& out,
+                 const std::vector<int>& devices, int streams, int64_t slice, int max_blocks, int64_t window,
+                 bool resume, bool durable, int stop_after) {
+        const GemmFn g = gpu_gemm(devices, streams, slice, max_blocks);
+        StreamReport r;
+        {
+          py::gil_scoped_release nogil;
+          r = decode_file_stream(file, conf, out, g, pinned_alloc(), stream_options(window, resume, durable, stop_after));
+        }
+        return stream_report(r);
+      },
+      py::arg("file"), py::arg("conf"), py::arg("out") = "", py::arg("devices") = std::vector<int>{0},
+      py::arg("streams") = 2, py::arg("slice") = 16 << 20, py::arg("max_blocks") = 0, py::arg("window") = 0,
+      py::arg("resume") = true, py::arg("durable") = true, py::arg("stop_after") = -1);
 }

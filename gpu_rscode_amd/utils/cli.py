@@ -41,6 +41,11 @@ def _parser() -> argparse.ArgumentParser:
     ap.add_argument("--mul", default="row", help="CPU multiply strategy")
     ap.add_argument("--dist", action="store_true", help="torch.distributed multi-GPU mode (torchrun)")
     ap.add_argument("--gather", choices=["rccl", "none"], default="rccl")
+    ap.add_argument("--window", type=int, default=None,
+                    help="bounded-memory streaming codec: column windows of this many bytes per chunk "
+                         "(0 = auto), checkpointed to <target>.PROGRESS and resumable")
+    ap.add_argument("--no-resume", action="store_true", help="with --window: ignore a matching checkpoint")
+    ap.add_argument("--no-sync", action="store_true", help="with --window: no fdatasync before checkpoints")
     ap.add_argument("-q", action="store_true", dest="quiet")
     return ap
 
@@ -65,13 +70,18 @@ def main(argv=None) -> int:
             print("encode needs -k K -n N -e FILE with 1 <= K <= N", file=sys.stderr)
             return 2
         t = time.perf_counter()
+        st = {} if a.window is None else dict(window=a.window, resume=not a.no_resume, durable=not a.no_sync)
         if backend == "gpu":
             ndev = hip().device_count()
             devs = list(range(a.gpus or ndev))
-            r = hip().encode_file(a.encode_file, a.k, a.n - a.k, a.matrix, a.cpu_meta, devs, a.streams, a.slice,
-                                  a.grid)
+            fn = hip().encode_file_stream if st else hip().encode_file
+            r = fn(a.encode_file, a.k, a.n - a.k, a.matrix, a.cpu_meta, devs, a.streams, a.slice, a.grid, **st)
         else:
-            r = cpu().encode_file(a.encode_file, a.k, a.n - a.k, a.matrix, a.cpu_meta, a.mul, a.threads)
+            fn = cpu().encode_file_stream if st else cpu().encode_file
+            r = fn(a.encode_file, a.k, a.n - a.k, a.matrix, a.cpu_meta, a.mul, a.threads, **st)
+        if st:
+            _say(a, f"Streamed {r['windows']} window(s) of {r['window']} bytes per chunk "
+                    f"(resumed at {r['resumed_from']})")
         _say(a, f"Total {backend.upper()} encoding time: {r['ms_compute']:.3f}ms "
                 f"({r['total_size'] / 1048576 / max(r['ms_compute'], 1e-9) * 1e3:.1f} MB/s; "
                 f"wall {1e3 * (time.perf_counter() - t):.1f}ms incl. file I/O)")
@@ -79,11 +89,14 @@ def main(argv=None) -> int:
     if not a.in_file or not a.conf:
         print("decode needs -d -i FILE -c CONF", file=sys.stderr)
         return 2
+    st = {} if a.window is None else dict(window=a.window, resume=not a.no_resume, durable=not a.no_sync)
     if backend == "gpu":
         ndev = hip().device_count()
-        r = hip().decode_file(a.in_file, a.conf, a.out, list(range(a.gpus or ndev)), a.streams, a.slice, a.grid)
+        fn = hip().decode_file_stream if st else hip().decode_file
+        r = fn(a.in_file, a.conf, a.out, list(range(a.gpus or ndev)), a.streams, a.slice, a.grid, **st)
     else:
-        r = cpu().decode_file(a.in_file, a.conf, a.out, a.mul, a.threads)
+        fn = cpu().decode_file_stream if st else cpu().decode_file
+        r = fn(a.in_file, a.conf, a.out, a.mul, a.threads, **st)
     _say(a, f"Total {backend.upper()} decoding time: {r['ms_compute']:.3f}ms ({r['erased']} erased native chunk(s))")
     return 0
 

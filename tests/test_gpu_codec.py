@@ -174,3 +174,28 @@ def test_batched_encode_decode_small_objects():
     out = rs.decode_batch(stripe[:, rows].contiguous(), rows)
     torch.cuda.synchronize()
     assert torch.equal(out, data)
+
+
+def test_stream_file_codec_gpu_equals_cpu_and_resumes(tmp_path):
+    payload = os.urandom(5_000_011)
+    g, c = tmp_path / "g", tmp_path / "c"
+    g.mkdir()
+    c.mkdir()
+    (g / "f.bin").write_bytes(payload)
+    (c / "f.bin").write_bytes(payload)
+    r1 = hip().encode_file_stream(str(g / "f.bin"), 10, 4, "vandermonde", False, [0], 2, 1 << 18, 0,
+                                  window=1 << 16, durable=False, stop_after=3)
+    assert not r1["complete"]
+    r2 = hip().encode_file_stream(str(g / "f.bin"), 10, 4, "vandermonde", False, [0], 2, 1 << 18, 0,
+                                  window=1 << 17, durable=False)
+    assert r2["complete"] and r2["resumed_from"] == 3 << 16
+    cpu().encode_file(str(c / "f.bin"), 10, 4)
+    for i in range(14):
+        assert (g / f"_{i}_f.bin").read_bytes() == (c / f"_{i}_f.bin").read_bytes(), i
+    assert (g / "f.bin.METADATA").read_bytes() == (c / "f.bin.METADATA").read_bytes()
+    conf = g / "conf"
+    ff.write_conf(str(conf), [ff.chunk_path(str(g / "f.bin"), r) for r in (4, 5, 6, 7, 8, 9, 10, 11, 12, 13)])
+    r = hip().decode_file_stream(str(g / "f.bin"), str(conf), str(g / "out"), [0], 2, 1 << 18, 0,
+                                 window=1 << 16, durable=False)
+    assert r["complete"] and r["erased"] == 4
+    assert (g / "out").read_bytes() == payload

@@ -49,3 +49,13 @@ def test_asan_wide_and_malformed(exe, tmp_path):
     assert _run(exe, ["-d", "-i", "w.bin", "-c", "c", "-o", "o"], tmp_path).returncode == 1
     (tmp_path / "bad").write_text("_999_w.bin\n")
     assert _run(exe, ["-d", "-i", "w.bin", "-c", "bad"], tmp_path).returncode == 1
+
+
+def test_asan_streaming_codec(exe, tmp_path):
+    payload = os.urandom(250_007)
+    (tmp_path / "s.bin").write_bytes(payload)
+    assert _run(exe, ["-k", "10", "-n", "14", "-e", "s.bin", "--window", "4099", "--no-sync"], tmp_path).returncode == 0
+    ff.write_conf(str(tmp_path / "c"), [f"_{r}_s.bin" for r in (0, 2, 3, 5, 6, 8, 10, 11, 12, 13)])
+    assert _run(exe, ["-d", "-i", "s.bin", "-c", "c", "-o", "o", "--window", "1000", "--no-sync"],
+                tmp_path).returncode == 0
+    assert (tmp_path / "o").read_bytes() == payload
