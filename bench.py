@@ -39,6 +39,7 @@ from gpu_rscode_amd import gf  # noqa: E402
 from gpu_rscode_amd.models import alloc_rows  # noqa: E402
 from gpu_rscode_amd.ops import GemmPlan, fill_random_, invert_into_plan  # noqa: E402
 from gpu_rscode_amd._native import cpu, hip  # noqa: E402
+from gpu_rscode_amd.utils.timing import trace_range  # noqa: E402
 
 BASELINE_GBPS = 2 * 1_096_310_784 / 1.72168 / 1e9  # 1.2736 GB/s
 
@@ -62,7 +63,8 @@ def parse():
     ap.add_argument("--preset", default="k10n14", choices=sorted(PRESETS),
                     help="BASELINE.json config: k10n14 (headline, #2/#3), k16n20_8g (#4 per GPU), k128n160 (#5), "
                          "k4n6 (the reference's published shape)")
-    ap.add_argument("--engine", default="valu", choices=["valu", "mfma"], help="encode GEMM engine")
+    ap.add_argument("--engine", default="auto", choices=["auto", "valu", "mfma"],
+                    help="encode GEMM engine (auto: FP4 matrix cores for wide stripes, v_perm otherwise)")
     ap.add_argument("--graph", action="store_true", help="replay each step from a captured hipGraph")
     a = ap.parse_args()
     pr = PRESETS[a.preset]
@@ -162,9 +164,10 @@ def main():
             flat = parity.as_strided((p * parity.stride(0),), (1,))
             dist.gather(flat, gathered if rank == 0 else None, dst=0)
 
-    for i in range(max(a.warmup, len(dec) if a.graph else 0)):
-        step(i)
-    torch.cuda.synchronize()
+    with trace_range("bench/warmup"):
+        for i in range(max(a.warmup, len(dec) if a.graph else 0)):
+            step(i)
+        torch.cuda.synchronize()
     if a.graph:
         # one captured graph per decode pattern: encode GEMM, side-stream inversion, decode GEMM
         graphs = []
@@ -177,6 +180,8 @@ def main():
         run_step = lambda i: graphs[i % len(graphs)].replay()  # noqa: E731
     else:
         run_step = step
+    timed = trace_range("bench/timed")  # roctx range opened before the bracket, closed after it
+    timed.__enter__()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -188,6 +193,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    timed.__exit__(None, None, None)
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -227,7 +233,7 @@ def main():
                    "global_batch": f"{a.bytes} B per GPU ({k} x {C} B chunks)", "seq_len": C,
                    "parallelism": f"dp{world} (stripe-sharded, RCCL broadcast of E)",
                    "erasures": a.erasures, "decode_invert": "device Gauss-Jordan per step",
-                   "gather": bool(a.gather), "engine": a.engine, "graph": bool(a.graph), "preset": a.preset},
+                   "gather": bool(a.gather), "engine": enc.engine, "graph": bool(a.graph), "preset": a.preset},
         "verified": ok,
         "baseline": {"gbps": round(BASELINE_GBPS, 4), "source": "k=8,n=11 1.1 GB Tesla C2050 (nearest published)"},
     }

@@ -10,6 +10,7 @@
 #include <stdexcept>
 
 #include "gfrs/format.h"
+#include "gfrs/trace.h"
 
 namespace gfrs {
 namespace {
@@ -52,7 +53,10 @@ FileReport encode_file(const std::string& file, int k, int p, MatrixKind kind, c
   r.chunk_size = std::max<int64_t>(1, chunk_size(r.total_size, k));
   const int64_t C = r.chunk_size;
   Buf data(alloc, size_t(k) * C), parity(alloc, size_t(std::max(p, 1)) * C);
-  read_into(file, 0, data.p, int64_t(k) * C);  // one contiguous read; tail zero-padded
+  {
+    TraceRange tr("encode/read");
+    read_into(file, 0, data.p, int64_t(k) * C);
+  }  // one contiguous read; tail zero-padded
   r.ms_read = ms_since(t);
 
   t = Clock::now();
@@ -61,6 +65,7 @@ FileReport encode_file(const std::string& file, int k, int p, MatrixKind kind, c
 
   t = Clock::now();
   if (p) {
+    TraceRange tr("encode/gemm");
     std::vector<const uint8_t*> in(k);
     std::vector<uint8_t*> out(p);
     for (int j = 0; j < k; ++j) in[j] = data.p + size_t(j) * C;
@@ -70,6 +75,7 @@ FileReport encode_file(const std::string& file, int k, int p, MatrixKind kind, c
   r.ms_compute = ms_since(t);
 
   t = Clock::now();
+  TraceRange tr_write("encode/crc+write");
   std::vector<uint32_t> crc;
   if (!cpu_meta) {  // per-chunk CRC-32 (METADATA extension): lets decode reject corrupted chunks
     crc.resize(size_t(k + p));
@@ -197,6 +203,7 @@ FileReport decode_file(const std::string& file, const std::string& conf, const s
   t = Clock::now();
   Buf rec(alloc, size_t(std::max<size_t>(erased.size(), 1)) * C);
   if (!erased.empty()) {
+    TraceRange tr("decode/gemm");
     Mat coeff(erased.size() * size_t(k));
     for (size_t e = 0; e < erased.size(); ++e)
       std::memcpy(&coeff[e * k], &dm[size_t(erased[e]) * k], size_t(k));

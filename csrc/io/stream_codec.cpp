@@ -18,6 +18,7 @@
 #include <thread>
 
 #include "gfrs/format.h"
+#include "gfrs/trace.h"
 
 namespace gfrs {
 namespace {
@@ -135,6 +136,7 @@ void run_windows(int64_t start, int64_t C, int64_t W, int stop_after, Read read,
     int64_t off, len;
     win(w, off, len);
     const auto t = Clock::now();
+    TraceRange tr("stream/read");
     read(int(w % 3), off, len);
     return ms_since(t);
   };
@@ -146,11 +148,15 @@ void run_windows(int64_t start, int64_t C, int64_t W, int stop_after, Read read,
     int64_t off, len;
     win(w, off, len);
     const auto t = Clock::now();
-    compute(int(w % 3), off, len);
+    {
+      TraceRange tr("stream/compute");
+      compute(int(w % 3), off, len);
+    }
     rep.ms_compute += ms_since(t);
     if (wr.valid()) rep.ms_write += wr.get();  // write(w-1) + its checkpoint
     wr = std::async(std::launch::async, [&, w, off, len] {
       const auto tw = Clock::now();
+      TraceRange tr("stream/write+checkpoint");
       write(int(w % 3), off, len);
       return ms_since(tw);
     });

@@ -10,6 +10,7 @@
 
 #include "gfrs/codec_file.h"
 #include "gfrs/stream_codec.h"
+#include "gfrs/trace.h"
 #include "gfrs/host_desc.h"
 #include "gfrs/matrix.h"
 
@@ -67,6 +68,14 @@ inline gfrs::StreamOptions stream_options(int64_t window, bool resume, bool dura
 
 // Bindings common to both modules: descriptors and matrix algebra.
 inline void bind_common(py::module_& m) {
+  m.def("roctx_available", &gfrs::Roctx::available);
+  m.def("trace_mark", [](const std::string& s) { gfrs::trace_mark(s.c_str()); });
+  m.def("trace_push", [](const std::string& s) {
+    if (gfrs::Roctx::get().push) gfrs::Roctx::get().push(s.c_str());
+  });
+  m.def("trace_pop", [] {
+    if (gfrs::Roctx::get().pop) gfrs::Roctx::get().pop();
+  });
   m.def("pad_m", &gfrs::pad_m);
   m.def("tile_for", &gfrs::tile_for);
   m.def("desc_layout", [](int k, int m_pad, int batch) {

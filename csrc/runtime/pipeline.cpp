@@ -1,5 +1,6 @@
 // Host<->device streaming pipeline. See gfrs/pipeline.h for the design notes.
 #include "gfrs/pipeline.h"
+#include "gfrs/trace.h"
 
 #include <algorithm>
 #include <chrono>
@@ -70,6 +71,7 @@ hipError_t gemm_host(int device, const std::vector<const uint8_t*>& in_rows, con
   st.ms_setup = ms_since(t_all);
 
   const auto t_stream = Clock::now();
+  TraceRange tr_stream("pipeline/stream-loop");
   for (int64_t t = 0; t < nslices; ++t) {
     Lane& L = lane[t % lanes];
     const int64_t a = c0 + t * slice;
@@ -82,7 +84,10 @@ hipError_t gemm_host(int device, const std::vector<const uint8_t*>& in_rows, con
     st.bytes_h2d += int64_t(k) * w;
     st.bytes_d2h += int64_t(m) * w;
   }
-  for (auto& L : lane) GFRS_TRY(hipStreamSynchronize(L.stream));
+  {
+    TraceRange tr("pipeline/drain");
+    for (auto& L : lane) GFRS_TRY(hipStreamSynchronize(L.stream));
+  }
   st.ms_stream = ms_since(t_stream);
 
   const auto t_free = Clock::now();

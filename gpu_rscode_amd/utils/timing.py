@@ -16,6 +16,27 @@ from contextlib import contextmanager
 import torch
 
 
+@contextmanager
+def trace_range(name: str):
+    """A roctx range (rocprofv3 --marker-trace) around host code; a no-op without the roctx library.
+
+    Uses the native module's dlopen'ed roctx (csrc/include/gfrs/trace.h), the same ranges the C++
+    pipeline and the streaming codec emit, so Python and native stages share one timeline.
+    """
+    try:
+        from .._native import cpu
+        c = cpu()
+    except Exception:  # native module not built: tracing is optional
+        c = None
+    if c is not None:
+        c.trace_push(name)
+    try:
+        yield
+    finally:
+        if c is not None:
+            c.trace_pop()
+
+
 class CudaTimer:
     """Elapsed device time of work enqueued on ``stream`` between start() and stop()."""
 

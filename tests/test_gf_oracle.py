@@ -143,3 +143,12 @@ def test_auto_engine_policy():
     assert _auto_engine(128, 32, False, True, False, 1) == "valu"  # device-written tables / GF(16) maps
     assert _auto_engine(128, 32, True, True, True, 1) == "valu"  # unaligned rows
     assert _auto_engine(128, 32, True, True, False, 4) == "valu"  # batched stripes
+
+
+def test_trace_ranges_are_safe_without_profiler():
+    from gpu_rscode_amd._native import cpu
+    from gpu_rscode_amd.utils.timing import trace_range
+    assert isinstance(cpu().roctx_available(), bool)
+    with trace_range("test/outer"):
+        with trace_range("test/inner"):
+            cpu().trace_mark("test/mark")
