@@ -10,6 +10,8 @@
 //     previous slice's kernel runs; buffers are reused round-robin in stream order;
 //   * host rows are used in place (no H2H staging copies, src/encode.cu:389-398,410-429); pinned
 //     rows give true async DMA;
+//   * streams, slice buffers and descriptors persist per device across calls (PipelineOptions::
+//     persistent), so per-window calls of the streaming file codec pay no allocation;
 //   * 64-bit column ranges (the reference is int-limited to < 2 GiB, src/encode.cu:303-322).
 #pragma once
 
@@ -27,6 +29,7 @@ struct PipelineOptions {
   int64_t slice_bytes = 16 << 20;  // column width per slice (rounded to 256)
   int max_blocks = 0;              // -p (grid cap), 0 = uncapped
   bool bytewise = false;           // force the byte kernel (debug/ablation)
+  bool persistent = true;          // keep streams/buffers/descriptor per device for the next call
 };
 
 struct PipelineStats {
@@ -41,6 +44,9 @@ struct PipelineStats {
 // out_rows[i][c] = XOR_j coeff[i][j] * in_rows[j][c] for c in [c0, c1) on `device`.
 hipError_t gemm_host(int device, const std::vector<const uint8_t*>& in_rows, const std::vector<uint8_t*>& out_rows,
                      const Mat& coeff, int64_t c0, int64_t c1, const PipelineOptions& opt, PipelineStats* stats);
+
+// Frees every persistent per-device workspace (streams, slice buffers, descriptors).
+hipError_t release_workspaces();
 
 // Column-sharded data parallelism over `devices` (one host thread each). Shard boundaries are
 // 4 KiB aligned; stats[d] receives device d's numbers. Returns the first error encountered.

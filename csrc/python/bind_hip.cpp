@@ -198,6 +198,7 @@ PYBIND11_MODULE(_hip, m) {
       },
       py::arg("file"), py::arg("conf"), py::arg("out") = "", py::arg("devices") = std::vector<int>{0},
       py::arg("streams") = 2, py::arg("slice") = 16 << 20, py::arg("max_blocks") = 0);
+  m.def("release_workspaces", [] { check(release_workspaces(), "release_workspaces"); });
   m.def(
       "encode_file_stream",
       [gpu_gemm](const std::string& file, int k, int p, const std::string& matrix, bool cpu_meta,

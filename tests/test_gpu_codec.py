@@ -126,6 +126,19 @@ def test_host_pipeline_streams(streams, slice_):
     assert np.array_equal(par.numpy(), GF256.gemm(e, host.numpy()))
 
 
+def test_host_pipeline_workspace_reuse_across_shapes_and_coefficients():
+    rng = np.random.default_rng(77)
+    h = hip()
+    for k, p, C in [(10, 4, 1_000_003), (10, 4, 1_000_003), (16, 8, 3_000_001), (4, 2, 999), (16, 8, 3_000_001)]:
+        host = torch.from_numpy(rng.integers(0, 256, size=(k, C), dtype=np.uint8)).pin_memory()
+        par = torch.zeros((p, C), dtype=torch.uint8).pin_memory()
+        e = rng.integers(0, 256, size=(p, k), dtype=np.uint8)  # a new matrix every call
+        h.gemm_host([0], [host[j].data_ptr() for j in range(k)], [par[i].data_ptr() for i in range(p)],
+                    e.tobytes(), C, 3, 1 << 18, 0, False)
+        assert np.array_equal(par.numpy(), GF256.gemm(e, host.numpy())), (k, p, C)
+    h.release_workspaces()
+
+
 def test_file_codec_gpu_and_cross_compat_with_cpu(tmp_path):
     f = tmp_path / "f.bin"
     payload = os.urandom(2_000_003)
