@@ -140,7 +140,6 @@ def main():
     if a.gather and world > 1 and rank == 0:
         gathered = [torch.empty_like(parity.as_strided((p * parity.stride(0),), (1,))) for _ in range(world)]
 
-    h = hip()
     stream = torch.cuda.Stream(dev)  # a non-default stream (hipGraph capture needs one)
     torch.cuda.set_stream(stream)
     side = torch.cuda.Stream(dev)  # decode-system inversion overlaps the encode GEMM
@@ -152,8 +151,9 @@ def main():
         inv_stream = stream if a.no_overlap else side
         if not a.no_overlap:
             side.wait_stream(stream)  # the previous step's decode has consumed this plan's tables
-        h.invert(plan.a_dev.data_ptr(), 0, k, 1, plan.status.data_ptr(), plan.desc.data_ptr(),
-                 plan.sel.data_ptr(), plan.m, plan.m_pad, inv_stream.cuda_stream)
+        # device Gauss-Jordan writing the decode tables (and, on the matrix-core engine, the
+        # bit-matrix) straight into the plan
+        invert_into_plan(plan.a_dev, plan, plan.sel, status=plan.status, stream=inv_stream)
         if not a.no_overlap:
             inv_done.record(side)
         enc.run(**kv)

@@ -59,10 +59,15 @@ size_t mfma_bitmat_bytes(int k, int m);
 // mg_cap bounds the M-tiles (4 output rows each) one block keeps in LDS/accumulators; the bitmat
 // must be built with the same cap. in_stride != 0 promises input row j == input row 0 + j*in_stride
 // (rows of one allocation): DMA addresses are then computed instead of read from a pointer table.
+// copies: also write input row j to the descriptor's copy[j] (fused survivor copy of decode).
 hipError_t launch_gf_gemm_fp4(const void* bitmat, const void* desc, int k, int m, int64_t col0,
-                              int64_t ncols, int mg_cap, int64_t in_stride, hipStream_t stream);
+                              int64_t ncols, int mg_cap, int64_t in_stride, bool copies, hipStream_t stream);
 size_t fp4_bitmat_bytes(int k, int m, int mg_cap);
 hipError_t launch_fp4_bitmat(const uint8_t* coeff, int m, int k, void* bitmat, int mg_cap, hipStream_t stream);
+// row o of the coefficient matrix = coeff + sel[o] * ld (device pointers; e.g. erased rows of a
+// device-computed inverse, so a decode needs no host round trip)
+hipError_t launch_fp4_bitmat_sel(const uint8_t* coeff, int ld, const int* sel, int m, int k, void* bitmat, int mg_cap,
+                                 hipStream_t stream);
 hipError_t launch_mfma_bitmat(const uint8_t* coeff, int m, int k, void* bitmat,
                               hipStream_t stream);
 

@@ -27,6 +27,7 @@ namespace {
 
 using i32x8 = int __attribute__((ext_vector_type(8)));
 using i32x4 = int __attribute__((ext_vector_type(4)));
+using u32x4 = unsigned __attribute__((ext_vector_type(4)));
 using f32x16 = float __attribute__((ext_vector_type(16)));
 template <typename T>
 using cptr = const __attribute__((address_space(4))) T*;
@@ -45,8 +46,10 @@ __host__ __device__ constexpr int out_bit_of(int r) { return ((r >> 3) & 1) * 4 
 
 // bitmat layout: [group][kstep][mt < MG][lane][16 bytes]; element j = nibble j of the 16 bytes (one
 // K-step's MG fragments are contiguous, so the kernel reads them with immediate LDS offsets).
-__global__ void fp4_bitmat_kernel(const uint8_t* __restrict__ coeff, int m, int k, int ksteps, int mg, int groups,
-                                  uint8_t* __restrict__ bitmat) {
+// coefficient (o, i) = coeff[row(o) * ld + i], row(o) = sel ? sel[o] : o (sel: rows of a device
+// matrix, e.g. the erased-native rows of a device-computed inverse)
+__global__ void fp4_bitmat_kernel(const uint8_t* __restrict__ coeff, int ld, const int* __restrict__ sel, int m, int k,
+                                  int ksteps, int mg, int groups, uint8_t* __restrict__ bitmat) {
   const int64_t total = int64_t(groups) * mg * ksteps * 64 * 16;
   for (int64_t idx = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; idx < total;
        idx += int64_t(gridDim.x) * blockDim.x) {
@@ -66,7 +69,8 @@ __global__ void fp4_bitmat_kernel(const uint8_t* __restrict__ coeff, int m, int 
       const int j = 2 * q + half;
       const int irow = 8 * s + 4 * h + (j >> 3);
       const int ibit = j & 7;
-      if (orow < m && irow < k && ((dmul(coeff[size_t(orow) * k + irow], uint8_t(1u << ibit)) >> obit) & 1))
+      if (orow < m && irow < k &&
+          ((dmul(coeff[size_t(sel ? sel[orow] : orow) * ld + irow], uint8_t(1u << ibit)) >> obit) & 1))
         v |= uint8_t(0x2u << (4 * half));
     }
     bitmat[idx] = v;
@@ -117,12 +121,16 @@ __device__ __forceinline__ void tie(T& v) {
 // UNI: input row j lives at in[0] + j * in_stride (rows from one allocation, the usual case), so
 // DMA addresses are pure VALU arithmetic; otherwise the row pointers come from an LDS table.
 // ksteps is even (the bitmat pads a zero K-step when ceil(k/8) is odd).
-template <int MG, bool UNI, int kRing>
+// COPY: fused survivor copy (decode): input row j is also written to copy[j] (when nonzero) from
+// the LDS ring slot the DMA already filled — one ds_read_b128 + one global_store_dwordx4 per lane
+// and K-pair, no second read of the survivors from HBM.
+template <int MG, bool UNI, bool COPY, int kRing>
 __global__ __launch_bounds__(256, 1) void gf_gemm_fp4_kernel(cptr<uint64_t> in, cptr<uint64_t> out,
-                                                             const i32x4* __restrict__ bitmat, int k, int m,
-                                                             int ksteps, int groups, int64_t col0, int64_t nchunks,
-                                                             int64_t chunk_slots, int64_t in_stride) {
-  // LDS: A [ksteps][MG][64] x 16 B | row pointers [256] | out pointers [32] | rings [4][kRing+1][1 KiB]
+                                                             cptr<uint64_t> copy, const i32x4* __restrict__ bitmat,
+                                                             int k, int m, int ksteps, int groups, int64_t col0,
+                                                             int64_t nchunks, int64_t chunk_slots, int64_t in_stride) {
+  // LDS: A [ksteps][MG][64] x 16 B | row pointers [256] | out pointers [32] | (COPY) copy pointers
+  // [256] | rings [4][kRing+1][1 KiB]
   extern __shared__ __attribute__((aligned(16))) i32x4 afrag[];
   const int bid = blockIdx.x;
   const int xcd = bid & 7;
@@ -142,6 +150,9 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4_kernel(cptr<uint64_t> in, 
     const int row = 4 * g * MG + i;
     outptr[i] = row < m ? out[row] : 0;
   }
+  uint64_t* copyptr = rowptr + 256 + 32;
+  if (COPY)
+    for (int i = threadIdx.x; i < k; i += 256) copyptr[i] = g == 0 ? copy[i] : 0;  // group 0 copies
   __syncthreads();
 
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 31, h = lane >> 5;
@@ -149,9 +160,11 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4_kernel(cptr<uint64_t> in, 
   const uint32_t a_addr = lds0 + 16u * lane;
   const uint32_t rowptr_addr = lds0 + uint32_t(a_bytes);
   const uint32_t optr_addr = rowptr_addr + 2048u + 16u * h;  // outptr[2h + u] of M-tile 0
-  lds_u8* ring =
-      (lds_u8*)(reinterpret_cast<uint8_t*>(afrag) + a_bytes + 2304 + size_t(wave) * (kRing + 1) * kSlotBytes);
+  const uint32_t cptr_addr = rowptr_addr + 2304u;
+  lds_u8* ring = (lds_u8*)(reinterpret_cast<uint8_t*>(afrag) + a_bytes + 2304 + (COPY ? 2048 : 0) +
+                           size_t(wave) * (kRing + 1) * kSlotBytes);
   const uint32_t ring_addr = uint32_t(reinterpret_cast<uintptr_t>(ring)) + uint32_t(256 * h + 2 * c);
+  const uint32_t ring_lane = uint32_t(reinterpret_cast<uintptr_t>(ring)) + 16u * lane;  // this lane's DMA'd 16 B
   const int scale = 0x7F7F7F7F;  // E8M0 1.0 for every block of 32
   const int my_chunks = int((nchunks - slot0 + chunk_slots - 1) / chunk_slots);
   const int kpairs = ksteps >> 1;
@@ -321,8 +334,26 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4_kernel(cptr<uint64_t> in, 
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kRing - 2) : "memory");
     read_x(x2, slot1, 0);
     read_a(an, s0 + 1);
-    step(s0, first_tag);
+    [[maybe_unused]] u32x4 cdat;
+    [[maybe_unused]] uint64_t cp = 0;
+    [[maybe_unused]] const int crow = 16 * sp + drow;
+    if constexpr (COPY) {  // this lane's 16 B of the current slot and its row's copy pointer
+      asm volatile("ds_read_b128 %0, %1" : "=&v"(cdat) : "v"(ring_lane + uint32_t(r_slot * kSlotBytes)) : "memory");
+      asm volatile("ds_read_b64 %0, %1"
+                   : "=&v"(cp)
+                   : "v"(cptr_addr + 8u * uint32_t(crow < k ? crow : k - 1))
+                   : "memory");
+    }
+    step(s0, first_tag);  // (its closing lgkmcnt(0) also retires the copy reads)
     if (!UNI) tie(pn);
+    if constexpr (COPY) {
+      tie(cdat);
+      tie(cp);
+      if (crow < k && cp) {
+        const int64_t col = col0 + (slot0 + int64_t(ci) * chunk_slots) * kBlockCols + dcol;
+        __builtin_nontemporal_store(cdat, (gptr<u32x4>)(cp + uint64_t(col)));
+      }
+    }
     read_x(x2, slot1, 1);
     read_a(an, s0 + 2 == ksteps ? 0 : s0 + 2);
     step(s0 + 1, rest_t{});
@@ -349,7 +380,7 @@ struct Fp4Geometry {
 
 constexpr size_t ring_lds(int r) { return 4 * size_t(r + 1) * kSlotBytes; }
 
-Fp4Geometry geometry(int k, int m, int mg_cap) {
+Fp4Geometry geometry(int k, int m, int mg_cap, bool copy = false) {
   Fp4Geometry g{};
   g.ksteps = ((k + 15) / 16) * 2;  // K-pairs: one 1-KiB DMA slot = 2 K-steps
   g.mtiles = (m + 3) / 4;
@@ -357,9 +388,10 @@ Fp4Geometry geometry(int k, int m, int mg_cap) {
   // until the block's A slice fits the LDS
   g.mg = 1;
   while (g.mg < g.mtiles && g.mg < mg_cap) g.mg <<= 1;
-  while (g.mg > 1 && g.mg * g.ksteps > kMaxLdsKiB) g.mg >>= 1;
+  // (the copy-pointer block is always budgeted, so the bitmat layout does not depend on `copy`)
+  while (g.mg > 1 && g.mg * g.ksteps > kMaxLdsKiB - 2) g.mg >>= 1;
   g.groups = (g.mtiles + g.mg - 1) / g.mg;
-  g.fixed = size_t(g.mg) * g.ksteps * 64 * 16 + 2304;
+  g.fixed = size_t(g.mg) * g.ksteps * 64 * 16 + 2304 + (copy ? 2048 : 0);
   return g;
 }
 
@@ -373,10 +405,10 @@ int cu_count() {
   return n;
 }
 
-template <int MG, bool UNI, int R>
+template <int MG, bool UNI, bool COPY, int R>
 const void* fp4_fn() {
   static const void* fn = [] {
-    const void* f = reinterpret_cast<const void*>(&gf_gemm_fp4_kernel<MG, UNI, R>);
+    const void* f = reinterpret_cast<const void*>(&gf_gemm_fp4_kernel<MG, UNI, COPY, R>);
     (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     return f;
   }();
@@ -384,43 +416,49 @@ const void* fp4_fn() {
 }
 
 // co-resident blocks per CU of the ring-depth-R kernel (LDS and VGPR bound); 0 if it does not fit
-template <int MG, bool UNI, int R>
+template <int MG, bool UNI, bool COPY, int R>
 int fp4_occupancy(size_t fixed) {
   const size_t lds = fixed + ring_lds(R);
   if (lds > 160 * 1024) return 0;
   int occ = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fp4_fn<MG, UNI, R>(), 256, lds) != hipSuccess) return 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fp4_fn<MG, UNI, COPY, R>(), 256, lds) != hipSuccess)
+    return 0;
   return occ;
 }
 
-template <int MG, bool UNI, int R>
-hipError_t launch_fp4(const Fp4Geometry& geo, int occ, cptr<uint64_t> in, cptr<uint64_t> out, const void* bitmat,
-                      int k, int m, int64_t col0, int64_t nchunks, int64_t in_stride, hipStream_t stream) {
+struct Fp4Args {
+  cptr<uint64_t> in, out, copy;
+  const void* bitmat;
+  int k, m;
+  int64_t col0, nchunks, in_stride;
+};
+
+template <int MG, bool UNI, bool COPY, int R>
+hipError_t launch_fp4(const Fp4Geometry& geo, int occ, const Fp4Args& a, hipStream_t stream) {
   // a persistent grid: as many blocks as are co-resident, chunk slots a multiple of 8 so each
   // slot stays on one XCD
   const size_t lds = geo.fixed + ring_lds(R);
-  (void)fp4_fn<MG, UNI, R>();
+  (void)fp4_fn<MG, UNI, COPY, R>();
   int64_t slots = std::max<int64_t>(8, (int64_t(cu_count()) * occ / geo.groups) / 8 * 8);
-  slots = std::min<int64_t>(slots, (nchunks + 7) / 8 * 8);
+  slots = std::min<int64_t>(slots, (a.nchunks + 7) / 8 * 8);
   const unsigned blocks = unsigned(slots * geo.groups);
-  gf_gemm_fp4_kernel<MG, UNI, R><<<blocks, 256, lds, stream>>>(in, out, static_cast<const i32x4*>(bitmat), k,
-                                                                   m, geo.ksteps, geo.groups, col0, nchunks, slots,
-                                                                   in_stride);
+  gf_gemm_fp4_kernel<MG, UNI, COPY, R><<<blocks, 256, lds, stream>>>(
+      a.in, a.out, a.copy, static_cast<const i32x4*>(a.bitmat), a.k, a.m, geo.ksteps, geo.groups, a.col0, a.nchunks,
+      slots, a.in_stride);
   return hipGetLastError();
 }
 
-template <int MG, bool UNI>
-hipError_t launch_fp4_ring(const Fp4Geometry& geo, cptr<uint64_t> in, cptr<uint64_t> out, const void* bitmat, int k,
-                           int m, int64_t col0, int64_t nchunks, int64_t in_stride, hipStream_t stream) {
+template <int MG, bool UNI, bool COPY>
+hipError_t launch_fp4_ring(const Fp4Geometry& geo, const Fp4Args& a, hipStream_t stream) {
   // ring depth: the most waves per SIMD first (up to 4: they hide each other's LDS/MFMA
   // latencies), then the deepest ring (bytes in flight) at that occupancy. Cached per A size.
   static int choice[161][2];  // [fixed KiB] -> {ring, occupancy}
   int (&ch)[2] = choice[std::min<size_t>(geo.fixed / 1024, 160)];
   if (!ch[0]) {
     const int rings[6] = {32, 16, 12, 8, 6, 4};
-    const int occs[6] = {fp4_occupancy<MG, UNI, 32>(geo.fixed), fp4_occupancy<MG, UNI, 16>(geo.fixed),
-                         fp4_occupancy<MG, UNI, 12>(geo.fixed), fp4_occupancy<MG, UNI, 8>(geo.fixed),
-                         fp4_occupancy<MG, UNI, 6>(geo.fixed), fp4_occupancy<MG, UNI, 4>(geo.fixed)};
+    const int occs[6] = {fp4_occupancy<MG, UNI, COPY, 32>(geo.fixed), fp4_occupancy<MG, UNI, COPY, 16>(geo.fixed),
+                         fp4_occupancy<MG, UNI, COPY, 12>(geo.fixed), fp4_occupancy<MG, UNI, COPY, 8>(geo.fixed),
+                         fp4_occupancy<MG, UNI, COPY, 6>(geo.fixed), fp4_occupancy<MG, UNI, COPY, 4>(geo.fixed)};
     int best = -1;
     for (int i = 0; i < 6; ++i)
       if (occs[i] > 0 && (best < 0 || std::min(occs[i], 4) > std::min(occs[best], 4))) best = i;
@@ -430,20 +468,21 @@ hipError_t launch_fp4_ring(const Fp4Geometry& geo, cptr<uint64_t> in, cptr<uint6
   }
   const int occ = ch[1];
   switch (ch[0]) {
-    case 32: return launch_fp4<MG, UNI, 32>(geo, occ, in, out, bitmat, k, m, col0, nchunks, in_stride, stream);
-    case 16: return launch_fp4<MG, UNI, 16>(geo, occ, in, out, bitmat, k, m, col0, nchunks, in_stride, stream);
-    case 12: return launch_fp4<MG, UNI, 12>(geo, occ, in, out, bitmat, k, m, col0, nchunks, in_stride, stream);
-    case 8: return launch_fp4<MG, UNI, 8>(geo, occ, in, out, bitmat, k, m, col0, nchunks, in_stride, stream);
-    case 6: return launch_fp4<MG, UNI, 6>(geo, occ, in, out, bitmat, k, m, col0, nchunks, in_stride, stream);
-    default: return launch_fp4<MG, UNI, 4>(geo, occ, in, out, bitmat, k, m, col0, nchunks, in_stride, stream);
+    case 32: return launch_fp4<MG, UNI, COPY, 32>(geo, occ, a, stream);
+    case 16: return launch_fp4<MG, UNI, COPY, 16>(geo, occ, a, stream);
+    case 12: return launch_fp4<MG, UNI, COPY, 12>(geo, occ, a, stream);
+    case 8: return launch_fp4<MG, UNI, COPY, 8>(geo, occ, a, stream);
+    case 6: return launch_fp4<MG, UNI, COPY, 6>(geo, occ, a, stream);
+    default: return launch_fp4<MG, UNI, COPY, 4>(geo, occ, a, stream);
   }
 }
 
+// variants: uniform-stride inputs (encode), scattered inputs, scattered inputs + fused copy (decode)
 template <int MG>
-hipError_t launch_fp4_any(const Fp4Geometry& geo, cptr<uint64_t> in, cptr<uint64_t> out, const void* bitmat, int k,
-                          int m, int64_t col0, int64_t nchunks, int64_t in_stride, hipStream_t stream) {
-  return in_stride ? launch_fp4_ring<MG, true>(geo, in, out, bitmat, k, m, col0, nchunks, in_stride, stream)
-                   : launch_fp4_ring<MG, false>(geo, in, out, bitmat, k, m, col0, nchunks, 0, stream);
+hipError_t launch_fp4_any(const Fp4Geometry& geo, const Fp4Args& a, hipStream_t stream) {
+  if (a.copy) return launch_fp4_ring<MG, false, true>(geo, a, stream);
+  return a.in_stride ? launch_fp4_ring<MG, true, false>(geo, a, stream)
+                     : launch_fp4_ring<MG, false, false>(geo, a, stream);
 }
 
 }  // namespace
@@ -453,32 +492,46 @@ size_t fp4_bitmat_bytes(int k, int m, int mg_cap) {
   return size_t(g.groups) * g.mg * g.ksteps * 64 * 16;
 }
 
-hipError_t launch_fp4_bitmat(const uint8_t* coeff, int m, int k, void* bitmat, int mg_cap, hipStream_t stream) {
-  if (m <= 0 || k <= 0 || m > 256 || k > 256 || mg_cap < 1) return hipErrorInvalidValue;
+hipError_t launch_fp4_bitmat_sel(const uint8_t* coeff, int ld, const int* sel, int m, int k, void* bitmat, int mg_cap,
+                                 hipStream_t stream) {
+  if (m <= 0 || k <= 0 || m > 256 || k > 256 || mg_cap < 1 || ld < k) return hipErrorInvalidValue;
   const Fp4Geometry g = geometry(k, m, mg_cap);
   const int64_t total = int64_t(fp4_bitmat_bytes(k, m, mg_cap));
   const int blocks = int(std::min<int64_t>((total + 255) / 256, 4096));
-  fp4_bitmat_kernel<<<blocks, 256, 0, stream>>>(coeff, m, k, g.ksteps, g.mg, g.groups, static_cast<uint8_t*>(bitmat));
+  fp4_bitmat_kernel<<<blocks, 256, 0, stream>>>(coeff, ld, sel, m, k, g.ksteps, g.mg, g.groups,
+                                                static_cast<uint8_t*>(bitmat));
   return hipGetLastError();
 }
 
+hipError_t launch_fp4_bitmat(const uint8_t* coeff, int m, int k, void* bitmat, int mg_cap, hipStream_t stream) {
+  return launch_fp4_bitmat_sel(coeff, k, nullptr, m, k, bitmat, mg_cap, stream);
+}
+
 hipError_t launch_gf_gemm_fp4(const void* bitmat, const void* desc, int k, int m, int64_t col0, int64_t ncols,
-                              int mg_cap, int64_t in_stride, hipStream_t stream) {
+                              int mg_cap, int64_t in_stride, bool copies, hipStream_t stream) {
   if (k <= 0 || m <= 0 || ncols < 0 || (col0 & 1) || mg_cap < 1) return hipErrorInvalidValue;
   const int m_pad = pad_m(m);
   const DescLayout l = desc_layout(k, m_pad);
   const char* b = static_cast<const char*>(desc);
-  const Fp4Geometry geo = geometry(k, m, mg_cap);
+  const Fp4Geometry geo = geometry(k, m, mg_cap, copies);
   const int64_t nchunks = ncols / kBlockCols;
   if (nchunks > 0) {
-    const auto in = (cptr<uint64_t>)(b + l.in_off);
-    const auto out = (cptr<uint64_t>)(b + l.out_off);
+    Fp4Args a{};
+    a.in = (cptr<uint64_t>)(b + l.in_off);
+    a.out = (cptr<uint64_t>)(b + l.out_off);
+    a.copy = copies ? (cptr<uint64_t>)(b + l.copy_off) : nullptr;
+    a.bitmat = bitmat;
+    a.k = k;
+    a.m = m;
+    a.col0 = col0;
+    a.nchunks = nchunks;
+    a.in_stride = copies ? 0 : in_stride;  // the copy variant reads row pointers from the table
     hipError_t e;
     switch (geo.mg) {
-      case 8: e = launch_fp4_any<8>(geo, in, out, bitmat, k, m, col0, nchunks, in_stride, stream); break;
-      case 4: e = launch_fp4_any<4>(geo, in, out, bitmat, k, m, col0, nchunks, in_stride, stream); break;
-      case 2: e = launch_fp4_any<2>(geo, in, out, bitmat, k, m, col0, nchunks, in_stride, stream); break;
-      default: e = launch_fp4_any<1>(geo, in, out, bitmat, k, m, col0, nchunks, in_stride, stream); break;
+      case 8: e = launch_fp4_any<8>(geo, a, stream); break;
+      case 4: e = launch_fp4_any<4>(geo, a, stream); break;
+      case 2: e = launch_fp4_any<2>(geo, a, stream); break;
+      default: e = launch_fp4_any<1>(geo, a, stream); break;
     }
     if (e != hipSuccess) return e;
   }

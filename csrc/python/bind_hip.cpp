@@ -106,10 +106,16 @@ PYBIND11_MODULE(_hip, m) {
                             as_stream(stream)),
           "fp4_bitmat");
   });
+  m.def("fp4_bitmat_sel", [](uint64_t coeff, int ld, uint64_t sel, int mm, int k, uint64_t bitmat, int mg_cap,
+                             uint64_t stream) {
+    check(launch_fp4_bitmat_sel(reinterpret_cast<const uint8_t*>(coeff), ld, reinterpret_cast<const int*>(sel), mm, k,
+                                reinterpret_cast<void*>(bitmat), mg_cap, as_stream(stream)),
+          "fp4_bitmat_sel");
+  });
   m.def("gemm_fp4", [](uint64_t bitmat, uint64_t desc, int k, int mm, int64_t col0, int64_t ncols, int mg_cap,
-                       int64_t in_stride, uint64_t stream) {
+                       int64_t in_stride, bool copies, uint64_t stream) {
     check(launch_gf_gemm_fp4(reinterpret_cast<const void*>(bitmat), reinterpret_cast<const void*>(desc), k, mm, col0,
-                             ncols, mg_cap, in_stride, as_stream(stream)),
+                             ncols, mg_cap, in_stride, copies, as_stream(stream)),
           "gf_gemm_fp4");
   });
   m.def("gen_matrix", [](uint64_t e, int k, int p, int kind, uint64_t stream) {

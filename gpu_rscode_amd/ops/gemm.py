@@ -209,24 +209,30 @@ class GemmPlan:
         self.desc = torch.from_numpy(host).to(self.device)
         self.layout = desc_layout(self.k, self.m_pad, self.batch)
         if engine == "auto":
-            engine = _auto_engine(self.k, self.m, coeff is not None and maps is None, self.copies is None,
-                                  self.bytewise, self.batch)
+            engine = _auto_engine(self.k, self.m, maps is None, self.bytewise, self.batch)
         self.engine = engine
         self.bitmat = None
         if engine in ("mfma", "mfma_i8"):
             # matrix-core GF(2) bit-matrix paths: "mfma" = FP4 block-scaled MFMA
             # (csrc/kernels/gf_mfma_fp4.hip), "mfma_i8" = int8 MFMA (csrc/kernels/gf_mfma.hip).
-            # GF(2^8) coefficients only, no fused copies, aligned rows; the column remainder of a
-            # chunk runs on the v_perm tables that the descriptor also carries.
-            if coeff is None or self.copies is not None or self.bytewise:
-                raise ValueError(f"engine={engine!r} needs coeff=, no copies and aligned rows")
+            # GF(2^8) coefficients (host coeff=, or device_tables=True and set_device_coeff /
+            # invert_into_plan later), aligned rows; fused copies on "mfma" only. The column
+            # remainder of a chunk runs on the v_perm tables that the descriptor also carries.
+            if maps is not None or self.bytewise or self.batch > 1:
+                raise ValueError(f"engine={engine!r} needs GF(2^8) coefficients, aligned rows, one stripe")
+            if engine == "mfma_i8" and (coeff is None or self.copies is not None):
+                raise ValueError("engine='mfma_i8' needs coeff= and no copies")
             self.mfma_mg = mfma_mg
             # equally spaced input rows (one allocation): the FP4 kernel computes DMA addresses
             ptrs = [ptr(r) for r in self.inputs]
             stride = ptrs[1] - ptrs[0] if self.k > 1 else 1
             uniform = stride != 0 and all(p - ptrs[0] == j * stride for j, p in enumerate(ptrs))
             self.in_stride = stride if uniform else 0
-            self._build_bitmat(coeff)
+            if coeff is not None:
+                self._build_bitmat(coeff)
+            else:  # filled on device later (set_device_coeff / invert_into_plan)
+                self.bitmat = torch.zeros(hip().fp4_bitmat_bytes(self.k, self.m, mfma_mg), dtype=torch.uint8,
+                                          device=self.device)
         elif engine != "valu":
             raise ValueError(f"unknown engine {engine!r}")
         self._mark_ready()
@@ -247,6 +253,28 @@ class GemmPlan:
                 self.bitmat = torch.empty(h.mfma_bitmat_bytes(self.k, self.m), dtype=torch.uint8, device=self.device)
             h.mfma_bitmat(c.data_ptr(), self.m, self.k, self.bitmat.data_ptr(), st)
         self._coeff_dev = c
+
+    def set_device_coeff(self, coeff: torch.Tensor, rows=None, stream: torch.cuda.Stream | None = None) -> None:
+        """Rebuild the matrix-core operand from a DEVICE matrix: coefficient row i = coeff[rows[i]]
+        (``rows`` a device int32 tensor, or None for coeff itself, m x k). No host round trip — the
+        decode path feeds it the device-computed inverse. (v_perm tables: see invert_into_plan.)"""
+        if self.engine != "mfma":
+            raise ValueError("set_device_coeff applies to engine='mfma' plans")
+        if coeff.dtype != torch.uint8 or coeff.device != self.device or coeff.dim() != 2 or coeff.shape[1] < self.k:
+            raise ValueError("coeff must be a 2-D uint8 tensor on the plan's device with >= k columns")
+        coeff = coeff.contiguous()
+        st = stream or torch.cuda.current_stream(self.device)
+        sel = 0
+        if rows is not None:
+            if rows.dtype != torch.int32 or rows.numel() != self.m:
+                raise ValueError("rows must be an int32 tensor of m row indices")
+            sel = rows.data_ptr()
+        elif coeff.shape[0] < self.m:
+            raise ValueError("coeff needs m rows")
+        hip().fp4_bitmat_sel(coeff.data_ptr(), coeff.stride(0), sel, self.m, self.k, self.bitmat.data_ptr(),
+                             self.mfma_mg, st.cuda_stream)
+        if not torch.cuda.is_current_stream_capturing():
+            coeff.record_stream(st)
 
     def _mark_ready(self) -> None:
         # descriptor writes are ordered on the current stream; launches on other streams wait on this
@@ -294,7 +322,7 @@ class GemmPlan:
             h.gemm_batched(int(self.desc.data_ptr()), self.k, self.m_pad, self.batch, col0, ncols, self.bytewise, s)
         elif self.engine == "mfma" and vec is None and col0 % 2 == 0:
             h.gemm_fp4(int(self.bitmat.data_ptr()), int(self.desc.data_ptr()), self.k, self.m, col0, ncols,
-                       self.mfma_mg, self.in_stride, s)
+                       self.mfma_mg, self.in_stride, self.copies is not None, s)
         elif self.engine == "mfma_i8" and vec is None and col0 % 2 == 0:
             h.gemm_mfma(int(self.bitmat.data_ptr()), int(self.desc.data_ptr()), self.k, self.m, col0, ncols, s)
         elif self.bytewise:
@@ -311,8 +339,8 @@ class GemmPlan:
 _MFMA_MIN_K, _MFMA_MIN_M = 64, 16
 
 
-def _auto_engine(k: int, m: int, have_coeff: bool, no_copies: bool, bytewise: bool, batch: int) -> str:
-    if have_coeff and no_copies and not bytewise and batch == 1 and k >= _MFMA_MIN_K and m >= _MFMA_MIN_M:
+def _auto_engine(k: int, m: int, gf256: bool, bytewise: bool, batch: int) -> str:
+    if gf256 and not bytewise and batch == 1 and k >= _MFMA_MIN_K and m >= _MFMA_MIN_M:
         return "mfma"
     return "valu"
 

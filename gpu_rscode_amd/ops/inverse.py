@@ -43,16 +43,30 @@ def invert_into_plan(a: torch.Tensor, plan: GemmPlan, sel_rows, *, status: torch
                      stream: torch.cuda.Stream | None = None) -> torch.Tensor:
     """Invert ``a`` (k x k, device) and write the v_perm tables of inverse rows ``sel_rows`` into
     ``plan`` — a decode with zero host round-trips. ``plan`` must have k inputs and len(sel_rows)
-    outputs. Returns the device status word (0 ok, 1 singular: tables left untouched)."""
+    outputs. ``sel_rows`` may be a device int32 tensor (no host->device copy: graph-capturable).
+    For an ``engine="mfma"`` plan the inverse is also written to a device buffer and the matrix-core
+    bit-matrix is rebuilt from its selected rows on the same stream.
+    Returns the device status word (0 ok, 1 singular: tables left untouched)."""
     n = a.shape[0]
     if plan.k != n or plan.m != len(sel_rows):
         raise ValueError("plan shape does not match (k inputs, len(sel_rows) outputs)")
-    sel = torch.as_tensor(np.asarray(sel_rows, dtype=np.int32)).to(a.device, non_blocking=True)
+    if isinstance(sel_rows, torch.Tensor) and sel_rows.device == a.device and sel_rows.dtype == torch.int32:
+        sel = sel_rows
+    else:
+        sel = torch.as_tensor(np.asarray(sel_rows, dtype=np.int32)).to(a.device, non_blocking=True)
     if status is None:
         status = torch.zeros(1, dtype=torch.int32, device=a.device)
     st = stream or torch.cuda.current_stream(a.device)
     a = a.contiguous()
-    hip().invert(a.data_ptr(), 0, n, 1, status.data_ptr(), plan.desc.data_ptr(), sel.data_ptr(), plan.m,
+    inv = 0
+    if plan.engine == "mfma":  # the matrix-core operand is rebuilt from the device inverse too
+        if getattr(plan, "_inv_buf", None) is None or plan._inv_buf.shape[0] != n:
+            plan._inv_buf = torch.empty((n, n), dtype=torch.uint8, device=a.device)
+        inv = plan._inv_buf.data_ptr()
+    hip().invert(a.data_ptr(), inv, n, 1, status.data_ptr(), plan.desc.data_ptr(), sel.data_ptr(), plan.m,
                  plan.m_pad, st.cuda_stream)
-    sel.record_stream(st)
+    if plan.engine == "mfma":
+        plan.set_device_coeff(plan._inv_buf, sel, stream=st)
+    if not torch.cuda.is_current_stream_capturing():
+        sel.record_stream(st)
     return status

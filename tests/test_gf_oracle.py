@@ -137,12 +137,12 @@ def test_gf16_nibble_maps_are_linear():
 
 def test_auto_engine_policy():
     from gpu_rscode_amd.ops.gemm import _auto_engine
-    assert _auto_engine(128, 32, True, True, False, 1) == "mfma"
-    assert _auto_engine(10, 4, True, True, False, 1) == "valu"  # narrow: v_perm is at the HBM roofline
-    assert _auto_engine(128, 32, True, False, False, 1) == "valu"  # fused survivor copies
-    assert _auto_engine(128, 32, False, True, False, 1) == "valu"  # device-written tables / GF(16) maps
-    assert _auto_engine(128, 32, True, True, True, 1) == "valu"  # unaligned rows
-    assert _auto_engine(128, 32, True, True, False, 4) == "valu"  # batched stripes
+    assert _auto_engine(128, 32, True, False, 1) == "mfma"
+    assert _auto_engine(64, 16, True, False, 1) == "mfma"
+    assert _auto_engine(10, 4, True, False, 1) == "valu"  # narrow: v_perm is at the HBM roofline
+    assert _auto_engine(128, 32, False, False, 1) == "valu"  # GF(16) nibble maps
+    assert _auto_engine(128, 32, True, True, 1) == "valu"  # unaligned rows
+    assert _auto_engine(128, 32, True, False, 4) == "valu"  # batched stripes
 
 
 def test_trace_ranges_are_safe_without_profiler():

@@ -111,6 +111,13 @@ def test_wide_stripe_k128_n160():
     out = rs.decode([stripe[r] for r in rows], rows, device_invert=True)
     torch.cuda.synchronize()
     assert np.array_equal(out.cpu().numpy(), host)
+    # mixed erasures (natives + parity), host-inverted: FP4 engine with fused survivor copies
+    erased = set(range(0, 128, 7)) | {130, 141, 150}
+    rows = [r for r in range(160) if r not in erased][:128]
+    for dev_inv in (False, True):
+        out = rs.decode([stripe[r] for r in rows], rows, device_invert=dev_inv)
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy(), host), dev_inv
 
 
 @pytest.mark.parametrize("streams,slice_", [(1, 1 << 20), (2, 1 << 20), (4, 3 << 18), (3, 256)])

@@ -264,3 +264,30 @@ def test_auto_engine_wide_stripe_uses_matrix_cores_and_matches():
     plan.run(col0=1, ncols=ncols - 1)  # odd column start: v_perm fallback on the same plan
     torch.cuda.synchronize()
     assert np.array_equal(out.cpu().numpy(), GF256.gemm(coeff2, host))
+
+
+@pytest.mark.parametrize("k,m,ncols", [(128, 32, 256 * 41 + 99), (80, 17, 256 * 9), (255, 20, 3000)])
+def test_fp4_fused_copy_and_device_coeff(k, m, ncols):
+    """FP4 engine with the decode shape: scattered survivor rows, fused copies of some inputs, and
+    the coefficient operand rebuilt on device from selected rows of a device matrix."""
+    _native_loaded()
+    rng = np.random.default_rng(k + m)
+    host, dev = _rand_rows(k, ncols, k)
+    rows = [dev[j].clone() for j in rng.permutation(k)]  # scattered allocations
+    perm_host = np.stack([r.cpu().numpy() for r in rows])
+    out = alloc_rows(m, ncols, "cuda", fill=0x33)
+    cdst = alloc_rows(k, ncols, "cuda", fill=0x44)
+    copies = [cdst[j] if j % 3 else None for j in range(k)]
+    big = rng.integers(0, 256, size=(k, k), dtype=np.uint8)  # rows of a "device inverse"
+    sel = sorted(rng.choice(k, size=m, replace=False).tolist())
+    coeff = big[sel]
+    plan = GemmPlan(rows, out, copies=copies, device_tables=True, engine="mfma")
+    assert plan.engine == "mfma"  # (the copy variant always reads the row-pointer table)
+    plan.set_coeff(coeff)  # v_perm tables (remainder columns) + bit-matrix
+    plan.set_device_coeff(torch.from_numpy(big).cuda(), torch.tensor(sel, dtype=torch.int32, device="cuda"))
+    plan.run()
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), GF256.gemm(coeff, perm_host))
+    got = cdst.cpu().numpy()
+    for j in range(k):
+        assert np.array_equal(got[j], perm_host[j] if j % 3 else np.full(ncols, 0x44, np.uint8)), j
