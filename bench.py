@@ -6,9 +6,10 @@ Metric (BASELINE.json): "encode+decode throughput (GB/s) at k=10,n=14 on 1 GiB; 
 One step on every rank (one process per GPU, torch.distributed/RCCL for N > 1):
   1. encode:  parity[4, C] = E . data[10, C]                          (gfx950 v_perm GF-GEMM)
   2. decode:  4 erasures drawn from a pool of recoverable patterns (natives AND parity erased);
-              the 10x10 decode system is inverted ON DEVICE (LDS Gauss-Jordan kernel writing the
-              GEMM tables), then the erased natives are rebuilt and surviving natives copied in one
-              fused pass into a fresh [10, C] output.
+              the decode system is solved ON DEVICE every step (LDS Gauss-Jordan on the e x (e+k)
+              systematic system [G[P, erased] | B'], writing the GEMM tables), then the erased
+              natives are rebuilt and surviving natives copied in one fused pass into a fresh
+              [10, C] output.
 C = ceil(2^30 / 10) = 107374183 bytes (odd, as in the reference, src/encode.cu:317). Data is synthetic
 random bytes generated in HBM; weights/matrices are the reference Vandermonde. Scaling is weak: every
 GPU encodes and decodes its own 1 GiB stripe set (the reference splits one file across GPUs with no
@@ -37,7 +38,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 from gpu_rscode_amd import gf  # noqa: E402
 from gpu_rscode_amd.models import alloc_rows  # noqa: E402
-from gpu_rscode_amd.ops import GemmPlan, fill_random_, invert_into_plan  # noqa: E402
+from gpu_rscode_amd.ops import GemmPlan, decode_system_into_plan, fill_random_  # noqa: E402
 from gpu_rscode_amd._native import cpu, hip  # noqa: E402
 from gpu_rscode_amd.utils.timing import trace_range  # noqa: E402
 
@@ -109,9 +110,11 @@ def main():
         if any(e < k for e in erased) and cpu().decode_matrix(g.tobytes(), k, rows) is not None:
             pool.append(rows)
     e_dev = torch.from_numpy(e_host.copy()).to(dev)
+    g_dev = torch.from_numpy(np.ascontiguousarray(g)).to(dev)
     pool_dev = torch.tensor(pool, dtype=torch.int32, device=dev)
     if world > 1:
         dist.broadcast(e_dev, 0)
+        dist.broadcast(g_dev, 0)
         dist.broadcast(pool_dev, 0)
     pool = pool_dev.cpu().tolist()
     e_mat = e_dev.cpu().numpy()
@@ -129,9 +132,8 @@ def main():
         ins = [stripe[r] for r in rows]
         copies = [out[r] if r < k else None for r in rows]
         plan = GemmPlan(ins, [out[i] for i in erased], copies=copies, device_tables=True)
-        plan.a_dev = torch.from_numpy(np.ascontiguousarray(g[rows])).to(dev)
-        plan.erased = erased
-        plan.sel = torch.tensor(erased, dtype=torch.int32, device=dev)
+        plan.rows_dev = torch.tensor(rows, dtype=torch.int32, device=dev)
+        plan.erased_dev = torch.tensor(erased, dtype=torch.int32, device=dev)
         plan.status = torch.zeros(1, dtype=torch.int32, device=dev)
         dec.append(plan)
     gathered = None
@@ -151,9 +153,9 @@ def main():
         inv_stream = stream if a.no_overlap else side
         if not a.no_overlap:
             side.wait_stream(stream)  # the previous step's decode has consumed this plan's tables
-        # device Gauss-Jordan writing the decode tables (and, on the matrix-core engine, the
-        # bit-matrix) straight into the plan
-        invert_into_plan(plan.a_dev, plan, plan.sel, status=plan.status, stream=inv_stream)
+        # the decode system solved on device (e x (e+k) Gauss-Jordan on [G[P, erased] | B'])
+        # writing the decode tables (and, on the matrix-core engine, the bit-matrix) into the plan
+        decode_system_into_plan(g_dev, plan.rows_dev, plan.erased_dev, plan, status=plan.status, stream=inv_stream)
         if not a.no_overlap:
             inv_done.record(side)
         enc.run(**kv)
@@ -232,7 +234,7 @@ def main():
         "config": {"model": f"RS(k={k},n={n}) reference Vandermonde, GF(2^8) poly 0x11D",
                    "global_batch": f"{a.bytes} B per GPU ({k} x {C} B chunks)", "seq_len": C,
                    "parallelism": f"dp{world} (stripe-sharded, RCCL broadcast of E)",
-                   "erasures": a.erasures, "decode_invert": "device Gauss-Jordan per step",
+                   "erasures": a.erasures, "decode_invert": "device Gauss-Jordan (systematic e x (e+k) system) per step",
                    "gather": bool(a.gather), "engine": enc.engine, "graph": bool(a.graph), "preset": a.preset},
         "verified": ok,
         "baseline": {"gbps": round(BASELINE_GBPS, 4), "source": "k=8,n=11 1.1 GB Tesla C2050 (nearest published)"},

@@ -32,6 +32,12 @@ hipError_t launch_gf_gemm_variant(const void* desc, int k, int m_pad, int64_t co
 // If `desc` is non-null, additionally writes the perm tables of rows `sel_rows[0..m)` of each
 // inverse into desc's table block (k = n, m_pad given) — the decode GEMM then runs without a
 // host round-trip. (batch must be 1 in that mode.)
+// Systematic decode rows without the k x k inverse: g = G (n x k, [I; E]), rows = the k survivor
+// ids, erased = the e erased native ids (device int32). Writes X (e x k, decode coefficients of the
+// erased natives in survivor order) to dm (optional), status (1 = unrecoverable), and the v_perm
+// tables tab[j][b] into desc (k inputs, m_pad >= e outputs) when given.
+hipError_t launch_gf_decode_system(const uint8_t* g, int k, const int* rows, const int* erased, int e, uint8_t* dm,
+                                   int* status, void* desc, int m_pad, hipStream_t stream);
 hipError_t launch_gf_invert(const uint8_t* a, uint8_t* a_inv, int n, int batch, int* status,
                             void* desc, const int* sel_rows, int m, int m_pad, hipStream_t stream);
 

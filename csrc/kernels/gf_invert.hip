@@ -172,7 +172,157 @@ __global__ __launch_bounds__(B) void gf_invert_kernel(const uint8_t* __restrict_
   }
 }
 
+
+// Systematic decode system, solved directly (SURVEY §3.2 decode, done the erasure-code way): with
+// G = [I; E] and survivors = (k-e) natives N + e parity rows P, the e erased natives x_E satisfy
+// E[P,E] x_E = y_P + E[P,N] x_N (characteristic 2), so the decode rows are
+// X = M^-1 B' with M = G[P, erased] (e x e) and B'[a][j] = G[P_a][rows_j] for a native survivor j,
+// [rows_j == P_a] for a parity survivor j. Gauss-Jordan on [M | B'] (e x (e+k)) yields X directly:
+// O(e^2 (e+k)) instead of inverting the whole k x k system (k=128, e=32: ~40x less work, and the
+// wide decode no longer waits ~1 ms for a 128x128 inverse — profiles/r01_p128).
+template <int B>
+__global__ __launch_bounds__(B) void gf_decode_system_kernel(const uint8_t* __restrict__ g, int k,
+                                                             const int* __restrict__ rows,
+                                                             const int* __restrict__ erased, int e,
+                                                             uint8_t* __restrict__ dm, int* __restrict__ status,
+                                                             uint32_t* __restrict__ tab, int m_pad) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int W = e + k;
+  const int PW = (((W + 3) / 4) | 1);
+  uint8_t* exp_s = smem;
+  uint16_t* log_s = reinterpret_cast<uint16_t*>(smem + 1024);
+  int* piv_s = reinterpret_cast<int*>(smem + 1536);
+  uint32_t* tinv_s = reinterpret_cast<uint32_t*>(smem + 1552);
+  int* prow = reinterpret_cast<int*>(smem + 1584);  // parity survivors (e of them), survivor order
+  uint32_t* T = reinterpret_cast<uint32_t*>(smem + 1584 + 4 * 256);
+  uint32_t* M = reinterpret_cast<uint32_t*>(smem + 1584 + 4 * 256 + 32 * e);
+  uint8_t* Mb = reinterpret_cast<uint8_t*>(M);
+  auto byte_at = [&](int r, int col) -> uint8_t& { return Mb[(r * PW) * 4 + col]; };
+
+  const int tid = threadIdx.x;
+  for (int i = tid; i < kExpLen; i += B) exp_s[i] = d_gf_tables.exp[i];
+  for (int i = kExpLen + tid; i < 1024; i += B) exp_s[i] = 0;
+  for (int i = tid; i < 256; i += B) log_s[i] = d_gf_tables.log[i];
+  for (int i = tid; i < e * PW; i += B) M[i] = 0;
+  if (tid == 0) {  // parity survivors in survivor order (a serial scan of <= 256 ids)
+    int a = 0;
+    for (int j = 0; j < k; ++j)
+      if (rows[j] >= k && a < e) prow[a++] = rows[j];
+    *piv_s = a;
+  }
+  __syncthreads();
+  int singular = *piv_s != e;  // not exactly e parity survivors: inconsistent pattern
+  if (!singular) {
+    for (int i = tid; i < e * W; i += B) {
+      const int a = i / W, col = i - a * W;
+      const size_t grow = size_t(prow[a]) * k;
+      uint8_t v;
+      if (col < e) {
+        v = g[grow + erased[col]];
+      } else {
+        const int r = rows[col - e];
+        v = r < k ? g[grow + r] : uint8_t(r == prow[a]);
+      }
+      byte_at(a, col) = v;
+    }
+  }
+  __syncthreads();
+
+  int TPR = 1;
+  while (TPR * 2 * e <= B && TPR < 64) TPR <<= 1;
+  const int my_row0 = tid / TPR, sub = tid % TPR, row_step = B / TPR;
+  for (int c = 0; c < e && !singular; ++c) {
+    if (tid == 0) *piv_s = e;
+    __syncthreads();
+    for (int r = c + tid; r < e; r += B)
+      if (byte_at(r, c)) atomicMin(piv_s, r);
+    __syncthreads();
+    const int p = *piv_s;
+    if (p == e) {
+      singular = 1;
+      break;
+    }
+    if (p != c) {
+      for (int w = tid; w < PW; w += B) {
+        const uint32_t t = M[p * PW + w];
+        M[p * PW + w] = M[c * PW + w];
+        M[c * PW + w] = t;
+      }
+      __syncthreads();
+    }
+    if (tid == 0) {
+      uint32_t t[5];
+      perm_of(exp_s[255 - log_s[byte_at(c, c)]], t);
+#pragma unroll
+      for (int q = 0; q < 5; ++q) tinv_s[q] = t[q];
+    }
+    __syncthreads();
+    {
+      uint32_t ti[5];
+#pragma unroll
+      for (int q = 0; q < 5; ++q) ti[q] = tinv_s[q];
+      for (int w = tid; w < PW; w += B) M[c * PW + w] = apply4(ti, M[c * PW + w]);
+      for (int r = tid; r < e; r += B) {
+        uint32_t t[5];
+        perm_of(r == c ? 0u : byte_at(r, c), t);
+#pragma unroll
+        for (int q = 0; q < 5; ++q) T[r * 8 + q] = t[q];
+      }
+    }
+    __syncthreads();
+    for (int r = my_row0; r < e; r += row_step) {
+      if (r == c) continue;
+      uint32_t t[5];
+#pragma unroll
+      for (int q = 0; q < 5; ++q) t[q] = T[r * 8 + q];
+      if ((t[0] | t[1] | t[2] | t[3] | t[4]) == 0) continue;
+      for (int w = sub; w < PW; w += TPR) M[r * PW + w] ^= apply4(t, M[c * PW + w]);
+    }
+    __syncthreads();
+  }
+
+  if (tid == 0 && status) *status = singular;
+  if (dm)
+    for (int i = tid; i < e * k; i += B) {
+      const int b = i / k, j = i - b * k;
+      dm[i] = singular ? 0 : byte_at(b, e + j);
+    }
+  if (tab && !singular)
+    for (int idx = tid; idx < k * e; idx += B) {  // tab[j][b] = perm(X[b][j])
+      const int j = idx / e, b = idx - j * e;
+      uint32_t t[5];
+      perm_of(byte_at(b, e + j), t);
+      uint32_t* dst = tab + (size_t(j) * m_pad + b) * kPermStride;
+#pragma unroll
+      for (int q = 0; q < 5; ++q) dst[q] = t[q];
+      dst[5] = dst[6] = dst[7] = 0;
+    }
+}
+
 }  // namespace
+
+hipError_t launch_gf_decode_system(const uint8_t* g, int k, const int* rows, const int* erased, int e, uint8_t* dm,
+                                   int* status, void* desc, int m_pad, hipStream_t stream) {
+  if (k <= 0 || k > 256 || e <= 0 || e > k || (desc && e > m_pad)) return hipErrorInvalidValue;
+  const int W = e + k;
+  const int PW = (((W + 3) / 4) | 1);
+  const size_t lds = 1584 + 4 * 256 + 32 * size_t(e) + 4 * size_t(e) * PW;
+  uint32_t* tab = nullptr;
+  if (desc) tab = reinterpret_cast<uint32_t*>(static_cast<char*>(desc) + desc_layout(k, m_pad).tab_off);
+  if (e <= 32) {
+    gf_decode_system_kernel<64><<<1, 64, lds, stream>>>(g, k, rows, erased, e, dm, status, tab, m_pad);
+    return hipGetLastError();
+  }
+  static bool attr_set = false;
+  if (lds > 65536 && !attr_set) {
+    const hipError_t err = hipFuncSetAttribute(reinterpret_cast<const void*>(&gf_decode_system_kernel<256>),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (err != hipSuccess) return err;
+    attr_set = true;
+  }
+  gf_decode_system_kernel<256><<<1, 256, lds, stream>>>(g, k, rows, erased, e, dm, status, tab, m_pad);
+  return hipGetLastError();
+}
 
 hipError_t launch_gf_invert(const uint8_t* a, uint8_t* a_inv, int n, int batch, int* status, void* desc,
                             const int* sel_rows, int m, int m_pad, hipStream_t stream) {

@@ -106,6 +106,14 @@ PYBIND11_MODULE(_hip, m) {
                             as_stream(stream)),
           "fp4_bitmat");
   });
+  m.def("decode_system", [](uint64_t g, int k, uint64_t rows, uint64_t erased, int e, uint64_t dm, uint64_t status,
+                            uint64_t desc, int m_pad, uint64_t stream) {
+    check(launch_gf_decode_system(reinterpret_cast<const uint8_t*>(g), k, reinterpret_cast<const int*>(rows),
+                                  reinterpret_cast<const int*>(erased), e, reinterpret_cast<uint8_t*>(dm),
+                                  reinterpret_cast<int*>(status), reinterpret_cast<void*>(desc), m_pad,
+                                  as_stream(stream)),
+          "decode_system");
+  });
   m.def("fp4_bitmat_sel", [](uint64_t coeff, int ld, uint64_t sel, int mm, int k, uint64_t bitmat, int mg_cap,
                              uint64_t stream) {
     check(launch_fp4_bitmat_sel(reinterpret_cast<const uint8_t*>(coeff), ld, reinterpret_cast<const int*>(sel), mm, k,

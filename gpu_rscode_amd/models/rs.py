@@ -20,7 +20,7 @@ import torch
 from .. import gf
 from .._native import cpu
 from ..ops.gemm import GemmPlan, _rows
-from ..ops.inverse import invert_into_plan
+from ..ops.inverse import decode_system_into_plan
 from ..ops.matrix import decode_matrix, encoding_matrix
 
 PITCH = 256
@@ -73,6 +73,7 @@ class ReedSolomon:
         self.G = np.vstack([np.eye(k, dtype=np.uint8), self.E]).astype(np.uint8)
         self._plans: dict = {}
         self._dm: dict = {}
+        self._g_dev: dict = {}  # (device, id(G)) -> G on device, for the on-device decode system
 
     # ---- helpers -----------------------------------------------------------------------------
     def _maps(self, coeff: np.ndarray) -> np.ndarray | None:
@@ -253,9 +254,15 @@ class ReedSolomon:
             if plan is None:
                 plan = GemmPlan(ins, [outs[i] for i in erased], copies=copies, device_tables=True)
                 self._plans[key] = plan
-                plan.a_dev = torch.from_numpy(self.G[rows].copy()).to(dev)
+                plan.rows_dev = torch.tensor(rows, dtype=torch.int32, device=dev)
+                plan.erased_dev = torch.tensor(erased, dtype=torch.int32, device=dev)
                 plan.status = torch.zeros(1, dtype=torch.int32, device=dev)
-            invert_into_plan(plan.a_dev, plan, erased, status=plan.status, stream=stream)
+            g_dev = self._g_dev.get((dev, id(self.G)))
+            if g_dev is None:
+                self._g_dev.clear()
+                g_dev = self._g_dev[(dev, id(self.G))] = torch.from_numpy(np.ascontiguousarray(self.G)).to(dev)
+            # systematic decode solved on device: e x (e+k) Gauss-Jordan, tables written in place
+            decode_system_into_plan(g_dev, plan.rows_dev, plan.erased_dev, plan, status=plan.status, stream=stream)
             self.last_status = plan.status
         else:
             dm = self.decode_matrix(rows)

@@ -70,3 +70,36 @@ def invert_into_plan(a: torch.Tensor, plan: GemmPlan, sel_rows, *, status: torch
     if not torch.cuda.is_current_stream_capturing():
         sel.record_stream(st)
     return status
+
+
+def decode_system_into_plan(g: torch.Tensor, rows: torch.Tensor, erased: torch.Tensor, plan: GemmPlan, *,
+                            status: torch.Tensor | None = None,
+                            stream: torch.cuda.Stream | None = None) -> torch.Tensor:
+    """Systematic decode with no k x k inverse: solve [G[P, erased] | B'] (e x (e+k)) on device and
+    write the decode tables (and, on the matrix-core engine, the bit-matrix) into ``plan``.
+
+    ``g``: the (n, k) generator [I; E] on device; ``rows``: the k survivor ids (device int32, the
+    plan's input order); ``erased``: the e erased native ids (device int32, the plan's output
+    order, e = plan.m). Graph-capturable (no host copies). Returns the device status word.
+    (csrc/kernels/gf_invert.hip::gf_decode_system_kernel.)
+    """
+    k = g.shape[1]
+    if plan.k != k or plan.m != erased.numel() or rows.numel() != k:
+        raise ValueError("plan shape does not match (k survivors in, e erased natives out)")
+    for t in (rows, erased):
+        if t.dtype != torch.int32 or t.device != g.device:
+            raise ValueError("rows / erased must be int32 tensors on the generator's device")
+    if status is None:
+        status = torch.zeros(1, dtype=torch.int32, device=g.device)
+    st = stream or torch.cuda.current_stream(g.device)
+    g = g.contiguous()
+    dm = 0
+    if plan.engine == "mfma":
+        if getattr(plan, "_dm_buf", None) is None or plan._dm_buf.shape != (plan.m, k):
+            plan._dm_buf = torch.empty((plan.m, k), dtype=torch.uint8, device=g.device)
+        dm = plan._dm_buf.data_ptr()
+    hip().decode_system(g.data_ptr(), k, rows.data_ptr(), erased.data_ptr(), plan.m, dm, status.data_ptr(),
+                        plan.desc.data_ptr(), plan.m_pad, st.cuda_stream)
+    if plan.engine == "mfma":
+        plan.set_device_coeff(plan._dm_buf, stream=st)
+    return status

@@ -7,6 +7,7 @@ from gpu_rscode_amd import gf
 from gpu_rscode_amd.gf import GF256
 from gpu_rscode_amd.models import alloc_rows
 from gpu_rscode_amd.ops import GemmPlan, fill_random_, gen_matrix_device, gf_invert, invert_into_plan
+from gpu_rscode_amd.ops.gemm import perm_tables_from_coeff
 
 pytestmark = pytest.mark.gpu
 
@@ -291,3 +292,42 @@ def test_fp4_fused_copy_and_device_coeff(k, m, ncols):
     got = cdst.cpu().numpy()
     for j in range(k):
         assert np.array_equal(got[j], perm_host[j] if j % 3 else np.full(ncols, 0x44, np.uint8)), j
+
+
+@pytest.mark.parametrize("k,n,matrix", [(10, 14, "vandermonde"), (128, 160, "cauchy"), (4, 6, "vandermonde"),
+                                        (200, 255, "sys_vandermonde")])
+def test_decode_system_matches_host_decode_matrix(k, n, matrix):
+    """The e x (e+k) systematic solve equals the rows of the full k x k inverse, and flags the
+    reference Vandermonde's singular patterns."""
+    from gpu_rscode_amd.ops import decode_system_into_plan
+    from gpu_rscode_amd.models.rs import ReedSolomon
+    _native_loaded()
+    rs = ReedSolomon(k, n, matrix=matrix)
+    g_dev = torch.from_numpy(np.ascontiguousarray(rs.G)).cuda()
+    rng = np.random.default_rng(k * n)
+    C = 4096
+    checked = singular = 0
+    for trial in range(12):
+        erased_all = sorted(rng.choice(n, size=n - k, replace=False).tolist())
+        rows = [r for r in range(n) if r not in erased_all]
+        erased = [i for i in range(k) if i not in rows]
+        if not erased:
+            continue
+        ins = alloc_rows(k, C, "cuda")
+        outs = alloc_rows(len(erased), C, "cuda")
+        plan = GemmPlan(ins, outs, device_tables=True, engine="valu")
+        status = torch.zeros(1, dtype=torch.int32, device="cuda")
+        decode_system_into_plan(g_dev, torch.tensor(rows, dtype=torch.int32, device="cuda"),
+                                torch.tensor(erased, dtype=torch.int32, device="cuda"), plan, status=status)
+        torch.cuda.synchronize()
+        recoverable = GF256.is_invertible(rs.G[rows])
+        assert int(status.item()) == (0 if recoverable else 1), (rows, erased)
+        if not recoverable:
+            singular += 1
+            continue
+        want = GF256.invert(rs.G[rows])[erased]
+        tabs = plan.table_view().cpu().numpy()  # (k, m_pad, 8) perm records
+        ref_tabs = np.transpose(perm_tables_from_coeff(want), (1, 0, 2))
+        assert np.array_equal(tabs[:, : len(erased), :].view(np.uint32), ref_tabs.astype(np.uint32)), (rows, erased)
+        checked += 1
+    assert checked > 0
