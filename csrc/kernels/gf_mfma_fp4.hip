@@ -303,20 +303,24 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4_kernel(cptr<uint64_t> in, 
   // through a loop-exit copy)
   auto store_chunk = [&](int ci) __attribute__((always_inline)) {
     const int64_t colw = col0 + (slot0 + int64_t(ci) * chunk_slots) * kBlockCols + wave * 64 + 2 * c;
+    // output row pointers: 32-bit LDS address + immediate, all issued before one wait (a C++ read
+    // of outptr[] would be hoisted out of the chunk loop as 2*MG live 64-bit flat addresses; one
+    // wait per pointer serialised 2*MG LDS round trips per chunk)
+    uint64_t op[2 * MG];
+#pragma unroll
+    for (int i = 0; i < 2 * MG; ++i)
+      asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(op[i]) : "v"(optr_addr), "n"(8 * (4 * (i >> 1) + (i & 1)))
+                   : "memory");
+    lgkm_wait();
+#pragma unroll
+    for (int i = 0; i < 2 * MG; ++i) tie(op[i]);
 #pragma unroll
     for (int mt = 0; mt < MG; ++mt)
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
-        // output row pointer by a 32-bit LDS address + immediate (a C++ read of outptr[] would be
-        // hoisted out of the chunk loop as 2*MG live 64-bit flat addresses)
-        uint64_t op;
-        asm volatile("ds_read_b64 %0, %1 offset:%2\n\ts_waitcnt lgkmcnt(0)"
-                     : "=v"(op)
-                     : "v"(optr_addr), "n"(8 * (4 * mt + u))
-                     : "memory");
-        if (op) {
+        if (op[2 * mt + u]) {
           const uint32_t w = pack_byte(acc[mt][0], u) | (pack_byte(acc[mt][1], u) << 8);
-          *(gptr<uint16_t>)(op + colw) = uint16_t(w);
+          *(gptr<uint16_t>)(op[2 * mt + u] + colw) = uint16_t(w);
         }
         __builtin_amdgcn_sched_barrier(0);
       }
