@@ -391,6 +391,10 @@ hipError_t launch_vec(const DescView& d, int k, int m_pad, int batch, int64_t co
   GFRS_CFG(2, 1, false)
   GFRS_CFG(2, 2, false)
   GFRS_CFG(2, 2, true)
+  GFRS_CFG(1, 8, true)
+  GFRS_CFG(1, 16, true)
+  GFRS_CFG(2, 4, true)
+  GFRS_CFG(2, 8, true)
 #undef GFRS_CFG
   return hipErrorInvalidValue;
 }

@@ -11,9 +11,13 @@
 //     byte 4x and was VALU-bound: 87 VALU per 8 MFMA, PMC in profiles/).
 // Per wave and K-step (8 input rows = 64 K bits): 2 N-tiles (64 interleaved columns: tile t holds
 // columns 2c + t, so one ushort load / store serves both), MG M-tiles (MG <= 8) from LDS,
-// 2 x MG MFMAs. Input bytes are expanded to 8 FP4 nibbles with one v_perm of a 4-entry pool
-// {0x00,0x02,0x20,0x22} indexed by the byte's 2-bit chunks.
-// Output bits are placed on MFMA rows exactly as in gf_mfma.hip so every lane owns whole bytes.
+// 2 x MG MFMAs. The order of the 64 K bits inside a step is free (the bit-matrix is built to
+// match), so it is the one that is cheapest to expand: a lane's 4 rows of one column are gathered
+// into one dword W (one shift-or + one v_perm per tile), and B dword q is ONE v_perm of the pool
+// {0x00,0x02,0x20,0x22} indexed by bit pair (2q, 2q+1) of every byte of W — 3 VALU per B dword,
+// ~26 per K-step for 16 MFMAs (was ~56 with one expansion per input byte).
+// Output bits are placed on MFMA rows exactly as in gf_mfma.hip so every lane owns whole bytes;
+// the parity of each f32 count is moved to its output bit by a biased add (see pack_byte).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -46,6 +50,8 @@ __host__ __device__ constexpr int out_bit_of(int r) { return ((r >> 3) & 1) * 4 
 
 // bitmat layout: [group][kstep][mt < MG][lane][16 bytes]; element j = nibble j of the 16 bytes (one
 // K-step's MG fragments are contiguous, so the kernel reads them with immediate LDS offsets).
+// K order inside a step (lane half h): nibble j <-> input row 8s + 4h + ((j >> 1) & 3), bit
+// 2 (j >> 3) + (j & 1) — the order the kernel's expansion produces (expand() below).
 // coefficient (o, i) = coeff[row(o) * ld + i], row(o) = sel ? sel[o] : o (sel: rows of a device
 // matrix, e.g. the erased-native rows of a device-computed inverse)
 __global__ void fp4_bitmat_kernel(const uint8_t* __restrict__ coeff, int ld, const int* __restrict__ sel, int m, int k,
@@ -67,8 +73,8 @@ __global__ void fp4_bitmat_kernel(const uint8_t* __restrict__ coeff, int ld, con
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
       const int j = 2 * q + half;
-      const int irow = 8 * s + 4 * h + (j >> 3);
-      const int ibit = j & 7;
+      const int irow = 8 * s + 4 * h + ((j >> 1) & 3);
+      const int ibit = 2 * (j >> 3) + (j & 1);
       if (orow < m && irow < k &&
           ((dmul(coeff[size_t(sel ? sel[orow] : orow) * ld + irow], uint8_t(1u << ibit)) >> obit) & 1))
         v |= uint8_t(0x2u << (4 * half));
@@ -77,22 +83,37 @@ __global__ void fp4_bitmat_kernel(const uint8_t* __restrict__ coeff, int ld, con
   }
 }
 
-// 8 bits of x -> 8 FP4 nibbles (bit b -> nibble b = 0x2 if set).
-__device__ __forceinline__ int expand_fp4(uint32_t x) {
-  const uint32_t sel = (((x & 0x33u) * 0x1001u) | ((x & 0xCCu) * 0x40040u)) & 0x03030303u;
-  return int(__builtin_amdgcn_perm(0u, 0x22200200u, sel));
+// B dword q of one tile from W (byte b = input row 4h + b of the step, this tile's column): byte b
+// of the result is pool[bits (2q, 2q+1) of W.b] = two FP4 nibbles 0x0 / 0x2 (0.0 / 1.0).
+__device__ __forceinline__ int expand_q(uint32_t w, int q) {
+  return int(__builtin_amdgcn_perm(0u, 0x22200200u, (w >> (2 * q)) & 0x03030303u));
 }
 
-__device__ __forceinline__ uint32_t parity(float v) { return uint32_t(v) & 1u; }
+using f32x2 = float __attribute__((ext_vector_type(2)));
+// (a & mask) | (b & ~mask) as ONE v_bfi_b32 (written as C the compiler splits it into and + or3)
+__device__ __forceinline__ uint32_t bfi(uint32_t mask, uint32_t a, uint32_t b) {
+  uint32_t r;
+  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "s"(mask), "v"(a), "v"(b));
+  return r;
+}
 
-// Output byte u (0/1) of one accumulator tile (regs 8u .. 8u+7).
+// Output byte u (0/1) of one accumulator tile: register 8u + b holds the exact integer count c_b
+// (<= 8k <= 2048) whose parity is output bit b. Adding 2^(23-b) (exact; c_b < 2^(23-b)) fixes the
+// f32 exponent so the mantissa field is c_b << b: the parity lands on bit b with zeros below, and
+// the byte is 7 bit-field inserts (v_bfi) — 4 packed adds + 7 bfi per byte instead of a
+// convert / mask / shift / or per bit. Bits 8+ of the result are garbage.
 __device__ __forceinline__ uint32_t pack_byte(const f32x16& acc, int u) {
-  uint32_t v = 0;
+  uint32_t y = 0;
 #pragma unroll
-  for (int q = 0; q < 2; ++q)
-#pragma unroll
-    for (int low = 0; low < 4; ++low) v |= parity(acc[4 * (2 * u + q) + low]) << (q * 4 + low);
-  return v;
+  for (int q = 0; q < 4; ++q) {
+    const f32x2 v = {acc[8 * u + 2 * q], acc[8 * u + 2 * q + 1]};
+    const f32x2 bias = {float(1u << (23 - 2 * q)), float(1u << (22 - 2 * q))};
+    const f32x2 sum = v + bias;
+    const uint32_t lo = __float_as_uint(sum.x), hi = __float_as_uint(sum.y);
+    y = q == 0 ? lo : bfi(1u << (2 * q), lo, y);
+    y = bfi(2u << (2 * q), hi, y);
+  }
+  return y;
 }
 
 // Per-wave input ring in LDS filled by LDS-DMA: a slot holds one K-PAIR (16 input rows x the
@@ -201,7 +222,8 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4_kernel(cptr<uint64_t> in, 
     d_chunk += (live && wrap) ? 1 : 0;
     d_slot = live ? (d_slot + 1 == kRing ? 0 : d_slot + 1) : d_slot;
   };
-  // the 4 bytes (rows 4h+i of the step, this lane's column pair) of K-step half `hs` of a slot
+  // rows 4h+i of K-step half `hs` of a slot, this lane's column pair (2c, 2c+1). (d16 reads cannot
+  // pack two rows into one register here: with SRAM ECC on, a d16 load zeroes the other half.)
   auto read_x = [&](uint32_t (&x)[4], int slot, int hs) {
     asm volatile(
         "ds_read_u16 %0, %4\n\t"
@@ -219,14 +241,17 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4_kernel(cptr<uint64_t> in, 
       asm volatile("ds_read_b128 %0, %1 offset:%2" : "=&v"(a[mt]) : "v"(base), "n"(mt * 1024) : "memory");
   };
 
-  // B operand of K-step t from its 4 raw ring words (rows 8t+4h+i; rows >= k masked to zero)
-  auto expand = [&](i32x4 (&bo)[kNTW], const uint32_t (&x)[4], int t) __attribute__((always_inline)) {
-    const int rbase = 8 * t + 4 * h;
+  // B operands of a K-step from its 4 ring words: W_t = the 4 rows' bytes of column 2c + t (two
+  // shift-ors and two v_perm for both tiles), then one v_perm per B dword. Rows >= k hold finite
+  // garbage (the DMA clamps to row k-1) that meets zero bit-matrix columns, so no masking.
+  auto expand = [&](i32x4 (&bo)[kNTW], const uint32_t (&x)[4]) __attribute__((always_inline)) {
+    const uint32_t p01 = x[0] | (x[1] << 16), p23 = x[2] | (x[3] << 16);
+    const uint32_t w0 = __builtin_amdgcn_perm(p23, p01, 0x06040200u);
+    const uint32_t w1 = __builtin_amdgcn_perm(p23, p01, 0x07050301u);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const uint32_t xi = rbase + i < k ? x[i] : 0u;
-#pragma unroll
-      for (int tt = 0; tt < kNTW; ++tt) bo[tt][i] = expand_fp4((xi >> (8 * tt)) & 0xFFu);
+    for (int q = 0; q < 4; ++q) {
+      bo[0][q] = expand_q(w0, q);
+      bo[1][q] = expand_q(w1, q);
     }
   };
 
@@ -251,7 +276,7 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4_kernel(cptr<uint64_t> in, 
   }
 #pragma unroll
   for (int mt = 0; mt < MG; ++mt) tie(ac[mt]);
-  expand(bc, x0, 0);
+  expand(bc, x0);
 
   f32x16 acc[MG][kNTW];
   // one K-step s: its 2 x MG MFMAs with the B operand of step s+1 expanded in between (VALU
@@ -261,7 +286,6 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4_kernel(cptr<uint64_t> in, 
   auto step = [&](int s, auto first_tag) __attribute__((always_inline)) {
     constexpr bool kFirst = decltype(first_tag)::value;
     __builtin_amdgcn_sched_barrier(0);
-    const int s1 = s + 1 == ksteps ? 0 : s + 1;
 #pragma unroll
     for (int mt = 0; mt < MG; ++mt) {
       const i32x8 a = {ac[mt][0], ac[mt][1], ac[mt][2], ac[mt][3], 0, 0, 0, 0};
@@ -272,12 +296,12 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4_kernel(cptr<uint64_t> in, 
                                                                       4, 0, scale, 0, scale);
       }
     }
-    expand(bn, x1, s1);
-    // interleave: one MFMA, then a quarter of the next step's expansion (~6 VALU per byte)
+    expand(bn, x1);
+    // interleave: one MFMA, then a slice of the next step's expansion (~26 VALU per step)
 #pragma unroll
     for (int i = 0; i < 2 * MG; ++i) {
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
-      __builtin_amdgcn_sched_group_barrier(0x002, (8 * 8 + 2 * MG - 1) / (2 * MG), 0);  // VALU
+      __builtin_amdgcn_sched_group_barrier(0x002, (26 + 2 * MG - 1) / (2 * MG), 0);  // VALU
     }
     __builtin_amdgcn_sched_barrier(0);
     lgkm_wait();
@@ -319,7 +343,7 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4_kernel(cptr<uint64_t> in, 
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         if (op[2 * mt + u]) {
-          const uint32_t w = pack_byte(acc[mt][0], u) | (pack_byte(acc[mt][1], u) << 8);
+          const uint32_t w = __builtin_amdgcn_perm(pack_byte(acc[mt][1], u), pack_byte(acc[mt][0], u), 0x0c0c0400u);
           *(gptr<uint16_t>)(op[2 * mt + u] + colw) = uint16_t(w);
         }
         __builtin_amdgcn_sched_barrier(0);

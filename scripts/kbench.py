@@ -63,6 +63,9 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--cases", default=None, help="comma-separated case names (default: all)")
+    ap.add_argument("--variants", default=None,
+                    help="semicolon-separated variants, e.g. 'None;1,2,1;1,16,1;mfma' (default: all)")
     a = ap.parse_args()
 
     res = {"device": torch.cuda.get_device_name(0), "cases": {}}
@@ -76,10 +79,24 @@ def main():
     cases = [make_case("enc_k10_p4", 10, 4, 0, a.bytes), make_case("dec_k10_e4_copy6", 10, 4, 6, a.bytes),
              make_case("enc_k4_p2", 4, 2, 0, a.bytes), make_case("enc_k16_p4", 16, 4, 0, a.bytes),
              make_case("enc_k128_p32", 128, 32, 0, a.bytes), make_case("dec_k10_e1_copy9", 10, 1, 9, a.bytes)]
+    if a.cases:
+        keep = set(a.cases.split(","))
+        cases = [c for c in cases if c["name"] in keep]
+    variants = VARIANTS
+    if a.variants:
+        variants = []
+        for tok in a.variants.split(";"):
+            if tok == "None":
+                variants.append(None)
+            elif tok.startswith("mfma"):
+                variants.append(tok)
+            else:
+                v, pf, nt = (int(x) for x in tok.split(","))
+                variants.append((v, pf, bool(nt)))
     for c in cases:
-        times = {str(v): [] for v in VARIANTS}
+        times = {str(v): [] for v in variants}
         for _ in range(a.rounds):
-            for v in VARIANTS:
+            for v in variants:
                 if isinstance(v, str):
                     if c["mplan"] is None:
                         continue
@@ -88,7 +105,10 @@ def main():
                     times[str(v)].append(timed(lambda: pl.run(), a.reps))
                     continue
                 kw = {} if v is None else dict(vec=v[0], pf=v[1], nt=v[2])
-                c["plan"].run(**kw)  # warm
+                try:
+                    c["plan"].run(**kw)  # warm
+                except RuntimeError as e:
+                    raise RuntimeError(f"{c['name']} variant {v}: {e}") from e
                 times[str(v)].append(timed(lambda: c["plan"].run(**kw), a.reps))
         out = {}
         for v, ts in times.items():
