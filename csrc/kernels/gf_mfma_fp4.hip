@@ -17,7 +17,8 @@
 // {0x00,0x02,0x20,0x22} indexed by bit pair (2q, 2q+1) of every byte of W — 3 VALU per B dword,
 // ~26 per K-step for 16 MFMAs (was ~56 with one expansion per input byte).
 // Output bits are placed on MFMA rows exactly as in gf_mfma.hip so every lane owns whole bytes;
-// the parity of each f32 count is moved to its output bit by a biased add (see pack_byte).
+// each accumulator starts at a bias that puts the parity of its f32 count on its output bit (see
+// bias_scale_of_lane).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -89,7 +90,6 @@ __device__ __forceinline__ int expand_q(uint32_t w, int q) {
   return int(__builtin_amdgcn_perm(0u, 0x22200200u, (w >> (2 * q)) & 0x03030303u));
 }
 
-using f32x2 = float __attribute__((ext_vector_type(2)));
 // (a & mask) | (b & ~mask) as ONE v_bfi_b32 (written as C the compiler splits it into and + or3)
 __device__ __forceinline__ uint32_t bfi(uint32_t mask, uint32_t a, uint32_t b) {
   uint32_t r;
@@ -97,24 +97,16 @@ __device__ __forceinline__ uint32_t bfi(uint32_t mask, uint32_t a, uint32_t b) {
   return r;
 }
 
-// Output byte u (0/1) of one accumulator tile: register 8u + b holds the exact integer count c_b
-// (<= 8k <= 2048) whose parity is output bit b. Adding 2^(23-b) (exact; c_b < 2^(23-b)) fixes the
-// f32 exponent so the mantissa field is c_b << b: the parity lands on bit b with zeros below, and
-// the byte is 7 bit-field inserts (v_bfi) — 4 packed adds + 7 bfi per byte instead of a
-// convert / mask / shift / or per bit. Bits 8+ of the result are garbage.
-__device__ __forceinline__ uint32_t pack_byte(const f32x16& acc, int u) {
-  uint32_t y = 0;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const f32x2 v = {acc[8 * u + 2 * q], acc[8 * u + 2 * q + 1]};
-    const f32x2 bias = {float(1u << (23 - 2 * q)), float(1u << (22 - 2 * q))};
-    const f32x2 sum = v + bias;
-    const uint32_t lo = __float_as_uint(sum.x), hi = __float_as_uint(sum.y);
-    y = q == 0 ? lo : bfi(1u << (2 * q), lo, y);
-    y = bfi(2u << (2 * q), hi, y);
-  }
-  return y;
-}
+// Parity placement. Accumulator register j of a 32x32 tile holds output bit b = j & 7 (of output
+// byte j >> 3) as an exact f32 integer count c (<= 8k <= 2048). Every chunk STARTS its
+// accumulators at 2^(23-b) instead of 0 (one extra "bias" MFMA per accumulator, below), which pins
+// the f32 exponent: the mantissa field of 2^(23-b) + c is c << b, so the parity of c sits on bit
+// b with zeros below, and an output byte is 7 bit-field inserts (v_bfi) of 8 raw accumulator words
+// — no convert / mask / shift per bit.
+//
+// Bias MFMA operands: A = B = 1.0 at K index 0 only (nibble 0 of the lanes holding K-block 0),
+// unit B scale, and an A scale (E8M0, per lane = per A row r) of 2^(23 - out_bit_of(r)).
+__device__ __forceinline__ int bias_scale_of_lane(int lane) { return 127 + 23 - out_bit_of(lane & 31); }
 
 // Per-wave input ring in LDS filled by LDS-DMA: a slot holds one K-PAIR (16 input rows x the
 // wave's 64 columns = 1 KiB, row r at byte 64r) and is written by ONE `global_load_lds_dwordx4`
@@ -187,6 +179,8 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4_kernel(cptr<uint64_t> in, 
   const uint32_t ring_addr = uint32_t(reinterpret_cast<uintptr_t>(ring)) + uint32_t(256 * h + 2 * c);
   const uint32_t ring_lane = uint32_t(reinterpret_cast<uintptr_t>(ring)) + 16u * lane;  // this lane's DMA'd 16 B
   const int scale = 0x7F7F7F7F;  // E8M0 1.0 for every block of 32
+  const int bias_scale = bias_scale_of_lane(lane);
+  const i32x8 one_k0 = {h == 0 ? 0x2 : 0, 0, 0, 0, 0, 0, 0, 0};  // 1.0 at K index 0 (A and B)
   const int my_chunks = int((nchunks - slot0 + chunk_slots - 1) / chunk_slots);
   const int kpairs = ksteps >> 1;
   if (my_chunks <= 0) return;
@@ -202,7 +196,7 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4_kernel(cptr<uint64_t> in, 
   uint64_t pn = 0;
   auto row_of = [&]() __attribute__((always_inline)) {
     const int r = 16 * d_p + drow;
-    return r < k ? r : k - 1;  // rows >= k are masked to zero at expansion time
+    return r < k ? r : k - 1;  // rows >= k meet zero bit-matrix columns
   };
   auto ptr_sync = [&]() __attribute__((always_inline)) { pn = rowptr[row_of()]; };
   auto ptr_async = [&]() __attribute__((always_inline)) {
@@ -279,12 +273,25 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4_kernel(cptr<uint64_t> in, 
   expand(bc, x0);
 
   f32x16 acc[MG][kNTW];
+  // (re)start M-tile mt's accumulators at the parity bias (see bias_scale_of_lane)
+  auto bias_init = [&](int mt) __attribute__((always_inline)) {
+    // (an opaque copy of the scale per MFMA keeps these loop-invariant, identical MFMAs from being
+    // hoisted out of the chunk loop or merged, either of which turns them into v_accvgpr_write
+    // copies of one result)
+#pragma unroll
+    for (int t = 0; t < kNTW; ++t) {
+      int bs = bias_scale;
+      asm volatile("" : "+v"(bs));
+      acc[mt][t] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(one_k0, one_k0, (f32x16)(0.0f), 4, 4, 0, bs, 0,
+                                                                    scale);
+    }
+  };
+#pragma unroll
+  for (int mt = 0; mt < MG; ++mt) bias_init(mt);
   // one K-step s: its 2 x MG MFMAs with the B operand of step s+1 expanded in between (VALU
-  // co-issues under the MFMA pipe; the first step of a chunk starts from the inline constant 0 —
-  // no zeroing pass, no zero copy kept live); then retire the LDS reads of A(s+1) and the raw
-  // bytes of step s+2, issued by the caller before the step
-  auto step = [&](int s, auto first_tag) __attribute__((always_inline)) {
-    constexpr bool kFirst = decltype(first_tag)::value;
+  // co-issues under the MFMA pipe); then retire the LDS reads of A(s+1) and the raw bytes of step
+  // s+2, issued by the caller before the step
+  auto step = [&](int s) __attribute__((always_inline)) {
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int mt = 0; mt < MG; ++mt) {
@@ -292,8 +299,7 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4_kernel(cptr<uint64_t> in, 
 #pragma unroll
       for (int t = 0; t < kNTW; ++t) {
         const i32x8 bb = {bc[t][0], bc[t][1], bc[t][2], bc[t][3], 0, 0, 0, 0};
-        acc[mt][t] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, bb, kFirst ? (f32x16)(0.0f) : acc[mt][t], 4,
-                                                                      4, 0, scale, 0, scale);
+        acc[mt][t] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, bb, acc[mt][t], 4, 4, 0, scale, 0, scale);
       }
     }
     expand(bn, x1);
@@ -318,7 +324,7 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4_kernel(cptr<uint64_t> in, 
 #pragma unroll
     for (int t = 0; t < kNTW; ++t) bc[t] = bn[t];
   };
-  using first_t = std::integral_constant<bool, true>;
+  using last_t = std::integral_constant<bool, true>;
   using rest_t = std::integral_constant<bool, false>;
 
   int r_slot = 0;
@@ -326,6 +332,12 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4_kernel(cptr<uint64_t> in, 
   // from the last MFMAs' accumulators (inside the last K-pair, so acc never leaves the AGPRs
   // through a loop-exit copy)
   auto store_chunk = [&](int ci) __attribute__((always_inline)) {
+    // pin the last step's MFMAs here: otherwise machine sinking moves each one into the
+    // conditional store block that reads it, and every block then waits out a full MFMA latency
+#pragma unroll
+    for (int mt = 0; mt < MG; ++mt)
+#pragma unroll
+      for (int t = 0; t < kNTW; ++t) asm volatile("" ::"a"(acc[mt][t]));
     const int64_t colw = col0 + (slot0 + int64_t(ci) * chunk_slots) * kBlockCols + wave * 64 + 2 * c;
     // output row pointers: 32-bit LDS address + immediate, all issued before one wait (a C++ read
     // of outptr[] would be hoisted out of the chunk loop as 2*MG live 64-bit flat addresses; one
@@ -339,22 +351,39 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4_kernel(cptr<uint64_t> in, 
 #pragma unroll
     for (int i = 0; i < 2 * MG; ++i) tie(op[i]);
 #pragma unroll
-    for (int mt = 0; mt < MG; ++mt)
+    for (int mt = 0; mt < MG; ++mt) {
+      // both byte rows of both N-tiles from one pass over the M-tile's 32 accumulators: 4
+      // interleaved chains of 7 v_bfi (no back-to-back dependency), computed (and pinned) before
+      // the conditional stores so they are not sunk into them either
+      uint32_t y[kNTW][2];
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        if (op[2 * mt + u]) {
-          const uint32_t w = __builtin_amdgcn_perm(pack_byte(acc[mt][1], u), pack_byte(acc[mt][0], u), 0x0c0c0400u);
-          *(gptr<uint16_t>)(op[2 * mt + u] + colw) = uint16_t(w);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      }
+      for (int b = 0; b < 8; ++b)
+#pragma unroll
+        for (int t = 0; t < kNTW; ++t)
+#pragma unroll
+          for (int u = 0; u < 2; ++u) {
+            const uint32_t v = __float_as_uint(acc[mt][t][8 * u + b]);
+            y[t][u] = b == 0 ? v : bfi(1u << b, v, y[t][u]);
+          }
+      uint32_t w[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) w[u] = __builtin_amdgcn_perm(y[1][u], y[0][u], 0x0c0c0400u);
+      asm volatile("" ::"v"(w[0]), "v"(w[1]));
+      // the next chunk's bias goes into this tile now: its MFMA pipe time runs under the next
+      // tile's packing (after the last chunk it is simply unused)
+      bias_init(mt);
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+        if (op[2 * mt + u]) *(gptr<uint16_t>)(op[2 * mt + u] + colw) = uint16_t(w[u]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
   };
 
   // one K-pair (slot r_slot): (1) the DMA kRing-1 pairs ahead; (2) wait for the next slot (the
   // oldest pair in flight) and, under the even step's MFMAs, read the next pair's even-step bytes
   // and A(s0+1); (3) under the odd step's MFMAs, the next pair's odd-step bytes and A(s0+2).
   // Reads past the last step hit valid LDS and are discarded.
-  auto pair = [&](int sp, int ci, auto first_tag, auto last_tag) __attribute__((always_inline)) {
+  auto pair = [&](int sp, int ci, auto last_tag) __attribute__((always_inline)) {
     dma_issue();
     if (!UNI) ptr_async();
     const int s0 = 2 * sp;
@@ -372,7 +401,7 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4_kernel(cptr<uint64_t> in, 
                    : "v"(cptr_addr + 8u * uint32_t(crow < k ? crow : k - 1))
                    : "memory");
     }
-    step(s0, first_tag);  // (its closing lgkmcnt(0) also retires the copy reads)
+    step(s0);  // (its closing lgkmcnt(0) also retires the copy reads)
     if (!UNI) tie(pn);
     if constexpr (COPY) {
       tie(cdat);
@@ -384,19 +413,14 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4_kernel(cptr<uint64_t> in, 
     }
     read_x(x2, slot1, 1);
     read_a(an, s0 + 2 == ksteps ? 0 : s0 + 2);
-    step(s0 + 1, rest_t{});
+    step(s0 + 1);
     r_slot = slot1;
     if constexpr (decltype(last_tag)::value) store_chunk(ci);
   };
 
   for (int ci = 0; ci < my_chunks; ++ci) {
-    if (kpairs == 1) {
-      pair(0, ci, first_t{}, first_t{});
-    } else {
-      pair(0, ci, first_t{}, rest_t{});
-      for (int sp = 1; sp < kpairs - 1; ++sp) pair(sp, ci, rest_t{}, rest_t{});
-      pair(kpairs - 1, ci, rest_t{}, first_t{});
-    }
+    for (int sp = 0; sp < kpairs - 1; ++sp) pair(sp, ci, rest_t{});
+    pair(kpairs - 1, ci, last_t{});
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA (dummy or not) outlives the wave
 }
