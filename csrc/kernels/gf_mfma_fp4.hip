@@ -123,6 +123,10 @@ __device__ __forceinline__ int bias_scale_of_lane(int lane) { return 127 + 23 - 
 // empty asm statements so no use can be scheduled above the wait; the compiler's own alias
 // tracking would otherwise put a vmcnt(0)/lgkmcnt(0) in front of every read.
 constexpr int kSlotBytes = 1024;
+// The bit-matrix allocation ends with a 128-byte sink: output rows past m (padding of the last
+// M-tile group) are stored there, so the epilogue has no branches — one basic block the
+// scheduler can interleave (MFMAs and conditional stores in separate blocks serialise).
+constexpr int kSinkBytes = 128;
 using lds_u8 = __attribute__((address_space(3))) uint8_t;
 
 __device__ __forceinline__ void lgkm_wait() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
@@ -156,6 +160,8 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4_kernel(cptr<uint64_t> in, 
   uint64_t* rowptr = reinterpret_cast<uint64_t*>(reinterpret_cast<uint8_t*>(afrag) + a_bytes);
   uint64_t* outptr = rowptr + 256;  // this group's 4*MG output rows
   const i32x4* src = bitmat + size_t(g) * MG * ksteps * 64;
+  // this lane's 2 bytes of the sink past the bit-matrix (kSinkBytes)
+  const uint64_t sink = uint64_t(bitmat + size_t(groups) * MG * ksteps * 64) + 2 * (threadIdx.x & 63);
   for (int i = threadIdx.x; i < MG * ksteps * 64; i += 256) afrag[i] = src[i];
   if (!UNI)
     for (int i = threadIdx.x; i < k; i += 256) rowptr[i] = in[i];
@@ -332,8 +338,8 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4_kernel(cptr<uint64_t> in, 
   // from the last MFMAs' accumulators (inside the last K-pair, so acc never leaves the AGPRs
   // through a loop-exit copy)
   auto store_chunk = [&](int ci) __attribute__((always_inline)) {
-    // pin the last step's MFMAs here: otherwise machine sinking moves each one into the
-    // conditional store block that reads it, and every block then waits out a full MFMA latency
+    // pin the last step's MFMAs here (before the epilogue had one basic block per store, machine
+    // sinking moved each MFMA into its reader's block, which then waited out its full latency)
 #pragma unroll
     for (int mt = 0; mt < MG; ++mt)
 #pragma unroll
@@ -353,8 +359,7 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4_kernel(cptr<uint64_t> in, 
 #pragma unroll
     for (int mt = 0; mt < MG; ++mt) {
       // both byte rows of both N-tiles from one pass over the M-tile's 32 accumulators: 4
-      // interleaved chains of 7 v_bfi (no back-to-back dependency), computed (and pinned) before
-      // the conditional stores so they are not sunk into them either
+      // interleaved chains of 7 v_bfi (no back-to-back dependency)
       uint32_t y[kNTW][2];
 #pragma unroll
       for (int b = 0; b < 8; ++b)
@@ -368,13 +373,14 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4_kernel(cptr<uint64_t> in, 
       uint32_t w[2];
 #pragma unroll
       for (int u = 0; u < 2; ++u) w[u] = __builtin_amdgcn_perm(y[1][u], y[0][u], 0x0c0c0400u);
-      asm volatile("" ::"v"(w[0]), "v"(w[1]));
       // the next chunk's bias goes into this tile now: its MFMA pipe time runs under the next
       // tile's packing (after the last chunk it is simply unused)
       bias_init(mt);
 #pragma unroll
-      for (int u = 0; u < 2; ++u)
-        if (op[2 * mt + u]) *(gptr<uint16_t>)(op[2 * mt + u] + colw) = uint16_t(w[u]);
+      for (int u = 0; u < 2; ++u) {
+        const uint64_t o = op[2 * mt + u];
+        *(gptr<uint16_t>)(o ? o + colw : sink) = uint16_t(w[u]);
+      }
       __builtin_amdgcn_sched_barrier(0);
     }
   };
@@ -429,6 +435,8 @@ struct Fp4Geometry {
   int ksteps, mtiles, mg, groups;
   size_t fixed;  // LDS bytes before the rings: A slice + row/out pointers
 };
+
+size_t bitmat_matrix_bytes(const Fp4Geometry& g) { return size_t(g.groups) * g.mg * g.ksteps * 64 * 16; }
 
 constexpr size_t ring_lds(int r) { return 4 * size_t(r + 1) * kSlotBytes; }
 
@@ -541,14 +549,14 @@ hipError_t launch_fp4_any(const Fp4Geometry& geo, const Fp4Args& a, hipStream_t 
 
 size_t fp4_bitmat_bytes(int k, int m, int mg_cap) {
   const Fp4Geometry g = geometry(k, m, mg_cap);
-  return size_t(g.groups) * g.mg * g.ksteps * 64 * 16;
+  return bitmat_matrix_bytes(g) + kSinkBytes;
 }
 
 hipError_t launch_fp4_bitmat_sel(const uint8_t* coeff, int ld, const int* sel, int m, int k, void* bitmat, int mg_cap,
                                  hipStream_t stream) {
   if (m <= 0 || k <= 0 || m > 256 || k > 256 || mg_cap < 1 || ld < k) return hipErrorInvalidValue;
   const Fp4Geometry g = geometry(k, m, mg_cap);
-  const int64_t total = int64_t(fp4_bitmat_bytes(k, m, mg_cap));
+  const int64_t total = int64_t(bitmat_matrix_bytes(g));
   const int blocks = int(std::min<int64_t>((total + 255) / 256, 4096));
   fp4_bitmat_kernel<<<blocks, 256, 0, stream>>>(coeff, ld, sel, m, k, g.ksteps, g.mg, g.groups,
                                                 static_cast<uint8_t*>(bitmat));
