@@ -75,10 +75,19 @@ __global__ __launch_bounds__(B) void gf_invert_kernel(const uint8_t* __restrict_
   for (int i = tid; i < 256; i += B) log_s[i] = d_gf_tables.log[i];
   for (int i = tid; i < n * PW; i += B) M[i] = 0;
   __syncthreads();
-  for (int i = tid; i < n * n; i += B) {
-    const int r = i / n, col = i - r * n;
-    byte_at(r, col) = a[base + i];
-    if (r == col) byte_at(r, n + col) = 1;
+  for (int i0 = tid; i0 < n * n; i0 += 8 * B) {  // 8 independent global loads in flight per lane
+    uint8_t v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (i0 + u * B < n * n) v[u] = a[base + i0 + u * B];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = i0 + u * B;
+      if (i >= n * n) break;
+      const int r = i / n, col = i - r * n;
+      byte_at(r, col) = v[u];
+      if (r == col) byte_at(r, n + col) = 1;
+    }
   }
   __syncthreads();
 
@@ -180,6 +189,11 @@ __global__ __launch_bounds__(B) void gf_invert_kernel(const uint8_t* __restrict_
 // [rows_j == P_a] for a parity survivor j. Gauss-Jordan on [M | B'] (e x (e+k)) yields X directly:
 // O(e^2 (e+k)) instead of inverting the whole k x k system (k=128, e=32: ~40x less work, and the
 // wide decode no longer waits ~1 ms for a 128x128 inverse — profiles/r01_p128).
+// LDS carve of the decode-system kernel before T and M: exp 1024 | log 512 | misc 16 | Tinv 32 |
+// parity survivors 256 | rows 256 | erased 256 (ids are bytes). Kept small so the solve fits next
+// to a full-LDS persistent GEMM block (k=128, e=32: 8.4 KiB; gf_mfma_fp4.hip kSideReserve).
+constexpr size_t kDecSysFixed = 1584 + 3 * 256;
+
 template <int B>
 __global__ __launch_bounds__(B) void gf_decode_system_kernel(const uint8_t* __restrict__ g, int k,
                                                              const int* __restrict__ rows,
@@ -193,9 +207,11 @@ __global__ __launch_bounds__(B) void gf_decode_system_kernel(const uint8_t* __re
   uint16_t* log_s = reinterpret_cast<uint16_t*>(smem + 1024);
   int* piv_s = reinterpret_cast<int*>(smem + 1536);
   uint32_t* tinv_s = reinterpret_cast<uint32_t*>(smem + 1552);
-  int* prow = reinterpret_cast<int*>(smem + 1584);  // parity survivors (e of them), survivor order
-  uint32_t* T = reinterpret_cast<uint32_t*>(smem + 1584 + 4 * 256);
-  uint32_t* M = reinterpret_cast<uint32_t*>(smem + 1584 + 4 * 256 + 32 * e);
+  uint8_t* prow = smem + 1584;  // parity survivors (e of them), survivor order (ids < 256)
+  uint8_t* rows_s = prow + 256;
+  uint8_t* erased_s = rows_s + 256;
+  uint32_t* T = reinterpret_cast<uint32_t*>(smem + kDecSysFixed);
+  uint32_t* M = reinterpret_cast<uint32_t*>(smem + kDecSysFixed + 32 * e);
   uint8_t* Mb = reinterpret_cast<uint8_t*>(M);
   auto byte_at = [&](int r, int col) -> uint8_t& { return Mb[(r * PW) * 4 + col]; };
 
@@ -204,26 +220,49 @@ __global__ __launch_bounds__(B) void gf_decode_system_kernel(const uint8_t* __re
   for (int i = kExpLen + tid; i < 1024; i += B) exp_s[i] = 0;
   for (int i = tid; i < 256; i += B) log_s[i] = d_gf_tables.log[i];
   for (int i = tid; i < e * PW; i += B) M[i] = 0;
-  if (tid == 0) {  // parity survivors in survivor order (a serial scan of <= 256 ids)
-    int a = 0;
-    for (int j = 0; j < k; ++j)
-      if (rows[j] >= k && a < e) prow[a++] = rows[j];
-    *piv_s = a;
+  for (int i = tid; i < k; i += B) rows_s[i] = uint8_t(rows[i]);
+  for (int i = tid; i < e; i += B) erased_s[i] = uint8_t(erased[i]);
+  __syncthreads();
+  // parity survivors in survivor order: a ballot prefix sum in wave 0 (a one-lane scan of the
+  // global ids was k dependent HBM round trips: ~130 us of the k=128 solve)
+  if (tid < 64) {
+    int base = 0;
+    for (int j0 = 0; j0 < k; j0 += 64) {
+      const int j = j0 + tid;
+      const bool is_par = j < k && rows_s[j] >= k;
+      const unsigned long long bal = __ballot(is_par);
+      const int a = base + __popcll(bal & ((1ull << tid) - 1ull));
+      if (is_par && a < e) prow[a] = rows_s[j];
+      base += __popcll(bal);
+    }
+    if (tid == 0) *piv_s = base < e ? base : e;
   }
   __syncthreads();
   int singular = *piv_s != e;  // not exactly e parity survivors: inconsistent pattern
   if (!singular) {
-    for (int i = tid; i < e * W; i += B) {
-      const int a = i / W, col = i - a * W;
-      const size_t grow = size_t(prow[a]) * k;
-      uint8_t v;
-      if (col < e) {
-        v = g[grow + erased[col]];
-      } else {
-        const int r = rows[col - e];
-        v = r < k ? g[grow + r] : uint8_t(r == prow[a]);
+    // the e x (e+k) system, 8 independent global loads in flight per lane
+    for (int i0 = tid; i0 < e * W; i0 += 8 * B) {
+      uint8_t v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int i = i0 + u * B;
+        if (i >= e * W) break;
+        const int a = i / W, col = i - a * W;
+        const size_t grow = size_t(prow[a]) * k;
+        if (col < e) {
+          v[u] = g[grow + erased_s[col]];
+        } else {
+          const int r = rows_s[col - e];
+          v[u] = r < k ? g[grow + r] : uint8_t(r == prow[a]);
+        }
       }
-      byte_at(a, col) = v;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int i = i0 + u * B;
+        if (i >= e * W) break;
+        const int a = i / W;
+        byte_at(a, i - a * W) = v[u];
+      }
     }
   }
   __syncthreads();
@@ -306,13 +345,11 @@ hipError_t launch_gf_decode_system(const uint8_t* g, int k, const int* rows, con
   if (k <= 0 || k > 256 || e <= 0 || e > k || (desc && e > m_pad)) return hipErrorInvalidValue;
   const int W = e + k;
   const int PW = (((W + 3) / 4) | 1);
-  const size_t lds = 1584 + 4 * 256 + 32 * size_t(e) + 4 * size_t(e) * PW;
+  const size_t lds = kDecSysFixed + 32 * size_t(e) + 4 * size_t(e) * PW;
   uint32_t* tab = nullptr;
   if (desc) tab = reinterpret_cast<uint32_t*>(static_cast<char*>(desc) + desc_layout(k, m_pad).tab_off);
-  if (e <= 32) {
-    gf_decode_system_kernel<64><<<1, 64, lds, stream>>>(g, k, rows, erased, e, dm, status, tab, m_pad);
-    return hipGetLastError();
-  }
+  // (256 lanes for every e: the system gather and the decode-table emission are O(e k) loads /
+  // stores that one wave serialised — 135 us at k=128, e=32)
   static bool attr_set = false;
   if (lds > 65536 && !attr_set) {
     const hipError_t err = hipFuncSetAttribute(reinterpret_cast<const void*>(&gf_decode_system_kernel<256>),

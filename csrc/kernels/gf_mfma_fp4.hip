@@ -123,10 +123,15 @@ __device__ __forceinline__ int bias_scale_of_lane(int lane) { return 127 + 23 - 
 // empty asm statements so no use can be scheduled above the wait; the compiler's own alias
 // tracking would otherwise put a vmcnt(0)/lgkmcnt(0) in front of every read.
 constexpr int kSlotBytes = 1024;
-// The bit-matrix allocation ends with a 128-byte sink: output rows past m (padding of the last
-// M-tile group) are stored there, so the epilogue has no branches — one basic block the
-// scheduler can interleave (MFMAs and conditional stores in separate blocks serialise).
-constexpr int kSinkBytes = 128;
+// The bit-matrix allocation ends with a 1-KiB sink: output rows past m (padding of the last
+// M-tile group) and fused copies with no destination are stored there, so neither the epilogue
+// nor the K loop branches — one basic block the scheduler can interleave (MFMAs and conditional
+// stores in separate blocks serialise). Nothing reads the sink.
+constexpr int kSinkBytes = 1024;
+// LDS the launcher tries to leave free next to a persistent block, so a side-stream kernel (the
+// decode-system solve, gf_invert.hip: 8.4 KiB at k=128, e=32) can co-reside instead of waiting
+// for the whole GEMM.
+constexpr size_t kSideReserve = 9 * 1024;
 using lds_u8 = __attribute__((address_space(3))) uint8_t;
 
 __device__ __forceinline__ void lgkm_wait() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
@@ -160,8 +165,8 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4_kernel(cptr<uint64_t> in, 
   uint64_t* rowptr = reinterpret_cast<uint64_t*>(reinterpret_cast<uint8_t*>(afrag) + a_bytes);
   uint64_t* outptr = rowptr + 256;  // this group's 4*MG output rows
   const i32x4* src = bitmat + size_t(g) * MG * ksteps * 64;
-  // this lane's 2 bytes of the sink past the bit-matrix (kSinkBytes)
-  const uint64_t sink = uint64_t(bitmat + size_t(groups) * MG * ksteps * 64) + 2 * (threadIdx.x & 63);
+  // this lane's 16 bytes of the sink past the bit-matrix (kSinkBytes)
+  const uint64_t sink = uint64_t(bitmat + size_t(groups) * MG * ksteps * 64) + 16 * (threadIdx.x & 63);
   for (int i = threadIdx.x; i < MG * ksteps * 64; i += 256) afrag[i] = src[i];
   if (!UNI)
     for (int i = threadIdx.x; i < k; i += 256) rowptr[i] = in[i];
@@ -412,10 +417,8 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4_kernel(cptr<uint64_t> in, 
     if constexpr (COPY) {
       tie(cdat);
       tie(cp);
-      if (crow < k && cp) {
-        const int64_t col = col0 + (slot0 + int64_t(ci) * chunk_slots) * kBlockCols + dcol;
-        __builtin_nontemporal_store(cdat, (gptr<u32x4>)(cp + uint64_t(col)));
-      }
+      const int64_t col = col0 + (slot0 + int64_t(ci) * chunk_slots) * kBlockCols + dcol;
+      __builtin_nontemporal_store(cdat, (gptr<u32x4>)(crow < k && cp ? cp + uint64_t(col) : sink));
     }
     read_x(x2, slot1, 1);
     read_a(an, s0 + 2 == ksteps ? 0 : s0 + 2);
@@ -519,9 +522,17 @@ hipError_t launch_fp4_ring(const Fp4Geometry& geo, const Fp4Args& a, hipStream_t
     const int occs[6] = {fp4_occupancy<MG, UNI, COPY, 32>(geo.fixed), fp4_occupancy<MG, UNI, COPY, 16>(geo.fixed),
                          fp4_occupancy<MG, UNI, COPY, 12>(geo.fixed), fp4_occupancy<MG, UNI, COPY, 8>(geo.fixed),
                          fp4_occupancy<MG, UNI, COPY, 6>(geo.fixed), fp4_occupancy<MG, UNI, COPY, 4>(geo.fixed)};
+    // at equal occupancy a ring that leaves kSideReserve of the CU's LDS free beats a deeper one
+    // (measured: the DMA latency costs ~2 % at ring 6 — profiles/r01_s3; a full-LDS persistent
+    // grid instead locks the side-stream decode solve out of every CU until the GEMM ends)
+    auto reserve_ok = [&](int i) { return geo.fixed + ring_lds(rings[i]) + kSideReserve <= 160 * 1024; };
     int best = -1;
-    for (int i = 0; i < 6; ++i)
-      if (occs[i] > 0 && (best < 0 || std::min(occs[i], 4) > std::min(occs[best], 4))) best = i;
+    for (int i = 0; i < 6; ++i) {
+      if (occs[i] <= 0) continue;
+      if (best < 0 || std::min(occs[i], 4) > std::min(occs[best], 4) ||
+          (std::min(occs[i], 4) == std::min(occs[best], 4) && reserve_ok(i) && !reserve_ok(best)))
+        best = i;
+    }
     if (best < 0) return hipErrorInvalidConfiguration;
     ch[0] = rings[best];
     ch[1] = occs[best];
