@@ -142,17 +142,39 @@ __device__ __forceinline__ void tie(T& v) {
 
 // UNI: input row j lives at in[0] + j * in_stride (rows from one allocation, the usual case), so
 // DMA addresses are pure VALU arithmetic; otherwise the row pointers come from an LDS table.
-// ksteps is even (the bitmat pads a zero K-step when ceil(k/8) is odd).
+// ksteps is a multiple of the K-steps per ring slot (the bitmat pads zero K-steps).
 // COPY: fused survivor copy (decode): input row j is also written to copy[j] (when nonzero) from
 // the LDS ring slot the DMA already filled — one ds_read_b128 + one global_store_dwordx4 per lane
-// and K-pair, no second read of the survivors from HBM.
+// and slot, no second read of the survivors from HBM.
+//
+// One wave per SIMD (4 waves, 64 columns each). Measured alternatives that lost (profiles/r01_s3):
+// two waves per SIMD with 32 columns each (128 AGPRs of accumulators: the rest no longer fits
+// the 256 registers, it spills; 1061 vs 848 us), and MG = 4 blocks two per CU (1051 us).
+//
+// vmcnt accounting. `s_waitcnt vmcnt(N)` retires everything but the wave's N youngest vector-memory
+// ops, loads, stores and LDS-DMA alike, in issue order (MI355X_MICROARCH.md). The wait for the next
+// slot therefore counts every op issued after that slot's DMA: the kRing-2 younger DMAs, the fused
+// copy stores (COPY; the prologue issues dummy ones to the sink so the pattern holds from slot 0)
+// and, in the first slots of a chunk, the previous chunk's 2*MG epilogue stores. A count that
+// ignored the stores (as before) also waited for them: a store-latency bubble at every chunk start.
 template <int MG, bool UNI, bool COPY, int kRing>
-__global__ __launch_bounds__(256, 1) void gf_gemm_fp4_kernel(cptr<uint64_t> in, cptr<uint64_t> out,
-                                                             cptr<uint64_t> copy, const i32x4* __restrict__ bitmat,
-                                                             int k, int m, int ksteps, int groups, int64_t col0,
-                                                             int64_t nchunks, int64_t chunk_slots, int64_t in_stride) {
+__global__ __launch_bounds__(256, 1) void gf_gemm_fp4_kernel(cptr<uint64_t> in, cptr<uint64_t> out, cptr<uint64_t> copy,
+                                                             const i32x4* __restrict__ bitmat, int k, int m,
+                                                             int ksteps, int groups, int64_t col0, int64_t nchunks,
+                                                             int64_t chunk_slots, int64_t in_stride) {
+  constexpr int NTW = kNTW;              // N-tiles (32 columns each) per wave
+  constexpr int kWaves = 4, kThreads = 256;
+  constexpr int kCW = 32 * NTW;          // columns per wave
+  constexpr int kRS = kSlotBytes / kCW;  // input rows per ring slot (16)
+  constexpr int kSPS = kRS / 8;          // K-steps per ring slot (2)
+  constexpr int kLPR = kCW / 16;         // DMA lanes per row (4)
+  constexpr int kCopyN = COPY ? kRing - 2 : 0;
+  // younger ops than the awaited DMA in steady state, and with the previous chunk's epilogue
+  // stores (clamped to the 6-bit counter: a smaller count only waits longer)
+  constexpr int kWaitN = std::min(kRing - 2 + kCopyN, 63);
+  constexpr int kWaitEpiN = std::min(kRing - 2 + kCopyN + 2 * MG, 63);
   // LDS: A [ksteps][MG][64] x 16 B | row pointers [256] | out pointers [32] | (COPY) copy pointers
-  // [256] | rings [4][kRing+1][1 KiB]
+  // [256] | rings [kWaves][kRing][1 KiB] | one spare slot shared by the waves' dummy DMAs
   extern __shared__ __attribute__((aligned(16))) i32x4 afrag[];
   const int bid = blockIdx.x;
   const int xcd = bid & 7;
@@ -167,16 +189,16 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4_kernel(cptr<uint64_t> in, 
   const i32x4* src = bitmat + size_t(g) * MG * ksteps * 64;
   // this lane's 16 bytes of the sink past the bit-matrix (kSinkBytes)
   const uint64_t sink = uint64_t(bitmat + size_t(groups) * MG * ksteps * 64) + 16 * (threadIdx.x & 63);
-  for (int i = threadIdx.x; i < MG * ksteps * 64; i += 256) afrag[i] = src[i];
+  for (int i = threadIdx.x; i < MG * ksteps * 64; i += kThreads) afrag[i] = src[i];
   if (!UNI)
-    for (int i = threadIdx.x; i < k; i += 256) rowptr[i] = in[i];
-  for (int i = threadIdx.x; i < 4 * MG; i += 256) {
+    for (int i = threadIdx.x; i < k; i += kThreads) rowptr[i] = in[i];
+  for (int i = threadIdx.x; i < 4 * MG; i += kThreads) {
     const int row = 4 * g * MG + i;
     outptr[i] = row < m ? out[row] : 0;
   }
   uint64_t* copyptr = rowptr + 256 + 32;
   if (COPY)
-    for (int i = threadIdx.x; i < k; i += 256) copyptr[i] = g == 0 ? copy[i] : 0;  // group 0 copies
+    for (int i = threadIdx.x; i < k; i += kThreads) copyptr[i] = g == 0 ? copy[i] : 0;  // group 0 copies
   __syncthreads();
 
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 31, h = lane >> 5;
@@ -185,28 +207,30 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4_kernel(cptr<uint64_t> in, 
   const uint32_t rowptr_addr = lds0 + uint32_t(a_bytes);
   const uint32_t optr_addr = rowptr_addr + 2048u + 16u * h;  // outptr[2h + u] of M-tile 0
   const uint32_t cptr_addr = rowptr_addr + 2304u;
-  lds_u8* ring = (lds_u8*)(reinterpret_cast<uint8_t*>(afrag) + a_bytes + 2304 + (COPY ? 2048 : 0) +
-                           size_t(wave) * (kRing + 1) * kSlotBytes);
-  const uint32_t ring_addr = uint32_t(reinterpret_cast<uintptr_t>(ring)) + uint32_t(256 * h + 2 * c);
+  lds_u8* rings = (lds_u8*)(reinterpret_cast<uint8_t*>(afrag) + a_bytes + 2304 + (COPY ? 2048 : 0));
+  lds_u8* ring = rings + size_t(wave) * kRing * kSlotBytes;
+  lds_u8* spare = rings + size_t(kWaves) * kRing * kSlotBytes;
+  // this lane's bytes of K-step half hs, row i: ring + hs*8*kCW + (4h + i)*kCW + NTW*c
+  const uint32_t ring_addr = uint32_t(reinterpret_cast<uintptr_t>(ring)) + uint32_t(4 * h * kCW + NTW * c);
   const uint32_t ring_lane = uint32_t(reinterpret_cast<uintptr_t>(ring)) + 16u * lane;  // this lane's DMA'd 16 B
   const int scale = 0x7F7F7F7F;  // E8M0 1.0 for every block of 32
   const int bias_scale = bias_scale_of_lane(lane);
   const i32x8 one_k0 = {h == 0 ? 0x2 : 0, 0, 0, 0, 0, 0, 0, 0};  // 1.0 at K index 0 (A and B)
   const int my_chunks = int((nchunks - slot0 + chunk_slots - 1) / chunk_slots);
-  const int kpairs = ksteps >> 1;
+  const int kslots = ksteps / kSPS;
   if (my_chunks <= 0) return;
   const uint64_t in0 = UNI ? in[0] : 0;
-  const int drow = lane >> 2;                // this lane's row within a DMA'd pair
-  const int dcol = wave * 64 + 16 * (lane & 3);
+  const int drow = lane / kLPR;  // this lane's row within a DMA'd slot
+  const int dcol = wave * kCW + 16 * (lane % kLPR);
 
-  // DMA cursor (odometer over my chunks x K-pairs) and, off the UNI path, the row pointer of the
-  // cursor's pair. Past the last pair the cursor keeps issuing "dummy" DMAs (a valid source, the
-  // wave's spare slot kRing as destination) so the number in flight — and with it every counted
-  // vmcnt below — stays the same and the K loop has no branches.
+  // DMA cursor (odometer over my chunks x slots) and, off the UNI path, the row pointer of the
+  // cursor's slot. Past the last slot the cursor keeps issuing "dummy" DMAs (a valid source, the
+  // spare slot as destination) so the number in flight — and with it every counted vmcnt below —
+  // stays the same and the K loop has no branches.
   int d_chunk = 0, d_p = 0, d_slot = 0;
   uint64_t pn = 0;
   auto row_of = [&]() __attribute__((always_inline)) {
-    const int r = 16 * d_p + drow;
+    const int r = kRS * d_p + drow;
     return r < k ? r : k - 1;  // rows >= k meet zero bit-matrix columns
   };
   auto ptr_sync = [&]() __attribute__((always_inline)) { pn = rowptr[row_of()]; };
@@ -221,8 +245,8 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4_kernel(cptr<uint64_t> in, 
       sa = in0 + uint64_t(int64_t(row_of()) * in_stride + col);
     else
       sa = pn + uint64_t(col);
-    __builtin_amdgcn_global_load_lds((gptr<const void>)sa, ring + (live ? d_slot : kRing) * kSlotBytes, 16, 0, 0);
-    const bool wrap = d_p + 1 == kpairs;
+    __builtin_amdgcn_global_load_lds((gptr<const void>)sa, live ? ring + d_slot * kSlotBytes : spare, 16, 0, 0);
+    const bool wrap = d_p + 1 == kslots;
     d_p = live ? (wrap ? 0 : d_p + 1) : d_p;
     d_chunk += (live && wrap) ? 1 : 0;
     d_slot = live ? (d_slot + 1 == kRing ? 0 : d_slot + 1) : d_slot;
@@ -236,7 +260,7 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4_kernel(cptr<uint64_t> in, 
         "ds_read_u16 %2, %4 offset:128\n\t"
         "ds_read_u16 %3, %4 offset:192"
         : "=&v"(x[0]), "=&v"(x[1]), "=&v"(x[2]), "=&v"(x[3])
-        : "v"(ring_addr + uint32_t(slot * kSlotBytes + 512 * hs))
+        : "v"(ring_addr + uint32_t(slot * kSlotBytes + hs * 8 * kCW))
         : "memory");
   };
   auto read_a = [&](i32x4 (&a)[MG], int s) {
@@ -249,7 +273,8 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4_kernel(cptr<uint64_t> in, 
   // B operands of a K-step from its 4 ring words: W_t = the 4 rows' bytes of column 2c + t (two
   // shift-ors and two v_perm for both tiles), then one v_perm per B dword. Rows >= k hold finite
   // garbage (the DMA clamps to row k-1) that meets zero bit-matrix columns, so no masking.
-  auto expand = [&](i32x4 (&bo)[kNTW], const uint32_t (&x)[4]) __attribute__((always_inline)) {
+  constexpr int kExpandValu = 26;
+  auto expand = [&](i32x4 (&bo)[NTW], const uint32_t (&x)[4]) __attribute__((always_inline)) {
     const uint32_t p01 = x[0] | (x[1] << 16), p23 = x[2] | (x[3] << 16);
     const uint32_t w0 = __builtin_amdgcn_perm(p23, p01, 0x06040200u);
     const uint32_t w1 = __builtin_amdgcn_perm(p23, p01, 0x07050301u);
@@ -260,16 +285,22 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4_kernel(cptr<uint64_t> in, 
     }
   };
 
-  // prologue: kRing-1 pairs in flight; B(0), A(0) and the raw bytes of step 1 in registers
+  // prologue: kRing-1 slots in flight (each followed, on the copy path, by a dummy store to the
+  // sink: the K loop's vmcnt count assumes one copy store after every DMA); B(0), A(0) and the
+  // raw bytes of step 1 in registers
   for (int i = 0; i < kRing - 1; ++i) {
     if (!UNI) ptr_sync();
     dma_issue();
+    if constexpr (COPY) {
+      const u32x4 zero = {0u, 0u, 0u, 0u};
+      asm volatile("global_store_dwordx4 %0, %1, off nt\n\ts_nop 1" ::"v"(sink), "v"(zero) : "memory");
+    }
   }
   if (!UNI) ptr_sync();
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kRing - 2) : "memory");
   uint32_t x0[4], x1[4], x2[4];  // raw bytes: x1 = step s+1 (in registers), x2 = step s+2 (in flight)
   i32x4 ac[MG], an[MG];
-  i32x4 bc[kNTW], bn[kNTW];
+  i32x4 bc[NTW], bn[NTW];
   read_x(x0, 0, 0);
   read_x(x1, 0, 1);
   read_a(ac, 0);
@@ -283,14 +314,14 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4_kernel(cptr<uint64_t> in, 
   for (int mt = 0; mt < MG; ++mt) tie(ac[mt]);
   expand(bc, x0);
 
-  f32x16 acc[MG][kNTW];
+  f32x16 acc[MG][NTW];
   // (re)start M-tile mt's accumulators at the parity bias (see bias_scale_of_lane)
   auto bias_init = [&](int mt) __attribute__((always_inline)) {
     // (an opaque copy of the scale per MFMA keeps these loop-invariant, identical MFMAs from being
     // hoisted out of the chunk loop or merged, either of which turns them into v_accvgpr_write
     // copies of one result)
 #pragma unroll
-    for (int t = 0; t < kNTW; ++t) {
+    for (int t = 0; t < NTW; ++t) {
       int bs = bias_scale;
       asm volatile("" : "+v"(bs));
       acc[mt][t] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(one_k0, one_k0, (f32x16)(0.0f), 4, 4, 0, bs, 0,
@@ -299,7 +330,7 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4_kernel(cptr<uint64_t> in, 
   };
 #pragma unroll
   for (int mt = 0; mt < MG; ++mt) bias_init(mt);
-  // one K-step s: its 2 x MG MFMAs with the B operand of step s+1 expanded in between (VALU
+  // one K-step s: its NTW x MG MFMAs with the B operand of step s+1 expanded in between (VALU
   // co-issues under the MFMA pipe); then retire the LDS reads of A(s+1) and the raw bytes of step
   // s+2, issued by the caller before the step
   auto step = [&](int s) __attribute__((always_inline)) {
@@ -308,17 +339,17 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4_kernel(cptr<uint64_t> in, 
     for (int mt = 0; mt < MG; ++mt) {
       const i32x8 a = {ac[mt][0], ac[mt][1], ac[mt][2], ac[mt][3], 0, 0, 0, 0};
 #pragma unroll
-      for (int t = 0; t < kNTW; ++t) {
+      for (int t = 0; t < NTW; ++t) {
         const i32x8 bb = {bc[t][0], bc[t][1], bc[t][2], bc[t][3], 0, 0, 0, 0};
         acc[mt][t] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, bb, acc[mt][t], 4, 4, 0, scale, 0, scale);
       }
     }
     expand(bn, x1);
-    // interleave: one MFMA, then a slice of the next step's expansion (~26 VALU per step)
+    // interleave: one MFMA, then a slice of the next step's expansion
 #pragma unroll
-    for (int i = 0; i < 2 * MG; ++i) {
+    for (int i = 0; i < NTW * MG; ++i) {
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
-      __builtin_amdgcn_sched_group_barrier(0x002, (26 + 2 * MG - 1) / (2 * MG), 0);  // VALU
+      __builtin_amdgcn_sched_group_barrier(0x002, (kExpandValu + NTW * MG - 1) / (NTW * MG), 0);  // VALU
     }
     __builtin_amdgcn_sched_barrier(0);
     lgkm_wait();
@@ -333,43 +364,49 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4_kernel(cptr<uint64_t> in, 
       ac[mt] = an[mt];
     }
 #pragma unroll
-    for (int t = 0; t < kNTW; ++t) bc[t] = bn[t];
+    for (int t = 0; t < NTW; ++t) bc[t] = bn[t];
   };
   using last_t = std::integral_constant<bool, true>;
   using rest_t = std::integral_constant<bool, false>;
 
   int r_slot = 0;
-  // the chunk's output: 2 bytes per lane per (M-tile, byte row), one tile at a time, straight
-  // from the last MFMAs' accumulators (inside the last K-pair, so acc never leaves the AGPRs
-  // through a loop-exit copy)
+  // the chunk's output: NTW bytes per lane per (M-tile, byte row), one M-tile at a time, straight
+  // from the last MFMAs' accumulators (inside the last slot, so acc never leaves the AGPRs
+  // through a loop-exit copy); exactly 2*MG stores per wave (kWaitEpiN)
   auto store_chunk = [&](int ci) __attribute__((always_inline)) {
     // pin the last step's MFMAs here (before the epilogue had one basic block per store, machine
     // sinking moved each MFMA into its reader's block, which then waited out its full latency)
 #pragma unroll
     for (int mt = 0; mt < MG; ++mt)
 #pragma unroll
-      for (int t = 0; t < kNTW; ++t) asm volatile("" ::"a"(acc[mt][t]));
-    const int64_t colw = col0 + (slot0 + int64_t(ci) * chunk_slots) * kBlockCols + wave * 64 + 2 * c;
-    // output row pointers: 32-bit LDS address + immediate, all issued before one wait (a C++ read
-    // of outptr[] would be hoisted out of the chunk loop as 2*MG live 64-bit flat addresses; one
-    // wait per pointer serialised 2*MG LDS round trips per chunk)
-    uint64_t op[2 * MG];
-#pragma unroll
-    for (int i = 0; i < 2 * MG; ++i)
-      asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(op[i]) : "v"(optr_addr), "n"(8 * (4 * (i >> 1) + (i & 1)))
+      for (int t = 0; t < NTW; ++t) asm volatile("" ::"a"(acc[mt][t]));
+    const int64_t colw = col0 + (slot0 + int64_t(ci) * chunk_slots) * kBlockCols + wave * kCW + NTW * c;
+    // output row pointers of M-tile mt: 32-bit LDS address + immediate (a C++ read of outptr[]
+    // would be hoisted out of the chunk loop as 2*MG live 64-bit flat addresses), read one M-tile
+    // ahead under the packing so only 4 pointer registers are live (all 2*MG at once made the
+    // two-waves-per-SIMD form spill)
+    auto read_op = [&](uint64_t (&o)[2], int mt) __attribute__((always_inline)) {
+      asm volatile("ds_read_b64 %0, %2 offset:%3\n\tds_read_b64 %1, %2 offset:%4"
+                   : "=&v"(o[0]), "=&v"(o[1])
+                   : "v"(optr_addr), "n"(32 * mt), "n"(32 * mt + 8)
                    : "memory");
+    };
+    uint64_t opn[2];
+    read_op(opn, 0);
     lgkm_wait();
-#pragma unroll
-    for (int i = 0; i < 2 * MG; ++i) tie(op[i]);
+    tie(opn[0]);
+    tie(opn[1]);
 #pragma unroll
     for (int mt = 0; mt < MG; ++mt) {
+      const uint64_t op[2] = {opn[0], opn[1]};
+      if (mt + 1 < MG) read_op(opn, mt + 1);
       // both byte rows of both N-tiles from one pass over the M-tile's 32 accumulators: 4
       // interleaved chains of 7 v_bfi (no back-to-back dependency)
-      uint32_t y[kNTW][2];
+      uint32_t y[NTW][2];
 #pragma unroll
       for (int b = 0; b < 8; ++b)
 #pragma unroll
-        for (int t = 0; t < kNTW; ++t)
+        for (int t = 0; t < NTW; ++t)
 #pragma unroll
           for (int u = 0; u < 2; ++u) {
             const uint32_t v = __float_as_uint(acc[mt][t][8 * u + b]);
@@ -383,28 +420,30 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4_kernel(cptr<uint64_t> in, 
       bias_init(mt);
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
-        const uint64_t o = op[2 * mt + u];
+        const uint64_t o = op[u];
         *(gptr<uint16_t>)(o ? o + colw : sink) = uint16_t(w[u]);
+      }
+      if (mt + 1 < MG) {
+        lgkm_wait();
+        tie(opn[0]);
+        tie(opn[1]);
       }
       __builtin_amdgcn_sched_barrier(0);
     }
   };
 
-  // one K-pair (slot r_slot): (1) the DMA kRing-1 pairs ahead; (2) wait for the next slot (the
-  // oldest pair in flight) and, under the even step's MFMAs, read the next pair's even-step bytes
-  // and A(s0+1); (3) under the odd step's MFMAs, the next pair's odd-step bytes and A(s0+2).
-  // Reads past the last step hit valid LDS and are discarded.
-  auto pair = [&](int sp, int ci, auto last_tag) __attribute__((always_inline)) {
+  // one ring slot (r_slot) = kSPS K-steps: (1) the DMA kRing-1 slots ahead; (2) under each step's
+  // MFMAs, the raw bytes of the step after next (from this slot, or — after waiting for it — the
+  // next one) and the A fragments of the next step. Reads past the last step hit valid LDS and are
+  // discarded.
+  auto slot_run = [&](int sp, int ci, auto last_tag) __attribute__((always_inline)) {
     dma_issue();
     if (!UNI) ptr_async();
-    const int s0 = 2 * sp;
+    const int s0 = kSPS * sp;
     const int slot1 = r_slot + 1 == kRing ? 0 : r_slot + 1;
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kRing - 2) : "memory");
-    read_x(x2, slot1, 0);
-    read_a(an, s0 + 1);
     [[maybe_unused]] u32x4 cdat;
     [[maybe_unused]] uint64_t cp = 0;
-    [[maybe_unused]] const int crow = 16 * sp + drow;
+    [[maybe_unused]] const int crow = kRS * sp + drow;
     if constexpr (COPY) {  // this lane's 16 B of the current slot and its row's copy pointer
       asm volatile("ds_read_b128 %0, %1" : "=&v"(cdat) : "v"(ring_lane + uint32_t(r_slot * kSlotBytes)) : "memory");
       asm volatile("ds_read_b64 %0, %1"
@@ -412,24 +451,37 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4_kernel(cptr<uint64_t> in, 
                    : "v"(cptr_addr + 8u * uint32_t(crow < k ? crow : k - 1))
                    : "memory");
     }
-    step(s0);  // (its closing lgkmcnt(0) also retires the copy reads)
-    if (!UNI) tie(pn);
-    if constexpr (COPY) {
-      tie(cdat);
-      tie(cp);
-      const int64_t col = col0 + (slot0 + int64_t(ci) * chunk_slots) * kBlockCols + dcol;
-      __builtin_nontemporal_store(cdat, (gptr<u32x4>)(crow < k && cp ? cp + uint64_t(col) : sink));
+#pragma unroll
+    for (int j = 0; j < kSPS; ++j) {
+      if (j + 2 == kSPS) {  // the next slot has landed: count the younger ops (see the header)
+        if (ci > 0 && sp + 3 <= kRing)
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kWaitEpiN) : "memory");
+        else
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kWaitN) : "memory");
+      }
+      if (j + 2 < kSPS)
+        read_x(x2, r_slot, j + 2);
+      else
+        read_x(x2, slot1, j + 2 - kSPS);
+      read_a(an, s0 + j + 1 == ksteps ? 0 : s0 + j + 1);
+      step(s0 + j);  // (the first step's closing lgkmcnt(0) also retires the copy / pointer reads)
+      if (j == 0) {
+        if (!UNI) tie(pn);
+        if constexpr (COPY) {
+          tie(cdat);
+          tie(cp);
+          const int64_t col = col0 + (slot0 + int64_t(ci) * chunk_slots) * kBlockCols + dcol;
+          __builtin_nontemporal_store(cdat, (gptr<u32x4>)(crow < k && cp ? cp + uint64_t(col) : sink));
+        }
+      }
     }
-    read_x(x2, slot1, 1);
-    read_a(an, s0 + 2 == ksteps ? 0 : s0 + 2);
-    step(s0 + 1);
     r_slot = slot1;
     if constexpr (decltype(last_tag)::value) store_chunk(ci);
   };
 
   for (int ci = 0; ci < my_chunks; ++ci) {
-    for (int sp = 0; sp < kpairs - 1; ++sp) pair(sp, ci, rest_t{});
-    pair(kpairs - 1, ci, last_t{});
+    for (int sp = 0; sp < kslots - 1; ++sp) slot_run(sp, ci, rest_t{});
+    slot_run(kslots - 1, ci, last_t{});
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA (dummy or not) outlives the wave
 }
@@ -441,11 +493,12 @@ struct Fp4Geometry {
 
 size_t bitmat_matrix_bytes(const Fp4Geometry& g) { return size_t(g.groups) * g.mg * g.ksteps * 64 * 16; }
 
-constexpr size_t ring_lds(int r) { return 4 * size_t(r + 1) * kSlotBytes; }
+// ring LDS of a block: R slots per wave plus the one spare slot the waves share
+constexpr size_t ring_lds(int r) { return (4 * size_t(r) + 1) * kSlotBytes; }
 
 Fp4Geometry geometry(int k, int m, int mg_cap, bool copy = false) {
   Fp4Geometry g{};
-  g.ksteps = ((k + 15) / 16) * 2;  // K-pairs: one 1-KiB DMA slot = 2 K-steps
+  g.ksteps = ((k + 15) / 16) * 2;  // ring slots: one 1-KiB DMA slot = 2 K-steps
   g.mtiles = (m + 3) / 4;
   // MG = M-tiles per block: next power of two >= mtiles (<= 8, the accumulator budget), halved
   // until the block's A slice fits the LDS
@@ -513,38 +566,41 @@ hipError_t launch_fp4(const Fp4Geometry& geo, int occ, const Fp4Args& a, hipStre
 
 template <int MG, bool UNI, bool COPY>
 hipError_t launch_fp4_ring(const Fp4Geometry& geo, const Fp4Args& a, hipStream_t stream) {
-  // ring depth: the most waves per SIMD first (up to 4: they hide each other's LDS/MFMA
-  // latencies), then the deepest ring (bytes in flight) at that occupancy. Cached per A size.
-  static int choice[161][2];  // [fixed KiB] -> {ring, occupancy}
+  // ring depth: the most blocks per CU first (up to 4), then — at equal occupancy — a ring that
+  // leaves kSideReserve of the CU's LDS free (measured: DMA latency costs ~2 % at ring 6,
+  // profiles/r01_s3; a full-LDS persistent grid instead locks the side-stream decode solve out of
+  // every CU until the GEMM ends), then the deepest ring. Cached per A size.
+  constexpr int kN = 6;
+  constexpr int rings[kN] = {32, 16, 12, 8, 6, 4};
+  static int choice[161][2];  // [fixed KiB] -> {ring index + 1, occupancy}
   int (&ch)[2] = choice[std::min<size_t>(geo.fixed / 1024, 160)];
   if (!ch[0]) {
-    const int rings[6] = {32, 16, 12, 8, 6, 4};
-    const int occs[6] = {fp4_occupancy<MG, UNI, COPY, 32>(geo.fixed), fp4_occupancy<MG, UNI, COPY, 16>(geo.fixed),
-                         fp4_occupancy<MG, UNI, COPY, 12>(geo.fixed), fp4_occupancy<MG, UNI, COPY, 8>(geo.fixed),
-                         fp4_occupancy<MG, UNI, COPY, 6>(geo.fixed), fp4_occupancy<MG, UNI, COPY, 4>(geo.fixed)};
-    // at equal occupancy a ring that leaves kSideReserve of the CU's LDS free beats a deeper one
-    // (measured: the DMA latency costs ~2 % at ring 6 — profiles/r01_s3; a full-LDS persistent
-    // grid instead locks the side-stream decode solve out of every CU until the GEMM ends)
+    const int occs[kN] = {fp4_occupancy<MG, UNI, COPY, rings[0]>(geo.fixed),
+                          fp4_occupancy<MG, UNI, COPY, rings[1]>(geo.fixed),
+                          fp4_occupancy<MG, UNI, COPY, rings[2]>(geo.fixed),
+                          fp4_occupancy<MG, UNI, COPY, rings[3]>(geo.fixed),
+                          fp4_occupancy<MG, UNI, COPY, rings[4]>(geo.fixed),
+                          fp4_occupancy<MG, UNI, COPY, rings[5]>(geo.fixed)};
     auto reserve_ok = [&](int i) { return geo.fixed + ring_lds(rings[i]) + kSideReserve <= 160 * 1024; };
     int best = -1;
-    for (int i = 0; i < 6; ++i) {
+    for (int i = 0; i < kN; ++i) {
       if (occs[i] <= 0) continue;
       if (best < 0 || std::min(occs[i], 4) > std::min(occs[best], 4) ||
           (std::min(occs[i], 4) == std::min(occs[best], 4) && reserve_ok(i) && !reserve_ok(best)))
         best = i;
     }
     if (best < 0) return hipErrorInvalidConfiguration;
-    ch[0] = rings[best];
+    ch[0] = best + 1;
     ch[1] = occs[best];
   }
   const int occ = ch[1];
-  switch (ch[0]) {
-    case 32: return launch_fp4<MG, UNI, COPY, 32>(geo, occ, a, stream);
-    case 16: return launch_fp4<MG, UNI, COPY, 16>(geo, occ, a, stream);
-    case 12: return launch_fp4<MG, UNI, COPY, 12>(geo, occ, a, stream);
-    case 8: return launch_fp4<MG, UNI, COPY, 8>(geo, occ, a, stream);
-    case 6: return launch_fp4<MG, UNI, COPY, 6>(geo, occ, a, stream);
-    default: return launch_fp4<MG, UNI, COPY, 4>(geo, occ, a, stream);
+  switch (ch[0] - 1) {
+    case 0: return launch_fp4<MG, UNI, COPY, rings[0]>(geo, occ, a, stream);
+    case 1: return launch_fp4<MG, UNI, COPY, rings[1]>(geo, occ, a, stream);
+    case 2: return launch_fp4<MG, UNI, COPY, rings[2]>(geo, occ, a, stream);
+    case 3: return launch_fp4<MG, UNI, COPY, rings[3]>(geo, occ, a, stream);
+    case 4: return launch_fp4<MG, UNI, COPY, rings[4]>(geo, occ, a, stream);
+    default: return launch_fp4<MG, UNI, COPY, rings[5]>(geo, occ, a, stream);
   }
 }
 

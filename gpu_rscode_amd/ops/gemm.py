@@ -222,6 +222,8 @@ class GemmPlan:
                 raise ValueError(f"engine={engine!r} needs GF(2^8) coefficients, aligned rows, one stripe")
             if engine == "mfma_i8" and (coeff is None or self.copies is not None):
                 raise ValueError("engine='mfma_i8' needs coeff= and no copies")
+            if not 1 <= mfma_mg <= 8:
+                raise ValueError("mfma_mg must be 1..8")
             self.mfma_mg = mfma_mg
             # equally spaced input rows (one allocation): the FP4 kernel computes DMA addresses
             ptrs = [ptr(r) for r in self.inputs]
@@ -231,7 +233,7 @@ class GemmPlan:
             if coeff is not None:
                 self._build_bitmat(coeff)
             else:  # filled on device later (set_device_coeff / invert_into_plan)
-                self.bitmat = torch.zeros(hip().fp4_bitmat_bytes(self.k, self.m, mfma_mg), dtype=torch.uint8,
+                self.bitmat = torch.zeros(hip().fp4_bitmat_bytes(self.k, self.m, self.mfma_mg), dtype=torch.uint8,
                                           device=self.device)
         elif engine != "valu":
             raise ValueError(f"unknown engine {engine!r}")

@@ -46,12 +46,11 @@ def make_case(name, k, m, ncopy, total_bytes):
         copies = [dst[j] if j < ncopy else None for j in range(k)]
     coeff = np.random.default_rng(k + m).integers(1, 256, size=(m, k), dtype=np.uint8)
     plan = GemmPlan(data, out, coeff, copies=copies, engine="valu")
-    mplan = None
+    mplan = {"mfma": GemmPlan(data, out, coeff, copies=copies, engine="mfma"),
+             "mfma_mg4": GemmPlan(data, out, coeff, copies=copies, engine="mfma", mfma_mg=4),
+             "mfma_mg2": GemmPlan(data, out, coeff, copies=copies, engine="mfma", mfma_mg=2)}
     if not ncopy:
-        mplan = {"mfma": GemmPlan(data, out, coeff, engine="mfma"),
-                 "mfma_mg4": GemmPlan(data, out, coeff, engine="mfma", mfma_mg=4),
-                 "mfma_mg2": GemmPlan(data, out, coeff, engine="mfma", mfma_mg=2),
-                 "mfma_i8": GemmPlan(data, out, coeff, engine="mfma_i8")}
+        mplan["mfma_i8"] = GemmPlan(data, out, coeff, engine="mfma_i8")
     traffic = (k + m + ncopy) * C
     return {"name": name, "k": k, "m": m, "copies": ncopy, "C": C, "plan": plan, "mplan": mplan,
             "traffic": traffic, "keep": (data, out, copies)}
@@ -78,7 +77,8 @@ def main():
 
     cases = [make_case("enc_k10_p4", 10, 4, 0, a.bytes), make_case("dec_k10_e4_copy6", 10, 4, 6, a.bytes),
              make_case("enc_k4_p2", 4, 2, 0, a.bytes), make_case("enc_k16_p4", 16, 4, 0, a.bytes),
-             make_case("enc_k128_p32", 128, 32, 0, a.bytes), make_case("dec_k10_e1_copy9", 10, 1, 9, a.bytes)]
+             make_case("enc_k128_p32", 128, 32, 0, a.bytes), make_case("dec_k10_e1_copy9", 10, 1, 9, a.bytes),
+             make_case("dec_k128_e32_copy96", 128, 32, 96, a.bytes)]
     if a.cases:
         keep = set(a.cases.split(","))
         cases = [c for c in cases if c["name"] in keep]
@@ -98,7 +98,7 @@ def main():
         for _ in range(a.rounds):
             for v in variants:
                 if isinstance(v, str):
-                    if c["mplan"] is None:
+                    if v not in c["mplan"]:
                         continue
                     pl = c["mplan"][v]
                     pl.run()
