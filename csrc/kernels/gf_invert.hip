@@ -189,10 +189,11 @@ __global__ __launch_bounds__(B) void gf_invert_kernel(const uint8_t* __restrict_
 // [rows_j == P_a] for a parity survivor j. Gauss-Jordan on [M | B'] (e x (e+k)) yields X directly:
 // O(e^2 (e+k)) instead of inverting the whole k x k system (k=128, e=32: ~40x less work, and the
 // wide decode no longer waits ~1 ms for a 128x128 inverse — profiles/r01_p128).
-// LDS carve of the decode-system kernel before T and M: exp 1024 | log 512 | misc 16 | Tinv 32 |
-// parity survivors 256 | rows 256 | erased 256 (ids are bytes). Kept small so the solve fits next
-// to a full-LDS persistent GEMM block (k=128, e=32: 8.4 KiB; gf_mfma_fp4.hip kSideReserve).
-constexpr size_t kDecSysFixed = 1584 + 3 * 256;
+// LDS carve of the decode-system kernel before M: exp 1024 | log 512 | pivot-search slots + count 16 |
+// pivot rows 256 | parity survivors 256 | rows 256 | erased 256 | pivot inverses 256 (ids are
+// bytes). Kept small so the solve fits next to a full-LDS persistent GEMM block (k=128, e=32:
+// 7.9 KiB; gf_mfma_fp4.hip kSideReserve).
+constexpr size_t kDecSysFixed = 1552 + 5 * 256;
 
 template <int B>
 __global__ __launch_bounds__(B) void gf_decode_system_kernel(const uint8_t* __restrict__ g, int k,
@@ -205,13 +206,13 @@ __global__ __launch_bounds__(B) void gf_decode_system_kernel(const uint8_t* __re
   const int PW = (((W + 3) / 4) | 1);
   uint8_t* exp_s = smem;
   uint16_t* log_s = reinterpret_cast<uint16_t*>(smem + 1024);
-  int* piv_s = reinterpret_cast<int*>(smem + 1536);
-  uint32_t* tinv_s = reinterpret_cast<uint32_t*>(smem + 1552);
-  uint8_t* prow = smem + 1584;  // parity survivors (e of them), survivor order (ids < 256)
+  int* piv_s = reinterpret_cast<int*>(smem + 1536);  // [0..2] pivot-search slots, [3] parity count
+  uint8_t* perm_s = smem + 1552;  // perm_s[c] = pivot row of column c
+  uint8_t* prow = perm_s + 256;   // parity survivors (e of them), survivor order (ids < 256)
   uint8_t* rows_s = prow + 256;
   uint8_t* erased_s = rows_s + 256;
-  uint32_t* T = reinterpret_cast<uint32_t*>(smem + kDecSysFixed);
-  uint32_t* M = reinterpret_cast<uint32_t*>(smem + kDecSysFixed + 32 * e);
+  uint8_t* pinv_s = erased_s + 256;  // 1 / M[perm_s[c]][c]
+  uint32_t* M = reinterpret_cast<uint32_t*>(smem + kDecSysFixed);
   uint8_t* Mb = reinterpret_cast<uint8_t*>(M);
   auto byte_at = [&](int r, int col) -> uint8_t& { return Mb[(r * PW) * 4 + col]; };
 
@@ -222,6 +223,7 @@ __global__ __launch_bounds__(B) void gf_decode_system_kernel(const uint8_t* __re
   for (int i = tid; i < e * PW; i += B) M[i] = 0;
   for (int i = tid; i < k; i += B) rows_s[i] = uint8_t(rows[i]);
   for (int i = tid; i < e; i += B) erased_s[i] = uint8_t(erased[i]);
+  if (tid < 3) piv_s[tid] = e;
   __syncthreads();
   // parity survivors in survivor order: a ballot prefix sum in wave 0 (a one-lane scan of the
   // global ids was k dependent HBM round trips: ~130 us of the k=128 solve)
@@ -235,10 +237,10 @@ __global__ __launch_bounds__(B) void gf_decode_system_kernel(const uint8_t* __re
       if (is_par && a < e) prow[a] = rows_s[j];
       base += __popcll(bal);
     }
-    if (tid == 0) *piv_s = base < e ? base : e;
+    if (tid == 0) piv_s[3] = base < e ? base : e;
   }
   __syncthreads();
-  int singular = *piv_s != e;  // not exactly e parity survivors: inconsistent pattern
+  int singular = piv_s[3] != e;  // not exactly e parity survivors: inconsistent pattern
   if (!singular) {
     // the e x (e+k) system, 8 independent global loads in flight per lane
     for (int i0 = tid; i0 < e * W; i0 += 8 * B) {
@@ -267,70 +269,75 @@ __global__ __launch_bounds__(B) void gf_decode_system_kernel(const uint8_t* __re
   }
   __syncthreads();
 
+  // Gauss-Jordan with one barrier per column and no row swaps. Column c's pivot p — the lowest
+  // unused row with a nonzero in column c, bid for with an LDS atomicMin while column c-1 was
+  // eliminated — is recorded (perm_s[c]) and left unnormalised; every other row r adds
+  // (M[r][c] / M[p][c]) * row p. The TPR lanes of row r (one wave: TPR divides 64) read that factor
+  // before any of them writes the row; the lane owning column c+1 of the updated row then bids
+  // for the next pivot. Three rotating bid slots: slot c%3 is read after the barrier, (c+1)%3 is
+  // bid into, (c+2)%3 is reset. Rows are normalised once, in the output pass. (The former loop
+  // had five barriers and a serial inverse per column: 75 us at e=32, k=128.)
   int TPR = 1;
   while (TPR * 2 * e <= B && TPR < 64) TPR <<= 1;
-  const int my_row0 = tid / TPR, sub = tid % TPR, row_step = B / TPR;
+  const int r = tid / TPR, sub = tid % TPR;  // at most one row per lane group: B / TPR >= e
+  bool used = false;
+  if (!singular && sub == 0 && r < e && byte_at(r, 0)) atomicMin(&piv_s[0], r);
+  __syncthreads();
   for (int c = 0; c < e && !singular; ++c) {
-    if (tid == 0) *piv_s = e;
-    __syncthreads();
-    for (int r = c + tid; r < e; r += B)
-      if (byte_at(r, c)) atomicMin(piv_s, r);
-    __syncthreads();
-    const int p = *piv_s;
-    if (p == e) {
+    const int p = piv_s[c % 3];
+    if (p >= e) {  // uniform: every lane read the same LDS word after the barrier
       singular = 1;
       break;
     }
-    if (p != c) {
-      for (int w = tid; w < PW; w += B) {
-        const uint32_t t = M[p * PW + w];
-        M[p * PW + w] = M[c * PW + w];
-        M[c * PW + w] = t;
-      }
-      __syncthreads();
-    }
     if (tid == 0) {
-      uint32_t t[5];
-      perm_of(exp_s[255 - log_s[byte_at(c, c)]], t);
-#pragma unroll
-      for (int q = 0; q < 5; ++q) tinv_s[q] = t[q];
+      piv_s[(c + 2) % 3] = e;
+      perm_s[c] = uint8_t(p);
     }
-    __syncthreads();
-    {
-      uint32_t ti[5];
-#pragma unroll
-      for (int q = 0; q < 5; ++q) ti[q] = tinv_s[q];
-      for (int w = tid; w < PW; w += B) M[c * PW + w] = apply4(ti, M[c * PW + w]);
-      for (int r = tid; r < e; r += B) {
+    if (r < e && r != p) {
+      const uint32_t f = byte_at(r, c);
+      if (f) {
         uint32_t t[5];
-        perm_of(r == c ? 0u : byte_at(r, c), t);
+        perm_of(exp_s[log_s[f] + 255 - log_s[byte_at(p, c)]], t);
+        // batches of 8 dwords: all LDS reads issued before the writes (r != p, so no aliasing)
+        int w = sub;
+        for (; w + 7 * TPR < PW; w += 8 * TPR) {
+          uint32_t pv[8], rv[8];
 #pragma unroll
-        for (int q = 0; q < 5; ++q) T[r * 8 + q] = t[q];
+          for (int u = 0; u < 8; ++u) {
+            pv[u] = M[p * PW + w + u * TPR];
+            rv[u] = M[r * PW + w + u * TPR];
+          }
+#pragma unroll
+          for (int u = 0; u < 8; ++u) M[r * PW + w + u * TPR] = rv[u] ^ apply4(t, pv[u]);
+        }
+        for (; w < PW; w += TPR) M[r * PW + w] ^= apply4(t, M[p * PW + w]);
       }
+      if (!used && c + 1 < e && sub == ((c + 1) >> 2) % TPR && byte_at(r, c + 1))
+        atomicMin(&piv_s[(c + 1) % 3], r);
     }
-    __syncthreads();
-    for (int r = my_row0; r < e; r += row_step) {
-      if (r == c) continue;
-      uint32_t t[5];
-#pragma unroll
-      for (int q = 0; q < 5; ++q) t[q] = T[r * 8 + q];
-      if ((t[0] | t[1] | t[2] | t[3] | t[4]) == 0) continue;
-      for (int w = sub; w < PW; w += TPR) M[r * PW + w] ^= apply4(t, M[c * PW + w]);
-    }
+    if (r == p) used = true;
     __syncthreads();
   }
 
   if (tid == 0 && status) *status = singular;
+  if (!singular) {
+    for (int b = tid; b < e; b += B) pinv_s[b] = exp_s[255 - log_s[byte_at(perm_s[b], b)]];
+    __syncthreads();
+  }
+  // X[b][j] = M[perm_s[b]][e + j] / M[perm_s[b]][b]
+  auto x_at = [&](int b, int j) -> uint32_t {
+    return exp_s[log_s[byte_at(perm_s[b], e + j)] + log_s[pinv_s[b]]];
+  };
   if (dm)
     for (int i = tid; i < e * k; i += B) {
       const int b = i / k, j = i - b * k;
-      dm[i] = singular ? 0 : byte_at(b, e + j);
+      dm[i] = singular ? 0 : uint8_t(x_at(b, j));
     }
   if (tab && !singular)
     for (int idx = tid; idx < k * e; idx += B) {  // tab[j][b] = perm(X[b][j])
       const int j = idx / e, b = idx - j * e;
       uint32_t t[5];
-      perm_of(byte_at(b, e + j), t);
+      perm_of(x_at(b, j), t);
       uint32_t* dst = tab + (size_t(j) * m_pad + b) * kPermStride;
 #pragma unroll
       for (int q = 0; q < 5; ++q) dst[q] = t[q];
@@ -345,7 +352,7 @@ hipError_t launch_gf_decode_system(const uint8_t* g, int k, const int* rows, con
   if (k <= 0 || k > 256 || e <= 0 || e > k || (desc && e > m_pad)) return hipErrorInvalidValue;
   const int W = e + k;
   const int PW = (((W + 3) / 4) | 1);
-  const size_t lds = kDecSysFixed + 32 * size_t(e) + 4 * size_t(e) * PW;
+  const size_t lds = kDecSysFixed + 4 * size_t(e) * PW;
   uint32_t* tab = nullptr;
   if (desc) tab = reinterpret_cast<uint32_t*>(static_cast<char*>(desc) + desc_layout(k, m_pad).tab_off);
   // (256 lanes for every e: the system gather and the decode-table emission are O(e k) loads /
