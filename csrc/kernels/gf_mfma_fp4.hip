@@ -13,9 +13,9 @@
 // columns 2c + t, so one ushort load / store serves both), MG M-tiles (MG <= 8) from LDS,
 // 2 x MG MFMAs. The order of the 64 K bits inside a step is free (the bit-matrix is built to
 // match), so it is the one that is cheapest to expand: a lane's 4 rows of one column are gathered
-// into one dword W (one shift-or + one v_perm per tile), and B dword q is ONE v_perm of the pool
-// {0x00,0x02,0x20,0x22} indexed by bit pair (2q, 2q+1) of every byte of W — 3 VALU per B dword,
-// ~26 per K-step for 16 MFMAs (was ~56 with one expansion per input byte).
+// into one dword W (one shift-or + one v_perm per tile), and B dword q is bit plane q of W masked
+// in place (kAOne below) — 1-2 VALU per B dword, 14 per K-step for 16 MFMAs (26 with one v_perm
+// pool lookup per dword, ~56 with one expansion per input byte).
 // Output bits are placed on MFMA rows exactly as in gf_mfma.hip so every lane owns whole bytes;
 // each accumulator starts at a bias that puts the parity of its f32 count on its output bit (see
 // bias_scale_of_lane).
@@ -49,10 +49,18 @@ __device__ __forceinline__ uint8_t dmul(uint8_t a, uint8_t b) { return d_tab.exp
 __host__ __device__ constexpr int out_row_of(int r) { return 2 * ((r >> 2) & 1) + (r >> 4); }
 __host__ __device__ constexpr int out_bit_of(int r) { return ((r >> 3) & 1) * 4 + (r & 3); }
 
+// B operand: dword q of a lane is bit plane {q, q + 4} of W (its 4 input bytes of the step, rows
+// 4h..4h+3 of its column) masked in place, with no shift into a common nibble position:
+// q = 0: W & 0x11111111 (FP4 0.5), q = 1: W & 0x22222222 (1.0), q = 2: W & 0x44444444 (2.0),
+// q = 3: (W >> 1) & 0x44444444 (2.0). The A entry at such a K index is the reciprocal weight
+// (2.0 / 1.0 / 0.5 / 0.5, all exact e2m1), so every product is exactly 0 or 1 and the f32 sum is
+// still the integer count whose parity is the GF(2) result.
+constexpr uint8_t kAOne[4] = {0x4, 0x2, 0x1, 0x1};
+
 // bitmat layout: [group][kstep][mt < MG][lane][16 bytes]; element j = nibble j of the 16 bytes (one
 // K-step's MG fragments are contiguous, so the kernel reads them with immediate LDS offsets).
-// K order inside a step (lane half h): nibble j <-> input row 8s + 4h + ((j >> 1) & 3), bit
-// 2 (j >> 3) + (j & 1) — the order the kernel's expansion produces (expand() below).
+// K order inside a step (lane half h): nibble j <-> input row 8s + 4h + ((j & 7) >> 1), bit
+// (j >> 3) + 4 (j & 1) — the order the kernel's expansion produces (expand() below).
 // coefficient (o, i) = coeff[row(o) * ld + i], row(o) = sel ? sel[o] : o (sel: rows of a device
 // matrix, e.g. the erased-native rows of a device-computed inverse)
 __global__ void fp4_bitmat_kernel(const uint8_t* __restrict__ coeff, int ld, const int* __restrict__ sel, int m, int k,
@@ -73,21 +81,16 @@ __global__ void fp4_bitmat_kernel(const uint8_t* __restrict__ coeff, int ld, con
     uint8_t v = 0;
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
-      const int j = 2 * q + half;
-      const int irow = 8 * s + 4 * h + ((j >> 1) & 3);
-      const int ibit = 2 * (j >> 3) + (j & 1);
+      const int j = 2 * q + half;       // nibble j: B dword j >> 3, nibble j & 7 of it
+      const int dq = j >> 3, jj = j & 7;
+      const int irow = 8 * s + 4 * h + (jj >> 1);
+      const int ibit = dq + 4 * (jj & 1);
       if (orow < m && irow < k &&
           ((dmul(coeff[size_t(sel ? sel[orow] : orow) * ld + irow], uint8_t(1u << ibit)) >> obit) & 1))
-        v |= uint8_t(0x2u << (4 * half));
+        v |= uint8_t(kAOne[dq] << (4 * half));
     }
     bitmat[idx] = v;
   }
-}
-
-// B dword q of one tile from W (byte b = input row 4h + b of the step, this tile's column): byte b
-// of the result is pool[bits (2q, 2q+1) of W.b] = two FP4 nibbles 0x0 / 0x2 (0.0 / 1.0).
-__device__ __forceinline__ int expand_q(uint32_t w, int q) {
-  return int(__builtin_amdgcn_perm(0u, 0x22200200u, (w >> (2 * q)) & 0x03030303u));
 }
 
 // (a & mask) | (b & ~mask) as ONE v_bfi_b32 (written as C the compiler splits it into and + or3)
@@ -271,17 +274,18 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4_kernel(cptr<uint64_t> in, 
   };
 
   // B operands of a K-step from its 4 ring words: W_t = the 4 rows' bytes of column 2c + t (two
-  // shift-ors and two v_perm for both tiles), then one v_perm per B dword. Rows >= k hold finite
-  // garbage (the DMA clamps to row k-1) that meets zero bit-matrix columns, so no masking.
-  constexpr int kExpandValu = 26;
+  // shift-ors and two v_perm for both tiles), then the bit planes of W_t masked in place (kAOne).
+  // Rows >= k hold finite garbage (the DMA clamps to row k-1) that meets zero bit-matrix columns.
+  constexpr int kExpandValu = 14;
   auto expand = [&](i32x4 (&bo)[NTW], const uint32_t (&x)[4]) __attribute__((always_inline)) {
     const uint32_t p01 = x[0] | (x[1] << 16), p23 = x[2] | (x[3] << 16);
-    const uint32_t w0 = __builtin_amdgcn_perm(p23, p01, 0x06040200u);
-    const uint32_t w1 = __builtin_amdgcn_perm(p23, p01, 0x07050301u);
+    const uint32_t w[2] = {__builtin_amdgcn_perm(p23, p01, 0x06040200u), __builtin_amdgcn_perm(p23, p01, 0x07050301u)};
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      bo[0][q] = expand_q(w0, q);
-      bo[1][q] = expand_q(w1, q);
+    for (int t = 0; t < NTW; ++t) {
+      bo[t][0] = int(w[t] & 0x11111111u);
+      bo[t][1] = int(w[t] & 0x22222222u);
+      bo[t][2] = int(w[t] & 0x44444444u);
+      bo[t][3] = int((w[t] >> 1) & 0x44444444u);
     }
   };
 
