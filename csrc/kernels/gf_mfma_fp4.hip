@@ -160,7 +160,11 @@ __device__ __forceinline__ void tie(T& v) {
 // copy stores (COPY; the prologue issues dummy ones to the sink so the pattern holds from slot 0)
 // and, in the first slots of a chunk, the previous chunk's 2*MG epilogue stores. A count that
 // ignored the stores (as before) also waited for them: a store-latency bubble at every chunk start.
-template <int MG, bool UNI, bool COPY, int kRing>
+//
+// KS > 0: the chunk's slot count is the compile-time KS (= ksteps / kSPS) and a multiple of kRing,
+// so every chunk starts at ring slot 0: the slot loop unrolls and every ring position, DMA cursor
+// and bit-matrix step is a constant (LDS immediates, no cursor bookkeeping per slot).
+template <int MG, bool UNI, bool COPY, int kRing, int KS>
 __global__ __launch_bounds__(256, 1) void gf_gemm_fp4_kernel(cptr<uint64_t> in, cptr<uint64_t> out, cptr<uint64_t> copy,
                                                              const i32x4* __restrict__ bitmat, int k, int m,
                                                              int ksteps, int groups, int64_t col0, int64_t nchunks,
@@ -171,6 +175,8 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4_kernel(cptr<uint64_t> in, 
   constexpr int kRS = kSlotBytes / kCW;  // input rows per ring slot (16)
   constexpr int kSPS = kRS / 8;          // K-steps per ring slot (2)
   constexpr int kLPR = kCW / 16;         // DMA lanes per row (4)
+  constexpr bool kStatic = KS > 0;
+  static_assert(!kStatic || KS % kRing == 0, "KS must be a multiple of the ring depth");
   constexpr int kCopyN = COPY ? kRing - 2 : 0;
   // younger ops than the awaited DMA in steady state, and with the previous chunk's epilogue
   // stores (clamped to the 6-bit counter: a smaller count only waits longer)
@@ -220,7 +226,7 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4_kernel(cptr<uint64_t> in, 
   const int bias_scale = bias_scale_of_lane(lane);
   const i32x8 one_k0 = {h == 0 ? 0x2 : 0, 0, 0, 0, 0, 0, 0, 0};  // 1.0 at K index 0 (A and B)
   const int my_chunks = int((nchunks - slot0 + chunk_slots - 1) / chunk_slots);
-  const int kslots = ksteps / kSPS;
+  const int kslots = kStatic ? KS : ksteps / kSPS;
   if (my_chunks <= 0) return;
   const uint64_t in0 = UNI ? in[0] : 0;
   const int drow = lane / kLPR;  // this lane's row within a DMA'd slot
@@ -441,6 +447,13 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4_kernel(cptr<uint64_t> in, 
   // next one) and the A fragments of the next step. Reads past the last step hit valid LDS and are
   // discarded.
   auto slot_run = [&](int sp, int ci, auto last_tag) __attribute__((always_inline)) {
+    if constexpr (kStatic) {  // the cursor of slot sp as constants (see the KS note above)
+      constexpr int lead = kRing - 1;
+      r_slot = sp % kRing;
+      d_p = (sp + lead) % KS;
+      d_slot = (sp + lead) % kRing;
+      d_chunk = ci + (sp + lead) / KS;
+    }
     dma_issue();
     if (!UNI) ptr_async();
     const int s0 = kSPS * sp;
@@ -467,7 +480,7 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4_kernel(cptr<uint64_t> in, 
         read_x(x2, r_slot, j + 2);
       else
         read_x(x2, slot1, j + 2 - kSPS);
-      read_a(an, s0 + j + 1 == ksteps ? 0 : s0 + j + 1);
+      read_a(an, s0 + j + 1 == kSPS * kslots ? 0 : s0 + j + 1);
       step(s0 + j);  // (the first step's closing lgkmcnt(0) also retires the copy / pointer reads)
       if (j == 0) {
         if (!UNI) tie(pn);
@@ -484,8 +497,14 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4_kernel(cptr<uint64_t> in, 
   };
 
   for (int ci = 0; ci < my_chunks; ++ci) {
-    for (int sp = 0; sp < kslots - 1; ++sp) slot_run(sp, ci, rest_t{});
-    slot_run(kslots - 1, ci, last_t{});
+    if constexpr (kStatic) {
+#pragma unroll
+      for (int sp = 0; sp < KS - 1; ++sp) slot_run(sp, ci, rest_t{});
+      slot_run(KS - 1, ci, last_t{});
+    } else {
+      for (int sp = 0; sp < kslots - 1; ++sp) slot_run(sp, ci, rest_t{});
+      slot_run(kslots - 1, ci, last_t{});
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA (dummy or not) outlives the wave
 }
@@ -525,10 +544,10 @@ int cu_count() {
   return n;
 }
 
-template <int MG, bool UNI, bool COPY, int R>
+template <int MG, bool UNI, bool COPY, int R, int KS>
 const void* fp4_fn() {
   static const void* fn = [] {
-    const void* f = reinterpret_cast<const void*>(&gf_gemm_fp4_kernel<MG, UNI, COPY, R>);
+    const void* f = reinterpret_cast<const void*>(&gf_gemm_fp4_kernel<MG, UNI, COPY, R, KS>);
     (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     return f;
   }();
@@ -536,12 +555,12 @@ const void* fp4_fn() {
 }
 
 // co-resident blocks per CU of the ring-depth-R kernel (LDS and VGPR bound); 0 if it does not fit
-template <int MG, bool UNI, bool COPY, int R>
+template <int MG, bool UNI, bool COPY, int R, int KS>
 int fp4_occupancy(size_t fixed) {
   const size_t lds = fixed + ring_lds(R);
   if (lds > 160 * 1024) return 0;
   int occ = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fp4_fn<MG, UNI, COPY, R>(), 256, lds) != hipSuccess)
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fp4_fn<MG, UNI, COPY, R, KS>(), 256, lds) != hipSuccess)
     return 0;
   return occ;
 }
@@ -553,38 +572,34 @@ struct Fp4Args {
   int64_t col0, nchunks, in_stride;
 };
 
-template <int MG, bool UNI, bool COPY, int R>
+template <int MG, bool UNI, bool COPY, int R, int KS>
 hipError_t launch_fp4(const Fp4Geometry& geo, int occ, const Fp4Args& a, hipStream_t stream) {
   // a persistent grid: as many blocks as are co-resident, chunk slots a multiple of 8 so each
   // slot stays on one XCD
   const size_t lds = geo.fixed + ring_lds(R);
-  (void)fp4_fn<MG, UNI, COPY, R>();
+  (void)fp4_fn<MG, UNI, COPY, R, KS>();
   int64_t slots = std::max<int64_t>(8, (int64_t(cu_count()) * occ / geo.groups) / 8 * 8);
   slots = std::min<int64_t>(slots, (a.nchunks + 7) / 8 * 8);
   const unsigned blocks = unsigned(slots * geo.groups);
-  gf_gemm_fp4_kernel<MG, UNI, COPY, R><<<blocks, 256, lds, stream>>>(
+  gf_gemm_fp4_kernel<MG, UNI, COPY, R, KS><<<blocks, 256, lds, stream>>>(
       a.in, a.out, a.copy, static_cast<const i32x4*>(a.bitmat), a.k, a.m, geo.ksteps, geo.groups, a.col0, a.nchunks,
       slots, a.in_stride);
   return hipGetLastError();
 }
 
-template <int MG, bool UNI, bool COPY>
+template <int MG, bool UNI, bool COPY, int KS, int... Rs>
 hipError_t launch_fp4_ring(const Fp4Geometry& geo, const Fp4Args& a, hipStream_t stream) {
-  // ring depth: the most blocks per CU first (up to 4), then — at equal occupancy — a ring that
-  // leaves kSideReserve of the CU's LDS free (measured: DMA latency costs ~2 % at ring 6,
-  // profiles/r01_s3; a full-LDS persistent grid instead locks the side-stream decode solve out of
-  // every CU until the GEMM ends), then the deepest ring. Cached per A size.
-  constexpr int kN = 6;
-  constexpr int rings[kN] = {32, 16, 12, 8, 6, 4};
+  // ring depth (candidates Rs, deepest first): the most blocks per CU first (up to 4), then — at
+  // equal occupancy — a ring that leaves kSideReserve of the CU's LDS free (measured: DMA latency
+  // costs ~2 % at ring 6, profiles/r01_s3; a full-LDS persistent grid instead locks the
+  // side-stream decode solve out of every CU until the GEMM ends), then the deepest ring. Cached
+  // per A size.
+  constexpr int kN = sizeof...(Rs);
+  constexpr int rings[kN] = {Rs...};
   static int choice[161][2];  // [fixed KiB] -> {ring index + 1, occupancy}
   int (&ch)[2] = choice[std::min<size_t>(geo.fixed / 1024, 160)];
   if (!ch[0]) {
-    const int occs[kN] = {fp4_occupancy<MG, UNI, COPY, rings[0]>(geo.fixed),
-                          fp4_occupancy<MG, UNI, COPY, rings[1]>(geo.fixed),
-                          fp4_occupancy<MG, UNI, COPY, rings[2]>(geo.fixed),
-                          fp4_occupancy<MG, UNI, COPY, rings[3]>(geo.fixed),
-                          fp4_occupancy<MG, UNI, COPY, rings[4]>(geo.fixed),
-                          fp4_occupancy<MG, UNI, COPY, rings[5]>(geo.fixed)};
+    const int occs[kN] = {fp4_occupancy<MG, UNI, COPY, Rs, KS>(geo.fixed)...};
     auto reserve_ok = [&](int i) { return geo.fixed + ring_lds(rings[i]) + kSideReserve <= 160 * 1024; };
     int best = -1;
     for (int i = 0; i < kN; ++i) {
@@ -597,23 +612,26 @@ hipError_t launch_fp4_ring(const Fp4Geometry& geo, const Fp4Args& a, hipStream_t
     ch[0] = best + 1;
     ch[1] = occs[best];
   }
-  const int occ = ch[1];
-  switch (ch[0] - 1) {
-    case 0: return launch_fp4<MG, UNI, COPY, rings[0]>(geo, occ, a, stream);
-    case 1: return launch_fp4<MG, UNI, COPY, rings[1]>(geo, occ, a, stream);
-    case 2: return launch_fp4<MG, UNI, COPY, rings[2]>(geo, occ, a, stream);
-    case 3: return launch_fp4<MG, UNI, COPY, rings[3]>(geo, occ, a, stream);
-    case 4: return launch_fp4<MG, UNI, COPY, rings[4]>(geo, occ, a, stream);
-    default: return launch_fp4<MG, UNI, COPY, rings[5]>(geo, occ, a, stream);
-  }
+  hipError_t err = hipErrorInvalidConfiguration;
+  int i = 0;
+  ((i++ == ch[0] - 1 ? (err = launch_fp4<MG, UNI, COPY, Rs, KS>(geo, ch[1], a, stream), 0) : 0), ...);
+  return err;
+}
+
+// k in (112, 128] (8 ring slots per chunk, the BASELINE wide stripe): the unrolled static-cursor
+// kernel with the rings that divide 8; any other k: the runtime-cursor kernel
+template <int MG, bool UNI, bool COPY>
+hipError_t launch_fp4_var(const Fp4Geometry& geo, const Fp4Args& a, hipStream_t stream) {
+  if (geo.ksteps == 16) return launch_fp4_ring<MG, UNI, COPY, 8, 8, 4>(geo, a, stream);
+  return launch_fp4_ring<MG, UNI, COPY, 0, 32, 16, 12, 8, 6, 4>(geo, a, stream);
 }
 
 // variants: uniform-stride inputs (encode), scattered inputs, scattered inputs + fused copy (decode)
 template <int MG>
 hipError_t launch_fp4_any(const Fp4Geometry& geo, const Fp4Args& a, hipStream_t stream) {
-  if (a.copy) return launch_fp4_ring<MG, false, true>(geo, a, stream);
-  return a.in_stride ? launch_fp4_ring<MG, true, false>(geo, a, stream)
-                     : launch_fp4_ring<MG, false, false>(geo, a, stream);
+  if (a.copy) return launch_fp4_var<MG, false, true>(geo, a, stream);
+  return a.in_stride ? launch_fp4_var<MG, true, false>(geo, a, stream)
+                     : launch_fp4_var<MG, false, false>(geo, a, stream);
 }
 
 }  // namespace

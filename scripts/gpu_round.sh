@@ -29,4 +29,5 @@ step stream_decode 300 bash -c "printf '/tmp/_%d_rs_in.bin\n' 0 2 3 5 6 8 10 11 
 step inmem_encode 300 bin/RS -k 10 -n 14 -e /tmp/rs_in.bin -s 4 &&
 step prof_stream 300 rocprofv3 --kernel-trace --marker-trace --stats -d $O/prof_stream -o run --output-format csv -- bin/RS -k 10 -n 14 -e /tmp/rs_in.bin --window 0 --no-sync -s 4 &&
 step prof_bench 300 rocprofv3 --kernel-trace --marker-trace --stats -d $O/prof_bench -o run --output-format csv -- python3 bench.py --steps 20 &&
+step prof_k128n160 300 rocprofv3 --kernel-trace --stats -d $O/prof_k128n160 -o run --output-format csv -- python3 bench.py --preset k128n160 --steps 20 &&
 echo ROUND-OK | tee -a $O/progress.log
