@@ -4,7 +4,7 @@
 set -euo pipefail
 cd "$(dirname "$0")"
 ROOT=..
-make -C "$ROOT/csrc" -j8 >/dev/null
+[ -x "$ROOT/bin/RS" ] && [ -x "$ROOT/bin/CPU-RS" ] || make -C "$ROOT/csrc" -j8 >/dev/null
 RS="$ROOT/bin/RS"
 if ! "$ROOT/bin/RS" -h >/dev/null 2>&1 || ! python3 -c "import torch,sys; sys.exit(0 if torch.cuda.is_available() else 1)"; then
   RS="$ROOT/bin/CPU-RS"
