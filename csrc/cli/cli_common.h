@@ -9,6 +9,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <string>
+#include <vector>
 
 namespace gfrs_cli {
 
@@ -21,6 +22,7 @@ struct Args {
   std::string matrix = "vandermonde";
   std::string mul = "row";
   int gpus = 0;  // 0 = all visible
+  std::vector<int> devices;  // --devices 0,1,...: explicit shard -> device list (entries may repeat)
   int threads = 1;
   long long slice = 16ll << 20;
   bool cpu_meta = false;
@@ -57,6 +59,7 @@ inline void usage(const char* prog, bool gpu) {
   std::printf("  -q                      quiet\n");
   if (gpu) {
     std::printf("  --gpus N                number of GPUs (default: all visible)\n");
+    std::printf("  --devices I,J,...       explicit column-shard -> device list (a device may repeat)\n");
     std::printf("  --slice BYTES           column slice per stream step (default 16 MiB)\n");
   } else {
     std::printf("  --mul logexp|logexp0|logexp1|logexp2|logexp3|loop|full|double|perm|row\n");
@@ -97,6 +100,7 @@ inline Args parse(int argc, char** argv, bool gpu) {
                                     {"window", required_argument, nullptr, 8},
                                     {"no-resume", no_argument, nullptr, 9},
                                     {"no-sync", no_argument, nullptr, 10},
+                                    {"devices", required_argument, nullptr, 11},
                                     {"help", no_argument, nullptr, 'h'},
                                     {nullptr, 0, nullptr, 0}};
   int c;
@@ -122,6 +126,18 @@ inline Args parse(int argc, char** argv, bool gpu) {
       case 8: a.window = to_ll(optarg, "window bytes", 0); break;
       case 9: a.resume = false; break;
       case 10: a.sync = false; break;
+      case 11: {
+        std::string list = optarg ? optarg : "";
+        size_t pos = 0;
+        while (pos <= list.size()) {
+          const size_t comma = list.find(',', pos);
+          const std::string item = list.substr(pos, comma == std::string::npos ? std::string::npos : comma - pos);
+          a.devices.push_back(to_int(item.c_str(), "device index", 0));
+          if (comma == std::string::npos) break;
+          pos = comma + 1;
+        }
+        break;
+      }
       case 'h': default: usage(argv[0], gpu); std::exit(c == 'h' ? 0 : 2);
     }
   }

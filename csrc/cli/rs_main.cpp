@@ -7,9 +7,11 @@
 
 #include <cstdio>
 #include <exception>
+#include <memory>
 #include <stdexcept>
 
 #include "cli_common.h"
+#include "gfrs/async_prepare.h"
 #include "gfrs/codec_file.h"
 #include "gfrs/format.h"
 #include "gfrs/pipeline.h"
@@ -48,6 +50,12 @@ int main(int argc, char** argv) {
     if (a.gpus > 0 && a.gpus < ndev) ndev = a.gpus;
     std::vector<int> devices(ndev);
     for (int d = 0; d < ndev; ++d) devices[d] = d;
+    if (!a.devices.empty()) {
+      for (int d : a.devices)
+        if (d >= ndev) throw std::runtime_error("--devices: device " + std::to_string(d) + " is not visible");
+      devices = a.devices;
+      ndev = int(devices.size());
+    }
 
     PipelineOptions opt;
     opt.streams = a.streams;
@@ -55,8 +63,19 @@ int main(int argc, char** argv) {
     opt.slice_bytes = a.slice;
     const bool enc = a.op == gfrs_cli::Args::kEncode;
     const char* verb = enc ? "encoding" : "decoding";
+    // device setup overlapped with the input reads (gfrs/async_prepare.h); the streaming codec sizes
+    // its windows itself and prepares on its first window
+    std::unique_ptr<AsyncPrepare> prep;
+    if (!a.streaming())
+      prep = enc ? prepare_for_encode(devices, opt, a.in_file, a.k, a.n - a.k)
+                 : prepare_for_decode(devices, opt, a.in_file);
     const GemmFn gemm = [&](const std::vector<const uint8_t*>& in, const std::vector<uint8_t*>& out,
                             const Mat& coeff, int64_t ncols) {
+      if (prep) {
+        const double ms = prep->wait();
+        if (!a.quiet) std::printf("GPU pipeline setup (overlapped with the file reads): %fms\n", ms);
+        prep.reset();
+      }
       std::vector<PipelineStats> st;
       double wall = 0;
       check(gemm_host_multi(devices, in, out, coeff, ncols, opt, &st, &wall), "GPU pipeline");

@@ -6,8 +6,9 @@
 //   * no event on the legacy default stream and no host sync inside the loop (the reference's
 //     encode_chunk blocks on cudaEventSynchronize every slice, src/matrix.cu:805-809, which is why
 //     its authors saw multi-stream *degrade*, doc/design.tex:530);
-//   * the slice ring is larger than the stream count, so copy engines (SDMA) stay busy while the
-//     previous slice's kernel runs; buffers are reused round-robin in stream order;
+//   * every lane ("stream" of -s) owns two slice buffers and two HIP streams — copy-in (H2D) and
+//     compute (kernel + D2H) — handing slots over with events, so even -s 1 overlaps the H2D of
+//     slice t+1 with the kernel and D2H of slice t (SDMA engines busy in both directions);
 //   * host rows are used in place (no H2H staging copies, src/encode.cu:389-398,410-429); pinned
 //     rows give true async DMA;
 //   * streams, slice buffers and descriptors persist per device across calls (PipelineOptions::
@@ -18,6 +19,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <utility>
 #include <vector>
 
 #include "gfrs/matrix.h"
@@ -39,11 +41,23 @@ struct PipelineStats {
   double ms_total = 0;     // everything (the reference's "Total GPU encoding time")
   int64_t bytes_h2d = 0, bytes_d2h = 0;
   int slices = 0;
+  int lanes = 0;
 };
 
 // out_rows[i][c] = XOR_j coeff[i][j] * in_rows[j][c] for c in [c0, c1) on `device`.
 hipError_t gemm_host(int device, const std::vector<const uint8_t*>& in_rows, const std::vector<uint8_t*>& out_rows,
                      const Mat& coeff, int64_t c0, int64_t c1, const PipelineOptions& opt, PipelineStats* stats);
+
+// Creates the device's streams, events and slice buffers for a later gemm_host over `ncols` columns
+// of k inputs / m outputs with `opt` (persistent workspace), and loads the kernels — so a caller can
+// overlap device setup with its file reads and keep it out of the timed GPU region.
+hipError_t prepare_pipeline(int device, int k, int m, int64_t ncols, const PipelineOptions& opt);
+// prepare_pipeline on every device for the shards gemm_host_multi will give it.
+hipError_t prepare_pipeline_multi(const std::vector<int>& devices, int k, int m, int64_t ncols,
+                                  const PipelineOptions& opt);
+
+// Column shard [first, second) of device index d of `devices` (4 KiB aligned, remainder last).
+std::pair<int64_t, int64_t> device_shard(int64_t ncols, int devices, int d);
 
 // Frees every persistent per-device workspace (streams, slice buffers, descriptors).
 hipError_t release_workspaces();

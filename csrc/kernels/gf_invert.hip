@@ -21,6 +21,7 @@
 #include <hip/hip_runtime.h>
 
 #include "gfrs/desc.h"
+#include "gfrs/device_cache.h"
 #include "gfrs/kernels.h"
 
 namespace gfrs {
@@ -357,12 +358,9 @@ hipError_t launch_gf_decode_system(const uint8_t* g, int k, const int* rows, con
   if (desc) tab = reinterpret_cast<uint32_t*>(static_cast<char*>(desc) + desc_layout(k, m_pad).tab_off);
   // (256 lanes for every e: the system gather and the decode-table emission are O(e k) loads /
   // stores that one wave serialised — 135 us at k=128, e=32)
-  static bool attr_set = false;
-  if (lds > 65536 && !attr_set) {
-    const hipError_t err = hipFuncSetAttribute(reinterpret_cast<const void*>(&gf_decode_system_kernel<256>),
-                                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  if (lds > 65536) {  // per device (one process may drive several GPUs from several threads)
+    const hipError_t err = ensure_lds_optin(reinterpret_cast<const void*>(&gf_decode_system_kernel<256>));
     if (err != hipSuccess) return err;
-    attr_set = true;
   }
   gf_decode_system_kernel<256><<<1, 256, lds, stream>>>(g, k, rows, erased, e, dm, status, tab, m_pad);
   return hipGetLastError();
@@ -380,12 +378,9 @@ hipError_t launch_gf_invert(const uint8_t* a, uint8_t* a_inv, int n, int batch, 
     gf_invert_kernel<64><<<batch, 64, lds, stream>>>(a, a_inv, n, status, tab, sel_rows, m, m_pad);
     return hipGetLastError();
   }
-  static bool attr_set = false;  // >64 KiB of dynamic LDS must be opted into once per process
-  if (lds > 65536 && !attr_set) {
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gf_invert_kernel<256>),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  if (lds > 65536) {  // >64 KiB of dynamic LDS is opted into once per device
+    const hipError_t e = ensure_lds_optin(reinterpret_cast<const void*>(&gf_invert_kernel<256>));
     if (e != hipSuccess) return e;
-    attr_set = true;
   }
   gf_invert_kernel<256><<<batch, 256, lds, stream>>>(a, a_inv, n, status, tab, sel_rows, m, m_pad);
   return hipGetLastError();

@@ -26,6 +26,7 @@
 #include <algorithm>
 
 #include "gfrs/desc.h"
+#include "gfrs/device_cache.h"
 #include "gfrs/kernels.h"
 
 namespace gfrs {
@@ -193,12 +194,9 @@ hipError_t launch_gf_gemm_mfma(const void* bitmat, const void* desc, int k, int 
     int64_t slots = std::max<int64_t>(8, (512 / groups) / 8 * 8);
     slots = std::min<int64_t>(slots, (nchunks + 7) / 8 * 8);
     const size_t lds = size_t(kMTW) * ksteps * 64 * 16;
-    static bool attr_set = false;
-    if (lds > 65536 && !attr_set) {
-      const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gf_gemm_mfma_kernel),
-                                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (lds > 65536) {  // per device
+      const hipError_t e = ensure_lds_optin(reinterpret_cast<const void*>(&gf_gemm_mfma_kernel));
       if (e != hipSuccess) return e;
-      attr_set = true;
     }
     const unsigned blocks = unsigned(slots * groups);
     gf_gemm_mfma_kernel<<<blocks, 256, lds, stream>>>(

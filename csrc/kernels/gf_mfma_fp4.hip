@@ -25,6 +25,7 @@
 #include <type_traits>
 
 #include "gfrs/desc.h"
+#include "gfrs/device_cache.h"
 #include "gfrs/kernels.h"
 
 namespace gfrs {
@@ -534,24 +535,13 @@ Fp4Geometry geometry(int k, int m, int mg_cap, bool copy = false) {
   return g;
 }
 
-int cu_count() {
-  static int n = 0;
-  if (!n) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
-      n = 256;
-  }
-  return n;
-}
-
+// the kernel's address, opted into the full 160 KiB of LDS on the current device (per device:
+// one process may drive several GPUs, gfrs/device_cache.h)
 template <int MG, bool UNI, bool COPY, int R, int KS>
 const void* fp4_fn() {
-  static const void* fn = [] {
-    const void* f = reinterpret_cast<const void*>(&gf_gemm_fp4_kernel<MG, UNI, COPY, R, KS>);
-    (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    return f;
-  }();
-  return fn;
+  const void* f = reinterpret_cast<const void*>(&gf_gemm_fp4_kernel<MG, UNI, COPY, R, KS>);
+  (void)ensure_lds_optin(f);
+  return f;
 }
 
 // co-resident blocks per CU of the ring-depth-R kernel (LDS and VGPR bound); 0 if it does not fit
@@ -578,7 +568,7 @@ hipError_t launch_fp4(const Fp4Geometry& geo, int occ, const Fp4Args& a, hipStre
   // slot stays on one XCD
   const size_t lds = geo.fixed + ring_lds(R);
   (void)fp4_fn<MG, UNI, COPY, R, KS>();
-  int64_t slots = std::max<int64_t>(8, (int64_t(cu_count()) * occ / geo.groups) / 8 * 8);
+  int64_t slots = std::max<int64_t>(8, (int64_t(device_cu_count()) * occ / geo.groups) / 8 * 8);
   slots = std::min<int64_t>(slots, (a.nchunks + 7) / 8 * 8);
   const unsigned blocks = unsigned(slots * geo.groups);
   gf_gemm_fp4_kernel<MG, UNI, COPY, R, KS><<<blocks, 256, lds, stream>>>(
@@ -596,9 +586,9 @@ hipError_t launch_fp4_ring(const Fp4Geometry& geo, const Fp4Args& a, hipStream_t
   // per A size.
   constexpr int kN = sizeof...(Rs);
   constexpr int rings[kN] = {Rs...};
-  static int choice[161][2];  // [fixed KiB] -> {ring index + 1, occupancy}
-  int (&ch)[2] = choice[std::min<size_t>(geo.fixed / 1024, 160)];
-  if (!ch[0]) {
+  // per (device, A size in KiB) -> {ring index + 1 (0 = nothing fits), occupancy}
+  static DeviceMemo<size_t, std::pair<int, int>> choice;
+  const std::pair<int, int> ch = choice.get_or(geo.fixed / 1024, [&] {
     const int occs[kN] = {fp4_occupancy<MG, UNI, COPY, Rs, KS>(geo.fixed)...};
     auto reserve_ok = [&](int i) { return geo.fixed + ring_lds(rings[i]) + kSideReserve <= 160 * 1024; };
     int best = -1;
@@ -608,13 +598,12 @@ hipError_t launch_fp4_ring(const Fp4Geometry& geo, const Fp4Args& a, hipStream_t
           (std::min(occs[i], 4) == std::min(occs[best], 4) && reserve_ok(i) && !reserve_ok(best)))
         best = i;
     }
-    if (best < 0) return hipErrorInvalidConfiguration;
-    ch[0] = best + 1;
-    ch[1] = occs[best];
-  }
+    return best < 0 ? std::pair<int, int>{0, 0} : std::pair<int, int>{best + 1, occs[best]};
+  });
+  if (ch.first == 0) return hipErrorInvalidConfiguration;
   hipError_t err = hipErrorInvalidConfiguration;
   int i = 0;
-  ((i++ == ch[0] - 1 ? (err = launch_fp4<MG, UNI, COPY, Rs, KS>(geo, ch[1], a, stream), 0) : 0), ...);
+  ((i++ == ch.first - 1 ? (err = launch_fp4<MG, UNI, COPY, Rs, KS>(geo, ch.second, a, stream), 0) : 0), ...);
   return err;
 }
 

@@ -6,6 +6,7 @@
 #include <stdexcept>
 
 #include "bind_common.h"
+#include "gfrs/async_prepare.h"
 #include "gfrs/kernels.h"
 #include "gfrs/pipeline.h"
 
@@ -25,7 +26,16 @@ py::dict stats_dict(const gfrs::PipelineStats& s) {
   d["bytes_h2d"] = s.bytes_h2d;
   d["bytes_d2h"] = s.bytes_d2h;
   d["slices"] = s.slices;
+  d["lanes"] = s.lanes;
   return d;
+}
+
+gfrs::PipelineOptions pipeline_options(int streams, int64_t slice, int max_blocks) {
+  gfrs::PipelineOptions opt;
+  opt.streams = streams;
+  opt.slice_bytes = slice;
+  opt.max_blocks = max_blocks;
+  return opt;
 }
 
 gfrs::HostAlloc pinned_alloc() {
@@ -173,25 +183,44 @@ PYBIND11_MODULE(_hip, m) {
       py::arg("devices"), py::arg("in_ptrs"), py::arg("out_ptrs"), py::arg("coeff"), py::arg("ncols"),
       py::arg("streams") = 2, py::arg("slice") = 16 << 20, py::arg("max_blocks") = 0, py::arg("bytewise") = false);
 
-  auto gpu_gemm = [](const std::vector<int>& devices, int streams, int64_t slice, int max_blocks) -> GemmFn {
+  // `prep` (optional): setup started before the file reads; waited for on the first call
+  m.def(
+      "prepare_pipeline",
+      [](const std::vector<int>& devices, int k, int mm, int64_t ncols, int streams, int64_t slice) {
+        hipError_t e;
+        {
+          py::gil_scoped_release nogil;
+          e = prepare_pipeline_multi(devices, k, mm, ncols, pipeline_options(streams, slice, 0));
+        }
+        check(e, "prepare_pipeline");
+      },
+      py::arg("devices"), py::arg("k"), py::arg("m"), py::arg("ncols"), py::arg("streams") = 2,
+      py::arg("slice") = 16 << 20);
+  m.def("device_shard", [](int64_t ncols, int devices, int d) { return device_shard(ncols, devices, d); });
+
+  auto gpu_gemm = [](const std::vector<int>& devices, int streams, int64_t slice, int max_blocks,
+                     std::unique_ptr<AsyncPrepare>* prep = nullptr) -> GemmFn {
     return [=](const std::vector<const uint8_t*>& in, const std::vector<uint8_t*>& out, const Mat& coeff,
                int64_t ncols) {
-      PipelineOptions opt;
-      opt.streams = streams;
-      opt.slice_bytes = slice;
-      opt.max_blocks = max_blocks;
-      check(gemm_host_multi(devices, in, out, coeff, ncols, opt, nullptr, nullptr), "GPU pipeline");
+      if (prep && *prep) {
+        (*prep)->wait();
+        prep->reset();
+      }
+      check(gemm_host_multi(devices, in, out, coeff, ncols, pipeline_options(streams, slice, max_blocks), nullptr,
+                            nullptr),
+            "GPU pipeline");
     };
   };
   m.def(
       "encode_file",
       [gpu_gemm](const std::string& file, int k, int p, const std::string& matrix, bool cpu_meta,
                  const std::vector<int>& devices, int streams, int64_t slice, int max_blocks) {
-        const GemmFn g = gpu_gemm(devices, streams, slice, max_blocks);
         FileReport r;
         {
           py::gil_scoped_release nogil;
-          r = encode_file(file, k, p, parse_matrix_kind(matrix), g, pinned_alloc(), cpu_meta);
+          auto prep = prepare_for_encode(devices, pipeline_options(streams, slice, max_blocks), file, k, p);
+          r = encode_file(file, k, p, parse_matrix_kind(matrix), gpu_gemm(devices, streams, slice, max_blocks, &prep),
+                          pinned_alloc(), cpu_meta);
         }
         return report(r);
       },
@@ -202,11 +231,11 @@ PYBIND11_MODULE(_hip, m) {
       "decode_file",
       [gpu_gemm](const std::string& file, const std::string& conf, const std::string& out,
                  const std::vector<int>& devices, int streams, int64_t slice, int max_blocks) {
-        const GemmFn g = gpu_gemm(devices, streams, slice, max_blocks);
         FileReport r;
         {
           py::gil_scoped_release nogil;
-          r = decode_file(file, conf, out, g, pinned_alloc());
+          auto prep = prepare_for_decode(devices, pipeline_options(streams, slice, max_blocks), file);
+          r = decode_file(file, conf, out, gpu_gemm(devices, streams, slice, max_blocks, &prep), pinned_alloc());
         }
         return report(r);
       },

@@ -26,17 +26,31 @@ double ms_since(Clock::time_point t0) {
     if (e__ != hipSuccess) return e__;   \
   } while (0)
 
-struct Lane {
-  hipStream_t stream = nullptr;
+constexpr int kSlots = 2;  // slice buffers per lane: H2D of one overlaps kernel + D2H of the other
+
+// One slice buffer set: k input rows, m output rows, the GEMM descriptor pointing at them, and the
+// two events that hand it between the lane's copy-in and compute streams.
+struct Slot {
   uint8_t* in = nullptr;   // k x slice
   uint8_t* out = nullptr;  // m x slice
   void* desc = nullptr;
   size_t in_cap = 0, out_cap = 0, desc_cap = 0;
   std::vector<uint8_t> desc_host;  // what `desc` holds (skip identical re-uploads)
+  hipEvent_t loaded = nullptr;     // H2D of the slice done (recorded on copy_in)
+  hipEvent_t freed = nullptr;      // D2H of the slice done (recorded on compute)
+  bool used = false;               // `freed` has been recorded at least once
 };
 
-// Per-device workspace kept across calls: streams, slice buffers and the descriptor are allocated
-// once and reused while they are large enough (the streaming file codec calls the pipeline once
+// A lane = the reference's "stream" (-s): its own copy-in stream (H2D) and compute stream
+// (kernel + D2H), and kSlots slice buffers used alternately.
+struct Lane {
+  hipStream_t copy_in = nullptr;
+  hipStream_t compute = nullptr;
+  Slot slot[kSlots];
+};
+
+// Per-device workspace kept across calls: streams, events, slice buffers and descriptors are
+// allocated once and reused while large enough (the streaming file codec calls the pipeline once
 // per window; re-creating streams and hipMalloc/hipFree-ing ~100s of MB each time cost ~20 ms per
 // call on MI355X, more than the transfers themselves — profiles/r01_round).
 struct Workspace {
@@ -66,14 +80,86 @@ hipError_t ensure(void** ptr, size_t& cap, size_t need) {
   return hipSuccess;
 }
 
+// Waits for everything queued on the lanes (also on error paths: a later call re-uploads
+// descriptors with a synchronous hipMemcpy that is not ordered against these non-blocking streams).
+hipError_t drain(std::vector<Lane>& lanes) {
+  hipError_t first = hipSuccess;
+  for (auto& L : lanes)
+    for (hipStream_t s : {L.copy_in, L.compute})
+      if (s) {
+        const hipError_t e = hipStreamSynchronize(s);
+        if (first == hipSuccess) first = e;
+      }
+  return first;
+}
+
 hipError_t free_lane(Lane& L) {
-  if (L.stream) GFRS_TRY(hipStreamSynchronize(L.stream));
-  if (L.in) GFRS_TRY(hipFree(L.in));
-  if (L.out) GFRS_TRY(hipFree(L.out));
-  if (L.desc) GFRS_TRY(hipFree(L.desc));
-  if (L.stream) GFRS_TRY(hipStreamDestroy(L.stream));
+  for (hipStream_t s : {L.copy_in, L.compute})
+    if (s) GFRS_TRY(hipStreamSynchronize(s));
+  for (auto& S : L.slot) {
+    if (S.in) GFRS_TRY(hipFree(S.in));
+    if (S.out) GFRS_TRY(hipFree(S.out));
+    if (S.desc) GFRS_TRY(hipFree(S.desc));
+    if (S.loaded) GFRS_TRY(hipEventDestroy(S.loaded));
+    if (S.freed) GFRS_TRY(hipEventDestroy(S.freed));
+  }
+  for (hipStream_t s : {L.copy_in, L.compute})
+    if (s) GFRS_TRY(hipStreamDestroy(s));
   L = Lane{};
   return hipSuccess;
+}
+
+struct Geometry {
+  int64_t slice = 0, nslices = 0;
+  int lanes = 0;
+};
+
+Geometry geometry(int64_t ncols, const PipelineOptions& opt) {
+  Geometry g;
+  const int S = opt.streams;
+  g.slice = std::max<int64_t>(256, (opt.slice_bytes + 255) / 256 * 256);
+  // at least kSlots slices per lane when the range allows it (so every lane double-buffers), never
+  // wider than needed
+  const int64_t per_slot = ((ncols + int64_t(S) * kSlots - 1) / (int64_t(S) * kSlots) + 255) / 256 * 256;
+  g.slice = std::min(g.slice, std::max<int64_t>(256, per_slot));
+  g.nslices = (ncols + g.slice - 1) / g.slice;
+  g.lanes = int(std::min<int64_t>(S, g.nslices));
+  return g;
+}
+
+// Streams, events and buffers for `lanes` lanes of k x slice in / m x slice out, descriptors built
+// from `coeff` (zeros when empty). Caller holds ws.mu and has set the device.
+hipError_t setup_lanes(Workspace& ws, int lanes, int k, int m, int64_t slice, const Mat& coeff) {
+  if (int(ws.lane.size()) < lanes) ws.lane.resize(size_t(lanes));
+  const Mat zero = coeff.empty() ? Mat(size_t(m) * k, 0) : Mat{};
+  const Mat& c = coeff.empty() ? zero : coeff;
+  for (int l = 0; l < lanes; ++l) {
+    Lane& L = ws.lane[size_t(l)];
+    if (!L.copy_in) GFRS_TRY(hipStreamCreateWithFlags(&L.copy_in, hipStreamNonBlocking));
+    if (!L.compute) GFRS_TRY(hipStreamCreateWithFlags(&L.compute, hipStreamNonBlocking));
+    for (auto& S : L.slot) {
+      if (!S.loaded) GFRS_TRY(hipEventCreateWithFlags(&S.loaded, hipEventDisableTiming));
+      if (!S.freed) GFRS_TRY(hipEventCreateWithFlags(&S.freed, hipEventDisableTiming));
+      GFRS_TRY(ensure(reinterpret_cast<void**>(&S.in), S.in_cap, size_t(k) * slice));
+      GFRS_TRY(ensure(reinterpret_cast<void**>(&S.out), S.out_cap, size_t(m) * slice));
+      std::vector<uint64_t> ip(k), op(m);
+      for (int j = 0; j < k; ++j) ip[j] = reinterpret_cast<uint64_t>(S.in + size_t(j) * slice);
+      for (int i = 0; i < m; ++i) op[i] = reinterpret_cast<uint64_t>(S.out + size_t(i) * slice);
+      std::vector<uint8_t> d = build_desc(k, m, ip, {}, op, c);
+      if (d != S.desc_host) {
+        GFRS_TRY(ensure(&S.desc, S.desc_cap, d.size()));
+        // every lane was drained before the previous call returned, so no kernel still reads it
+        GFRS_TRY(hipMemcpy(S.desc, d.data(), d.size(), hipMemcpyHostToDevice));
+        S.desc_host = std::move(d);
+      }
+    }
+  }
+  return hipSuccess;
+}
+
+bool valid(int k, int m, size_t coeff_size, int64_t c0, int64_t c1, const PipelineOptions& opt) {
+  return k > 0 && m > 0 && k <= 256 && m <= 256 && (coeff_size == 0 || coeff_size == size_t(m) * k) && c1 >= c0 &&
+         opt.streams > 0;
 }
 
 }  // namespace
@@ -89,12 +175,47 @@ hipError_t release_workspaces() {
   return hipSuccess;
 }
 
+hipError_t prepare_pipeline(int device, int k, int m, int64_t ncols, const PipelineOptions& opt) {
+  if (!valid(k, m, 0, 0, ncols, opt)) return hipErrorInvalidValue;
+  if (ncols == 0) return hipSuccess;
+  GFRS_TRY(hipSetDevice(device));
+  const Geometry g = geometry(ncols, opt);
+  Workspace& ws = workspace(device);
+  std::lock_guard<std::mutex> guard(ws.mu);
+  TraceRange tr("pipeline/prepare");
+  GFRS_TRY(setup_lanes(ws, g.lanes, k, m, g.slice, {}));
+  // one launch per lane over a few columns of its buffers: loads the code object and warms the
+  // launch path before anyone's clock starts
+  for (int l = 0; l < g.lanes; ++l) {
+    Lane& L = ws.lane[size_t(l)];
+    GFRS_TRY(hipMemsetAsync(L.slot[0].in, 0, size_t(k) * g.slice, L.compute));
+    GFRS_TRY(launch_gf_gemm(L.slot[0].desc, k, pad_m(m), 0, std::min<int64_t>(g.slice, 4096), opt.bytewise, 0,
+                            L.compute));
+  }
+  return drain(ws.lane);
+}
+
+hipError_t prepare_pipeline_multi(const std::vector<int>& devices, int k, int m, int64_t ncols,
+                                  const PipelineOptions& opt) {
+  const int D = int(devices.size());
+  if (D <= 0) return hipErrorInvalidValue;
+  std::vector<hipError_t> err(D, hipSuccess);
+  std::vector<std::thread> th;
+  for (int d = 0; d < D; ++d) {
+    const auto [a, b] = device_shard(ncols, D, d);
+    th.emplace_back([&, d, a = a, b = b] { err[d] = prepare_pipeline(devices[d], k, m, b - a, opt); });
+  }
+  for (auto& t : th) t.join();
+  for (auto e : err)
+    if (e != hipSuccess) return e;
+  return hipSuccess;
+}
+
 hipError_t gemm_host(int device, const std::vector<const uint8_t*>& in_rows, const std::vector<uint8_t*>& out_rows,
                      const Mat& coeff, int64_t c0, int64_t c1, const PipelineOptions& opt, PipelineStats* stats) {
   const int k = int(in_rows.size());
   const int m = int(out_rows.size());
-  if (k <= 0 || m <= 0 || coeff.size() != size_t(m) * k || c1 < c0 || opt.streams <= 0)
-    return hipErrorInvalidValue;
+  if (!valid(k, m, coeff.size(), c0, c1, opt) || coeff.empty()) return hipErrorInvalidValue;
   PipelineStats st;
   const auto t_all = Clock::now();
   const int64_t ncols = c1 - c0;
@@ -103,60 +224,58 @@ hipError_t gemm_host(int device, const std::vector<const uint8_t*>& in_rows, con
     return hipSuccess;
   }
   GFRS_TRY(hipSetDevice(device));
-
-  const int S = opt.streams;
-  int64_t slice = std::max<int64_t>(256, (opt.slice_bytes + 255) / 256 * 256);
-  // at least one slice per stream so every stream has work, never wider than needed
-  const int64_t per_stream = ((ncols + S - 1) / S + 255) / 256 * 256;
-  slice = std::min(slice, std::max<int64_t>(256, per_stream));
-  const int64_t nslices = (ncols + slice - 1) / slice;
-  const int lanes = int(std::min<int64_t>(S, nslices));
+  const Geometry g = geometry(ncols, opt);
+  const int64_t slice = g.slice;
+  const int lanes = g.lanes;
   const int m_pad = pad_m(m);
 
   Workspace& ws = workspace(device);
   std::lock_guard<std::mutex> guard(ws.mu);
   {
     TraceRange tr("pipeline/setup");
-    if (int(ws.lane.size()) < lanes) ws.lane.resize(size_t(lanes));
-    for (int l = 0; l < lanes; ++l) {
-      Lane& L = ws.lane[size_t(l)];
-      if (!L.stream) GFRS_TRY(hipStreamCreateWithFlags(&L.stream, hipStreamNonBlocking));
-      GFRS_TRY(ensure(reinterpret_cast<void**>(&L.in), L.in_cap, size_t(k) * slice));
-      GFRS_TRY(ensure(reinterpret_cast<void**>(&L.out), L.out_cap, size_t(m) * slice));
-      std::vector<uint64_t> ip(k), op(m);
-      for (int j = 0; j < k; ++j) ip[j] = reinterpret_cast<uint64_t>(L.in + size_t(j) * slice);
-      for (int i = 0; i < m; ++i) op[i] = reinterpret_cast<uint64_t>(L.out + size_t(i) * slice);
-      std::vector<uint8_t> d = build_desc(k, m, ip, {}, op, coeff);
-      if (d != L.desc_host) {
-        GFRS_TRY(ensure(&L.desc, L.desc_cap, d.size()));
-        // (the previous call drained every lane before returning, so no kernel still reads it)
-        GFRS_TRY(hipMemcpy(L.desc, d.data(), d.size(), hipMemcpyHostToDevice));
-        L.desc_host = std::move(d);
-      }
+    const hipError_t e = setup_lanes(ws, lanes, k, m, slice, coeff);
+    if (e != hipSuccess) {
+      (void)drain(ws.lane);
+      return e;
     }
   }
   st.ms_setup = ms_since(t_all);
 
   const auto t_stream = Clock::now();
+  hipError_t err = hipSuccess;
   {
     TraceRange tr_stream("pipeline/stream-loop");
-    for (int64_t t = 0; t < nslices; ++t) {
+    // slice t -> lane t % lanes, slot (t / lanes) % kSlots. Copy-in waits until the slot's previous
+    // D2H has drained; compute waits for the slot's H2D. No host synchronisation inside the loop.
+    for (int64_t t = 0; t < g.nslices && err == hipSuccess; ++t) {
       Lane& L = ws.lane[size_t(t % lanes)];
+      Slot& S = L.slot[(t / lanes) % kSlots];
       const int64_t a = c0 + t * slice;
       const int64_t w = std::min(slice, c1 - a);
-      for (int j = 0; j < k; ++j)
-        GFRS_TRY(hipMemcpyAsync(L.in + size_t(j) * slice, in_rows[j] + a, w, hipMemcpyHostToDevice, L.stream));
-      GFRS_TRY(launch_gf_gemm(L.desc, k, m_pad, 0, w, opt.bytewise, opt.max_blocks, L.stream));
-      for (int i = 0; i < m; ++i)
-        GFRS_TRY(hipMemcpyAsync(out_rows[i] + a, L.out + size_t(i) * slice, w, hipMemcpyDeviceToHost, L.stream));
+      auto body = [&]() -> hipError_t {
+        if (S.used) GFRS_TRY(hipStreamWaitEvent(L.copy_in, S.freed, 0));
+        for (int j = 0; j < k; ++j)
+          GFRS_TRY(hipMemcpyAsync(S.in + size_t(j) * slice, in_rows[j] + a, w, hipMemcpyHostToDevice, L.copy_in));
+        GFRS_TRY(hipEventRecord(S.loaded, L.copy_in));
+        GFRS_TRY(hipStreamWaitEvent(L.compute, S.loaded, 0));
+        GFRS_TRY(launch_gf_gemm(S.desc, k, m_pad, 0, w, opt.bytewise, opt.max_blocks, L.compute));
+        for (int i = 0; i < m; ++i)
+          GFRS_TRY(hipMemcpyAsync(out_rows[i] + a, S.out + size_t(i) * slice, w, hipMemcpyDeviceToHost, L.compute));
+        GFRS_TRY(hipEventRecord(S.freed, L.compute));
+        S.used = true;
+        return hipSuccess;
+      };
+      err = body();
       st.bytes_h2d += int64_t(k) * w;
       st.bytes_d2h += int64_t(m) * w;
     }
   }
   {
     TraceRange tr("pipeline/drain");
-    for (int l = 0; l < lanes; ++l) GFRS_TRY(hipStreamSynchronize(ws.lane[size_t(l)].stream));
+    const hipError_t e = drain(ws.lane);
+    if (err == hipSuccess) err = e;
   }
+  if (err != hipSuccess) return err;
   st.ms_stream = ms_since(t_stream);
   if (!opt.persistent) {
     const auto t_free = Clock::now();
@@ -165,9 +284,18 @@ hipError_t gemm_host(int device, const std::vector<const uint8_t*>& in_rows, con
     st.ms_teardown = ms_since(t_free);
   }
   st.ms_total = ms_since(t_all);
-  st.slices = int(nslices);
+  st.slices = int(g.nslices);
+  st.lanes = lanes;
   if (stats) *stats = st;
   return hipSuccess;
+}
+
+std::pair<int64_t, int64_t> device_shard(int64_t ncols, int devices, int d) {
+  // contiguous column shards, 4 KiB aligned, remainder to the last device (src/encode.cu:368-381)
+  const int64_t per = (ncols / devices) / 4096 * 4096;
+  const int64_t a = int64_t(d) * per;
+  const int64_t b = (d == devices - 1) ? ncols : a + per;
+  return {a, b};
 }
 
 hipError_t gemm_host_multi(const std::vector<int>& devices, const std::vector<const uint8_t*>& in_rows,
@@ -177,14 +305,13 @@ hipError_t gemm_host_multi(const std::vector<int>& devices, const std::vector<co
   if (D <= 0) return hipErrorInvalidValue;
   std::vector<PipelineStats> st(D);
   std::vector<hipError_t> err(D, hipSuccess);
-  // contiguous column shards, 4 KiB aligned, remainder to the last device (src/encode.cu:368-381)
-  const int64_t per = (ncols / D) / 4096 * 4096;
   const auto t0 = Clock::now();
   std::vector<std::thread> th;
   for (int d = 0; d < D; ++d) {
-    const int64_t a = int64_t(d) * per;
-    const int64_t b = (d == D - 1) ? ncols : a + per;
-    th.emplace_back([&, d, a, b] { err[d] = gemm_host(devices[d], in_rows, out_rows, coeff, a, b, opt, &st[d]); });
+    const auto [a, b] = device_shard(ncols, D, d);
+    th.emplace_back([&, d, a = a, b = b] {
+      err[d] = gemm_host(devices[d], in_rows, out_rows, coeff, a, b, opt, &st[d]);
+    });
   }
   for (auto& t : th) t.join();
   if (wall_ms) *wall_ms = ms_since(t0);

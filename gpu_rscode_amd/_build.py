@@ -30,6 +30,23 @@ def build(target: str = "all", jobs: int | None = None, quiet: bool = True) -> N
         print(res.stdout)
 
 
+SOURCE_SUFFIXES = (".hip", ".cpp", ".h", ".hpp")
+
+
+def newest_source_mtime() -> float:
+    """Latest modification time over the native sources under ``csrc/`` (and its Makefile)."""
+    newest = (CSRC / "Makefile").stat().st_mtime
+    for p in CSRC.rglob("*"):
+        if p.suffix in SOURCE_SUFFIXES:
+            newest = max(newest, p.stat().st_mtime)
+    return newest
+
+
+def stale(path: Path) -> bool:
+    """True when ``path`` is missing or older than some native source."""
+    return not path.exists() or path.stat().st_mtime < newest_source_mtime()
+
+
 def artifact(name: str) -> Path:
     return PKG / name
 

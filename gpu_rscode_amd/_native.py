@@ -25,8 +25,10 @@ def _load(name: str, target: str):
         # incremental: a no-op when the .so is newer than every source
         try:
             _build.build(target)
-        except RuntimeError:
-            if not so.exists():
+        except (RuntimeError, OSError):
+            # a failed rebuild is only tolerable when the existing module is up to date with every
+            # source (e.g. no toolchain on this machine); a stale .so would silently run old code
+            if not so.exists() or _build.stale(so):
                 raise
     mod = importlib.import_module(f"gpu_rscode_amd._{name}")
     _mods[name] = mod

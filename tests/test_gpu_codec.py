@@ -219,3 +219,70 @@ def test_stream_file_codec_gpu_equals_cpu_and_resumes(tmp_path):
                                  window=1 << 16, durable=False)
     assert r["complete"] and r["erased"] == 4
     assert (g / "out").read_bytes() == payload
+
+
+@pytest.mark.parametrize("devices", [[0, 0], [0, 0, 0]])
+def test_gemm_host_multi_shards_on_one_gpu(devices):
+    """The one-process multi-device path (one host thread per shard entry, src/encode.cu:368-429):
+    repeated entries of device 0 exercise the shard split, 4 KiB alignment, remainder on the last
+    shard and the thread join on a 1-GPU box."""
+    k, p = 10, 4
+    D = len(devices)
+    C = 3 * 4096 * D + 12345  # odd, not a multiple of the shard alignment: remainder on the last entry
+    rng = np.random.default_rng(D)
+    host = torch.from_numpy(rng.integers(0, 256, size=(k, C), dtype=np.uint8)).pin_memory()
+    par = torch.zeros((p, C), dtype=torch.uint8).pin_memory()
+    e = GF256.vandermonde_ref(k, p)
+    res = hip().gemm_host(devices, [host[j].data_ptr() for j in range(k)], [par[i].data_ptr() for i in range(p)],
+                          e.tobytes(), C, 1, 1 << 14, 0, False)
+    assert len(res["devices"]) == D
+    shards = [hip().device_shard(C, D, d) for d in range(D)]
+    assert shards[0][0] == 0 and shards[-1][1] == C
+    assert all(a % 4096 == 0 for a, _ in shards) and all(shards[d][1] == shards[d + 1][0] for d in range(D - 1))
+    for d, (a, b) in enumerate(shards):
+        assert res["devices"][d]["bytes_h2d"] == k * (b - a)
+        assert res["devices"][d]["lanes"] >= 1
+    assert np.array_equal(par.numpy(), GF256.gemm(e, host.numpy()))
+
+
+def test_prepare_pipeline_then_gemm_single_stream_double_buffers():
+    """prepare_pipeline builds the workspace ahead of time; -s 1 splits the range into >= 2 slices
+    so the lane's two slots alternate (H2D of slice t+1 under the kernel + D2H of slice t)."""
+    k, p, C = 8, 3, 2_000_001
+    h = hip()
+    h.prepare_pipeline([0], k, p, C, 1, 1 << 26)
+    rng = np.random.default_rng(5)
+    host = torch.from_numpy(rng.integers(0, 256, size=(k, C), dtype=np.uint8)).pin_memory()
+    par = torch.zeros((p, C), dtype=torch.uint8).pin_memory()
+    e = rng.integers(0, 256, size=(p, k), dtype=np.uint8)
+    res = h.gemm_host([0], [host[j].data_ptr() for j in range(k)], [par[i].data_ptr() for i in range(p)],
+                      e.tobytes(), C, 1, 1 << 26, 0, False)
+    st = res["devices"][0]
+    assert st["lanes"] == 1 and st["slices"] >= 2
+    assert np.array_equal(par.numpy(), GF256.gemm(e, host.numpy()))
+
+
+@pytest.mark.parametrize("devices", ["0,0", "0,0,0"])
+def test_rs_cli_device_list_shards(tmp_path, devices):
+    """bin/RS --devices with several shard entries: per-shard "DeviceN" lines, output bit-exact with
+    the CPU codec, decode through the same sharded path."""
+    exe = str(binary("RS"))
+    payload = os.urandom(5_000_017)
+    (tmp_path / "f.bin").write_bytes(payload)
+    r = subprocess.run([exe, "-k", "10", "-n", "14", "-e", "f.bin", "-s", "2", "--devices", devices], cwd=tmp_path,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    D = len(devices.split(","))
+    assert all(f"Device{d}: Total GPU encoding time" in r.stdout for d in range(D)), r.stdout
+    c = tmp_path / "c"
+    c.mkdir()
+    (c / "f.bin").write_bytes(payload)
+    cpu().encode_file(str(c / "f.bin"), 10, 4)
+    for i in range(14):
+        assert (tmp_path / f"_{i}_f.bin").read_bytes() == (c / f"_{i}_f.bin").read_bytes(), i
+    conf = tmp_path / "conf"
+    ff.write_conf(str(conf), [f"_{i}_f.bin" for i in (1, 2, 4, 5, 6, 8, 10, 11, 12, 13)])
+    r = subprocess.run([exe, "-d", "-i", "f.bin", "-c", "conf", "-o", "out.bin", "--devices", devices], cwd=tmp_path,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert (tmp_path / "out.bin").read_bytes() == payload
