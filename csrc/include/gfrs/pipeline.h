@@ -32,6 +32,8 @@ struct PipelineOptions {
   int max_blocks = 0;              // -p (grid cap), 0 = uncapped
   bool bytewise = false;           // force the byte kernel (debug/ablation)
   bool persistent = true;          // keep streams/buffers/descriptor per device for the next call
+  int copy_streams = 1;            // 1: H2D on a per-lane copy-in stream; 0: everything on one stream
+  bool rect = true;                // equally spaced host rows: one 2-D copy per slice instead of k / m
 };
 
 struct PipelineStats {

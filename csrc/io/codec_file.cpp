@@ -198,10 +198,12 @@ FileReport decode_file(const std::string& file, const std::string& conf, const s
   for (int i = 0; i < k; ++i)
     if (pos_of_native[i] < 0) erased.push_back(i);
   r.erased = int(erased.size());
+  // (the output rows are allocated outside the timed GEMM region, like encode's parity buffer:
+  // a pinned hipHostMalloc of ~GBs takes tens of ms)
+  Buf rec(alloc, size_t(std::max<size_t>(erased.size(), 1)) * C);
   r.ms_matrix = ms_since(t);
 
   t = Clock::now();
-  Buf rec(alloc, size_t(std::max<size_t>(erased.size(), 1)) * C);
   if (!erased.empty()) {
     TraceRange tr("decode/gemm");
     Mat coeff(erased.size() * size_t(k));

@@ -156,12 +156,15 @@ PYBIND11_MODULE(_hip, m) {
   m.def(
       "gemm_host",
       [](const std::vector<int>& devices, const std::vector<uint64_t>& in, const std::vector<uint64_t>& out,
-         const py::bytes& coeff, int64_t ncols, int streams, int64_t slice, int max_blocks, bool bytewise) {
+         const py::bytes& coeff, int64_t ncols, int streams, int64_t slice, int max_blocks, bool bytewise,
+         int copy_streams, bool rect) {
         PipelineOptions opt;
         opt.streams = streams;
         opt.slice_bytes = slice;
         opt.max_blocks = max_blocks;
         opt.bytewise = bytewise;
+        opt.copy_streams = copy_streams;
+        opt.rect = rect;
         const Mat c = to_mat(coeff);
         auto ip = ptrs<const uint8_t*>(in);
         auto op = ptrs<uint8_t*>(out);
@@ -181,7 +184,8 @@ PYBIND11_MODULE(_hip, m) {
         return d;
       },
       py::arg("devices"), py::arg("in_ptrs"), py::arg("out_ptrs"), py::arg("coeff"), py::arg("ncols"),
-      py::arg("streams") = 2, py::arg("slice") = 16 << 20, py::arg("max_blocks") = 0, py::arg("bytewise") = false);
+      py::arg("streams") = 2, py::arg("slice") = 16 << 20, py::arg("max_blocks") = 0, py::arg("bytewise") = false,
+      py::arg("copy_streams") = 1, py::arg("rect") = true);
 
   // `prep` (optional): setup started before the file reads; waited for on the first call
   m.def(
@@ -196,6 +200,13 @@ PYBIND11_MODULE(_hip, m) {
       },
       py::arg("devices"), py::arg("k"), py::arg("m"), py::arg("ncols"), py::arg("streams") = 2,
       py::arg("slice") = 16 << 20);
+  // pinned host memory with explicit hipHostMalloc flags (pipeline experiments: cold vs warm DMA)
+  m.def("host_alloc", [](int64_t bytes, unsigned flags) {
+    void* p = nullptr;
+    check(hipHostMalloc(&p, size_t(bytes), flags), "hipHostMalloc");
+    return reinterpret_cast<uint64_t>(p);
+  });
+  m.def("host_free", [](uint64_t p) { check(hipHostFree(reinterpret_cast<void*>(p)), "hipHostFree"); });
   m.def("device_shard", [](int64_t ncols, int devices, int d) { return device_shard(ncols, devices, d); });
 
   auto gpu_gemm = [](const std::vector<int>& devices, int streams, int64_t slice, int max_blocks,

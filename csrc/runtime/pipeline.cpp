@@ -129,13 +129,15 @@ Geometry geometry(int64_t ncols, const PipelineOptions& opt) {
 
 // Streams, events and buffers for `lanes` lanes of k x slice in / m x slice out, descriptors built
 // from `coeff` (zeros when empty). Caller holds ws.mu and has set the device.
-hipError_t setup_lanes(Workspace& ws, int lanes, int k, int m, int64_t slice, const Mat& coeff) {
+hipError_t setup_lanes(Workspace& ws, int lanes, int k, int m, int64_t slice, const Mat& coeff, bool split) {
   if (int(ws.lane.size()) < lanes) ws.lane.resize(size_t(lanes));
   const Mat zero = coeff.empty() ? Mat(size_t(m) * k, 0) : Mat{};
   const Mat& c = coeff.empty() ? zero : coeff;
   for (int l = 0; l < lanes; ++l) {
     Lane& L = ws.lane[size_t(l)];
-    if (!L.copy_in) GFRS_TRY(hipStreamCreateWithFlags(&L.copy_in, hipStreamNonBlocking));
+    // (streams map onto a few hardware queues — 4 per process by default — so the copy-in stream
+    // exists only when it is used)
+    if (split && !L.copy_in) GFRS_TRY(hipStreamCreateWithFlags(&L.copy_in, hipStreamNonBlocking));
     if (!L.compute) GFRS_TRY(hipStreamCreateWithFlags(&L.compute, hipStreamNonBlocking));
     for (auto& S : L.slot) {
       if (!S.loaded) GFRS_TRY(hipEventCreateWithFlags(&S.loaded, hipEventDisableTiming));
@@ -155,6 +157,44 @@ hipError_t setup_lanes(Workspace& ws, int lanes, int k, int m, int64_t slice, co
     }
   }
   return hipSuccess;
+}
+
+// rows [first, first + count) of a host row list, `pitch` bytes apart (count == 1: pitch unused)
+struct Run {
+  int first = 0, count = 0;
+  int64_t pitch = 0;
+};
+
+// Maximal runs of equally spaced rows with spacing >= min_pitch (min_pitch 0: every row alone).
+template <class Ptr>
+std::vector<Run> row_runs(const std::vector<Ptr>& rows, int64_t min_pitch) {
+  std::vector<Run> runs;
+  auto at = [&](size_t i) { return reinterpret_cast<const uint8_t*>(rows[i]); };
+  for (size_t i = 0; i < rows.size();) {
+    Run r{int(i), 1, 0};
+    if (min_pitch > 0 && i + 1 < rows.size()) {
+      const int64_t d = at(i + 1) - at(i);
+      if (d >= min_pitch) {
+        r.pitch = d;
+        while (i + r.count < rows.size() && at(i + r.count) - at(i + r.count - 1) == d) ++r.count;
+      }
+    }
+    runs.push_back(r);
+    i += size_t(r.count);
+  }
+  return runs;
+}
+
+// One run of rows between host memory (pitch r.pitch) and a slot buffer (pitch `slot_pitch`),
+// columns [0, w) of the given base pointers. `dst`/`src` point at the run's first row.
+template <class Dst, class Src>
+hipError_t copy_run(Dst* dst, size_t slot_pitch, const Src* src, const Run& r, int64_t w, hipMemcpyKind kind,
+                    hipStream_t s) {
+  const bool h2d = kind == hipMemcpyHostToDevice;
+  if (r.count == 1) return hipMemcpyAsync(dst, src, size_t(w), kind, s);
+  const size_t dpitch = h2d ? slot_pitch : size_t(r.pitch);
+  const size_t spitch = h2d ? size_t(r.pitch) : slot_pitch;
+  return hipMemcpy2DAsync(dst, dpitch, src, spitch, size_t(w), size_t(r.count), kind, s);
 }
 
 bool valid(int k, int m, size_t coeff_size, int64_t c0, int64_t c1, const PipelineOptions& opt) {
@@ -183,16 +223,40 @@ hipError_t prepare_pipeline(int device, int k, int m, int64_t ncols, const Pipel
   Workspace& ws = workspace(device);
   std::lock_guard<std::mutex> guard(ws.mu);
   TraceRange tr("pipeline/prepare");
-  GFRS_TRY(setup_lanes(ws, g.lanes, k, m, g.slice, {}));
-  // one launch per lane over a few columns of its buffers: loads the code object and warms the
-  // launch path before anyone's clock starts
-  for (int l = 0; l < g.lanes; ++l) {
+  GFRS_TRY(setup_lanes(ws, g.lanes, k, m, g.slice, {}, opt.copy_streams > 0));
+  // Before anyone's clock starts, run every path the stream loop will take once, on a few columns:
+  // the kernel launch (code-object load), and H2D / D2H copies in both the 1-D and the 2-D form
+  // on the streams that will issue them. The first DMA of a process sets up its copy engines and
+  // blit kernels: ~15 ms of a 1 GiB encode when it lands inside the loop (profiles/r02c).
+  constexpr size_t kProbe = 4096;
+  const size_t probe = std::min<size_t>(kProbe, size_t(g.slice));
+  void* host = nullptr;
+  GFRS_TRY(hipHostMalloc(&host, 2 * kProbe, hipHostMallocDefault));
+  auto* h = static_cast<uint8_t*>(host);
+  hipError_t err = hipSuccess;
+  for (int l = 0; l < g.lanes && err == hipSuccess; ++l) {
     Lane& L = ws.lane[size_t(l)];
-    GFRS_TRY(hipMemsetAsync(L.slot[0].in, 0, size_t(k) * g.slice, L.compute));
-    GFRS_TRY(launch_gf_gemm(L.slot[0].desc, k, pad_m(m), 0, std::min<int64_t>(g.slice, 4096), opt.bytewise, 0,
-                            L.compute));
+    hipStream_t cin = L.copy_in ? L.copy_in : L.compute;
+    auto warm = [&]() -> hipError_t {
+      GFRS_TRY(hipMemsetAsync(L.slot[0].in, 0, size_t(k) * g.slice, L.compute));
+      GFRS_TRY(hipStreamSynchronize(L.compute));
+      GFRS_TRY(hipMemcpyAsync(L.slot[0].in, h, probe, hipMemcpyHostToDevice, cin));
+      GFRS_TRY(hipMemcpy2DAsync(L.slot[1].in, size_t(g.slice), h, probe, probe, 1, hipMemcpyHostToDevice, cin));
+      GFRS_TRY(hipStreamSynchronize(cin));
+      GFRS_TRY(launch_gf_gemm(L.slot[0].desc, k, pad_m(m), 0, std::min<int64_t>(g.slice, int64_t(probe)),
+                              opt.bytewise, 0, L.compute));
+      GFRS_TRY(hipMemcpyAsync(h + kProbe, L.slot[0].out, probe, hipMemcpyDeviceToHost, L.compute));
+      GFRS_TRY(hipMemcpy2DAsync(h + kProbe, probe, L.slot[1].out, size_t(g.slice), probe, 1, hipMemcpyDeviceToHost,
+                                L.compute));
+      return hipSuccess;
+    };
+    err = warm();
   }
-  return drain(ws.lane);
+  const hipError_t e2 = drain(ws.lane);
+  const hipError_t e3 = hipHostFree(host);
+  if (err != hipSuccess) return err;
+  if (e2 != hipSuccess) return e2;
+  return e3;
 }
 
 hipError_t prepare_pipeline_multi(const std::vector<int>& devices, int k, int m, int64_t ncols,
@@ -233,7 +297,7 @@ hipError_t gemm_host(int device, const std::vector<const uint8_t*>& in_rows, con
   std::lock_guard<std::mutex> guard(ws.mu);
   {
     TraceRange tr("pipeline/setup");
-    const hipError_t e = setup_lanes(ws, lanes, k, m, slice, coeff);
+    const hipError_t e = setup_lanes(ws, lanes, k, m, slice, coeff, opt.copy_streams > 0);
     if (e != hipSuccess) {
       (void)drain(ws.lane);
       return e;
@@ -241,6 +305,12 @@ hipError_t gemm_host(int device, const std::vector<const uint8_t*>& in_rows, con
   }
   st.ms_setup = ms_since(t_all);
 
+  // Host rows grouped into maximal runs at one fixed distance >= the slice (e.g. the codec's k x C
+  // buffer is one run; a decode's survivors are a run of natives plus a run of parity rows): each
+  // run moves as ONE 2-D copy per slice. Measured on MI355X (profiles/r02b): k separate 1-D copies
+  // per slice cost up to 30% of the H2D rate on 4 lanes.
+  const std::vector<Run> in_runs = row_runs(in_rows, opt.rect ? slice : 0);
+  const std::vector<Run> out_runs = row_runs(out_rows, opt.rect ? slice : 0);
   const auto t_stream = Clock::now();
   hipError_t err = hipSuccess;
   {
@@ -252,15 +322,20 @@ hipError_t gemm_host(int device, const std::vector<const uint8_t*>& in_rows, con
       Slot& S = L.slot[(t / lanes) % kSlots];
       const int64_t a = c0 + t * slice;
       const int64_t w = std::min(slice, c1 - a);
+      hipStream_t cin = (opt.copy_streams && L.copy_in) ? L.copy_in : L.compute;
       auto body = [&]() -> hipError_t {
-        if (S.used) GFRS_TRY(hipStreamWaitEvent(L.copy_in, S.freed, 0));
-        for (int j = 0; j < k; ++j)
-          GFRS_TRY(hipMemcpyAsync(S.in + size_t(j) * slice, in_rows[j] + a, w, hipMemcpyHostToDevice, L.copy_in));
-        GFRS_TRY(hipEventRecord(S.loaded, L.copy_in));
-        GFRS_TRY(hipStreamWaitEvent(L.compute, S.loaded, 0));
+        if (S.used && cin != L.compute) GFRS_TRY(hipStreamWaitEvent(cin, S.freed, 0));
+        for (const Run& r : in_runs)
+          GFRS_TRY(copy_run(S.in + size_t(r.first) * slice, size_t(slice), in_rows[r.first] + a, r, w,
+                            hipMemcpyHostToDevice, cin));
+        if (cin != L.compute) {
+          GFRS_TRY(hipEventRecord(S.loaded, cin));
+          GFRS_TRY(hipStreamWaitEvent(L.compute, S.loaded, 0));
+        }
         GFRS_TRY(launch_gf_gemm(S.desc, k, m_pad, 0, w, opt.bytewise, opt.max_blocks, L.compute));
-        for (int i = 0; i < m; ++i)
-          GFRS_TRY(hipMemcpyAsync(out_rows[i] + a, S.out + size_t(i) * slice, w, hipMemcpyDeviceToHost, L.compute));
+        for (const Run& r : out_runs)
+          GFRS_TRY(copy_run(out_rows[r.first] + a, size_t(slice), S.out + size_t(r.first) * slice, r, w,
+                            hipMemcpyDeviceToHost, L.compute));
         GFRS_TRY(hipEventRecord(S.freed, L.compute));
         S.used = true;
         return hipSuccess;

@@ -13,7 +13,8 @@ recomputed per device (``:141``) and the decode inverse shared by host pointer
   E generated on every device (:141)     :func:`broadcast_matrix` from rank 0
   A^-1 shared by host pointer            :func:`broadcast_matrix` (or identical device inverse)
   stripe scatter via H2H (:389-398)      :func:`scatter_columns` (point-to-point isend/irecv)
-  parity gather via H2H (:410-429)       :func:`gather_columns`  (point-to-point into rank 0)
+  parity gather via H2H (:410-429)       :func:`gather_columns` / :func:`gather_pieces`
+                                         (point-to-point, received in place on rank 0)
   =====================================  ====================================================
 
 xGMI is point-to-point (7 links per GPU), so scatter/gather use one send per peer — each peer
@@ -105,63 +106,74 @@ def broadcast_matrix(mat: np.ndarray | None, device: torch.device, src: int = 0)
 
 def scatter_columns(full: torch.Tensor | None, rows: int, ncols: int, device: torch.device, src: int = 0,
                     align: int = SHARD_ALIGN) -> torch.Tensor:
-    """Rank ``src`` holds ``full`` [rows, ncols]; every rank receives its column shard
-    [rows, b - a] (256-byte pitched rows). Point-to-point, one send per peer."""
+    """Rank ``src`` holds ``full`` [rows, ncols] (unit column stride); every rank gets its column
+    shard [rows, b - a].
+
+    Point-to-point, one message per (peer, row): every row piece travels straight from its place in
+    ``full`` into the receiver's pitched shard (256-byte row pitch, 16-byte aligned rows for the GEMM
+    kernels) — no staging copies on either side. Rank ``src`` returns a view of its own shard inside
+    ``full`` (nothing moves)."""
     world, rank = _world(), _rank()
     a, b = shard_range(ncols, world, rank, align)
-    local = alloc_rows(rows, b - a, device)
+    if rank == src:
+        if full is None or full.dim() != 2 or full.stride(1) != 1 or full.shape[0] != rows or full.shape[1] < ncols:
+            raise ValueError("scatter_columns: rank src needs full [rows, >= ncols] with unit column stride")
+        local = full[:, a:b]
+    else:
+        local = alloc_rows(rows, b - a, device)
     if world == 1:
-        local.copy_(full[:, a:b])
         return local
-    recv = torch.empty((rows, b - a), dtype=torch.uint8, device=device)
     ops = []
-    keep = []
     if rank == src:
         for r in range(world):
             ra, rb = shard_range(ncols, world, r, align)
-            if r == src:
-                recv.copy_(full[:, ra:rb])
-                continue
-            piece = full[:, ra:rb].contiguous()
-            keep.append(piece)
-            ops.append(dist.P2POp(dist.isend, piece, r))
-    else:
-        ops.append(dist.P2POp(dist.irecv, recv, src))
+            if r != src and rb > ra:
+                ops += [dist.P2POp(dist.isend, full[i, ra:rb], r) for i in range(rows)]
+    elif b > a:
+        ops += [dist.P2POp(dist.irecv, local[i], src) for i in range(rows)]
     if ops:
         for w in dist.batch_isend_irecv(ops):
             w.wait()
-    local.copy_(recv)
     return local
+
+
+def gather_pieces(local: torch.Tensor, widths: list[int], dst: int = 0) -> torch.Tensor | None:
+    """Rank r contributes ``local`` [rows, widths[r]] (rows 1-D contiguous); rank ``dst`` returns the
+    pieces side by side in rank order as one pitched [rows, sum(widths)] tensor, others None.
+
+    One point-to-point message per (peer, row), received in place into the destination's column
+    slice — each peer drives its own xGMI link into ``dst``; the only copy is dst's own piece."""
+    world, rank = _world(), _rank()
+    rows = local.shape[0]
+    if len(widths) != world or local.shape[1] != widths[rank]:
+        raise ValueError("gather_pieces: widths must list every rank's piece width (this rank's = local.shape[1])")
+    if world == 1:
+        return local
+    ops = []
+    full = None
+    if rank == dst:
+        offs = [0]
+        for w in widths:
+            offs.append(offs[-1] + w)
+        full = alloc_rows(rows, offs[-1], local.device)
+        if widths[dst]:
+            full[:, offs[dst]:offs[dst + 1]].copy_(local)
+        for r in range(world):
+            if r != dst and widths[r]:
+                ops += [dist.P2POp(dist.irecv, full[i, offs[r]:offs[r + 1]], r) for i in range(rows)]
+    elif widths[rank]:
+        ops += [dist.P2POp(dist.isend, local[i], dst) for i in range(rows)]
+    if ops:
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+    return full
 
 
 def gather_columns(local: torch.Tensor, ncols: int, dst: int = 0, align: int = SHARD_ALIGN) -> torch.Tensor | None:
     """Inverse of :func:`scatter_columns`: rank ``dst`` returns [rows, ncols], others None."""
-    world, rank = _world(), _rank()
-    if world == 1:
-        return local.clone()
-    rows = local.shape[0]
-    ops, bufs = [], {}
-    if rank == dst:
-        full = torch.empty((rows, ncols), dtype=torch.uint8, device=local.device)
-        for r in range(world):
-            ra, rb = shard_range(ncols, world, r, align)
-            if r == dst:
-                full[:, ra:rb].copy_(local)
-                continue
-            bufs[r] = torch.empty((rows, rb - ra), dtype=torch.uint8, device=local.device)
-            ops.append(dist.P2POp(dist.irecv, bufs[r], r))
-    else:
-        send = local.contiguous()
-        ops.append(dist.P2POp(dist.isend, send, dst))
-    if ops:
-        for w in dist.batch_isend_irecv(ops):
-            w.wait()
-    if rank != dst:
-        return None
-    for r, buf in bufs.items():
-        ra, rb = shard_range(ncols, world, r, align)
-        full[:, ra:rb].copy_(buf)
-    return full
+    world = _world()
+    widths = [b - a for a, b in (shard_range(ncols, world, r, align) for r in range(world))]
+    return gather_pieces(local, widths, dst)
 
 
 class DistributedRS:

@@ -6,9 +6,10 @@
 
 Single-process modes call the native file codec (``csrc/io/codec_file.cpp``) with either the gfx950
 streaming pipeline or the C++ CPU codec. ``--dist`` is the multi-GPU mode: every rank reads its own
-4 KiB-aligned column range of every chunk straight from the file (no scatter), encodes/decodes it
-on its GPU, and the results are either gathered into rank 0 over RCCL point-to-point (default) or
-written in place by each rank (``--gather none``, parallel pwrite).
+4 KiB-aligned column range of every chunk straight from the file (no scatter) in bounded column
+windows (``--window``, default 64 MiB per chunk row), encodes/decodes it on its GPU, and the results
+are either gathered into rank 0 over RCCL point-to-point (default) or written in place by each rank
+(``--gather none``, parallel pwrite).
 """
 from __future__ import annotations
 
@@ -102,36 +103,78 @@ def main(argv=None) -> int:
 
 
 # ---- distributed mode -------------------------------------------------------------------------
+DIST_WINDOW = 64 << 20  # default column window per chunk row and rank (host RAM ~ (k + p) x window)
+
+
 def _read_cols(path: str, offset: int, nbytes: int, out: np.ndarray) -> None:
-    """pread ``nbytes`` at ``offset`` into ``out``; zero-fill past EOF."""
-    out[:] = 0
-    if nbytes <= 0:
-        return
-    with open(path, "rb") as f:
-        f.seek(offset)
-        buf = f.read(nbytes)
-    out[: len(buf)] = np.frombuffer(buf, dtype=np.uint8)
+    """pread ``nbytes`` at ``offset`` into ``out``; zero-fill the rest (past EOF / past nbytes)."""
+    got = 0
+    if nbytes > 0:
+        fd = os.open(path, os.O_RDONLY)
+        try:
+            view = memoryview(out)[:nbytes]
+            while got < nbytes:
+                n = os.preadv(fd, [view[got:]], offset + got)
+                if n <= 0:
+                    break
+                got += n
+        finally:
+            os.close(fd)
+    out[got:] = 0
 
 
-def _pwrite(path: str, offset: int, data: np.ndarray) -> None:
-    fd = os.open(path, os.O_WRONLY | os.O_CREAT, 0o644)
-    try:
-        os.pwrite(fd, data.tobytes(), offset)
-    finally:
-        os.close(fd)
+def _pwrite(fd: int, offset: int, data: np.ndarray) -> None:
+    view = memoryview(np.ascontiguousarray(data)).cast("B")
+    done = 0
+    while done < len(view):
+        done += os.pwrite(fd, view[done:], offset + done)
+
+
+def _windows(world: int, C: int, window: int):
+    """Per window index t: every rank's (column offset, width) — identical on all ranks, so the
+    collective per window lines up even where a rank's shard is exhausted (width 0)."""
+    from ..parallel.dist import shard_range
+
+    spans = [shard_range(C, world, r) for r in range(world)]
+    nwin = max(((b - a) + window - 1) // window for a, b in spans) if C else 0
+    for t in range(nwin):
+        yield [(a + t * window, max(0, min(window, b - a - t * window))) for a, b in spans]
 
 
 def _main_dist(a) -> int:
+    """Windowed, column-sharded encode/decode over torch.distributed.
+
+    Every rank owns a 4 KiB-aligned column range of every chunk (the reference's per-device split,
+    src/encode.cu:368-381) and walks it in windows of ``--window`` bytes per chunk row, so host
+    memory stays bounded at ~(k + p) x window per rank whatever the file size. Per window: pread
+    of the rank's columns, H2D, GF-GEMM on the rank's GPU, then either every rank pwrites its own
+    columns (``--gather none``) or the window's results travel to rank 0 over RCCL point-to-point
+    (received in place, one xGMI link per peer) and rank 0 writes them (``--gather rccl``, the
+    reference's gather-to-one-writer, src/encode.cu:410-429). Rank 0 creates every output at its
+    final size first, so no stale bytes of an older, longer file survive."""
     import torch
     import torch.distributed as dist
 
     from ..models import ReedSolomon
-    from ..parallel.dist import broadcast_matrix, gather_columns, init_distributed, shard_range
+    from ..parallel.dist import broadcast_matrix, gather_pieces, init_distributed
     from . import fileformat as ff
 
     ctx = init_distributed()
     world, rank = ctx.world, ctx.rank
+    window = max(4096, ((a.window or DIST_WINDOW) + 4095) // 4096 * 4096)
     t0 = time.perf_counter()
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    def create(path: str, size: int) -> None:
+        fd = os.open(path, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644)
+        try:
+            os.ftruncate(fd, size)
+        finally:
+            os.close(fd)
+
     if a.encode_file:
         path = a.encode_file
         total = os.path.getsize(path)
@@ -139,78 +182,107 @@ def _main_dist(a) -> int:
         C = ff.chunk_size(total, k)
         e = ReedSolomon(k, a.n, matrix=a.matrix).E if ctx.is_root else None
         e = broadcast_matrix(e, ctx.device)
-        lo, hi = shard_range(C, world, rank)
-        host = np.zeros((k, hi - lo), dtype=np.uint8)
-        for j in range(k):  # each rank reads its own columns of every native chunk: no scatter
-            start = j * C + lo
-            _read_cols(path, start, max(0, min(hi - lo, total - start)), host[j])
         rs = ReedSolomon(k, a.n)
         rs.E, rs.G = e, np.vstack([np.eye(k, dtype=np.uint8), e])
-        data = torch.from_numpy(host).to(ctx.device)
-        parity = rs.encode(data)
-        if ctx.device.type == "cuda":
-            torch.cuda.synchronize()
-        if a.gather == "rccl":
-            full = gather_columns(parity.contiguous(), C)
-            if ctx.is_root:
-                fullh = full.cpu().numpy()
-                with open(path, "rb") as f:
-                    blob = f.read()
-                for j in range(k):
-                    seg = np.zeros(C, dtype=np.uint8)
-                    chunk = np.frombuffer(blob[j * C : (j + 1) * C], dtype=np.uint8)
-                    seg[: len(chunk)] = chunk
-                    seg.tofile(ff.chunk_path(path, j))
-                for i in range(p):
-                    fullh[i].tofile(ff.chunk_path(path, k + i))
-        else:
-            ph = parity.cpu().numpy()
-            for j in range(k):
-                _pwrite(ff.chunk_path(path, j), lo, host[j])
-            for i in range(p):
-                _pwrite(ff.chunk_path(path, k + i), lo, ph[i])
+        if ctx.is_root:
+            for i in range(a.n):
+                create(ff.chunk_path(path, i), C)
+        barrier()
+        fds = [os.open(ff.chunk_path(path, i), os.O_WRONLY) for i in range(a.n)]
+        host = np.zeros((k, window), dtype=np.uint8)
+        try:
+            for spans in _windows(world, C, window):
+                o, w = spans[rank]
+                if w:
+                    for j in range(k):  # natives: this rank's columns of chunk j, zero past EOF
+                        start = j * C + o
+                        _read_cols(path, start, max(0, min(w, total - start)), host[j, :w])
+                        _pwrite(fds[j], o, host[j, :w])
+                    parity = rs.encode(torch.from_numpy(host[:, :w]).to(ctx.device))
+                else:
+                    parity = torch.empty((p, 0), dtype=torch.uint8, device=ctx.device)
+                if a.gather == "rccl" and world > 1:
+                    if ctx.device.type == "cuda":
+                        torch.cuda.synchronize()
+                    full = gather_pieces(parity, [ww for _, ww in spans])
+                    if ctx.is_root:
+                        ph = full.cpu().numpy()
+                        col = 0
+                        for ro, rw in spans:
+                            for i in range(p):
+                                _pwrite(fds[k + i], ro, ph[i, col:col + rw])
+                            col += rw
+                elif w:
+                    ph = parity.cpu().numpy()
+                    for i in range(p):
+                        _pwrite(fds[k + i], o, ph[i, :w])
+        finally:
+            for fd in fds:
+                os.close(fd)
         if ctx.is_root:
             ff.write_metadata(ff.metadata_path(path), total, p, k, e, with_matrix=not a.cpu_meta)
-        if world > 1:
-            dist.barrier()
-        _say(a, f"[rank {rank}] encoded columns [{lo}, {hi}) in {1e3 * (time.perf_counter() - t0):.1f}ms")
+        barrier()
+        lo, hi = spans_of(world, C, rank)
+        _say(a, f"[rank {rank}] encoded columns [{lo}, {hi}) in windows of {window} B "
+                f"in {1e3 * (time.perf_counter() - t0):.1f}ms")
     else:
         md = ff.read_metadata(ff.metadata_path(a.in_file))
         names = ff.read_conf(a.conf)[: md.k]
         rows = [ff.chunk_index(nm) for nm in names]
         k, C = md.k, ff.chunk_size(md.total_size, md.k)
-        lo, hi = shard_range(C, world, rank)
-        host = np.zeros((k, hi - lo), dtype=np.uint8)
-        for j, nm in enumerate(names):
-            _read_cols(ff.resolve_chunk(nm, a.in_file), lo, hi - lo, host[j])
         rs = ReedSolomon(k, md.n)
         rs.E, rs.G = md.e, md.g
-        out = rs.decode(torch.from_numpy(host).to(ctx.device), rows)
-        if ctx.device.type == "cuda":
-            torch.cuda.synchronize()
         dst = a.out or a.in_file
-        if a.gather == "rccl":
-            full = gather_columns(out.contiguous(), C)
-            if ctx.is_root:
-                full.cpu().numpy().reshape(-1)[: md.total_size].tofile(dst)
-        else:
-            oh = out.cpu().numpy()
-            if ctx.is_root:
-                with open(dst, "wb") as f:
-                    f.truncate(md.total_size)
-            if world > 1:
-                dist.barrier()
+        if ctx.is_root:
+            create(dst, md.total_size)
+        barrier()
+        paths = [ff.resolve_chunk(nm, a.in_file) for nm in names]
+        fd_out = os.open(dst, os.O_WRONLY)
+        host = np.zeros((k, window), dtype=np.uint8)
+
+        def write_natives(nat: np.ndarray, o: int, w: int) -> None:
             for j in range(k):
-                start = j * C + lo
-                n = max(0, min(hi - lo, md.total_size - start))
+                start = j * C + o
+                n = max(0, min(w, md.total_size - start))
                 if n:
-                    _pwrite(dst, start, oh[j, :n])
-        if world > 1:
-            dist.barrier()
-        _say(a, f"[rank {rank}] decoded columns [{lo}, {hi}) in {1e3 * (time.perf_counter() - t0):.1f}ms")
+                    _pwrite(fd_out, start, nat[j, :n])
+
+        try:
+            for spans in _windows(world, C, window):
+                o, w = spans[rank]
+                if w:
+                    for j, pth in enumerate(paths):
+                        _read_cols(pth, o, w, host[j, :w])
+                    out = rs.decode(torch.from_numpy(host[:, :w]).to(ctx.device), rows)
+                else:
+                    out = torch.empty((k, 0), dtype=torch.uint8, device=ctx.device)
+                if a.gather == "rccl" and world > 1:
+                    if ctx.device.type == "cuda":
+                        torch.cuda.synchronize()
+                    full = gather_pieces(out, [ww for _, ww in spans])
+                    if ctx.is_root:
+                        fh = full.cpu().numpy()
+                        col = 0
+                        for ro, rw in spans:
+                            write_natives(fh[:, col:col + rw], ro, rw)
+                            col += rw
+                elif w:
+                    write_natives(out.cpu().numpy(), o, w)
+        finally:
+            os.close(fd_out)
+        barrier()
+        lo, hi = spans_of(world, C, rank)
+        _say(a, f"[rank {rank}] decoded columns [{lo}, {hi}) in windows of {window} B "
+                f"in {1e3 * (time.perf_counter() - t0):.1f}ms")
     if world > 1:
         dist.destroy_process_group()
     return 0
+
+
+def spans_of(world: int, C: int, rank: int) -> tuple[int, int]:
+    from ..parallel.dist import shard_range
+
+    return shard_range(C, world, rank)
 
 
 if __name__ == "__main__":

@@ -1,0 +1,207 @@
+#!/usr/bin/env python3
+"""The reference's published k-sweep, reproduced: k in {4, 8, 16, 32, 64, 128}, n-k in {2, 3}, on
+1.1 GB (1,070,616 KB = 1,096,310,784 bytes) of random input.
+
+Published points (Tesla C2050 / Xeon E5620, ms): doc/result-graph/Total-{GPU,CPU}-{en,de}coding-
+time-{2,3}.pdf, doc/design.tex:400-425 (table in BASELINE.md). The reference's GPU time is
+H2D + kernel + D2H (+ alloc/free), its CPU time is matrix generation + GEMM (encode) or inversion +
+GEMM (decode), one thread, no file I/O (src/cpu-rs.c:523-532,650-665).
+
+Measured per point:
+  gpu_enc_ms / gpu_dec_ms   device-resident: encode GEMM; on-device decode-system solve + decode
+                            GEMM with fused survivor copy (the bench.py step), 1.1 GB in HBM
+  e2e_enc_ms / e2e_dec_ms   the reference's definition: pinned host -> H2D -> GEMM -> D2H through
+                            the native streaming pipeline (-s 4)
+  cpu_enc_ms / cpu_dec_ms   the C++ CPU codec, one thread (the reference's single-threaded CPU-RS),
+                            GEMM + matrix generation / inversion
+Decode erases the first n-k natives (the reference's src/unit-test.sh worst case: conf = last k).
+
+  python scripts/sweep.py --part gpu --out profiles/r02_sweep/gpu.json     (on an MI355X)
+  python scripts/sweep.py --part cpu --out profiles/r02_sweep/cpu.json     (any host)
+  python scripts/sweep.py --table profiles/r02_sweep                       (README table)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+SIZE = 1_096_310_784
+KS = [4, 8, 16, 32, 64, 128]
+PS = [2, 3]
+PUBLISHED = {  # (p, what) -> ms per k in KS
+    (2, "gpu_enc"): [576.41, 665.97, 947.59, 1495.11, 2702.54, 5060.78],
+    (2, "gpu_dec"): [751.38, 1028.64, 1210.73, 1856.64, 3167.55, 5958.09],
+    (3, "gpu_enc"): [766.31, 695.00, 934.14, 1509.53, 2674.74, 5053.13],
+    (3, "gpu_dec"): [873.92, 1026.68, 1345.65, 1875.05, 3167.34, 5960.18],
+    (2, "cpu_enc"): [29983.57, 31949.64, 33551.97, 35640.56, 37578.67, 38976.97],
+    (2, "cpu_dec"): [56727.41, 102329.37, 180925.46, 350517.56, 717487.56, 1503671.79],
+    (3, "cpu_enc"): [63576.18, 69742.70, 76632.81, 88753.94, 92687.19, 90481.19],
+    (3, "cpu_dec"): [86035.54, 152057.25, 265409.99, 529962.25, 1052574.52, 2054669.45],
+}
+
+
+def gpu_point(k: int, p: int, reps: int = 5) -> dict:
+    import torch
+
+    from gpu_rscode_amd import ReedSolomon, alloc_rows
+    from gpu_rscode_amd._native import hip
+    from gpu_rscode_amd.ops import GemmPlan, decode_system_into_plan, fill_random_
+
+    n = k + p
+    C = (SIZE + k - 1) // k
+    dev = torch.device("cuda", 0)
+    rs = ReedSolomon(k, n)
+    data = alloc_rows(k, C, dev)
+    fill_random_(data.as_strided((data.untyped_storage().nbytes(),), (1,)), seed=k * 7 + p)
+    parity = alloc_rows(p, C, dev)
+    out = alloc_rows(k, C, dev)
+    enc = GemmPlan(data, parity, rs.E)
+    rows = list(range(p, n))  # unit-test.sh: keep the last k chunks
+    erased = list(range(p))
+    stripe = [data[i] for i in range(k)] + [parity[i] for i in range(p)]
+    dec = GemmPlan([stripe[r] for r in rows], [out[i] for i in erased], copies=[out[r] if r < k else None for r in rows],
+                   device_tables=True)
+    g_dev = torch.from_numpy(np.ascontiguousarray(rs.G)).to(dev)
+    rows_dev = torch.tensor(rows, dtype=torch.int32, device=dev)
+    er_dev = torch.tensor(erased, dtype=torch.int32, device=dev)
+    status = torch.zeros(1, dtype=torch.int32, device=dev)
+
+    def t_cuda(fn):
+        fn()
+        torch.cuda.synchronize()
+        best = 1e30
+        for _ in range(reps):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            fn()
+            b.record()
+            b.synchronize()
+            best = min(best, a.elapsed_time(b))
+        return best
+
+    enc_ms = t_cuda(lambda: enc.run())
+
+    def decode():
+        decode_system_into_plan(g_dev, rows_dev, er_dev, dec, status=status)
+        dec.run()
+
+    dec_ms = t_cuda(decode)
+    ok = int(status.item()) == 0 and torch.equal(out, data)
+
+    # e2e: pinned host rows through the streaming pipeline
+    h = hip()
+    host = torch.empty((k, C), dtype=torch.uint8, pin_memory=True)
+    host.copy_(data)
+    par = torch.empty((p, C), dtype=torch.uint8, pin_memory=True)
+    rec = torch.empty((p, C), dtype=torch.uint8, pin_memory=True)
+    dm = rs.decode_matrix(rows)[erased]
+    h.prepare_pipeline([0], k, p, C, 4, 32 << 20)
+
+    def host_run(ins, outs, mat):
+        h.gemm_host([0], ins, outs, mat, C, 4, 32 << 20, 0, False)
+        best = 1e30
+        for _ in range(3):
+            best = min(best, h.gemm_host([0], ins, outs, mat, C, 4, 32 << 20, 0, False)["devices"][0]["ms_total"])
+        return best
+
+    e2e_enc = host_run([host[j].data_ptr() for j in range(k)], [par[i].data_ptr() for i in range(p)],
+                       np.ascontiguousarray(rs.E).tobytes())
+    e2e_dec = host_run([host[r].data_ptr() if r < k else par[r - k].data_ptr() for r in rows],
+                       [rec[i].data_ptr() for i in range(p)], np.ascontiguousarray(dm).tobytes())
+    ok = ok and torch.equal(rec, host[erased])
+    return dict(k=k, p=p, C=C, gpu_enc_ms=enc_ms, gpu_dec_ms=dec_ms, e2e_enc_ms=e2e_enc, e2e_dec_ms=e2e_dec,
+                engine=enc.engine, dec_engine=dec.engine, verified=bool(ok))
+
+
+def cpu_point(k: int, p: int, threads: int = 1, strategy: str = "row") -> dict:
+    from gpu_rscode_amd import ReedSolomon
+    from gpu_rscode_amd._native import cpu
+
+    n = k + p
+    C = (SIZE + k - 1) // k
+    rng = np.random.default_rng(k * 7 + p)
+    data = rng.integers(0, 256, size=(k, C), dtype=np.uint8)
+    parity = np.zeros((p, C), dtype=np.uint8)
+    rec = np.zeros((p, C), dtype=np.uint8)
+    c = cpu()
+    t0 = time.perf_counter()
+    rs = ReedSolomon(k, n)  # matrix generation inside the timed region, like the reference
+    c.gemm([data[j].ctypes.data for j in range(k)], [parity[i].ctypes.data for i in range(p)],
+           np.ascontiguousarray(rs.E).tobytes(), C, strategy, threads)
+    enc_ms = (time.perf_counter() - t0) * 1e3
+    rows = list(range(p, n))
+    surv = [data[r] if r < k else parity[r - k] for r in rows]
+    t0 = time.perf_counter()
+    dm = rs.decode_matrix(rows)[list(range(p))]  # inversion inside the timed region
+    c.gemm([s.ctypes.data for s in surv], [rec[i].ctypes.data for i in range(p)], np.ascontiguousarray(dm).tobytes(),
+           C, strategy, threads)
+    dec_ms = (time.perf_counter() - t0) * 1e3
+    return dict(k=k, p=p, C=C, cpu_enc_ms=enc_ms, cpu_dec_ms=dec_ms, threads=threads, strategy=strategy,
+                verified=bool(np.array_equal(rec, data[:p])))
+
+
+def table(d: str) -> str:
+    def load(name):
+        path = os.path.join(d, name)
+        if not os.path.exists(path):
+            return {}
+        return {(r["k"], r["p"]): r for r in json.load(open(path))["points"]}
+
+    g, c = load("gpu.json"), load("cpu.json")
+    mb = SIZE / 1048576
+    lines = ["| n-k | k | ref GPU enc ms | e2e enc ms | dev enc ms | ref GPU dec ms | e2e dec ms | dev dec ms | "
+             "ref CPU enc ms | CPU enc ms (1 thr) | ref CPU dec ms | CPU dec ms (1 thr) | e2e enc+dec MB/s (ref) |",
+             "|---|---|---|---|---|---|---|---|---|---|---|---|---|"]
+    for p in PS:
+        for i, k in enumerate(KS):
+            gr, cr = g.get((k, p), {}), c.get((k, p), {})
+
+            def f(x):
+                return "—" if x is None else (f"{x:,.1f}" if x >= 10 else f"{x:.3f}")
+
+            ref_e, ref_d = PUBLISHED[(p, "gpu_enc")][i], PUBLISHED[(p, "gpu_dec")][i]
+            mbps = "—"
+            if gr:
+                mbps = f"{2 * mb / ((gr['e2e_enc_ms'] + gr['e2e_dec_ms']) / 1e3):,.0f} ({2 * mb / ((ref_e + ref_d) / 1e3):,.0f})"
+            lines.append(f"| {p} | {k} | {ref_e:,.2f} | {f(gr.get('e2e_enc_ms'))} | {f(gr.get('gpu_enc_ms'))} | "
+                         f"{ref_d:,.2f} | {f(gr.get('e2e_dec_ms'))} | {f(gr.get('gpu_dec_ms'))} | "
+                         f"{PUBLISHED[(p, 'cpu_enc')][i]:,.0f} | {f(cr.get('cpu_enc_ms'))} | "
+                         f"{PUBLISHED[(p, 'cpu_dec')][i]:,.0f} | {f(cr.get('cpu_dec_ms'))} | {mbps} |")
+    return "\n".join(lines)
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--part", choices=["gpu", "cpu"])
+    ap.add_argument("--out")
+    ap.add_argument("--ks", default=",".join(map(str, KS)))
+    ap.add_argument("--ps", default=",".join(map(str, PS)))
+    ap.add_argument("--threads", type=int, default=1)
+    ap.add_argument("--table", metavar="DIR")
+    a = ap.parse_args()
+    if a.table:
+        print(table(a.table))
+        return 0
+    pts = []
+    for p in map(int, a.ps.split(",")):
+        for k in map(int, a.ks.split(",")):
+            r = gpu_point(k, p) if a.part == "gpu" else cpu_point(k, p, a.threads)
+            print(json.dumps(r), flush=True)
+            pts.append(r)
+    if a.out:
+        os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
+        with open(a.out, "w") as f:
+            json.dump({"size_bytes": SIZE, "part": a.part, "points": pts}, f, indent=1)
+    return 0 if all(r["verified"] for r in pts) else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())

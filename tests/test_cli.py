@@ -58,3 +58,35 @@ def test_torchrun_dist_cli_matches_single_process(tmp_path, gather):
                        text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     assert (d1 / "o.bin").read_bytes() == payload
+
+
+@pytest.mark.parametrize("gather", ["rccl", "none"])
+def test_torchrun_dist_cli_windows_world3_and_stale_outputs(tmp_path, gather):
+    """3 ranks walking their shards in 4 KiB windows (uneven shard sizes, so some ranks run out of
+    columns while the window collective continues), over stale, longer chunk / output files."""
+    payload = os.urandom(7 * 4096 * 12 + 4321)
+    d1, d2 = tmp_path / "dist", tmp_path / "single"
+    d1.mkdir()
+    d2.mkdir()
+    (d1 / "f.bin").write_bytes(payload)
+    (d2 / "f.bin").write_bytes(payload)
+    for i in range(16):  # stale chunk files from an older, longer encode
+        (d1 / f"_{i}_f.bin").write_bytes(b"\xee" * (len(payload) // 4))
+    (d1 / "o.bin").write_bytes(b"\xee" * (2 * len(payload)))
+    env = dict(os.environ, PYTHONPATH=ROOT, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    base = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=3",
+            "--master-addr=127.0.0.1", f"--master-port={_port()}", "-m", "gpu_rscode_amd", "--dist", "--gather", gather,
+            "--window", "4096"]
+    r = subprocess.run(base + ["-k", "12", "-n", "16", "-e", "f.bin"], cwd=d1, capture_output=True, text=True,
+                       timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    r = _py(["-k", "12", "-n", "16", "-e", "f.bin", "--backend", "cpu"], d2)
+    assert r.returncode == 0, r.stderr
+    for i in range(16):
+        assert (d1 / f"_{i}_f.bin").read_bytes() == (d2 / f"_{i}_f.bin").read_bytes(), i
+    ff.write_conf(str(d1 / "conf"), [f"_{i}_f.bin" for i in (0, 2, 3, 4, 6, 7, 8, 10, 12, 13, 14, 15)])
+    base[6] = f"--master-port={_port()}"
+    r = subprocess.run(base + ["-d", "-i", "f.bin", "-c", "conf", "-o", "o.bin"], cwd=d1, capture_output=True,
+                       text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert (d1 / "o.bin").read_bytes() == payload
