@@ -331,3 +331,47 @@ def test_decode_system_matches_host_decode_matrix(k, n, matrix):
         assert np.array_equal(tabs[:, : len(erased), :].view(np.uint32), ref_tabs.astype(np.uint32)), (rows, erased)
         checked += 1
     assert checked > 0
+
+
+@pytest.mark.parametrize("k,m", [(20, 16), (40, 32), (72, 24), (100, 17), (128, 32), (128, 16)])
+@pytest.mark.parametrize("variant", ["uniform", "scattered", "copy"])
+def test_fp4_double_buffered_kernel_chunk_counts(k, m, variant, monkeypatch):
+    """The double-buffered FP4 kernel (gf_gemm_fp4db_kernel: 128-column chunks processed in pairs,
+    the epilogue of chunk i under the MFMAs of chunk i+1) for every K-slot count (KS = 1..4), both
+    M-group sizes, uniform / scattered / fused-copy inputs, and a column count that gives the
+    persistent blocks both even and odd chunk counts plus a v_perm remainder — bit-exact against the
+    oracle and against the single-buffered kernel (GFRS_FP4_KERNEL=v1)."""
+    _native_loaded()
+    ncols = 128 * (256 * 3 + 5) + 77
+    rng = np.random.default_rng(k * 31 + m)
+    coeff = rng.integers(0, 256, size=(m, k), dtype=np.uint8)
+    host, dev = _rand_rows(k, ncols, k + m)
+    inputs, want_in = dev, host
+    copies = None
+    if variant in ("scattered", "copy"):
+        perm = rng.permutation(k)
+        inputs = [dev[j].clone() for j in perm]
+        want_in = host[perm]
+    if variant == "copy":
+        cdst = alloc_rows(k, ncols, "cuda", fill=0x44)
+        copies = [cdst[j] if j % 4 else None for j in range(k)]
+    results = []
+    for kernel in ("db", "v1"):
+        if kernel == "v1":
+            monkeypatch.setenv("GFRS_FP4_KERNEL", "v1")
+        else:
+            monkeypatch.delenv("GFRS_FP4_KERNEL", raising=False)
+        out = alloc_rows(m, ncols, "cuda", fill=0x5A)
+        if copies is not None:
+            cdst.fill_(0x44)
+        plan = GemmPlan(inputs, out, coeff, copies=copies, engine="mfma")
+        plan.run()
+        torch.cuda.synchronize()
+        got = out.cpu().numpy()
+        assert np.array_equal(got, GF256.gemm(coeff, want_in)), kernel
+        if copies is not None:
+            c = cdst.cpu().numpy()
+            for j in range(k):
+                assert np.array_equal(c[j], want_in[j] if j % 4 else np.full(ncols, 0x44, np.uint8)), (kernel, j)
+        results.append(got)
+    assert np.array_equal(results[0], results[1])
