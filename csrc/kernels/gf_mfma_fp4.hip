@@ -538,17 +538,16 @@ __device__ __forceinline__ void static_for(F&& f) {
   static_for_impl(f, std::make_integer_sequence<int, N>{});
 }
 
-// K-step of a chunk during which the epilogue of M-tile e of the previous chunk runs
-__host__ __device__ constexpr int db_tile_step(int e, int mg, int ns) { return e * ns / mg; }
-__host__ __device__ constexpr int db_tile_at(int s, int mg, int ns) {
-  for (int e = 0; e < mg; ++e)
-    if (db_tile_step(e, mg, ns) == s) return e;
-  return -1;
+// The epilogue of M-tile e of the previous chunk runs during K-step e * ns / mg of a chunk: K-step
+// s handles tiles [db_first_tile(s), db_first_tile(s + 1)) — none, one, or (mg > ns) several.
+__host__ __device__ constexpr int db_first_tile(int s, int mg, int ns) { return (s * mg + ns - 1) / ns; }
+__host__ __device__ constexpr int db_tiles_at(int s, int mg, int ns) {
+  return db_first_tile(s + 1, mg, ns) - db_first_tile(s, mg, ns);
 }
 // epilogue stores (2 per tile) in chunk-relative steps [s0, s1) (steps wrap around the chunk)
 __host__ __device__ constexpr int db_stores_in(int s0, int s1, int mg, int ns) {
   int n = 0;
-  for (int s = s0; s < s1; ++s) n += db_tile_at(((s % ns) + ns) % ns, mg, ns) >= 0 ? 2 : 0;
+  for (int s = s0; s < s1; ++s) n += 2 * db_tiles_at(((s % ns) + ns) % ns, mg, ns);
   return n;
 }
 // vm ops issued after the DMA of slot sp+1 by the time its data is awaited (start of step 2 of
@@ -754,7 +753,7 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4db_kernel(cptr<uint64_t> in
       static_for<kSPS>([&](auto j_tag) {
         constexpr int J = decltype(j_tag)::value;
         constexpr int S = SP * kSPS + J;
-        constexpr int E = db_tile_at(S, MG, NS);
+        constexpr int E0 = db_first_tile(S, MG, NS), NT = db_tiles_at(S, MG, NS);
         if constexpr (J == kSPS - 2)  // the next slot has landed: count the younger ops (header)
           asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kWait) : "memory");
         if constexpr (J + 2 < kSPS)
@@ -762,14 +761,18 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4db_kernel(cptr<uint64_t> in
         else
           read_x(x2, std::integral_constant<int, RS1>{}, std::integral_constant<int, J + 2 - kSPS>{});
         read_a(an, std::integral_constant<int, (S + 1) % NS>{});
-        [[maybe_unused]] uint64_t op[2];
-        if constexpr (E >= 0) {
+        [[maybe_unused]] uint64_t op[NT > 0 ? NT : 1][2];
+        static_for<NT>([&](auto t_tag) {
+          constexpr int E = E0 + decltype(t_tag)::value;
           const uint32_t addr = optr_addr;
+          uint64_t o0, o1;  // (locals: clang does not capture asm operands in generic lambdas)
           asm volatile("ds_read_b64 %0, %2 offset:%3\n\tds_read_b64 %1, %2 offset:%4"
-                       : "=&v"(op[0]), "=&v"(op[1])
-                       : "v"(addr), "n"(32 * (E >= 0 ? E : 0)), "n"(32 * (E >= 0 ? E : 0) + 8)
+                       : "=&v"(o0), "=&v"(o1)
+                       : "v"(addr), "n"(32 * E), "n"(32 * E + 8)
                        : "memory");
-        }
+          op[decltype(t_tag)::value][0] = o0;
+          op[decltype(t_tag)::value][1] = o1;
+        });
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int mt = 0; mt < MG; ++mt) {
@@ -778,20 +781,21 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4db_kernel(cptr<uint64_t> in
           acc[CUR][mt] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, bb, acc[CUR][mt], 4, 4, 0, scale, 0, scale);
         }
         expand(bn, x1);
-        [[maybe_unused]] uint32_t y[2];
-        if constexpr (E >= 0) {
-          // output bytes of rows 2h, 2h+1 of M-tile E of the previous chunk: 7 v_bfi per byte over
-          // the biased accumulators (the parity of bit b's count sits at bit b), then re-bias
+        [[maybe_unused]] uint32_t y[NT > 0 ? NT : 1][2];
+        // output bytes of rows 2h, 2h+1 of M-tiles E0.. of the previous chunk: 7 v_bfi per byte over
+        // the biased accumulators (the parity of bit b's count sits at bit b), then re-bias
+        static_for<NT>([&](auto t_tag) {
+          constexpr int T = decltype(t_tag)::value, E = E0 + T;
 #pragma unroll
           for (int b = 0; b < 8; ++b)
 #pragma unroll
             for (int u = 0; u < 2; ++u) {
-              const uint32_t v = __float_as_uint(acc[PREV][E >= 0 ? E : 0][8 * u + b]);
-              y[u] = b == 0 ? v : bfi(1u << b, v, y[u]);
+              const uint32_t v = __float_as_uint(acc[PREV][E][8 * u + b]);
+              y[T][u] = b == 0 ? v : bfi(1u << b, v, y[T][u]);
             }
-          acc[PREV][E >= 0 ? E : 0] = kBias;
-        }
-        constexpr int kValu = kExpandValu + (E >= 0 ? 16 + 14 + 16 : 0);
+          acc[PREV][E] = kBias;
+        });
+        constexpr int kValu = kExpandValu + NT * (16 + 14 + 16);
 #pragma unroll
         for (int i = 0; i < MG; ++i) {
           __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                      // MFMA
@@ -810,15 +814,19 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4db_kernel(cptr<uint64_t> in
           ac[mt] = an[mt];
         }
         bc = bn;
-        if constexpr (E >= 0) {
-          tie(op[0]);
-          tie(op[1]);
+        static_for<NT>([&](auto t_tag) {
+          constexpr int T = decltype(t_tag)::value;
+          uint64_t o0 = op[T][0], o1 = op[T][1];
+          tie(o0);
+          tie(o1);
+          op[T][0] = o0;
+          op[T][1] = o1;
 #pragma unroll
           for (int u = 0; u < 2; ++u) {
-            const uint64_t o = op[u];
-            *(gptr<uint8_t>)(plive && o ? o + uint64_t(pcol) : sink) = uint8_t(y[u]);
+            const uint64_t o = op[T][u];
+            *(gptr<uint8_t>)(plive && o ? o + uint64_t(pcol) : sink) = uint8_t(y[T][u]);
           }
-        }
+        });
         if constexpr (COPY && J == 0) {
           tie(cdat);
           const int crow = kRS * SP + drow;
