@@ -689,13 +689,20 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4db_kernel(cptr<uint64_t> in
   };
 
   f32x16 acc[2][MG];
-  // parity bias of accumulator register j: 2^(23 - (j & 7)) (see bias_scale_of_lane)
-  const f32x16 kBias = {8388608.f, 4194304.f, 2097152.f, 1048576.f, 524288.f, 262144.f, 131072.f, 65536.f,
-                        8388608.f, 4194304.f, 2097152.f, 1048576.f, 524288.f, 262144.f, 131072.f, 65536.f};
+  // parity bias of accumulator register j: 2^(23 - (j & 7)) (see bias_scale_of_lane). Laundered
+  // through an empty asm so the compiler cannot treat a re-biased accumulator as a constant: it
+  // then kept one shared constant AGPR block as every chunk's first MFMA C operand, which left no
+  // room for the second accumulator set and moved the previous chunk's 128 accumulators into VGPRs
+  // in one burst at every chunk start.
+  f32x16 kBias = {8388608.f, 4194304.f, 2097152.f, 1048576.f, 524288.f, 262144.f, 131072.f, 65536.f,
+                  8388608.f, 4194304.f, 2097152.f, 1048576.f, 524288.f, 262144.f, 131072.f, 65536.f};
+  asm volatile("" : "+v"(kBias));
 #pragma unroll
   for (int mt = 0; mt < MG; ++mt) {
     acc[0][mt] = kBias;
     acc[1][mt] = kBias;
+    asm volatile("" : "+a"(acc[0][mt]));
+    asm volatile("" : "+a"(acc[1][mt]));
   }
 
   // prologue: R-1 slots in flight, each followed by the stores a steady-state slot issues after its
@@ -786,6 +793,9 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4db_kernel(cptr<uint64_t> in
         // the biased accumulators (the parity of bit b's count sits at bit b), then re-bias
         static_for<NT>([&](auto t_tag) {
           constexpr int T = decltype(t_tag)::value, E = E0 + T;
+          // (a new opaque value here: the accumulator reads below cannot be hoisted to the chunk
+          // start, where all 128 of them would burst out of the AGPRs at once)
+          asm volatile("" : "+a"(acc[PREV][E]));
 #pragma unroll
           for (int b = 0; b < 8; ++b)
 #pragma unroll
@@ -794,6 +804,7 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4db_kernel(cptr<uint64_t> in
               y[T][u] = b == 0 ? v : bfi(1u << b, v, y[T][u]);
             }
           acc[PREV][E] = kBias;
+          asm volatile("" : "+a"(acc[PREV][E]));  // (an opaque accumulator from here on, see kBias)
         });
         constexpr int kValu = kExpandValu + NT * (16 + 14 + 16);
 #pragma unroll
@@ -1009,10 +1020,13 @@ template <int MG, bool UNI, bool COPY>
 hipError_t launch_fp4db_ks(int ks, const Fp4Geometry& geo, const Fp4Args& a, hipStream_t stream) {
   switch (ks) {
     case 1: return launch_fp4db<MG, UNI, COPY, 2, 1>(geo, a, stream);
-    case 2: return launch_fp4db<MG, UNI, COPY, 4, 2>(geo, a, stream);
-    case 3: return launch_fp4db<MG, UNI, COPY, 6, 3>(geo, a, stream);
     case 4: return launch_fp4db<MG, UNI, COPY, 4, 4>(geo, a, stream);
-    default: return hipErrorInvalidConfiguration;
+    default:
+      if constexpr (MG == 4) {  // (see db_slots)
+        if (ks == 2) return launch_fp4db<MG, UNI, COPY, 4, 2>(geo, a, stream);
+        if (ks == 3) return launch_fp4db<MG, UNI, COPY, 6, 3>(geo, a, stream);
+      }
+      return hipErrorInvalidConfiguration;
   }
 }
 
@@ -1029,6 +1043,8 @@ int db_slots(const Fp4Geometry& geo) {
   const char* env = std::getenv("GFRS_FP4_KERNEL");
   if (env && std::strcmp(env, "v1") == 0) return 0;
   const int ks = (geo.ksteps + 3) / 4;
+  // (MG = 8 with 2 or 3 slots per chunk spills VGPRs in the db form: those stay on v1)
+  if (geo.mg == 8 && (ks == 2 || ks == 3)) return 0;
   return (geo.mg == 4 || geo.mg == 8) && ks >= 1 && ks <= 4 ? ks : 0;
 }
 
