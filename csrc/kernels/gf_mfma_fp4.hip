@@ -513,21 +513,34 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4_kernel(cptr<uint64_t> in, 
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA (dummy or not) outlives the wave
 }
 
-// ---- the double-buffered-accumulator form ("db") ---------------------------------------------
-// The kernel above idles its matrix pipe through every chunk epilogue: the 256 accumulators of a
-// 64-column wave tile fill all AGPRs, so the next chunk cannot start before the 256 accumulator
-// reads, 224 bit-field inserts and 16 bias MFMAs of the previous one are done — 65 % MFMA-pipe
-// utilisation at k=128, p=32 (profiles/r02_pmc_fp4). Here a wave owns 32 columns (one N-tile):
-// a chunk's accumulators take 128 AGPRs, so two chunks' fit, and the epilogue of chunk i (M-tile e
-// at K-step db_tile_step(e)) runs as VALU between the MFMAs of chunk i+1. Its accumulators are
-// re-biased with v_accvgpr_write instead of a bias MFMA (the bias of register j is 2^(23-(j&7)),
-// independent of the lane: see bias_scale_of_lane). Per K-step and wave: MG MFMAs, MG A fragments
-// from LDS, 4 byte reads + 8 VALU of B expansion, and ~MG/NS of a tile's epilogue.
-// Ring: per wave R slots of 1 KiB = 32 input rows x 32 columns (4 K-steps), one
-// global_load_lds_dwordx4 each (lane l: row l/2, columns 16 (l%2)..+15). Chunks are processed in
-// pairs (accumulator set 0, then 1) and 2*KS is a multiple of R, so every ring position, DMA
-// target and epilogue slot is a compile-time constant.
-constexpr int kDbCols = 128;  // columns per block chunk (4 waves x 32)
+// ---- the tile-staggered form ("sk", k in (112, 128]) -------------------------------------------
+// The kernel above idles its matrix pipe through every chunk epilogue: its 256 accumulators fill
+// the AGPRs, so a chunk cannot start before the 256 accumulator reads, 224 bit-field inserts and
+// 16 bias MFMAs of the previous one are done (65 % MFMA-pipe utilisation at k=128, p=32,
+// profiles/r02_pmc_fp4). Here the M-tiles run their K loops STAGGERED by one K-step each: at step
+// j of a chunk, M-tile mt works on K-step (j - mt) mod NS (of the previous chunk while mt > j).
+// Tile j therefore finishes its chunk at step j-1 and is packed, stored and re-biased during step
+// j — one tile's epilogue per step over the first MG steps of every chunk, interleaved with the 14
+// MFMAs of the other tiles instead of serialised after all of them. Same registers (one
+// accumulator per tile), same operands: the B operand of K-step s is kept for MG steps in a
+// window bw[s mod MG] (tile MG-1 uses it last), A fragments are read per (tile, K-step).
+// The last real chunk is drained by one phantom chunk (dummy DMAs, results discarded): its first
+// MG steps pack the real chunk's tiles. Every ring position, DMA target and counted wait is a
+// compile-time constant (KS slots per chunk, a multiple of the ring depth R).
+__host__ __device__ constexpr int sk_mod(int a, int n) { return ((a % n) + n) % n; }
+// ushort epilogue stores (2 per packed tile) in chunk-relative steps [s0, s1)
+__host__ __device__ constexpr int sk_stores_in(int s0, int s1, int mg, int ns) {
+  int n = 0;
+  for (int s = s0; s < s1; ++s) n += sk_mod(s, ns) < mg ? 2 : 0;
+  return n;
+}
+// vm ops issued after the DMA of slot sp+1 when its data is awaited (start of slot sp): R-2 DMAs,
+// the copy stores of slots sp+2-R .. sp-1 and the epilogue stores of their steps (exact: the
+// prologue issues the stores of the virtual slots before chunk 0 as dummies)
+__host__ __device__ constexpr int sk_wait_count(int sp, int mg, int ks, int r, bool copy) {
+  const int n = (r - 2) + (copy ? r - 2 : 0) + sk_stores_in(2 * (sp + 2 - r), 2 * sp, mg, 2 * ks);
+  return n < 63 ? n : 63;
+}
 
 template <typename F, int... I>
 __device__ __forceinline__ void static_for_impl(F& f, std::integer_sequence<int, I...>) {
@@ -538,49 +551,20 @@ __device__ __forceinline__ void static_for(F&& f) {
   static_for_impl(f, std::make_integer_sequence<int, N>{});
 }
 
-// The epilogue of M-tile e of the previous chunk runs during K-step e * ns / mg of a chunk: K-step
-// s handles tiles [db_first_tile(s), db_first_tile(s + 1)) — none, one, or (mg > ns) several.
-__host__ __device__ constexpr int db_first_tile(int s, int mg, int ns) { return (s * mg + ns - 1) / ns; }
-__host__ __device__ constexpr int db_tiles_at(int s, int mg, int ns) {
-  return db_first_tile(s + 1, mg, ns) - db_first_tile(s, mg, ns);
-}
-// epilogue stores (2 per tile) in chunk-relative steps [s0, s1) (steps wrap around the chunk)
-__host__ __device__ constexpr int db_stores_in(int s0, int s1, int mg, int ns) {
-  int n = 0;
-  for (int s = s0; s < s1; ++s) n += 2 * db_tiles_at(((s % ns) + ns) % ns, mg, ns);
-  return n;
-}
-// vm ops issued after the DMA of slot sp+1 by the time its data is awaited (start of step 2 of
-// slot sp), minimised over sp mod KS: R-2 DMAs, R-1 copy stores (one per slot, at its step 0) and
-// the epilogue stores of steps [4 (sp+2-R), 4 sp + 2). A lower bound keeps the wait exact or early.
-__host__ __device__ constexpr int db_wait_count(int mg, int ks, int r, bool copy) {
-  int best = 1 << 30;
-  for (int q = 0; q < ks; ++q) {
-    const int n = db_stores_in(4 * (q + 2 - r), 4 * q + 2, mg, 4 * ks);
-    best = n < best ? n : best;
-  }
-  const int n = (r - 2) + (copy ? r - 1 : 0) + best;
-  return n < 63 ? n : 63;
-}
-__host__ __device__ constexpr int db_max_slot_stores(int mg, int ks) {
-  int best = 0;
-  for (int q = 0; q < ks; ++q) {
-    const int n = db_stores_in(4 * q, 4 * q + 4, mg, 4 * ks);
-    best = n > best ? n : best;
-  }
-  return best;
-}
-
 template <int MG, bool UNI, bool COPY, int R, int KS>
-__global__ __launch_bounds__(256, 1) void gf_gemm_fp4db_kernel(cptr<uint64_t> in, cptr<uint64_t> out,
+__global__ __launch_bounds__(256, 1) void gf_gemm_fp4sk_kernel(cptr<uint64_t> in, cptr<uint64_t> out,
                                                                cptr<uint64_t> copy, const i32x4* __restrict__ bitmat,
-                                                               int k, int m, int bm_ksteps, int groups, int64_t col0,
-                                                               int64_t nchunks, int64_t chunk_slots, int64_t in_stride) {
-  constexpr int kWaves = 4, kThreads = 256, kCW = 32, kRS = 32, kSPS = 4;
-  constexpr int NS = KS * kSPS;  // K-steps per chunk
-  static_assert((2 * KS) % R == 0 && R >= 2, "ring depth must divide a chunk pair");
-  constexpr int kWait = db_wait_count(MG, KS, R, COPY);
-  constexpr int kDummyEpi = db_max_slot_stores(MG, KS);
+                                                               int k, int m, int groups, int64_t col0, int64_t nchunks,
+                                                               int64_t chunk_slots, int64_t in_stride) {
+  constexpr int NTW = kNTW;              // N-tiles (32 columns each) per wave
+  constexpr int kWaves = 4, kThreads = 256;
+  constexpr int kCW = 32 * NTW;          // columns per wave (64)
+  constexpr int kRS = kSlotBytes / kCW;  // input rows per ring slot (16)
+  constexpr int kSPS = kRS / 8;          // K-steps per ring slot (2)
+  constexpr int kLPR = kCW / 16;         // DMA lanes per row (4)
+  constexpr int NS = KS * kSPS;          // K-steps per chunk
+  static_assert(kSPS == 2, "the wait / read pattern below assumes two K-steps per slot");
+  static_assert(KS % R == 0 && NS % MG == 0 && R >= 2, "ring depth must divide the chunk; MG must divide NS");
   extern __shared__ __attribute__((aligned(16))) i32x4 afrag[];
   const int bid = blockIdx.x;
   const int xcd = bid & 7;
@@ -589,18 +573,15 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4db_kernel(cptr<uint64_t> in
   const int64_t slot0 = int64_t(local / groups) * 8 + xcd;
   if (slot0 >= chunk_slots) return;
 
-  // LDS: A [NS][MG][64] x 16 B | row pointers [256] | out pointers [32] | (COPY) copy pointers [256] |
-  // rings [kWaves][R][1 KiB] | one spare slot for the dummy DMAs past the last chunk
+  // LDS: A [NS][MG][64] x 16 B | row pointers [256] | out pointers [32] | (COPY) copy pointers
+  // [256] | rings [kWaves][R][1 KiB] | one spare slot shared by the waves' dummy DMAs
   const size_t a_bytes = size_t(MG) * NS * 1024;
   uint64_t* rowptr = reinterpret_cast<uint64_t*>(reinterpret_cast<uint8_t*>(afrag) + a_bytes);
   uint64_t* outptr = rowptr + 256;
   uint64_t* copyptr = rowptr + 256 + 32;
-  const i32x4* src = bitmat + size_t(g) * MG * bm_ksteps * 64;
-  const uint64_t sink = uint64_t(bitmat + size_t(groups) * MG * bm_ksteps * 64) + 16 * (threadIdx.x & 63);
-  for (int i = threadIdx.x; i < MG * NS * 64; i += kThreads) {
-    const i32x4 zero = {0, 0, 0, 0};
-    afrag[i] = i / (MG * 64) < bm_ksteps ? src[i] : zero;  // K-steps past the bit-matrix: zero A
-  }
+  const i32x4* src = bitmat + size_t(g) * MG * NS * 64;
+  const uint64_t sink = uint64_t(bitmat + size_t(groups) * MG * NS * 64) + 16 * (threadIdx.x & 63);
+  for (int i = threadIdx.x; i < MG * NS * 64; i += kThreads) afrag[i] = src[i];
   if (!UNI)
     for (int i = threadIdx.x; i < k; i += kThreads) rowptr[i] = in[i];
   for (int i = threadIdx.x; i < 4 * MG; i += kThreads) {
@@ -614,119 +595,118 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4db_kernel(cptr<uint64_t> in
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 31, h = lane >> 5;
   const uint32_t lds0 = uint32_t(reinterpret_cast<uintptr_t>((lds_u8*)afrag));
   const uint32_t a_addr = lds0 + 16u * lane;
+  const uint32_t a_addr_hi = a_addr + 65536u;  // (A offsets past 64 KiB: second base, immediates)
   const uint32_t optr_addr = lds0 + uint32_t(a_bytes) + 2048u + 16u * h;  // outptr[4e + 2h + u]: + 32e + 8u
   lds_u8* rings = (lds_u8*)(reinterpret_cast<uint8_t*>(afrag) + a_bytes + 2304 + (COPY ? 2048 : 0));
   lds_u8* ring = rings + size_t(wave) * R * kSlotBytes;
   lds_u8* spare = rings + size_t(kWaves) * R * kSlotBytes;
-  const uint32_t ring_x = uint32_t(reinterpret_cast<uintptr_t>(ring)) + uint32_t(4 * h * kCW + c);
+  const uint32_t ring_x = uint32_t(reinterpret_cast<uintptr_t>(ring)) + uint32_t(4 * h * kCW + NTW * c);
   const uint32_t ring_lane = uint32_t(reinterpret_cast<uintptr_t>(ring)) + 16u * lane;
   const int scale = 0x7F7F7F7F;  // E8M0 1.0 for every block of 32
+  const int bias_scale = bias_scale_of_lane(lane);
+  const i32x8 one_k0 = {h == 0 ? 0x2 : 0, 0, 0, 0, 0, 0, 0, 0};  // 1.0 at K index 0 (A and B)
   const int my_chunks = int((nchunks - slot0 + chunk_slots - 1) / chunk_slots);
   if (my_chunks <= 0) return;
   const uint64_t in0 = UNI ? in[0] : 0;
-  const int drow = lane >> 1;                    // this lane's row within a DMA'd slot
-  const int dcol = wave * kCW + 16 * (lane & 1);  // and its 16 columns within the chunk
-  // per slot-of-chunk p: the source row pointer (scattered inputs) and the copy destination
-  uint64_t rp[KS], cpp[KS];
-#pragma unroll
-  for (int p = 0; p < KS; ++p) {
-    const int r = kRS * p + drow;
-    rp[p] = UNI ? 0 : rowptr[r < k ? r : k - 1];  // rows >= k meet zero bit-matrix columns
-    cpp[p] = COPY && r < k ? copyptr[r] : 0;
-  }
+  const int drow = lane / kLPR;  // this lane's row within a DMA'd slot
+  const int dcol = wave * kCW + 16 * (lane % kLPR);
+  // this lane's DMA row of slot-of-chunk p (rows >= k meet zero bit-matrix columns)
+  auto dma_row = [&](int p) __attribute__((always_inline)) { return kRS * p + drow < k ? kRS * p + drow : k - 1; };
+  const uint32_t rowptr_addr = lds0 + uint32_t(a_bytes);
+  const uint32_t cptr_addr = rowptr_addr + 2304u;
+  // scattered inputs: the row pointer of the next DMA, read from LDS one slot ahead (a register
+  // per slot of the chunk would cost 16 VGPRs)
+  uint64_t pn = UNI ? 0 : rowptr[dma_row((R - 1) % KS)];
 
-  // DMA of absolute slot t (= chunk t / KS, slot t % KS; chunk pairs start at ring slot 0). Past
-  // the last chunk the DMA lands in the spare slot (a valid source address), so the number in
-  // flight, and every counted vmcnt, stays the same.
-  auto dma_issue = [&](int pair_base_chunk, auto t_tag) __attribute__((always_inline)) {
+  // DMA of slot T (chunk-relative, T may reach past the chunk) of chunk ci: past the last chunk
+  // it lands in the spare slot (valid source), so the number in flight stays the same
+  auto dma_issue = [&](int ci, auto t_tag, uint64_t rowp) __attribute__((always_inline)) {
     constexpr int T = decltype(t_tag)::value;
-    const int chunk = pair_base_chunk + T / KS;
-    constexpr int p = T % KS;
-    constexpr int ring_slot = T % R;
+    constexpr int p = T % KS, ring_slot = T % R;
+    const int chunk = ci + T / KS;
     const bool live = chunk < my_chunks;
-    const int64_t col = col0 + (slot0 + int64_t(live ? chunk : 0) * chunk_slots) * kDbCols + dcol;
-    const int row = kRS * p + drow < k ? kRS * p + drow : k - 1;
+    const int64_t col = col0 + (slot0 + int64_t(live ? chunk : 0) * chunk_slots) * kBlockCols + dcol;
     uint64_t sa;
     if constexpr (UNI)
-      sa = in0 + uint64_t(int64_t(row) * in_stride + col);
+      sa = in0 + uint64_t(int64_t(dma_row(p)) * in_stride + col);
     else
-      sa = rp[p] + uint64_t(col);
+      sa = rowp + uint64_t(col);
     __builtin_amdgcn_global_load_lds((gptr<const void>)sa, live ? ring + ring_slot * kSlotBytes : spare, 16, 0, 0);
   };
-  // rows 4h+i of K-step J of ring slot SL, this lane's column c (all offsets immediates: one
-  // address register for the whole ring)
-  auto read_x = [&](uint32_t (&x)[4], auto sl_tag, auto j_tag) __attribute__((always_inline)) {
-    constexpr int off = decltype(sl_tag)::value * kSlotBytes + decltype(j_tag)::value * 8 * kCW;
+  // rows 4h+i of K-step half HS of ring slot SL, this lane's column pair (2c, 2c+1)
+  auto read_x = [&](uint32_t (&x)[4], auto sl_tag, auto hs_tag) __attribute__((always_inline)) {
+    constexpr int off = decltype(sl_tag)::value * kSlotBytes + decltype(hs_tag)::value * 8 * kCW;
     const uint32_t addr = ring_x;
+    uint32_t x0, x1, x2, x3;  // (locals: clang does not capture asm operands in generic lambdas)
     asm volatile(
-        "ds_read_u8 %0, %4 offset:%5\n\t"
-        "ds_read_u8 %1, %4 offset:%6\n\t"
-        "ds_read_u8 %2, %4 offset:%7\n\t"
-        "ds_read_u8 %3, %4 offset:%8"
-        : "=&v"(x[0]), "=&v"(x[1]), "=&v"(x[2]), "=&v"(x[3])
-        : "v"(addr), "n"(off), "n"(off + 32), "n"(off + 64), "n"(off + 96)
+        "ds_read_u16 %0, %4 offset:%5\n\t"
+        "ds_read_u16 %1, %4 offset:%6\n\t"
+        "ds_read_u16 %2, %4 offset:%7\n\t"
+        "ds_read_u16 %3, %4 offset:%8"
+        : "=&v"(x0), "=&v"(x1), "=&v"(x2), "=&v"(x3)
+        : "v"(addr), "n"(off), "n"(off + 64), "n"(off + 128), "n"(off + 192)
         : "memory");
+    x[0] = x0;
+    x[1] = x1;
+    x[2] = x2;
+    x[3] = x3;
   };
-  // A fragments of K-step ST: two base registers (+0, +64 KiB) cover every step with immediates
-  const uint32_t a_addr_hi = a_addr + 65536u;
-  auto read_a = [&](i32x4 (&a)[MG], auto s_tag) __attribute__((always_inline)) {
-    constexpr int off0 = decltype(s_tag)::value * MG * 1024;
-    const uint32_t base = off0 >= 65536 ? a_addr_hi : a_addr;
+  // A fragment of (K-step S, tile MT)
+  auto read_a1 = [&](i32x4& a, auto s_tag, auto mt_tag) __attribute__((always_inline)) {
+    constexpr int off = (decltype(s_tag)::value * MG + decltype(mt_tag)::value) * 1024;
+    const uint32_t base = off >= 65536 ? a_addr_hi : a_addr;
+    i32x4 v;
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=&v"(v) : "v"(base), "n"(off % 65536) : "memory");
+    a = v;
+  };
+  constexpr int kExpandValu = 14;
+  auto expand = [&](i32x4 (&bo)[NTW], const uint32_t (&x)[4]) __attribute__((always_inline)) {
+    const uint32_t p01 = x[0] | (x[1] << 16), p23 = x[2] | (x[3] << 16);
+    const uint32_t w[2] = {__builtin_amdgcn_perm(p23, p01, 0x06040200u), __builtin_amdgcn_perm(p23, p01, 0x07050301u)};
 #pragma unroll
-    for (int mt = 0; mt < MG; ++mt)
-      asm volatile("ds_read_b128 %0, %1 offset:%2" : "=&v"(a[mt]) : "v"(base), "n"(off0 % 65536 + mt * 1024) : "memory");
-  };
-  // B operand of a K-step: W = the 4 rows' bytes of column c (byte i = row 4h+i), then the bit
-  // planes of W masked in place (kAOne) — the K order the bit-matrix is built for (fp4_bitmat_kernel)
-  constexpr int kExpandValu = 8;
-  auto expand = [&](i32x4& bo, const uint32_t (&x)[4]) __attribute__((always_inline)) {
-    const uint32_t w = __builtin_amdgcn_perm(x[1], x[0], 0x0c0c0400u) |
-                       (__builtin_amdgcn_perm(x[3], x[2], 0x0c0c0400u) << 16);
-    bo[0] = int(w & 0x11111111u);
-    bo[1] = int(w & 0x22222222u);
-    bo[2] = int(w & 0x44444444u);
-    bo[3] = int((w >> 1) & 0x44444444u);
+    for (int t = 0; t < NTW; ++t) {
+      bo[t][0] = int(w[t] & 0x11111111u);
+      bo[t][1] = int(w[t] & 0x22222222u);
+      bo[t][2] = int(w[t] & 0x44444444u);
+      bo[t][3] = int((w[t] >> 1) & 0x44444444u);
+    }
   };
 
-  f32x16 acc[2][MG];
-  // parity bias of accumulator register j: 2^(23 - (j & 7)) (see bias_scale_of_lane). Laundered
-  // through an empty asm so the compiler cannot treat a re-biased accumulator as a constant: it
-  // then kept one shared constant AGPR block as every chunk's first MFMA C operand, which left no
-  // room for the second accumulator set and moved the previous chunk's 128 accumulators into VGPRs
-  // in one burst at every chunk start.
-  f32x16 kBias = {8388608.f, 4194304.f, 2097152.f, 1048576.f, 524288.f, 262144.f, 131072.f, 65536.f,
-                  8388608.f, 4194304.f, 2097152.f, 1048576.f, 524288.f, 262144.f, 131072.f, 65536.f};
-  asm volatile("" : "+v"(kBias));
+  f32x16 acc[MG][NTW];
+  auto bias_init = [&](auto mt_tag) __attribute__((always_inline)) {
+    constexpr int MT = decltype(mt_tag)::value;
 #pragma unroll
-  for (int mt = 0; mt < MG; ++mt) {
-    acc[0][mt] = kBias;
-    acc[1][mt] = kBias;
-    asm volatile("" : "+a"(acc[0][mt]));
-    asm volatile("" : "+a"(acc[1][mt]));
-  }
+    for (int t = 0; t < NTW; ++t) {
+      int bs = bias_scale;  // (opaque: keeps these identical MFMAs from being hoisted or merged)
+      asm volatile("" : "+v"(bs));
+      acc[MT][t] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(one_k0, one_k0, (f32x16)(0.0f), 4, 4, 0, bs, 0,
+                                                                    scale);
+    }
+  };
 
-  // prologue: R-1 slots in flight, each followed by the stores a steady-state slot issues after its
-  // DMA (one copy store, the busiest slot's epilogue stores) as dummies to the sink, so the counted
-  // waits below hold from the first slot on
+  // prologue: R-1 slots in flight, each followed by the stores its steady-state slot issues after
+  // its DMA (copy store; epilogue stores of those steps of the previous chunk) as dummies
   static_for<R - 1>([&](auto t) {
-    dma_issue(0, t);
-    const uint64_t sk = sink;  // (a local: clang does not capture operands of asm in generic lambdas)
+    dma_issue(0, t, UNI ? 0 : rowptr[dma_row(decltype(t)::value % KS)]);
+    constexpr int v = KS + decltype(t)::value - (R - 1);  // the virtual slot of chunk -1 issuing it
+    constexpr int n_epi = sk_stores_in(2 * v, 2 * v + 2, MG, NS);
+    const uint64_t sk = sink;
     if constexpr (COPY) {
       const u32x4 zero = {0u, 0u, 0u, 0u};
       asm volatile("global_store_dwordx4 %0, %1, off nt" ::"v"(sk), "v"(zero) : "memory");
     }
 #pragma unroll
-    for (int i = 0; i < kDummyEpi; ++i) asm volatile("global_store_byte %0, %1, off" ::"v"(sk), "v"(0) : "memory");
+    for (int i = 0; i < n_epi; ++i) asm volatile("global_store_short %0, %1, off" ::"v"(sk), "v"(0) : "memory");
   });
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(R - 2) : "memory");
-  uint32_t x0[4], x1[4], x2[4];  // raw bytes: x1 = step s+1 (in registers), x2 = step s+2 (in flight)
-  i32x4 ac[MG], an[MG];
-  i32x4 bc, bn;
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
+  uint32_t x0[4], x1[4], x2[4];  // raw bytes: x1 = step s+1 (in registers), x2 = step s+2 (in flight)
+  i32x4 ac[MG], an[MG];          // A fragments of the current / next step, per tile
+  i32x4 bw[MG][NTW];             // B operands of the last MG K-steps (bw[s % MG])
   read_x(x0, I0{}, I0{});
   read_x(x1, I0{}, I1{});
-  read_a(ac, I0{});
+  static_for<MG>([&](auto mt) { read_a1(ac[decltype(mt)::value], std::integral_constant<int, sk_mod(-decltype(mt)::value, NS)>{}, mt); });
   lgkm_wait();
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -735,82 +715,112 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4db_kernel(cptr<uint64_t> in
   }
 #pragma unroll
   for (int mt = 0; mt < MG; ++mt) tie(ac[mt]);
-  expand(bc, x0);
+#pragma unroll
+  for (int s = 1; s < MG; ++s)
+#pragma unroll
+    for (int t = 0; t < NTW; ++t) bw[s][t] = i32x4{0, 0, 0, 0};  // K-steps of "chunk -1": discarded
+  expand(bw[0], x0);
+  static_for<MG>([&](auto mt) { bias_init(mt); });
 
-  // One chunk on accumulator set CUR (chunk ci of the pair starting at pair_base), with the
-  // epilogue of the previous chunk (set 1-CUR, chunk ci-1) spread over its K-steps.
-  auto chunk_body = [&](int pair_base, auto cur_tag) __attribute__((always_inline)) {
-    constexpr int CUR = decltype(cur_tag)::value, PREV = 1 - CUR;
-    const int ci = pair_base + CUR;
+  // one chunk (ci == my_chunks: the phantom that drains the last real chunk)
+  auto chunk_body = [&](int ci) __attribute__((always_inline)) {
     const bool live = ci < my_chunks;
-    const int64_t cbase = col0 + (slot0 + int64_t(ci) * chunk_slots) * kDbCols;
-    // the previous chunk's output columns of this lane (sink when there is none)
-    const bool plive = ci >= 1 && ci - 1 < my_chunks;
-    const int64_t pcol = cbase - chunk_slots * kDbCols + wave * kCW + c;
+    const int64_t cbase = col0 + (slot0 + int64_t(ci) * chunk_slots) * kBlockCols;
+    const bool plive = ci > 0;  // packs of "chunk -1" (steps < MG of chunk 0) go to the sink
+    const int64_t pcolw = cbase - chunk_slots * kBlockCols + wave * kCW + NTW * c;
     static_for<KS>([&](auto sp_tag) {
       constexpr int SP = decltype(sp_tag)::value;
-      constexpr int P = CUR * KS + SP;  // slot within the pair
-      constexpr int RS = P % R, RS1 = (P + 1) % R;
-      dma_issue(pair_base, std::integral_constant<int, P + R - 1>{});
-      [[maybe_unused]] u32x4 cdat;
-      if constexpr (COPY) {  // this lane's 16 B of the current slot
-        const uint32_t addr = ring_lane + uint32_t(RS * kSlotBytes);
-        asm volatile("ds_read_b128 %0, %1" : "=&v"(cdat) : "v"(addr) : "memory");
+      constexpr int RS = SP % R, RS1 = (SP + 1) % R;
+      dma_issue(ci, std::integral_constant<int, SP + R - 1>{}, pn);
+      if constexpr (!UNI) {  // the next slot's DMA row pointer (retired by this slot's first step)
+        const uint32_t addr = rowptr_addr + 8u * uint32_t(dma_row((SP + R) % KS));
+        uint64_t v;
+        asm volatile("ds_read_b64 %0, %1" : "=&v"(v) : "v"(addr) : "memory");
+        pn = v;
       }
-      static_for<kSPS>([&](auto j_tag) {
-        constexpr int J = decltype(j_tag)::value;
-        constexpr int S = SP * kSPS + J;
-        constexpr int E0 = db_first_tile(S, MG, NS), NT = db_tiles_at(S, MG, NS);
-        if constexpr (J == kSPS - 2)  // the next slot has landed: count the younger ops (header)
-          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kWait) : "memory");
-        if constexpr (J + 2 < kSPS)
-          read_x(x2, std::integral_constant<int, RS>{}, std::integral_constant<int, J + 2>{});
-        else
-          read_x(x2, std::integral_constant<int, RS1>{}, std::integral_constant<int, J + 2 - kSPS>{});
-        read_a(an, std::integral_constant<int, (S + 1) % NS>{});
-        [[maybe_unused]] uint64_t op[NT > 0 ? NT : 1][2];
-        static_for<NT>([&](auto t_tag) {
-          constexpr int E = E0 + decltype(t_tag)::value;
+      [[maybe_unused]] u32x4 cdat;
+      [[maybe_unused]] uint64_t cp = 0;
+      [[maybe_unused]] const int crow = kRS * SP + drow;
+      if constexpr (COPY) {  // this lane's 16 B of the current slot and its row's copy pointer
+        const uint32_t addr = ring_lane + uint32_t(RS * kSlotBytes);
+        const uint32_t caddr = cptr_addr + 8u * uint32_t(crow < k ? crow : k - 1);
+        u32x4 v;
+        uint64_t cv;
+        asm volatile("ds_read_b128 %0, %1" : "=&v"(v) : "v"(addr) : "memory");
+        asm volatile("ds_read_b64 %0, %1" : "=&v"(cv) : "v"(caddr) : "memory");
+        cdat = v;
+        cp = cv;
+      }
+      static_for<kSPS>([&](auto jj_tag) {
+        constexpr int JJ = decltype(jj_tag)::value;
+        constexpr int J = SP * kSPS + JJ;                          // K-step of the chunk
+        constexpr int EP = J < MG ? J : -1;                        // tile packed and restarted
+        constexpr int EE = (J + 1) % NS < MG ? (J + 1) % NS : -1;  // tile finishing its chunk
+        if constexpr (JJ == 0)  // the next slot has landed: count the younger ops exactly
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(sk_wait_count(SP, MG, KS, R, COPY)) : "memory");
+        read_x(x2, std::integral_constant<int, RS1>{}, jj_tag);
+        static_for<MG>([&](auto mt) {
+          constexpr int MT = decltype(mt)::value;
+          read_a1(an[MT], std::integral_constant<int, sk_mod(J + 1 - MT, NS)>{}, mt);
+        });
+        [[maybe_unused]] uint64_t op[2];
+        if constexpr (EP >= 0) {
           const uint32_t addr = optr_addr;
-          uint64_t o0, o1;  // (locals: clang does not capture asm operands in generic lambdas)
+          uint64_t o0, o1;
           asm volatile("ds_read_b64 %0, %2 offset:%3\n\tds_read_b64 %1, %2 offset:%4"
                        : "=&v"(o0), "=&v"(o1)
-                       : "v"(addr), "n"(32 * E), "n"(32 * E + 8)
+                       : "v"(addr), "n"(32 * (EP >= 0 ? EP : 0)), "n"(32 * (EP >= 0 ? EP : 0) + 8)
                        : "memory");
-          op[decltype(t_tag)::value][0] = o0;
-          op[decltype(t_tag)::value][1] = o1;
-        });
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int mt = 0; mt < MG; ++mt) {
-          const i32x8 a = {ac[mt][0], ac[mt][1], ac[mt][2], ac[mt][3], 0, 0, 0, 0};
-          const i32x8 bb = {bc[0], bc[1], bc[2], bc[3], 0, 0, 0, 0};
-          acc[CUR][mt] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, bb, acc[CUR][mt], 4, 4, 0, scale, 0, scale);
+          op[0] = o0;
+          op[1] = o1;
         }
-        expand(bn, x1);
-        [[maybe_unused]] uint32_t y[NT > 0 ? NT : 1][2];
-        // output bytes of rows 2h, 2h+1 of M-tiles E0.. of the previous chunk: 7 v_bfi per byte over
-        // the biased accumulators (the parity of bit b's count sits at bit b), then re-bias
-        static_for<NT>([&](auto t_tag) {
-          constexpr int T = decltype(t_tag)::value, E = E0 + T;
-          // (a new opaque value here: the accumulator reads below cannot be hoisted to the chunk
-          // start, where all 128 of them would burst out of the AGPRs at once)
-          asm volatile("" : "+a"(acc[PREV][E]));
+        __builtin_amdgcn_sched_barrier(0);
+        auto mfma_tile = [&](auto mt) __attribute__((always_inline)) {
+          constexpr int MT = decltype(mt)::value;
+          constexpr int B = sk_mod(J - MT, MG);
+          const i32x8 a = {ac[MT][0], ac[MT][1], ac[MT][2], ac[MT][3], 0, 0, 0, 0};
+#pragma unroll
+          for (int t = 0; t < NTW; ++t) {
+            const i32x8 bb = {bw[B][t][0], bw[B][t][1], bw[B][t][2], bw[B][t][3], 0, 0, 0, 0};
+            acc[MT][t] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, bb, acc[MT][t], 4, 4, 0, scale, 0, scale);
+          }
+        };
+        // the finishing tile first (so it is complete when packed next step), the others, then the
+        // packed tile's bias and its first K-step of the new chunk
+        if constexpr (EE >= 0 && EE != EP) mfma_tile(std::integral_constant<int, (EE >= 0 ? EE : 0)>{});
+        static_for<MG>([&](auto mt) {
+          constexpr int MT = decltype(mt)::value;
+          if constexpr (MT != EE && MT != EP) mfma_tile(mt);
+        });
+        [[maybe_unused]] uint32_t w[2];
+        if constexpr (EP >= 0) {
+          constexpr int E = EP >= 0 ? EP : 0;
+          // output bytes of tile E (rows 2h, 2h+1; columns 2c, 2c+1): 7 v_bfi per byte over the
+          // biased accumulators (the parity of bit b's count sits at bit b)
+          uint32_t y[NTW][2];
 #pragma unroll
           for (int b = 0; b < 8; ++b)
 #pragma unroll
-            for (int u = 0; u < 2; ++u) {
-              const uint32_t v = __float_as_uint(acc[PREV][E][8 * u + b]);
-              y[T][u] = b == 0 ? v : bfi(1u << b, v, y[T][u]);
-            }
-          acc[PREV][E] = kBias;
-          asm volatile("" : "+a"(acc[PREV][E]));  // (an opaque accumulator from here on, see kBias)
-        });
-        constexpr int kValu = kExpandValu + NT * (16 + 14 + 16);
+            for (int t = 0; t < NTW; ++t)
 #pragma unroll
-        for (int i = 0; i < MG; ++i) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                      // MFMA
-          __builtin_amdgcn_sched_group_barrier(0x002, (kValu + MG - 1) / MG, 0);  // VALU
+              for (int u = 0; u < 2; ++u) {
+                const uint32_t v = __float_as_uint(acc[E][t][8 * u + b]);
+                y[t][u] = b == 0 ? v : bfi(1u << b, v, y[t][u]);
+              }
+#pragma unroll
+          for (int u = 0; u < 2; ++u) w[u] = __builtin_amdgcn_perm(y[1][u], y[0][u], 0x0c0c0400u);
+          bias_init(std::integral_constant<int, E>{});
+          mfma_tile(std::integral_constant<int, E>{});
+        }
+        if constexpr (EE >= 0 && EE == EP) mfma_tile(std::integral_constant<int, (EE >= 0 ? EE : 0)>{});
+        // B of the next K-step (into the window slot the last reader just used)
+        expand(bw[(J + 1) % MG], x1);
+        constexpr int kMfma = MG * NTW + (EP >= 0 ? NTW : 0);
+        constexpr int kValu = kExpandValu + (EP >= 0 ? 2 * NTW * 16 + NTW * 2 * 7 + 2 : 0);
+#pragma unroll
+        for (int i = 0; i < kMfma; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                          // MFMA
+          __builtin_amdgcn_sched_group_barrier(0x002, (kValu + kMfma - 1) / kMfma, 0);  // VALU
         }
         __builtin_amdgcn_sched_barrier(0);
         lgkm_wait();
@@ -824,57 +834,31 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4db_kernel(cptr<uint64_t> in
           tie(an[mt]);
           ac[mt] = an[mt];
         }
-        bc = bn;
-        static_for<NT>([&](auto t_tag) {
-          constexpr int T = decltype(t_tag)::value;
-          uint64_t o0 = op[T][0], o1 = op[T][1];
-          tie(o0);
-          tie(o1);
-          op[T][0] = o0;
-          op[T][1] = o1;
+        if constexpr (EP >= 0) {
 #pragma unroll
           for (int u = 0; u < 2; ++u) {
-            const uint64_t o = op[T][u];
-            *(gptr<uint8_t>)(plive && o ? o + uint64_t(pcol) : sink) = uint8_t(y[T][u]);
+            uint64_t o = op[u];
+            tie(o);
+            *(gptr<uint16_t>)(plive && o ? o + uint64_t(pcolw) : sink) = uint16_t(w[u]);
           }
-        });
-        if constexpr (COPY && J == 0) {
-          tie(cdat);
-          const int crow = kRS * SP + drow;
-          const uint64_t cp = cpp[SP];
-          __builtin_nontemporal_store(cdat, (gptr<u32x4>)(live && crow < k && cp ? cp + uint64_t(cbase + dcol) : sink));
+        }
+        if constexpr (JJ == 0 && !UNI) {
+          uint64_t v = pn;
+          tie(v);
+          pn = v;
+        }
+        if constexpr (COPY && JJ == 0) {
+          u32x4 d = cdat;
+          uint64_t cv = cp;
+          tie(d);
+          tie(cv);
+          __builtin_nontemporal_store(d, (gptr<u32x4>)(live && crow < k && cv ? cv + uint64_t(cbase + dcol) : sink));
         }
       });
     });
   };
 
-  for (int pair = 0; pair < my_chunks; pair += 2) {
-    chunk_body(pair, std::integral_constant<int, 0>{});
-    chunk_body(pair, std::integral_constant<int, 1>{});
-  }
-  // tail: the epilogue of the last chunk of the last pair (set 1; a phantom chunk past my_chunks
-  // when their number is odd — then everything goes to the sink)
-  {
-    const int ci = (my_chunks + 1) / 2 * 2 - 1;
-    const bool tlive = ci < my_chunks;
-    const int64_t tcol = col0 + (slot0 + int64_t(ci) * chunk_slots) * kDbCols + wave * kCW + c;
-#pragma unroll
-    for (int e = 0; e < MG; ++e) {
-      uint32_t y[2];
-#pragma unroll
-      for (int b = 0; b < 8; ++b)
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          const uint32_t v = __float_as_uint(acc[1][e][8 * u + b]);
-          y[u] = b == 0 ? v : bfi(1u << b, v, y[u]);
-        }
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const uint64_t o = outptr[4 * e + 2 * h + u];
-        *(gptr<uint8_t>)(tlive && o ? o + uint64_t(tcol) : sink) = uint8_t(y[u]);
-      }
-    }
-  }
+  for (int ci = 0; ci <= my_chunks; ++ci) chunk_body(ci);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA (dummy or not) outlives the wave
 }
 
@@ -991,11 +975,13 @@ hipError_t launch_fp4_any(const Fp4Geometry& geo, const Fp4Args& a, hipStream_t 
                      : launch_fp4_var<MG, false, false>(geo, a, stream);
 }
 
-// db kernel: ring depth per K-slot count (2 KS must be a multiple of R; deepest that fits)
-template <int MG, bool UNI, bool COPY, int R, int KS>
-hipError_t launch_fp4db(const Fp4Geometry& geo, const Fp4Args& a, hipStream_t stream) {
-  const void* f = reinterpret_cast<const void*>(&gf_gemm_fp4db_kernel<MG, UNI, COPY, R, KS>);
-  const size_t lds = size_t(MG) * KS * 4 * 1024 + 2304 + (COPY ? 2048 : 0) + ring_lds(R);
+// sk kernel (k in (112, 128]: 8 ring slots per chunk): ring depth 8 or 4, deepest that fits the LDS
+// with the side reserve, else without it
+template <int MG, bool UNI, bool COPY, int R>
+hipError_t launch_fp4sk(const Fp4Geometry& geo, const Fp4Args& a, hipStream_t stream) {
+  constexpr int KS = 8;
+  const void* f = reinterpret_cast<const void*>(&gf_gemm_fp4sk_kernel<MG, UNI, COPY, R, KS>);
+  const size_t lds = size_t(MG) * KS * 2 * 1024 + 2304 + (COPY ? 2048 : 0) + ring_lds(R);
   if (lds > 160 * 1024) return hipErrorInvalidConfiguration;
   hipError_t e = ensure_lds_optin(f);
   if (e != hipSuccess) return e;
@@ -1006,46 +992,35 @@ hipError_t launch_fp4db(const Fp4Geometry& geo, const Fp4Args& a, hipStream_t st
     return o;
   });
   if (occ <= 0) return hipErrorInvalidConfiguration;
-  const int64_t nchunks = a.nchunks;
   int64_t slots = std::max<int64_t>(8, (int64_t(device_cu_count()) * occ / geo.groups) / 8 * 8);
-  slots = std::min<int64_t>(slots, (nchunks + 7) / 8 * 8);
+  slots = std::min<int64_t>(slots, (a.nchunks + 7) / 8 * 8);
   const unsigned blocks = unsigned(slots * geo.groups);
-  gf_gemm_fp4db_kernel<MG, UNI, COPY, R, KS><<<blocks, 256, lds, stream>>>(
-      a.in, a.out, a.copy, static_cast<const i32x4*>(a.bitmat), a.k, a.m, geo.ksteps, geo.groups, a.col0, nchunks,
-      slots, a.in_stride);
+  gf_gemm_fp4sk_kernel<MG, UNI, COPY, R, KS><<<blocks, 256, lds, stream>>>(
+      a.in, a.out, a.copy, static_cast<const i32x4*>(a.bitmat), a.k, a.m, geo.groups, a.col0, a.nchunks, slots,
+      a.in_stride);
   return hipGetLastError();
 }
 
 template <int MG, bool UNI, bool COPY>
-hipError_t launch_fp4db_ks(int ks, const Fp4Geometry& geo, const Fp4Args& a, hipStream_t stream) {
-  switch (ks) {
-    case 1: return launch_fp4db<MG, UNI, COPY, 2, 1>(geo, a, stream);
-    case 4: return launch_fp4db<MG, UNI, COPY, 4, 4>(geo, a, stream);
-    default:
-      if constexpr (MG == 4) {  // (see db_slots)
-        if (ks == 2) return launch_fp4db<MG, UNI, COPY, 4, 2>(geo, a, stream);
-        if (ks == 3) return launch_fp4db<MG, UNI, COPY, 6, 3>(geo, a, stream);
-      }
-      return hipErrorInvalidConfiguration;
-  }
+hipError_t launch_fp4sk_ring(const Fp4Geometry& geo, const Fp4Args& a, hipStream_t stream) {
+  const size_t base = size_t(MG) * 16 * 1024 + 2304 + (COPY ? 2048 : 0);
+  if (base + ring_lds(8) + kSideReserve <= 160 * 1024) return launch_fp4sk<MG, UNI, COPY, 8>(geo, a, stream);
+  return launch_fp4sk<MG, UNI, COPY, 4>(geo, a, stream);
 }
 
 template <int MG>
-hipError_t launch_fp4db_any(int ks, const Fp4Geometry& geo, const Fp4Args& a, hipStream_t stream) {
-  if (a.copy) return launch_fp4db_ks<MG, false, true>(ks, geo, a, stream);
-  return a.in_stride ? launch_fp4db_ks<MG, true, false>(ks, geo, a, stream)
-                     : launch_fp4db_ks<MG, false, false>(ks, geo, a, stream);
+hipError_t launch_fp4sk_any(const Fp4Geometry& geo, const Fp4Args& a, hipStream_t stream) {
+  if (a.copy) return launch_fp4sk_ring<MG, false, true>(geo, a, stream);
+  return a.in_stride ? launch_fp4sk_ring<MG, true, false>(geo, a, stream)
+                     : launch_fp4sk_ring<MG, false, false>(geo, a, stream);
 }
 
-// The db kernel covers M-groups of 4 or 8 tiles and k <= 128 (4 ring slots of 32 rows per chunk);
-// GFRS_FP4_KERNEL=v1 selects the single-buffered kernel everywhere (A/B measurements).
-int db_slots(const Fp4Geometry& geo) {
+// the staggered kernel covers the static 8-slot chunk (k in (112, 128]) with 4 or 8 M-tiles per
+// group; GFRS_FP4_KERNEL=v1 selects the single-schedule kernel (A/B measurements)
+bool use_sk(const Fp4Geometry& geo) {
   const char* env = std::getenv("GFRS_FP4_KERNEL");
-  if (env && std::strcmp(env, "v1") == 0) return 0;
-  const int ks = (geo.ksteps + 3) / 4;
-  // (MG = 8 with 2 or 3 slots per chunk spills VGPRs in the db form: those stay on v1)
-  if (geo.mg == 8 && (ks == 2 || ks == 3)) return 0;
-  return (geo.mg == 4 || geo.mg == 8) && ks >= 1 && ks <= 4 ? ks : 0;
+  if (env && std::strcmp(env, "v1") == 0) return false;
+  return geo.ksteps == 16 && (geo.mg == 4 || geo.mg == 8);
 }
 
 }  // namespace
@@ -1077,8 +1052,8 @@ hipError_t launch_gf_gemm_fp4(const void* bitmat, const void* desc, int k, int m
   const DescLayout l = desc_layout(k, m_pad);
   const char* b = static_cast<const char*>(desc);
   const Fp4Geometry geo = geometry(k, m, mg_cap, copies);
-  const int db_ks = db_slots(geo);
-  const int64_t chunk_cols = db_ks ? kDbCols : kBlockCols;
+  const bool sk = use_sk(geo);
+  const int64_t chunk_cols = kBlockCols;
   const int64_t nchunks = ncols / chunk_cols;
   if (nchunks > 0) {
     Fp4Args a{};
@@ -1092,8 +1067,8 @@ hipError_t launch_gf_gemm_fp4(const void* bitmat, const void* desc, int k, int m
     a.nchunks = nchunks;
     a.in_stride = copies ? 0 : in_stride;  // the copy variant reads row pointers from the table
     hipError_t e;
-    if (db_ks) {
-      e = geo.mg == 8 ? launch_fp4db_any<8>(db_ks, geo, a, stream) : launch_fp4db_any<4>(db_ks, geo, a, stream);
+    if (sk) {
+      e = geo.mg == 8 ? launch_fp4sk_any<8>(geo, a, stream) : launch_fp4sk_any<4>(geo, a, stream);
     } else {
       switch (geo.mg) {
         case 8: e = launch_fp4_any<8>(geo, a, stream); break;

@@ -333,16 +333,17 @@ def test_decode_system_matches_host_decode_matrix(k, n, matrix):
     assert checked > 0
 
 
-@pytest.mark.parametrize("k,m", [(20, 16), (40, 32), (72, 24), (100, 17), (128, 32), (128, 16)])
+@pytest.mark.parametrize("k,m", [(128, 32), (128, 16), (120, 24), (113, 17), (100, 17), (40, 32)])
 @pytest.mark.parametrize("variant", ["uniform", "scattered", "copy"])
-def test_fp4_double_buffered_kernel_chunk_counts(k, m, variant, monkeypatch):
-    """The double-buffered FP4 kernel (gf_gemm_fp4db_kernel: 128-column chunks processed in pairs,
-    the epilogue of chunk i under the MFMAs of chunk i+1) for every K-slot count (KS = 1..4), both
-    M-group sizes, uniform / scattered / fused-copy inputs, and a column count that gives the
-    persistent blocks both even and odd chunk counts plus a v_perm remainder — bit-exact against the
-    oracle and against the single-buffered kernel (GFRS_FP4_KERNEL=v1)."""
+def test_fp4_staggered_kernel_matches_v1_and_oracle(k, m, variant, monkeypatch):
+    """The tile-staggered FP4 kernel (gf_gemm_fp4sk_kernel, k in (112, 128]: M-tile mt runs K-step
+    (j - mt) of its chunk, one tile's epilogue per step, a phantom chunk draining the last one)
+    with 4 or 8 M-tiles, padding output rows, uniform / scattered / fused-copy inputs and a column
+    count giving the persistent blocks several chunks plus a v_perm remainder — bit-exact against
+    the oracle and against the single-schedule kernel (GFRS_FP4_KERNEL=v1). Other k run v1 both
+    times (a control)."""
     _native_loaded()
-    ncols = 128 * (256 * 3 + 5) + 77
+    ncols = 256 * (256 * 3 + 5) + 77
     rng = np.random.default_rng(k * 31 + m)
     coeff = rng.integers(0, 256, size=(m, k), dtype=np.uint8)
     host, dev = _rand_rows(k, ncols, k + m)
@@ -356,7 +357,7 @@ def test_fp4_double_buffered_kernel_chunk_counts(k, m, variant, monkeypatch):
         cdst = alloc_rows(k, ncols, "cuda", fill=0x44)
         copies = [cdst[j] if j % 4 else None for j in range(k)]
     results = []
-    for kernel in ("db", "v1"):
+    for kernel in ("sk", "v1"):
         if kernel == "v1":
             monkeypatch.setenv("GFRS_FP4_KERNEL", "v1")
         else:
