@@ -534,11 +534,12 @@ __host__ __device__ constexpr int sk_stores_in(int s0, int s1, int mg, int ns) {
   for (int s = s0; s < s1; ++s) n += sk_mod(s, ns) < mg ? 2 : 0;
   return n;
 }
-// vm ops issued after the DMA of slot sp+1 when its data is awaited (start of slot sp): R-2 DMAs,
-// the copy stores of slots sp+2-R .. sp-1 and the epilogue stores of their steps (exact: the
-// prologue issues the stores of the virtual slots before chunk 0 as dummies)
+// vm ops issued after the DMA of slot sp+1 when its data is awaited (first step of slot sp, before
+// that slot's own DMA): R-3 DMAs, the copy stores of slots sp+2-R .. sp-1 and the epilogue stores
+// of their steps (exact: the prologue issues the stores of the virtual slots before chunk 0 as
+// dummies)
 __host__ __device__ constexpr int sk_wait_count(int sp, int mg, int ks, int r, bool copy) {
-  const int n = (r - 2) + (copy ? r - 2 : 0) + sk_stores_in(2 * (sp + 2 - r), 2 * sp, mg, 2 * ks);
+  const int n = (r - 3) + (copy ? r - 2 : 0) + sk_stores_in(2 * (sp + 2 - r), 2 * sp, mg, 2 * ks);
   return n < 63 ? n : 63;
 }
 
@@ -564,7 +565,7 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4sk_kernel(cptr<uint64_t> in
   constexpr int kLPR = kCW / 16;         // DMA lanes per row (4)
   constexpr int NS = KS * kSPS;          // K-steps per chunk
   static_assert(kSPS == 2, "the wait / read pattern below assumes two K-steps per slot");
-  static_assert(KS % R == 0 && NS % MG == 0 && R >= 2, "ring depth must divide the chunk; MG must divide NS");
+  static_assert(KS % R == 0 && NS % MG == 0 && R >= 3, "ring depth must divide the chunk; MG must divide NS");
   extern __shared__ __attribute__((aligned(16))) i32x4 afrag[];
   const int bid = blockIdx.x;
   const int xcd = bid & 7;
@@ -722,59 +723,40 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4sk_kernel(cptr<uint64_t> in
   expand(bw[0], x0);
   static_for<MG>([&](auto mt) { bias_init(mt); });
 
-  // one chunk (ci == my_chunks: the phantom that drains the last real chunk)
+  // output row pointers of the tile packed at the next step, read one step ahead
+  uint64_t opc[2] = {0, 0};
+  {
+    const uint32_t addr = optr_addr;
+    uint64_t o0, o1;
+    asm volatile("ds_read_b64 %0, %2\n\tds_read_b64 %1, %2 offset:8" : "=&v"(o0), "=&v"(o1) : "v"(addr) : "memory");
+    lgkm_wait();
+    tie(o0);
+    tie(o1);
+    opc[0] = o0;
+    opc[1] = o1;
+  }
+
+  // One chunk (ci == my_chunks: the phantom that drains the last real chunk). Step layout, so the
+  // matrix pipe never waits on a step boundary: [2 MFMAs] [this slot's counted wait, the LDS reads
+  // of the next step, the DMA of the slot R-1 ahead] [the remaining MFMAs, with the B expansion
+  // and the packed tile's epilogue as VALU between them] [its two stores] [lgkmcnt(0)].
   auto chunk_body = [&](int ci) __attribute__((always_inline)) {
     const bool live = ci < my_chunks;
     const int64_t cbase = col0 + (slot0 + int64_t(ci) * chunk_slots) * kBlockCols;
     const bool plive = ci > 0;  // packs of "chunk -1" (steps < MG of chunk 0) go to the sink
     const int64_t pcolw = cbase - chunk_slots * kBlockCols + wave * kCW + NTW * c;
+    [[maybe_unused]] u32x4 cdat;
+    [[maybe_unused]] uint64_t cp = 0;
     static_for<KS>([&](auto sp_tag) {
       constexpr int SP = decltype(sp_tag)::value;
       constexpr int RS = SP % R, RS1 = (SP + 1) % R;
-      dma_issue(ci, std::integral_constant<int, SP + R - 1>{}, pn);
-      if constexpr (!UNI) {  // the next slot's DMA row pointer (retired by this slot's first step)
-        const uint32_t addr = rowptr_addr + 8u * uint32_t(dma_row((SP + R) % KS));
-        uint64_t v;
-        asm volatile("ds_read_b64 %0, %1" : "=&v"(v) : "v"(addr) : "memory");
-        pn = v;
-      }
-      [[maybe_unused]] u32x4 cdat;
-      [[maybe_unused]] uint64_t cp = 0;
       [[maybe_unused]] const int crow = kRS * SP + drow;
-      if constexpr (COPY) {  // this lane's 16 B of the current slot and its row's copy pointer
-        const uint32_t addr = ring_lane + uint32_t(RS * kSlotBytes);
-        const uint32_t caddr = cptr_addr + 8u * uint32_t(crow < k ? crow : k - 1);
-        u32x4 v;
-        uint64_t cv;
-        asm volatile("ds_read_b128 %0, %1" : "=&v"(v) : "v"(addr) : "memory");
-        asm volatile("ds_read_b64 %0, %1" : "=&v"(cv) : "v"(caddr) : "memory");
-        cdat = v;
-        cp = cv;
-      }
       static_for<kSPS>([&](auto jj_tag) {
         constexpr int JJ = decltype(jj_tag)::value;
         constexpr int J = SP * kSPS + JJ;                          // K-step of the chunk
         constexpr int EP = J < MG ? J : -1;                        // tile packed and restarted
-        constexpr int EE = (J + 1) % NS < MG ? (J + 1) % NS : -1;  // tile finishing its chunk
-        if constexpr (JJ == 0)  // the next slot has landed: count the younger ops exactly
-          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(sk_wait_count(SP, MG, KS, R, COPY)) : "memory");
-        read_x(x2, std::integral_constant<int, RS1>{}, jj_tag);
-        static_for<MG>([&](auto mt) {
-          constexpr int MT = decltype(mt)::value;
-          read_a1(an[MT], std::integral_constant<int, sk_mod(J + 1 - MT, NS)>{}, mt);
-        });
-        [[maybe_unused]] uint64_t op[2];
-        if constexpr (EP >= 0) {
-          const uint32_t addr = optr_addr;
-          uint64_t o0, o1;
-          asm volatile("ds_read_b64 %0, %2 offset:%3\n\tds_read_b64 %1, %2 offset:%4"
-                       : "=&v"(o0), "=&v"(o1)
-                       : "v"(addr), "n"(32 * (EP >= 0 ? EP : 0)), "n"(32 * (EP >= 0 ? EP : 0) + 8)
-                       : "memory");
-          op[0] = o0;
-          op[1] = o1;
-        }
-        __builtin_amdgcn_sched_barrier(0);
+        constexpr int EN = (J + 1) % NS < MG ? (J + 1) % NS : -1;  // tile packed at the next step
+        constexpr int EE = (J + 1) % NS < MG ? (J + 1) % NS : -1;  // tile finishing its chunk now
         auto mfma_tile = [&](auto mt) __attribute__((always_inline)) {
           constexpr int MT = decltype(mt)::value;
           constexpr int B = sk_mod(J - MT, MG);
@@ -785,12 +767,53 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4sk_kernel(cptr<uint64_t> in
             acc[MT][t] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, bb, acc[MT][t], 4, 4, 0, scale, 0, scale);
           }
         };
-        // the finishing tile first (so it is complete when packed next step), the others, then the
-        // packed tile's bias and its first K-step of the new chunk
-        if constexpr (EE >= 0 && EE != EP) mfma_tile(std::integral_constant<int, (EE >= 0 ? EE : 0)>{});
+        // MFMA order: the finishing tile first (complete when packed next step), then the others,
+        // then the packed tile's bias and its first K-step of the new chunk
+        constexpr int kFirst = EE >= 0 && EE != EP ? EE : (EP == 0 ? 1 : 0);
+        __builtin_amdgcn_sched_barrier(0);
+        mfma_tile(std::integral_constant<int, kFirst>{});
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (JJ == 0)  // slot SP+1 has landed: exact count of the younger ops
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(sk_wait_count(SP, MG, KS, R, COPY)) : "memory");
+        read_x(x2, std::integral_constant<int, RS1>{}, jj_tag);
         static_for<MG>([&](auto mt) {
           constexpr int MT = decltype(mt)::value;
-          if constexpr (MT != EE && MT != EP) mfma_tile(mt);
+          read_a1(an[MT], std::integral_constant<int, sk_mod(J + 1 - MT, NS)>{}, mt);
+        });
+        [[maybe_unused]] uint64_t opn[2];
+        if constexpr (EN >= 0) {
+          const uint32_t addr = optr_addr;
+          uint64_t o0, o1;
+          asm volatile("ds_read_b64 %0, %2 offset:%3\n\tds_read_b64 %1, %2 offset:%4"
+                       : "=&v"(o0), "=&v"(o1)
+                       : "v"(addr), "n"(32 * (EN >= 0 ? EN : 0)), "n"(32 * (EN >= 0 ? EN : 0) + 8)
+                       : "memory");
+          opn[0] = o0;
+          opn[1] = o1;
+        }
+        if constexpr (JJ == 0) {
+          dma_issue(ci, std::integral_constant<int, SP + R - 1>{}, pn);
+          if constexpr (!UNI) {  // the next slot's DMA row pointer
+            const uint32_t addr = rowptr_addr + 8u * uint32_t(dma_row((SP + R) % KS));
+            uint64_t v;
+            asm volatile("ds_read_b64 %0, %1" : "=&v"(v) : "v"(addr) : "memory");
+            pn = v;
+          }
+          if constexpr (COPY) {  // this lane's 16 B of the current slot and its row's copy pointer
+            const uint32_t addr = ring_lane + uint32_t(RS * kSlotBytes);
+            const uint32_t caddr = cptr_addr + 8u * uint32_t(crow < k ? crow : k - 1);
+            u32x4 v;
+            uint64_t cv;
+            asm volatile("ds_read_b128 %0, %1" : "=&v"(v) : "v"(addr) : "memory");
+            asm volatile("ds_read_b64 %0, %1" : "=&v"(cv) : "v"(caddr) : "memory");
+            cdat = v;
+            cp = cv;
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        static_for<MG>([&](auto mt) {
+          constexpr int MT = decltype(mt)::value;
+          if constexpr (MT != kFirst && MT != EP) mfma_tile(mt);
         });
         [[maybe_unused]] uint32_t w[2];
         if constexpr (EP >= 0) {
@@ -810,17 +833,27 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4sk_kernel(cptr<uint64_t> in
 #pragma unroll
           for (int u = 0; u < 2; ++u) w[u] = __builtin_amdgcn_perm(y[1][u], y[0][u], 0x0c0c0400u);
           bias_init(std::integral_constant<int, E>{});
-          mfma_tile(std::integral_constant<int, E>{});
+          if constexpr (E != kFirst) mfma_tile(std::integral_constant<int, E>{});
         }
-        if constexpr (EE >= 0 && EE == EP) mfma_tile(std::integral_constant<int, (EE >= 0 ? EE : 0)>{});
-        // B of the next K-step (into the window slot the last reader just used)
+        // B of the next K-step (into the window slot whose last reader is this step's tile MG-1)
         expand(bw[(J + 1) % MG], x1);
-        constexpr int kMfma = MG * NTW + (EP >= 0 ? NTW : 0);
+        constexpr int kMfma = MG * NTW + (EP >= 0 ? NTW : 0) - NTW;
         constexpr int kValu = kExpandValu + (EP >= 0 ? 2 * NTW * 16 + NTW * 2 * 7 + 2 : 0);
 #pragma unroll
         for (int i = 0; i < kMfma; ++i) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                          // MFMA
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                            // MFMA
           __builtin_amdgcn_sched_group_barrier(0x002, (kValu + kMfma - 1) / kMfma, 0);  // VALU
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (EP >= 0) {
+#pragma unroll
+          for (int u = 0; u < 2; ++u) {
+            const uint64_t o = opc[u];
+            *(gptr<uint16_t>)(plive && o ? o + uint64_t(pcolw) : sink) = uint16_t(w[u]);
+          }
+        }
+        if constexpr (COPY && JJ == 1) {  // (cdat / cp retired by step 0's lgkmcnt(0))
+          __builtin_nontemporal_store(cdat, (gptr<u32x4>)(live && crow < k && cp ? cp + uint64_t(cbase + dcol) : sink));
         }
         __builtin_amdgcn_sched_barrier(0);
         lgkm_wait();
@@ -834,25 +867,27 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4sk_kernel(cptr<uint64_t> in
           tie(an[mt]);
           ac[mt] = an[mt];
         }
-        if constexpr (EP >= 0) {
-#pragma unroll
-          for (int u = 0; u < 2; ++u) {
-            uint64_t o = op[u];
-            tie(o);
-            *(gptr<uint16_t>)(plive && o ? o + uint64_t(pcolw) : sink) = uint16_t(w[u]);
+        if constexpr (EN >= 0) {
+          uint64_t o0 = opn[0], o1 = opn[1];
+          tie(o0);
+          tie(o1);
+          opc[0] = o0;
+          opc[1] = o1;
+        }
+        if constexpr (JJ == 0) {
+          if constexpr (!UNI) {
+            uint64_t v = pn;
+            tie(v);
+            pn = v;
           }
-        }
-        if constexpr (JJ == 0 && !UNI) {
-          uint64_t v = pn;
-          tie(v);
-          pn = v;
-        }
-        if constexpr (COPY && JJ == 0) {
-          u32x4 d = cdat;
-          uint64_t cv = cp;
-          tie(d);
-          tie(cv);
-          __builtin_nontemporal_store(d, (gptr<u32x4>)(live && crow < k && cv ? cv + uint64_t(cbase + dcol) : sink));
+          if constexpr (COPY) {
+            u32x4 d = cdat;
+            uint64_t cv = cp;
+            tie(d);
+            tie(cv);
+            cdat = d;
+            cp = cv;
+          }
         }
       });
     });
