@@ -81,10 +81,45 @@ def _case_distributed_codec(ctx):
         assert torch.equal(out, data)
 
 
-@pytest.mark.parametrize("case", ["_case_broadcast", "_case_scatter_gather", "_case_distributed_codec"])
+def _case_parity_exchange(ctx):
+    """ParityExchange delivers exactly the senders' bytes: owners = piece `rank` of every rank's
+    block, in source order; root = every peer's whole block on rank 0. Two alternating slots."""
+    from gpu_rscode_amd.parallel.placement import ParityExchange, even_splits
+
+    nbytes = 3 * 4096 + 17  # not divisible by the world size: uneven pieces
+
+    def block(r, slot):
+        return torch.arange(nbytes, dtype=torch.int64).add(7 * r + 131 * slot).remainder(251).to(torch.uint8)
+
+    srcs = [block(ctx.rank, s) for s in range(2)]
+    for mode in ("owners", "root", "none"):
+        x = ParityExchange(srcs, mode)
+        for slot in (0, 1, 0):
+            x.start(slot)
+            x.wait(slot)
+            if mode == "owners":
+                sp = even_splits(nbytes, ctx.world)
+                off = sum(sp[: ctx.rank])
+                mine = sp[ctx.rank]
+                want = torch.cat([block(r, slot)[off:off + mine] for r in range(ctx.world)])
+                assert torch.equal(x.recv, want), (mode, slot)
+                assert x.bytes_sent == nbytes - mine and x.bytes_received == mine * (ctx.world - 1)
+            elif mode == "root" and ctx.rank == 0:
+                for r in range(1, ctx.world):
+                    assert torch.equal(x.recv_list[r], block(r, slot)), (mode, slot, r)
+            assert x.verify(slot)
+        x.drain()
+
+
+@pytest.mark.parametrize("case", ["_case_broadcast", "_case_scatter_gather", "_case_distributed_codec",
+                                  "_case_parity_exchange"])
 def test_distributed_world2(case):
     _run(case, 2)
 
 
 def test_distributed_codec_world3():
     _run("_case_distributed_codec", 3)
+
+
+def test_parity_exchange_world3():
+    _run("_case_parity_exchange", 3)
