@@ -12,9 +12,9 @@ One step on every rank:
   1. encode:  parity[4, C] = E . data[10, C]                          (gfx950 v_perm GF-GEMM)
   2. decode:  4 erasures drawn from a pool of recoverable patterns (natives AND parity erased);
               the decode system is solved ON DEVICE every step (LDS Gauss-Jordan on the e x (e+k)
-              systematic system [G[P, erased] | B'], on a side stream under the encode), then the
-              erased natives are rebuilt and surviving natives copied in one fused pass into a
-              fresh [10, C] output.
+              systematic system [G[P, erased] | B'], on a side stream, one step ahead, beside the
+              previous step's decode GEMM), then the erased natives are rebuilt and surviving
+              natives copied in one fused pass into a fresh [10, C] output.
   3. N > 1:   the step's parity leaves the GPU over xGMI (parallel/placement.py), asynchronously on
               RCCL's stream while the next step computes (parity double-buffered):
               --comm owners (default) places parity chunk-contiguously: one all_to_all in which each
@@ -176,27 +176,67 @@ class GpuWorkload:
         self.inv_done = torch.cuda.Event()
         self.kv = dict(vec=a.vec, pf=a.pf, nt=a.nt)
         self.last = None
+        self.graph_mode = False
 
     def flat_parity(self, slot: int) -> torch.Tensor:
         par = self.parity[slot]
         return par.as_strided((par.untyped_storage().nbytes(),), (1,))
 
-    def step(self, i: int, slot: int) -> None:
+    def _plan(self, i: int, slot: int):
+        return self.dec[slot][i % len(self.dec[slot])]
+
+    def _solve(self, plan, stream) -> None:
         from gpu_rscode_amd.ops import decode_system_into_plan
 
-        plan = self.dec[slot][i % len(self.dec[slot])]
+        decode_system_into_plan(self.g_dev, plan.rows_dev, plan.erased_dev, plan, status=plan.status, stream=stream)
+
+    def step(self, i: int, slot: int) -> None:
+        """One encode + one on-device decode solve + one decode GEMM.
+
+        Default schedule: the decode system of step i+1 is solved on a side stream right after step
+        i's decode GEMM is queued, so the one-workgroup solve runs beside that GEMM (whose register
+        use leaves room for it; the staggered FP4 encode kernel of wide stripes does not). Each
+        plan's solve waits for the previous decode that read the same tables (event per plan)."""
+        plan = self._plan(i, slot)
         self.last = plan
-        inv_stream = self.stream if self.a.no_overlap else self.side
-        if not self.a.no_overlap:
-            self.side.wait_stream(self.stream)  # the previous use of this plan's tables is done
-        decode_system_into_plan(self.g_dev, plan.rows_dev, plan.erased_dev, plan, status=plan.status,
-                                stream=inv_stream)
-        if not self.a.no_overlap:
+        if self.a.no_overlap:  # everything on one stream, solve first
+            self._solve(plan, self.stream)
+            self.enc[slot].run(**self.kv)
+            plan.run(**self.kv)
+            return
+        if self.graph_mode:  # captured per pattern: solve under this step's encode
+            self.side.wait_stream(self.stream)
+            self._solve(plan, self.side)
             self.inv_done.record(self.side)
-        self.enc[slot].run(**self.kv)
-        if not self.a.no_overlap:
+            self.enc[slot].run(**self.kv)
             self.stream.wait_event(self.inv_done)
+            plan.run(**self.kv)
+            return
+        if not getattr(plan, "pending", False):  # (first step of a loop)
+            self._issue_solve(plan)
+        self.enc[slot].run(**self.kv)
+        self.stream.wait_event(plan.solved)
         plan.run(**self.kv)
+        plan.used.record(self.stream)
+        plan.pending = False
+        nxt = self._plan(i + 1, (i + 1) % len(self.dec))
+        self._issue_solve(nxt)
+
+    def reset(self) -> None:
+        """Start a loop with no solve in flight: its first step solves its own system (so a timed
+        loop of K steps runs K + 1 solves — one more than it needs)."""
+        for plans in self.dec:
+            for plan in plans:
+                plan.pending = False
+
+    def _issue_solve(self, plan) -> None:
+        if not hasattr(plan, "solved"):
+            plan.solved, plan.used = torch.cuda.Event(), torch.cuda.Event()
+            plan.used.record(self.stream)
+        self.side.wait_event(plan.used)  # the last decode that read these tables is done
+        self._solve(plan, self.side)
+        plan.solved.record(self.side)
+        plan.pending = True
 
     def sync(self) -> None:
         torch.cuda.synchronize()
@@ -233,6 +273,9 @@ class CpuWorkload:
     def sync(self) -> None:
         pass
 
+    def reset(self) -> None:
+        pass
+
     def verify(self) -> bool:
         want = gf.GF256.gemm(self.rs.E, self.data.numpy())
         return torch.equal(self.out, self.data) and all(np.array_equal(par.numpy(), want) for par in self.parity)
@@ -249,6 +292,7 @@ def timed_loop(work, xchg: ParityExchange, steps: int, world: int, dev, label: s
         work.step(i, slot)
         xchg.start(slot)
 
+    work.reset()
     with trace_range(f"bench/{label}"):
         if world > 1:
             dist.barrier()
@@ -269,6 +313,7 @@ def timed_loop(work, xchg: ParityExchange, steps: int, world: int, dev, label: s
 
 
 def warm(work, xchg: ParityExchange, steps: int) -> None:
+    work.reset()
     slots = len(xchg.sources)
     for i in range(steps):
         xchg.wait(i % slots)
@@ -393,6 +438,7 @@ def main(argv=None) -> int:
         steps = a.steps if mi == 0 else min(a.steps, 20)
         warm(work, xchg, a.warmup if mi == 0 else 2)
         if a.graph and mode == a.comm:
+            work.graph_mode = True
             graphs = []
             for i in range(len(work.dec[0])):
                 gph = torch.cuda.CUDAGraph()

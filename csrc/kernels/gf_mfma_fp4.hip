@@ -811,9 +811,10 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4sk_kernel(cptr<uint64_t> in
           }
         }
         __builtin_amdgcn_sched_barrier(0);
+        // (descending: tile MG-1 reads the oldest window slot, which the expansion below refills)
         static_for<MG>([&](auto mt) {
-          constexpr int MT = decltype(mt)::value;
-          if constexpr (MT != kFirst && MT != EP) mfma_tile(mt);
+          constexpr int MT = MG - 1 - decltype(mt)::value;
+          if constexpr (MT != kFirst && MT != EP) mfma_tile(std::integral_constant<int, MT>{});
         });
         [[maybe_unused]] uint32_t w[2];
         if constexpr (EP >= 0) {
@@ -1052,10 +1053,12 @@ hipError_t launch_fp4sk_any(const Fp4Geometry& geo, const Fp4Args& a, hipStream_
 
 // the staggered kernel covers the static 8-slot chunk (k in (112, 128]) with 4 or 8 M-tiles per
 // group; GFRS_FP4_KERNEL=v1 selects the single-schedule kernel (A/B measurements)
-bool use_sk(const Fp4Geometry& geo) {
+bool use_sk(const Fp4Geometry& geo, bool copies) {
   const char* env = std::getenv("GFRS_FP4_KERNEL");
   if (env && std::strcmp(env, "v1") == 0) return false;
-  return geo.ksteps == 16 && (geo.mg == 4 || geo.mg == 8);
+  if (env && std::strcmp(env, "sk") == 0) copies = false;  // (force it for the fused-copy form too)
+  // measured (profiles/r02_fp4): 6 % faster than v1 for plain GEMMs, 1 % slower with fused copies
+  return !copies && geo.ksteps == 16 && (geo.mg == 4 || geo.mg == 8);
 }
 
 }  // namespace
@@ -1087,7 +1090,7 @@ hipError_t launch_gf_gemm_fp4(const void* bitmat, const void* desc, int k, int m
   const DescLayout l = desc_layout(k, m_pad);
   const char* b = static_cast<const char*>(desc);
   const Fp4Geometry geo = geometry(k, m, mg_cap, copies);
-  const bool sk = use_sk(geo);
+  const bool sk = use_sk(geo, copies);
   const int64_t chunk_cols = kBlockCols;
   const int64_t nchunks = ncols / chunk_cols;
   if (nchunks > 0) {

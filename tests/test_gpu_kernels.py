@@ -358,10 +358,7 @@ def test_fp4_staggered_kernel_matches_v1_and_oracle(k, m, variant, monkeypatch):
         copies = [cdst[j] if j % 4 else None for j in range(k)]
     results = []
     for kernel in ("sk", "v1"):
-        if kernel == "v1":
-            monkeypatch.setenv("GFRS_FP4_KERNEL", "v1")
-        else:
-            monkeypatch.delenv("GFRS_FP4_KERNEL", raising=False)
+        monkeypatch.setenv("GFRS_FP4_KERNEL", kernel)  # "sk" also forces the fused-copy form onto it
         out = alloc_rows(m, ncols, "cuda", fill=0x5A)
         if copies is not None:
             cdst.fill_(0x44)
