@@ -63,13 +63,16 @@ int main(int argc, char** argv) {
     opt.slice_bytes = a.slice;
     const bool enc = a.op == gfrs_cli::Args::kEncode;
     const char* verb = enc ? "encoding" : "decoding";
-    // device setup overlapped with the input reads (gfrs/async_prepare.h); the streaming codec sizes
-    // its windows itself and prepares on its first window
-    std::unique_ptr<AsyncPrepare> prep;
+    // device setup overlapped with the input reads (gfrs/async_prepare.h), sized for the whole
+    // stripe or, streamed, for one window of the streaming codec
+    StreamOptions so;
+    so.window = a.window;
+    so.resume = a.resume;
+    so.durable = a.sync;
+    const StreamOptions* sop = a.streaming() ? &so : nullptr;
     double gpu_ms = 0;  // the reference's "Total GPU ... time" (transfers + kernels, all devices)
-    if (!a.streaming())
-      prep = enc ? prepare_for_encode(devices, opt, a.in_file, a.k, a.n - a.k)
-                 : prepare_for_decode(devices, opt, a.in_file);
+    std::unique_ptr<AsyncPrepare> prep = enc ? prepare_for_encode(devices, opt, a.in_file, a.k, a.n - a.k, sop)
+                                             : prepare_for_decode(devices, opt, a.in_file, sop);
     const GemmFn gemm = [&](const std::vector<const uint8_t*>& in, const std::vector<uint8_t*>& out,
                             const Mat& coeff, int64_t ncols) {
       if (prep) {
@@ -94,10 +97,6 @@ int main(int argc, char** argv) {
     };
     FileReport r;
     if (a.streaming()) {
-      StreamOptions so;
-      so.window = a.window;
-      so.resume = a.resume;
-      so.durable = a.sync;
       const StreamReport sr = enc ? encode_file_stream(a.in_file, a.k, a.n - a.k, parse_matrix_kind(a.matrix),
                                                        gemm, pinned_alloc(), so, a.cpu_meta)
                                   : decode_file_stream(a.in_file, a.conf, a.out, gemm, pinned_alloc(), so);

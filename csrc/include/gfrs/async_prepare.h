@@ -17,6 +17,7 @@
 
 #include "gfrs/format.h"
 #include "gfrs/pipeline.h"
+#include "gfrs/stream_codec.h"
 
 namespace gfrs {
 
@@ -47,22 +48,27 @@ class AsyncPrepare {
   std::thread th_;  // last member: starts after err_/ms_ exist
 };
 
-// Encode of `file` with k natives and p parity rows: k x C in, p x C out.
+// Encode of `file` with k natives and p parity rows: k x C in, p x C out (or, streamed, k x W
+// windows of the streaming codec's width).
 inline std::unique_ptr<AsyncPrepare> prepare_for_encode(const std::vector<int>& devices, const PipelineOptions& opt,
-                                                        const std::string& file, int k, int p) {
+                                                        const std::string& file, int k, int p,
+                                                        const StreamOptions* stream = nullptr) {
   if (k <= 0 || p <= 0 || k + p > 256) return nullptr;
-  const int64_t C = chunk_size(file_size(file), k);
+  int64_t C = chunk_size(file_size(file), k);
   if (C <= 0) return nullptr;
+  if (stream) C = stream_window(*stream, k + p, C);
   return std::make_unique<AsyncPrepare>(devices, opt, k, p, C);
 }
 
 // Decode of `file` (reads its METADATA): k x C in, at most min(k, p) erased rows out.
 inline std::unique_ptr<AsyncPrepare> prepare_for_decode(const std::vector<int>& devices, const PipelineOptions& opt,
-                                                        const std::string& file) {
+                                                        const std::string& file,
+                                                        const StreamOptions* stream = nullptr) {
   const Metadata md = read_metadata(metadata_path(file));
   const int m = std::min(md.k, md.p);
-  const int64_t C = chunk_size(md.total_size, md.k);
+  int64_t C = chunk_size(md.total_size, md.k);
   if (md.k <= 0 || m <= 0 || C <= 0 || md.k > 256) return nullptr;
+  if (stream) C = stream_window(*stream, 2 * md.k, C);
   return std::make_unique<AsyncPrepare>(devices, opt, md.k, m, C);
 }
 

@@ -43,4 +43,8 @@ StreamReport decode_file_stream(const std::string& file, const std::string& conf
 
 std::string progress_path(const std::string& target);
 
+// Column window (bytes per chunk row) the streaming codecs use for `rows` buffered rows per window
+// (encode: n, decode: 2k) of C-byte chunks.
+int64_t stream_window(const StreamOptions& opt, int rows, int64_t C);
+
 }  // namespace gfrs

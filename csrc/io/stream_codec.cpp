@@ -186,6 +186,8 @@ std::string join_u32(const std::vector<uint32_t>& v) {
 
 }  // namespace
 
+int64_t stream_window(const StreamOptions& opt, int rows, int64_t C) { return pick_window(opt, rows, C); }
+
 std::string progress_path(const std::string& target) { return target + ".PROGRESS"; }
 
 StreamReport encode_file_stream(const std::string& file, int k, int p, MatrixKind kind, const GemmFn& gemm,
