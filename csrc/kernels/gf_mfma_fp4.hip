@@ -534,12 +534,13 @@ __host__ __device__ constexpr int sk_stores_in(int s0, int s1, int mg, int ns) {
   for (int s = s0; s < s1; ++s) n += sk_mod(s, ns) < mg ? 2 : 0;
   return n;
 }
-// vm ops issued after the DMA of slot sp+1 when its data is awaited (first step of slot sp, before
-// that slot's own DMA): R-3 DMAs, the copy stores of slots sp+2-R .. sp-1 and the epilogue stores
-// of their steps (exact: the prologue issues the stores of the virtual slots before chunk 0 as
-// dummies)
+// DMA(t) (ring slot t % R) is issued in the second K-step of slot t-R, right after that slot's data
+// has been consumed. vm ops younger than DMA(sp+1) when it is awaited (first step of slot sp): R-2
+// DMAs, the copy stores of slots sp+1-R .. sp-1 (issued at the end of their second step) and the
+// epilogue stores of steps [2 (sp+1-R) + 1, 2 sp) (exact: the prologue issues the stores of the
+// virtual slots before chunk 0 as dummies in the same order)
 __host__ __device__ constexpr int sk_wait_count(int sp, int mg, int ks, int r, bool copy) {
-  const int n = (r - 3) + (copy ? r - 2 : 0) + sk_stores_in(2 * (sp + 2 - r), 2 * sp, mg, 2 * ks);
+  const int n = (r - 2) + (copy ? r - 1 : 0) + sk_stores_in(2 * (sp + 1 - r) + 1, 2 * sp, mg, 2 * ks);
   return n < 63 ? n : 63;
 }
 
@@ -617,7 +618,7 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4sk_kernel(cptr<uint64_t> in
   const uint32_t cptr_addr = rowptr_addr + 2304u;
   // scattered inputs: the row pointer of the next DMA, read from LDS one slot ahead (a register
   // per slot of the chunk would cost 16 VGPRs)
-  uint64_t pn = UNI ? 0 : rowptr[dma_row((R - 1) % KS)];
+  uint64_t pn = UNI ? 0 : rowptr[dma_row(R % KS)];
 
   // DMA of slot T (chunk-relative, T may reach past the chunk) of chunk ci: past the last chunk
   // it lands in the spare slot (valid source), so the number in flight stays the same
@@ -685,12 +686,15 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4sk_kernel(cptr<uint64_t> in
     }
   };
 
-  // prologue: R-1 slots in flight, each followed by the stores its steady-state slot issues after
-  // its DMA (copy store; epilogue stores of those steps of the previous chunk) as dummies
-  static_for<R - 1>([&](auto t) {
-    dma_issue(0, t, UNI ? 0 : rowptr[dma_row(decltype(t)::value % KS)]);
-    constexpr int v = KS + decltype(t)::value - (R - 1);  // the virtual slot of chunk -1 issuing it
-    constexpr int n_epi = sk_stores_in(2 * v, 2 * v + 2, MG, NS);
+  // prologue: R slots in flight; around each DMA the stores its steady-state position has (the
+  // issuing virtual slot's second-step epilogue stores and copy store after it, the next virtual
+  // slot's first-step epilogue stores before the next DMA) as dummies to the sink
+  static_for<R>([&](auto t) {
+    constexpr int T = decltype(t)::value;
+    dma_issue(0, t, UNI ? 0 : rowptr[dma_row(T % KS)]);
+    constexpr int v = KS + T - R;  // the virtual slot of chunk -1 issuing it
+    constexpr int n_epi = sk_stores_in(2 * v + 1, 2 * v + 2, MG, NS) +
+                          (T + 1 < R ? sk_stores_in(2 * v + 2, 2 * v + 3, MG, NS) : 0);
     const uint64_t sk = sink;
     if constexpr (COPY) {
       const u32x4 zero = {0u, 0u, 0u, 0u};
@@ -699,7 +703,7 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4sk_kernel(cptr<uint64_t> in
 #pragma unroll
     for (int i = 0; i < n_epi; ++i) asm volatile("global_store_short %0, %1, off" ::"v"(sk), "v"(0) : "memory");
   });
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(R - 2) : "memory");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(R - 1) : "memory");
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
   uint32_t x0[4], x1[4], x2[4];  // raw bytes: x1 = step s+1 (in registers), x2 = step s+2 (in flight)
@@ -791,14 +795,16 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4sk_kernel(cptr<uint64_t> in
           opn[0] = o0;
           opn[1] = o1;
         }
-        if constexpr (JJ == 0) {
-          dma_issue(ci, std::integral_constant<int, SP + R - 1>{}, pn);
+        if constexpr (JJ == 1) {  // this slot's data is consumed: refill its ring slot R ahead
+          dma_issue(ci, std::integral_constant<int, SP + R>{}, pn);
           if constexpr (!UNI) {  // the next slot's DMA row pointer
-            const uint32_t addr = rowptr_addr + 8u * uint32_t(dma_row((SP + R) % KS));
+            const uint32_t addr = rowptr_addr + 8u * uint32_t(dma_row((SP + 1 + R) % KS));
             uint64_t v;
             asm volatile("ds_read_b64 %0, %1" : "=&v"(v) : "v"(addr) : "memory");
             pn = v;
           }
+        }
+        if constexpr (JJ == 0) {
           if constexpr (COPY) {  // this lane's 16 B of the current slot and its row's copy pointer
             const uint32_t addr = ring_lane + uint32_t(RS * kSlotBytes);
             const uint32_t caddr = cptr_addr + 8u * uint32_t(crow < k ? crow : k - 1);
@@ -875,12 +881,12 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4sk_kernel(cptr<uint64_t> in
           opc[0] = o0;
           opc[1] = o1;
         }
+        if constexpr (JJ == 1 && !UNI) {
+          uint64_t v = pn;
+          tie(v);
+          pn = v;
+        }
         if constexpr (JJ == 0) {
-          if constexpr (!UNI) {
-            uint64_t v = pn;
-            tie(v);
-            pn = v;
-          }
           if constexpr (COPY) {
             u32x4 d = cdat;
             uint64_t cv = cp;
