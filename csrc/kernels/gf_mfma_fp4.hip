@@ -826,7 +826,11 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4sk_kernel(cptr<uint64_t> in
         if constexpr (EP >= 0) {
           constexpr int E = EP >= 0 ? EP : 0;
           // output bytes of tile E (rows 2h, 2h+1; columns 2c, 2c+1): 7 v_bfi per byte over the
-          // biased accumulators (the parity of bit b's count sits at bit b)
+          // biased accumulators (the parity of bit b's count sits at bit b). The empty asm makes
+          // the accumulators a new value here, so their reads stay in this segment (between the
+          // MFMAs) instead of being hoisted to the head of the step.
+#pragma unroll
+          for (int t = 0; t < NTW; ++t) asm volatile("" : "+a"(acc[E][t]));
           uint32_t y[NTW][2];
 #pragma unroll
           for (int b = 0; b < 8; ++b)
