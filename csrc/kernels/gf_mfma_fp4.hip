@@ -908,6 +908,93 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4sk_kernel(cptr<uint64_t> in
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA (dummy or not) outlives the wave
 }
 
+// Survivor copy beside the matrix-core decode GEMM (the "split" form of the fused copy): the wide
+// FP4 GEMM is matrix-core bound and reads HBM at ~1.3 TB/s, so a copy kernel that fits in the
+// registers the persistent GEMM leaves free (the sk kernel allocates 448 of a SIMD's 512; this
+// kernel stays at <= 32 VGPRs, no LDS) streams the survivors through the idle HBM bandwidth on a
+// side stream. copy[j] != 0: bytes [col0, col0 + ncols) of input row j go to copy[j]. 16-byte
+// loads four deep per lane, non-temporal stores; rows whose two addresses are not 16-byte aligned
+// alike take a byte loop (never the case for pitched alloc_rows buffers).
+__global__ __launch_bounds__(256) void copy_rows_kernel(cptr<uint64_t> in, cptr<uint64_t> copy, int k, int64_t col0,
+                                                        int64_t ncols) {
+  const int64_t nthr = int64_t(gridDim.x) * blockDim.x;
+  const int64_t t = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  for (int j = 0; j < k; ++j) {
+    const uint64_t dst = copy[j];
+    if (!dst) continue;
+    gptr<const uint8_t> s = (gptr<const uint8_t>)(in[j] + uint64_t(col0));
+    gptr<uint8_t> d = (gptr<uint8_t>)(dst + uint64_t(col0));
+    int64_t done = 0;
+    if ((((in[j] + uint64_t(col0)) | (dst + uint64_t(col0))) & 15) == 0 && ncols < (int64_t(1) << 32)) {
+      // wave-uniform row bases (SGPRs) + 32-bit lane byte offsets: saddr + voffset addressing, so
+      // four loads in flight cost 16 data VGPRs and one offset
+      const int64_t n16 = ncols >> 4;
+      const uint32_t step = uint32_t(nthr) * 16;
+      const uint32_t end = uint32_t(n16) * 16;
+      uint32_t o = uint32_t(t) * 16;
+      for (; uint64_t(o) + 3ull * step < end; o += 4 * step) {
+        const u32x4 v0 = *(gptr<const u32x4>)(s + o);
+        const u32x4 v1 = *(gptr<const u32x4>)(s + (o + step));
+        const u32x4 v2 = *(gptr<const u32x4>)(s + (o + 2 * step));
+        const u32x4 v3 = *(gptr<const u32x4>)(s + (o + 3 * step));
+        __builtin_nontemporal_store(v0, (gptr<u32x4>)(d + o));
+        __builtin_nontemporal_store(v1, (gptr<u32x4>)(d + (o + step)));
+        __builtin_nontemporal_store(v2, (gptr<u32x4>)(d + (o + 2 * step)));
+        __builtin_nontemporal_store(v3, (gptr<u32x4>)(d + (o + 3 * step)));
+      }
+      for (; o < end; o += step) __builtin_nontemporal_store(*(gptr<const u32x4>)(s + o), (gptr<u32x4>)(d + o));
+      done = n16 << 4;
+    }
+    for (int64_t b = done + t; b < ncols; b += nthr) d[b] = s[b];
+  }
+}
+
+// side stream + fork/join events per (device, launch stream): the split copy runs beside the GEMM
+// and the launch stream waits for both (capturable into a hipGraph: event fork/join)
+struct SideCtx {
+  hipStream_t side = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
+};
+
+hipError_t side_ctx(hipStream_t stream, SideCtx* out) {
+  static std::mutex mu;
+  static std::map<std::pair<int, hipStream_t>, SideCtx>* ctxs = new std::map<std::pair<int, hipStream_t>, SideCtx>();
+  const std::pair<int, hipStream_t> key{current_device(), stream};
+  std::lock_guard<std::mutex> g(mu);
+  auto it = ctxs->find(key);
+  if (it != ctxs->end()) {
+    *out = it->second;
+    return hipSuccess;
+  }
+  SideCtx c;
+  hipError_t e = hipStreamCreateWithFlags(&c.side, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&c.fork, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&c.join, hipEventDisableTiming);
+  if (e != hipSuccess) return e;
+  (*ctxs)[key] = c;
+  *out = c;
+  return hipSuccess;
+}
+
+hipError_t launch_copy_rows(cptr<uint64_t> in, cptr<uint64_t> copy, int k, int64_t col0, int64_t ncols,
+                            hipStream_t stream) {
+  const unsigned blocks = unsigned(2 * device_cu_count());  // two waves per SIMD beside the GEMM's one
+  copy_rows_kernel<<<blocks, 256, 0, stream>>>(in, copy, k, col0, ncols);
+  return hipGetLastError();
+}
+
+// GFRS_FP4_COPY: fused (default) = copy inside the GEMM kernel; split = staggered GEMM, then the
+// side-stream copy; split_first = the copy launched first. Measured on k=128, 26 rebuilt rows +
+// 102 copies, 1 GiB (profiles/r02_split): fused 1019 us, split 1034, split_first 1081 (medians;
+// the plain GEMM alone 762, the copy alone 334) — the co-running copy costs the GEMM more than it
+// saves: re-reading the survivors adds 0.8 GB of HBM traffic, the chip holds a lower clock, and
+// the copy waves take issue slots on the GEMM's SIMDs. Kept as the measured alternative.
+int split_copy_mode() {
+  const char* env = std::getenv("GFRS_FP4_COPY");
+  if (!env || std::strcmp(env, "split") != 0) return env && std::strcmp(env, "split_first") == 0 ? 2 : 0;
+  return 1;
+}
+
 struct Fp4Geometry {
   int ksteps, mtiles, mg, groups;
   size_t fixed;  // LDS bytes before the rings: A slice + row/out pointers
@@ -1100,22 +1187,40 @@ hipError_t launch_gf_gemm_fp4(const void* bitmat, const void* desc, int k, int m
   const DescLayout l = desc_layout(k, m_pad);
   const char* b = static_cast<const char*>(desc);
   const Fp4Geometry geo = geometry(k, m, mg_cap, copies);
-  const bool sk = use_sk(geo, copies);
+  // split copy (GFRS_FP4_COPY=split, measured and not the default: split_copy_mode)
+  const int split = copies && use_sk(geo, false) ? split_copy_mode() : 0;
+  const bool fused = copies && !split;
+  const bool sk = use_sk(geo, fused);
   const int64_t chunk_cols = kBlockCols;
   const int64_t nchunks = ncols / chunk_cols;
   if (nchunks > 0) {
     Fp4Args a{};
     a.in = (cptr<uint64_t>)(b + l.in_off);
     a.out = (cptr<uint64_t>)(b + l.out_off);
-    a.copy = copies ? (cptr<uint64_t>)(b + l.copy_off) : nullptr;
+    a.copy = fused ? (cptr<uint64_t>)(b + l.copy_off) : nullptr;
     a.bitmat = bitmat;
     a.k = k;
     a.m = m;
     a.col0 = col0;
     a.nchunks = nchunks;
     a.in_stride = copies ? 0 : in_stride;  // the copy variant reads row pointers from the table
+    SideCtx side{};
+    if (split) {
+      hipError_t e = side_ctx(stream, &side);
+      if (e == hipSuccess) e = hipEventRecord(side.fork, stream);
+      if (e == hipSuccess) e = hipStreamWaitEvent(side.side, side.fork, 0);
+      if (e == hipSuccess && split == 2)
+        e = launch_copy_rows(a.in, (cptr<uint64_t>)(b + l.copy_off), k, col0, nchunks * chunk_cols, side.side);
+      if (e != hipSuccess) return e;
+    }
     hipError_t e;
-    if (sk) {
+    if (split) {
+      e = geo.mg == 8 ? launch_fp4sk_any<8>(geo, a, stream) : launch_fp4sk_any<4>(geo, a, stream);
+      if (e == hipSuccess && split == 1)
+        e = launch_copy_rows(a.in, (cptr<uint64_t>)(b + l.copy_off), k, col0, nchunks * chunk_cols, side.side);
+      if (e == hipSuccess) e = hipEventRecord(side.join, side.side);
+      if (e == hipSuccess) e = hipStreamWaitEvent(stream, side.join, 0);
+    } else if (sk) {
       e = geo.mg == 8 ? launch_fp4sk_any<8>(geo, a, stream) : launch_fp4sk_any<4>(geo, a, stream);
     } else {
       switch (geo.mg) {

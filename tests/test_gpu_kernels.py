@@ -357,8 +357,12 @@ def test_fp4_staggered_kernel_matches_v1_and_oracle(k, m, variant, monkeypatch):
         cdst = alloc_rows(k, ncols, "cuda", fill=0x44)
         copies = [cdst[j] if j % 4 else None for j in range(k)]
     results = []
-    for kernel in ("sk", "v1"):
-        monkeypatch.setenv("GFRS_FP4_KERNEL", kernel)  # "sk" also forces the fused-copy form onto it
+    for kernel in ("sk", "v1") + (("split",) if variant == "copy" else ()):
+        if kernel == "split":  # the plain kernel + the side-stream copy kernel (GFRS_FP4_COPY=split)
+            monkeypatch.delenv("GFRS_FP4_KERNEL", raising=False)
+            monkeypatch.setenv("GFRS_FP4_COPY", "split")
+        else:
+            monkeypatch.setenv("GFRS_FP4_KERNEL", kernel)  # "sk" also forces the fused-copy form onto it
         out = alloc_rows(m, ncols, "cuda", fill=0x5A)
         if copies is not None:
             cdst.fill_(0x44)
@@ -372,4 +376,4 @@ def test_fp4_staggered_kernel_matches_v1_and_oracle(k, m, variant, monkeypatch):
             for j in range(k):
                 assert np.array_equal(c[j], want_in[j] if j % 4 else np.full(ncols, 0x44, np.uint8)), (kernel, j)
         results.append(got)
-    assert np.array_equal(results[0], results[1])
+    assert all(np.array_equal(results[0], r) for r in results[1:])
