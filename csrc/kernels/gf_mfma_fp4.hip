@@ -1015,6 +1015,17 @@ Fp4Geometry geometry(int k, int m, int mg_cap, bool copy = false) {
   while (g.mg < g.mtiles && g.mg < mg_cap) g.mg <<= 1;
   // (the copy-pointer block is always budgeted, so the bitmat layout does not depend on `copy`)
   while (g.mg > 1 && g.mg * g.ksteps > kMaxLdsKiB - 2) g.mg >>= 1;
+  // the static wide-stripe chunk (k in (112, 128], the instantiated MG = 5..7 kernels): exactly
+  // mtiles M-tiles instead of a padded 8 — a decode rebuilding 20..28 natives skips 1..3 tiles of
+  // MFMAs that would only compute padding rows (12.5-37.5 % of the matrix-core work)
+  // (GFRS_FP4_EXACT_MG=0: the padded 8, for A/B measurements; read once per process so a plan's
+  // bit-matrix and its launches always agree)
+  static const bool exact = [] {
+    const char* env = std::getenv("GFRS_FP4_EXACT_MG");
+    return !(env && std::strcmp(env, "0") == 0);
+  }();
+  if (exact && g.ksteps == 16 && ((g.mg == 8 && g.mtiles > 4 && g.mtiles < 8) || (g.mg == 4 && g.mtiles == 3)))
+    g.mg = g.mtiles;
   g.groups = (g.mtiles + g.mg - 1) / g.mg;
   g.fixed = size_t(g.mg) * g.ksteps * 64 * 16 + 2304 + (copy ? 2048 : 0);
   return g;
@@ -1076,6 +1087,12 @@ hipError_t launch_fp4_ring(const Fp4Geometry& geo, const Fp4Args& a, hipStream_t
   const std::pair<int, int> ch = choice.get_or(geo.fixed / 1024, [&] {
     const int occs[kN] = {fp4_occupancy<MG, UNI, COPY, Rs, KS>(geo.fixed)...};
     auto reserve_ok = [&](int i) { return geo.fixed + ring_lds(rings[i]) + kSideReserve <= 160 * 1024; };
+    static const int forced = [] {  // GFRS_FP4_RING=R: that depth when it fits (A/B measurements)
+      const char* env = std::getenv("GFRS_FP4_RING");
+      return env ? std::atoi(env) : 0;
+    }();
+    for (int i = 0; i < kN; ++i)
+      if (forced && rings[i] == forced && occs[i] > 0) return std::pair<int, int>{i + 1, occs[i]};
     int best = -1;
     for (int i = 0; i < kN; ++i) {
       if (occs[i] <= 0) continue;
@@ -1096,7 +1113,10 @@ hipError_t launch_fp4_ring(const Fp4Geometry& geo, const Fp4Args& a, hipStream_t
 // kernel with the rings that divide 8; any other k: the runtime-cursor kernel
 template <int MG, bool UNI, bool COPY>
 hipError_t launch_fp4_var(const Fp4Geometry& geo, const Fp4Args& a, hipStream_t stream) {
-  if (geo.ksteps == 16) return launch_fp4_ring<MG, UNI, COPY, 8, 8, 4>(geo, a, stream);
+  // (fused-copy form: ring 4 only — the depth-8 form ran 0-6 % slower at m = 8..16,
+  // profiles/r02_exact_mg/session_k_*)
+  if (geo.ksteps == 16)
+    return COPY ? launch_fp4_ring<MG, UNI, COPY, 8, 4>(geo, a, stream) : launch_fp4_ring<MG, UNI, COPY, 8, 8, 4>(geo, a, stream);
   return launch_fp4_ring<MG, UNI, COPY, 0, 32, 16, 12, 8, 6, 4>(geo, a, stream);
 }
 
@@ -1106,6 +1126,17 @@ hipError_t launch_fp4_any(const Fp4Geometry& geo, const Fp4Args& a, hipStream_t 
   if (a.copy) return launch_fp4_var<MG, false, true>(geo, a, stream);
   return a.in_stride ? launch_fp4_var<MG, true, false>(geo, a, stream)
                      : launch_fp4_var<MG, false, false>(geo, a, stream);
+}
+
+// MG = 3, 5..7 exist for the static 8-slot chunk only (geometry() picks them there), ring depth 4:
+// the depth-8 forms fit the LDS but need ~90 more VGPRs (256 with spills into AGPRs) and ran
+// 0-19 % slower at every shape (profiles/r02_exact_mg: k=128, m=28 + 100 copies 885 vs 1050 us)
+template <int MG>
+hipError_t launch_fp4_static_any(const Fp4Geometry& geo, const Fp4Args& a, hipStream_t stream) {
+  if (geo.ksteps != 16) return hipErrorInvalidConfiguration;
+  if (a.copy) return launch_fp4_ring<MG, false, true, 8, 4>(geo, a, stream);
+  return a.in_stride ? launch_fp4_ring<MG, true, false, 8, 4>(geo, a, stream)
+                     : launch_fp4_ring<MG, false, false, 8, 4>(geo, a, stream);
 }
 
 // sk kernel (k in (112, 128]: 8 ring slots per chunk): ring depth 8 or 4, deepest that fits the LDS
@@ -1225,8 +1256,12 @@ hipError_t launch_gf_gemm_fp4(const void* bitmat, const void* desc, int k, int m
     } else {
       switch (geo.mg) {
         case 8: e = launch_fp4_any<8>(geo, a, stream); break;
-      case 4: e = launch_fp4_any<4>(geo, a, stream); break;
-      case 2: e = launch_fp4_any<2>(geo, a, stream); break;
+        case 7: e = launch_fp4_static_any<7>(geo, a, stream); break;
+        case 6: e = launch_fp4_static_any<6>(geo, a, stream); break;
+        case 5: e = launch_fp4_static_any<5>(geo, a, stream); break;
+        case 4: e = launch_fp4_any<4>(geo, a, stream); break;
+        case 3: e = launch_fp4_static_any<3>(geo, a, stream); break;
+        case 2: e = launch_fp4_any<2>(geo, a, stream); break;
         default: e = launch_fp4_any<1>(geo, a, stream); break;
       }
     }

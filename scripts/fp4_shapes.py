@@ -1,0 +1,54 @@
+#!/usr/bin/env python3
+"""Median kernel time of wide FP4 GEMM shapes (k=128; m rebuilt rows; optional fused copies), one
+JSON line. Run once per environment setting to A/B kernel choices (e.g. GFRS_FP4_EXACT_MG=0)."""
+from __future__ import annotations
+
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from gpu_rscode_amd import gf  # noqa: E402
+from gpu_rscode_amd.models import alloc_rows  # noqa: E402
+from gpu_rscode_amd.ops import GemmPlan, fill_random_  # noqa: E402
+
+
+def main():
+    k, C, iters = 128, (1 << 30) // 128, 15
+    data = alloc_rows(k, C, "cuda")
+    fill_random_(data.as_strided((data.untyped_storage().nbytes(),), (1,)), seed=3)
+    dst = alloc_rows(k, C, "cuda")
+    res = {"env": {x: os.environ.get(x) for x in ("GFRS_FP4_EXACT_MG", "GFRS_FP4_KERNEL", "GFRS_FP4_COPY")}}
+    rng = np.random.default_rng(5)
+    ms = [int(x) for x in sys.argv[1].split(",")] if len(sys.argv) > 1 else [20, 24, 28, 32]
+    for m in ms:
+        coeff = rng.integers(1, 256, size=(m, k), dtype=np.uint8)
+        out = alloc_rows(m, C, "cuda")
+        for ncopy in (0, 128 - m):
+            copies = [dst[j] if j < ncopy else None for j in range(k)] if ncopy else None
+            plan = GemmPlan(data, out, coeff, copies=copies, engine="mfma")
+            plan.run()
+            torch.cuda.synchronize()
+            ts = []
+            for _ in range(iters):
+                s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                s.record()
+                plan.run()
+                e.record()
+                torch.cuda.synchronize()
+                ts.append(s.elapsed_time(e) * 1e3)
+            cols = 1 << 16
+            ok = np.array_equal(out[:, :cols].cpu().numpy(), gf.GF256.gemm(coeff, data[:, :cols].cpu().numpy()))
+            if ncopy:
+                ok = ok and torch.equal(dst[:ncopy], data[:ncopy])
+            res[f"m{m}_copies{ncopy}"] = {"median_us": round(float(np.median(ts)), 1), "min_us": round(min(ts), 1),
+                                          "ok": bool(ok)}
+    print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()
