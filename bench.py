@@ -24,6 +24,10 @@ One step on every rank:
               --comm none: no traffic.
               The JSON carries the headline (default mode) plus the other two modes, each timed in
               its own barrier-bracketed loop ("value_by_comm").
+Consecutive steps alternate between two lanes (--lanes 2: a stream, a parity slot and a decode
+output each), so step i+1's encode runs into the launch gap and the tail wave of step i's decode
+instead of after them; every step still encodes and decodes its whole stripe (measured: 0.663 ->
+0.657 ms at k=10, 1.569 -> 1.537 ms at k=128, profiles/r02_lanes).
 C = ceil(2^30 / 10) = 107374183 bytes (odd, as in the reference, src/encode.cu:317). Data is synthetic
 random bytes generated in HBM; the matrices are the reference Vandermonde, RCCL-broadcast from rank 0
 together with the erasure-pattern pool. Scaling is weak: every GPU encodes and decodes its own 1 GiB.
@@ -92,6 +96,8 @@ def parse(argv=None):
     ap.add_argument("--pf", type=int, default=2, help="kernel variant: rows in flight (with --vec)")
     ap.add_argument("--nt", action="store_true", help="kernel variant: non-temporal (with --vec)")
     ap.add_argument("--no-overlap", action="store_true", help="invert on the main stream (no side stream)")
+    ap.add_argument("--lanes", type=int, default=2,
+                    help="streams that consecutive steps alternate between (own parity slot + decode output)")
     ap.add_argument("--preset", default="k10n14", choices=sorted(PRESETS),
                     help="BASELINE.json config: k10n14 (headline, #2/#3), k16n20_8g (#4 per GPU), k128n160 (#5), "
                          "k4n6 (the reference's published shape)")
@@ -149,28 +155,36 @@ class GpuWorkload:
 
         hip()  # fail loudly if the native extension is missing
         self.a, self.k, self.p = a, k, n - k
+        # lanes: consecutive steps alternate between `lanes` streams, each with its own parity slot
+        # and decode output, so step i+1's encode fills the launch gap and the tail of step i's
+        # decode (every step still encodes and decodes its whole 1 GiB)
+        self.lanes = 1 if a.graph else max(1, a.lanes)
+        slots = max(slots, self.lanes)
         self.data = alloc_rows(k, C, dev)
         fill_random_(self.data.as_strided((self.data.untyped_storage().nbytes(),), (1,)), seed=rank + 1)
         self.parity = [alloc_rows(self.p, C, dev) for _ in range(slots)]
-        self.out = alloc_rows(k, C, dev)
+        self.outs = [alloc_rows(k, C, dev) for _ in range(self.lanes)]
+        self.out = self.outs[0]
         self.g_dev = torch.from_numpy(np.ascontiguousarray(g)).to(dev)
         self.e_mat = e_mat
         self.enc = [GemmPlan(self.data, par, e_mat, engine=a.engine) for par in self.parity]
         self.dec = []
-        for par in self.parity:
+        for si, par in enumerate(self.parity):
             stripe = [self.data[i] for i in range(k)] + [par[i] for i in range(self.p)]
+            out = self.outs[si % self.lanes]
             plans = []
             for rows in pool:
                 erased = [i for i in range(k) if i not in rows]
-                copies = [self.out[r] if r < k else None for r in rows]
-                plan = GemmPlan([stripe[r] for r in rows], [self.out[i] for i in erased], copies=copies,
+                copies = [out[r] if r < k else None for r in rows]
+                plan = GemmPlan([stripe[r] for r in rows], [out[i] for i in erased], copies=copies,
                                 device_tables=True)
                 plan.rows_dev = torch.tensor(rows, dtype=torch.int32, device=dev)
                 plan.erased_dev = torch.tensor(erased, dtype=torch.int32, device=dev)
                 plan.status = torch.zeros(1, dtype=torch.int32, device=dev)
                 plans.append(plan)
             self.dec.append(plans)
-        self.stream = torch.cuda.Stream(dev)  # a non-default stream (hipGraph capture needs one)
+        self.streams = [torch.cuda.Stream(dev) for _ in range(self.lanes)]  # non-default (hipGraph capture)
+        self.stream = self.streams[0]
         torch.cuda.set_stream(self.stream)
         self.side = torch.cuda.Stream(dev)  # decode-system solve overlaps the encode GEMM
         self.inv_done = torch.cuda.Event()
@@ -189,6 +203,16 @@ class GpuWorkload:
         from gpu_rscode_amd.ops import decode_system_into_plan
 
         decode_system_into_plan(self.g_dev, plan.rows_dev, plan.erased_dev, plan, status=plan.status, stream=stream)
+
+    def lane_stream(self, slot: int):
+        """The stream of the lane that owns parity slot `slot`."""
+        return self.streams[slot % self.lanes]
+
+    def use_lane(self, slot: int) -> None:
+        """Make slot's lane stream current: the step's kernels and the exchange of its parity (and
+        the wait before that parity buffer is overwritten) are ordered on it."""
+        self.stream = self.lane_stream(slot)
+        torch.cuda.set_stream(self.stream)
 
     def step(self, i: int, slot: int) -> None:
         """One encode + one on-device decode solve + one decode GEMM.
@@ -219,8 +243,9 @@ class GpuWorkload:
         plan.run(**self.kv)
         plan.used.record(self.stream)
         plan.pending = False
-        nxt = self._plan(i + 1, (i + 1) % len(self.dec))
-        self._issue_solve(nxt)
+        nxt_slot = (i + 1) % len(self.dec)
+        nxt = self._plan(i + 1, nxt_slot)
+        self._issue_solve(nxt, self.lane_stream(nxt_slot))
 
     def reset(self) -> None:
         """Start a loop with no solve in flight: its first step solves its own system (so a timed
@@ -229,10 +254,10 @@ class GpuWorkload:
             for plan in plans:
                 plan.pending = False
 
-    def _issue_solve(self, plan) -> None:
+    def _issue_solve(self, plan, stream=None) -> None:
         if not hasattr(plan, "solved"):
             plan.solved, plan.used = torch.cuda.Event(), torch.cuda.Event()
-            plan.used.record(self.stream)
+            plan.used.record(stream or self.stream)
         self.side.wait_event(plan.used)  # the last decode that read these tables is done
         self._solve(plan, self.side)
         plan.solved.record(self.side)
@@ -242,7 +267,8 @@ class GpuWorkload:
         torch.cuda.synchronize()
 
     def verify(self) -> bool:
-        ok = self.last is not None and int(self.last.status.item()) == 0 and torch.equal(self.out, self.data)
+        ok = self.last is not None and int(self.last.status.item()) == 0
+        ok = ok and all(torch.equal(out, self.data) for out in self.outs)
         cols = min(self.data.shape[1], 1 << 16)
         want = gf.GF256.gemm(self.e_mat, self.data[:, :cols].cpu().numpy())
         return bool(ok and all(np.array_equal(par[:, :cols].cpu().numpy(), want) for par in self.parity))
@@ -263,6 +289,9 @@ class CpuWorkload:
 
     def flat_parity(self, slot: int) -> torch.Tensor:
         return self.parity[slot].view(-1)
+
+    def use_lane(self, slot: int) -> None:
+        pass
 
     def step(self, i: int, slot: int) -> None:
         self.rs.encode(self.data, self.parity[slot])
@@ -288,6 +317,7 @@ def timed_loop(work, xchg: ParityExchange, steps: int, world: int, dev, label: s
 
     def one(i):
         slot = i % slots
+        work.use_lane(slot)
         xchg.wait(slot)  # the exchange that last read this parity buffer is done
         work.step(i, slot)
         xchg.start(slot)
@@ -316,6 +346,7 @@ def warm(work, xchg: ParityExchange, steps: int) -> None:
     work.reset()
     slots = len(xchg.sources)
     for i in range(steps):
+        work.use_lane(i % slots)
         xchg.wait(i % slots)
         work.step(i, i % slots)
         xchg.start(i % slots)
@@ -429,6 +460,7 @@ def main(argv=None) -> int:
         work = GpuWorkload(a, k, n, C, e_mat, rs.G, pool, rank, dev, slots)
     else:
         work = CpuWorkload(a, k, n, C, e_mat, rs.G, pool, rank, slots)
+    slots = len(work.parity)  # (the GPU workload gives every lane its own slot)
     flats = [work.flat_parity(s) for s in range(slots)]
 
     results = {}
