@@ -77,4 +77,19 @@ hipError_t launch_fp4_bitmat_sel(const uint8_t* coeff, int ld, const int* sel, i
 hipError_t launch_mfma_bitmat(const uint8_t* coeff, int m, int k, void* bitmat,
                               hipStream_t stream);
 
+// ---- FP4 A-resident form (csrc/kernels/gf_mfma_fp4ar.hip; called by launch_gf_gemm_fp4) ---------
+// k in (112, 128], one bitmat group of mg <= 8 M-tiles (the layout launch_fp4_bitmat builds).
+// Processes the leading whole chunks of [col0, col0 + ncols) and reports how many columns in
+// *done (the caller finishes the rest).
+struct Fp4ArLaunch {
+  const uint64_t* in;    // descriptor in_ptr[k]
+  const uint64_t* out;   // descriptor out_ptr[m_pad]
+  const uint64_t* copy;  // descriptor copy_ptr[k] (nullptr: no fused copy)
+  const void* bitmat;
+  int k, m, mg;
+  int64_t col0, ncols, in_stride;
+};
+bool fp4ar_supported(int k, int mg);
+hipError_t launch_gf_gemm_fp4ar(const Fp4ArLaunch& a, int64_t* done, hipStream_t stream);
+
 }  // namespace gfrs

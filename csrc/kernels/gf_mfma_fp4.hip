@@ -553,7 +553,11 @@ __device__ __forceinline__ void static_for(F&& f) {
   static_for_impl(f, std::make_integer_sequence<int, N>{});
 }
 
-template <int MG, bool UNI, bool COPY, int R, int KS>
+// ABL (ablation builds for measurements only, GFRS_FP4_ABL; 0 = the product kernel): bit 0 skips
+// the epilogue's accumulator reads and inserts (stores a constant), bit 1 skips the B expansion
+// masks (raw gathered words as the B operand), bit 2 points every DMA at the block's first chunk
+// (L2-resident input: no HBM latency or bandwidth). Results are wrong for ABL != 0.
+template <int MG, bool UNI, bool COPY, int R, int KS, int ABL = 0>
 __global__ __launch_bounds__(256, 1) void gf_gemm_fp4sk_kernel(cptr<uint64_t> in, cptr<uint64_t> out,
                                                                cptr<uint64_t> copy, const i32x4* __restrict__ bitmat,
                                                                int k, int m, int groups, int64_t col0, int64_t nchunks,
@@ -627,7 +631,7 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4sk_kernel(cptr<uint64_t> in
     constexpr int p = T % KS, ring_slot = T % R;
     const int chunk = ci + T / KS;
     const bool live = chunk < my_chunks;
-    const int64_t col = col0 + (slot0 + int64_t(live ? chunk : 0) * chunk_slots) * kBlockCols + dcol;
+    const int64_t col = col0 + (slot0 + int64_t(live && !(ABL & 4) ? chunk : 0) * chunk_slots) * kBlockCols + dcol;
     uint64_t sa;
     if constexpr (UNI)
       sa = in0 + uint64_t(int64_t(dma_row(p)) * in_stride + col);
@@ -665,6 +669,11 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4sk_kernel(cptr<uint64_t> in
   auto expand = [&](i32x4 (&bo)[NTW], const uint32_t (&x)[4]) __attribute__((always_inline)) {
     const uint32_t p01 = x[0] | (x[1] << 16), p23 = x[2] | (x[3] << 16);
     const uint32_t w[2] = {__builtin_amdgcn_perm(p23, p01, 0x06040200u), __builtin_amdgcn_perm(p23, p01, 0x07050301u)};
+    if constexpr ((ABL & 2) != 0) {
+#pragma unroll
+      for (int t = 0; t < NTW; ++t) bo[t] = i32x4{int(w[t]), int(w[t]), int(w[t]), int(w[t])};
+      return;
+    }
 #pragma unroll
     for (int t = 0; t < NTW; ++t) {
       bo[t][0] = int(w[t] & 0x11111111u);
@@ -832,17 +841,21 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4sk_kernel(cptr<uint64_t> in
 #pragma unroll
           for (int t = 0; t < NTW; ++t) asm volatile("" : "+a"(acc[E][t]));
           uint32_t y[NTW][2];
+          if constexpr ((ABL & 1) != 0) {
+            w[0] = w[1] = uint32_t(lane);
+          } else {
 #pragma unroll
-          for (int b = 0; b < 8; ++b)
+            for (int b = 0; b < 8; ++b)
 #pragma unroll
-            for (int t = 0; t < NTW; ++t)
+              for (int t = 0; t < NTW; ++t)
 #pragma unroll
-              for (int u = 0; u < 2; ++u) {
-                const uint32_t v = __float_as_uint(acc[E][t][8 * u + b]);
-                y[t][u] = b == 0 ? v : bfi(1u << b, v, y[t][u]);
-              }
+                for (int u = 0; u < 2; ++u) {
+                  const uint32_t v = __float_as_uint(acc[E][t][8 * u + b]);
+                  y[t][u] = b == 0 ? v : bfi(1u << b, v, y[t][u]);
+                }
 #pragma unroll
-          for (int u = 0; u < 2; ++u) w[u] = __builtin_amdgcn_perm(y[1][u], y[0][u], 0x0c0c0400u);
+            for (int u = 0; u < 2; ++u) w[u] = __builtin_amdgcn_perm(y[1][u], y[0][u], 0x0c0c0400u);
+          }
           bias_init(std::integral_constant<int, E>{});
           if constexpr (E != kFirst) mfma_tile(std::integral_constant<int, E>{});
         }
@@ -1141,10 +1154,10 @@ hipError_t launch_fp4_static_any(const Fp4Geometry& geo, const Fp4Args& a, hipSt
 
 // sk kernel (k in (112, 128]: 8 ring slots per chunk): ring depth 8 or 4, deepest that fits the LDS
 // with the side reserve, else without it
-template <int MG, bool UNI, bool COPY, int R>
+template <int MG, bool UNI, bool COPY, int R, int ABL = 0>
 hipError_t launch_fp4sk(const Fp4Geometry& geo, const Fp4Args& a, hipStream_t stream) {
   constexpr int KS = 8;
-  const void* f = reinterpret_cast<const void*>(&gf_gemm_fp4sk_kernel<MG, UNI, COPY, R, KS>);
+  const void* f = reinterpret_cast<const void*>(&gf_gemm_fp4sk_kernel<MG, UNI, COPY, R, KS, ABL>);
   const size_t lds = size_t(MG) * KS * 2 * 1024 + 2304 + (COPY ? 2048 : 0) + ring_lds(R);
   if (lds > 160 * 1024) return hipErrorInvalidConfiguration;
   hipError_t e = ensure_lds_optin(f);
@@ -1159,7 +1172,7 @@ hipError_t launch_fp4sk(const Fp4Geometry& geo, const Fp4Args& a, hipStream_t st
   int64_t slots = std::max<int64_t>(8, (int64_t(device_cu_count()) * occ / geo.groups) / 8 * 8);
   slots = std::min<int64_t>(slots, (a.nchunks + 7) / 8 * 8);
   const unsigned blocks = unsigned(slots * geo.groups);
-  gf_gemm_fp4sk_kernel<MG, UNI, COPY, R, KS><<<blocks, 256, lds, stream>>>(
+  gf_gemm_fp4sk_kernel<MG, UNI, COPY, R, KS, ABL><<<blocks, 256, lds, stream>>>(
       a.in, a.out, a.copy, static_cast<const i32x4*>(a.bitmat), a.k, a.m, geo.groups, a.col0, a.nchunks, slots,
       a.in_stride);
   return hipGetLastError();
@@ -1169,6 +1182,20 @@ template <int MG, bool UNI, bool COPY>
 hipError_t launch_fp4sk_ring(const Fp4Geometry& geo, const Fp4Args& a, hipStream_t stream) {
   const size_t base = size_t(MG) * 16 * 1024 + 2304 + (COPY ? 2048 : 0);
   if (base + ring_lds(8) + kSideReserve <= 160 * 1024) return launch_fp4sk<MG, UNI, COPY, 8>(geo, a, stream);
+  if constexpr (MG == 8 && UNI && !COPY) {  // ablation builds (measurements only, see the kernel)
+    static const int abl = [] {
+      const char* env = std::getenv("GFRS_FP4_ABL");
+      return env ? std::atoi(env) : 0;
+    }();
+    switch (abl) {
+      case 1: return launch_fp4sk<MG, UNI, COPY, 4, 1>(geo, a, stream);
+      case 2: return launch_fp4sk<MG, UNI, COPY, 4, 2>(geo, a, stream);
+      case 3: return launch_fp4sk<MG, UNI, COPY, 4, 3>(geo, a, stream);
+      case 4: return launch_fp4sk<MG, UNI, COPY, 4, 4>(geo, a, stream);
+      case 7: return launch_fp4sk<MG, UNI, COPY, 4, 7>(geo, a, stream);
+      default: break;
+    }
+  }
   return launch_fp4sk<MG, UNI, COPY, 4>(geo, a, stream);
 }
 
@@ -1187,6 +1214,21 @@ bool use_sk(const Fp4Geometry& geo, bool copies) {
   if (env && std::strcmp(env, "sk") == 0) copies = false;  // (force it for the fused-copy form too)
   // measured (profiles/r02_fp4): 6 % faster than v1 for plain GEMMs, 1 % slower with fused copies
   return !copies && geo.ksteps == 16 && (geo.mg == 4 || geo.mg == 8);
+}
+
+// The A-resident kernel (gf_mfma_fp4ar.hip; k in (112, 128], all M-tiles in one group) where it
+// measured faster (profiles/r02_fp4_ablate, k=128, 1 GiB, medians of alternating runs): plain
+// GEMMs with 6 or 8 M-tiles (two row halves of 3 / 4, no padding tile: m=24 670 vs 714 us, m=32
+// 809 vs 842 — the p=32 encode) and 4 M-tiles with or without fused copies (one wave per column
+// group: m=16 490 vs 530 us plain, 659 vs 722 with 112 copies). It loses with padding tiles
+// (5, 7 M-tiles), at 1-3 M-tiles (memory-bound shapes), and with fused copies at two row halves
+// (1060-1360 vs 760-970 us). GFRS_FP4_KERNEL=ar forces it wherever supported; =sk / =v1 never.
+bool use_ar(const Fp4Geometry& geo, int k, bool copies) {
+  if (geo.groups != 1 || !fp4ar_supported(k, geo.mg)) return false;
+  const char* env = std::getenv("GFRS_FP4_KERNEL");
+  if (env && std::strcmp(env, "ar") == 0) return true;
+  if (env && (std::strcmp(env, "sk") == 0 || std::strcmp(env, "v1") == 0)) return false;
+  return geo.mg == 4 || (!copies && (geo.mg == 6 || geo.mg == 8));
 }
 
 }  // namespace
@@ -1219,6 +1261,24 @@ hipError_t launch_gf_gemm_fp4(const void* bitmat, const void* desc, int k, int m
   const char* b = static_cast<const char*>(desc);
   const Fp4Geometry geo = geometry(k, m, mg_cap, copies);
   // split copy (GFRS_FP4_COPY=split, measured and not the default: split_copy_mode)
+  if (use_ar(geo, k, copies) && !(copies && split_copy_mode())) {  // the A-resident form (gf_mfma_fp4ar.hip)
+    Fp4ArLaunch a{};
+    a.in = reinterpret_cast<const uint64_t*>(b + l.in_off);
+    a.out = reinterpret_cast<const uint64_t*>(b + l.out_off);
+    a.copy = copies ? reinterpret_cast<const uint64_t*>(b + l.copy_off) : nullptr;
+    a.bitmat = bitmat;
+    a.k = k;
+    a.m = m;
+    a.mg = geo.mg;
+    a.col0 = col0;
+    a.ncols = ncols;
+    a.in_stride = copies ? 0 : in_stride;
+    int64_t done = 0;
+    const hipError_t e = launch_gf_gemm_fp4ar(a, &done, stream);
+    if (e != hipSuccess) return e;
+    if (done < ncols) return launch_gf_gemm(desc, k, m_pad, col0 + done, ncols - done, false, 0, stream);
+    return hipSuccess;
+  }
   const int split = copies && use_sk(geo, false) ? split_copy_mode() : 0;
   const bool fused = copies && !split;
   const bool sk = use_sk(geo, fused);

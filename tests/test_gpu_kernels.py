@@ -357,7 +357,7 @@ def test_fp4_staggered_kernel_matches_v1_and_oracle(k, m, variant, monkeypatch):
         cdst = alloc_rows(k, ncols, "cuda", fill=0x44)
         copies = [cdst[j] if j % 4 else None for j in range(k)]
     results = []
-    for kernel in ("sk", "v1") + (("split",) if variant == "copy" else ()):
+    for kernel in ("sk", "v1", "ar") + (("split",) if variant == "copy" else ()):
         if kernel == "split":  # the plain kernel + the side-stream copy kernel (GFRS_FP4_COPY=split)
             monkeypatch.delenv("GFRS_FP4_KERNEL", raising=False)
             monkeypatch.setenv("GFRS_FP4_COPY", "split")
@@ -377,3 +377,37 @@ def test_fp4_staggered_kernel_matches_v1_and_oracle(k, m, variant, monkeypatch):
                 assert np.array_equal(c[j], want_in[j] if j % 4 else np.full(ncols, 0x44, np.uint8)), (kernel, j)
         results.append(got)
     assert all(np.array_equal(results[0], r) for r in results[1:])
+
+
+@pytest.mark.parametrize("k,m", [(128, 32), (128, 28), (128, 20), (127, 13), (120, 8), (113, 4), (128, 1)])
+@pytest.mark.parametrize("variant", ["uniform", "scattered", "copy"])
+def test_fp4_a_resident_kernel_matches_oracle(k, m, variant, monkeypatch):
+    """The A-resident FP4 kernel (gf_gemm_fp4ar_kernel: A in AGPRs, accumulators in VGPRs, bias as
+    the first MFMA's C operand) for every tile split it instantiates — 1..4 M-tiles per wave and one
+    wave per column group, or two row halves (3 or 4 tiles each, padding tiles reading zero A) —
+    with uniform / scattered / fused-copy inputs, several chunks per persistent block and a v_perm
+    remainder: bit-exact against the oracle, copies included."""
+    _native_loaded()
+    ncols = 128 * (256 * 5 + 3) + 45
+    rng = np.random.default_rng(k * 7 + m)
+    coeff = rng.integers(0, 256, size=(m, k), dtype=np.uint8)
+    host, dev = _rand_rows(k, ncols, k * 3 + m)
+    inputs, want_in = dev, host
+    copies = None
+    if variant in ("scattered", "copy"):
+        perm = rng.permutation(k)
+        inputs = [dev[j].clone() for j in perm]
+        want_in = host[perm]
+    if variant == "copy":
+        cdst = alloc_rows(k, ncols, "cuda", fill=0x44)
+        copies = [cdst[j] if j % 3 else None for j in range(k)]
+    monkeypatch.setenv("GFRS_FP4_KERNEL", "ar")
+    out = alloc_rows(m, ncols, "cuda", fill=0x5A)
+    plan = GemmPlan(inputs, out, coeff, copies=copies, engine="mfma")
+    plan.run()
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), GF256.gemm(coeff, want_in))
+    if copies is not None:
+        c = cdst.cpu().numpy()
+        for j in range(k):
+            assert np.array_equal(c[j], want_in[j] if j % 3 else np.full(ncols, 0x44, np.uint8)), j
