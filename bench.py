@@ -485,7 +485,8 @@ def main(argv=None) -> int:
         else:
             elapsed = timed_loop(work, xchg, steps, world, dev, f"timed/{mode}")
         ok = xchg.verify((steps - 1) % slots)
-        results[mode] = dict(elapsed=elapsed, steps=steps, ok=ok, sent=xchg.bytes_sent, recv=xchg.bytes_received)
+        results[mode] = dict(elapsed=elapsed, steps=steps, ok=ok, sent=xchg.bytes_sent, recv=xchg.bytes_received,
+                             link=xchg.bytes_per_link)
         verified = verified and ok
         del xchg
 
@@ -537,9 +538,14 @@ def main(argv=None) -> int:
         "baseline": {"gbps": round(BASELINE_GBPS, 4), "source": "k=8,n=11 1.1 GB Tesla C2050 (nearest published)"},
     }
     if world > 1:
+        # busiest xGMI link: bytes it carries per step, and the rate the measured step implies for
+        # it (a lower bound on what the link sustained; when the step is link-bound, its rate)
         rec["value_by_comm"] = {m: {"GBps": round(gbps(r), 3), "ms_per_step": round(r["elapsed"] / r["steps"] * 1e3, 4),
                                     "steps": r["steps"], "bytes_sent_per_rank_step": r["sent"],
-                                    "bytes_recv_rank0_step": r["recv"] if rank == 0 else None, "verified": r["ok"]}
+                                    "bytes_recv_rank0_step": r["recv"] if rank == 0 else None,
+                                    "busiest_link_bytes_per_step": r["link"],
+                                    "busiest_link_GBps_implied": round(r["link"] / (r["elapsed"] / r["steps"]) / 1e9, 2),
+                                    "verified": r["ok"]}
                                 for m, r in results.items()}
         if "none" in results:
             rec["value_no_comm"] = round(gbps(results["none"]), 3)

@@ -95,6 +95,17 @@ class ParityExchange:
             return self.nbytes * (self.world - 1) if self.rank == self.root else 0
         return 0
 
+    @property
+    def bytes_per_link(self) -> int:
+        """Bytes the busiest point-to-point link carries per step (one direction): owners — one
+        rank's piece (every ordered pair of ranks exchanges one piece over its direct xGMI link);
+        root — a whole block into the root."""
+        if self.mode == "owners":
+            return max(self.in_splits)
+        if self.mode == "root":
+            return self.nbytes
+        return 0
+
     # ---- per-step ------------------------------------------------------------------------------
     def start(self, slot: int) -> None:
         """Launch the exchange of ``sources[slot]`` asynchronously (ordered after the work queued so

@@ -40,6 +40,9 @@ def test_launcher_runs_world_ranks_and_reports_every_comm_mode(gpus):
     assert par_bytes > 0 and by["none"]["bytes_sent_per_rank_step"] == 0
     assert by["root"]["bytes_recv_rank0_step"] > par_bytes  # rank 0 takes whole blocks from every peer
     assert rec["value"] == by["owners"]["GBps"] and rec["value_no_comm"] == by["none"]["GBps"]
+    # busiest link: one piece per ordered pair (owners) vs a whole block into rank 0 (root)
+    assert by["root"]["busiest_link_bytes_per_step"] > by["owners"]["busiest_link_bytes_per_step"] > 0
+    assert by["none"]["busiest_link_bytes_per_step"] == 0 and by["owners"]["busiest_link_GBps_implied"] > 0
 
 
 def test_single_rank_record_and_comm_choice():
