@@ -25,6 +25,11 @@ def main():
     res = {"env": {x: os.environ.get(x) for x in ("GFRS_FP4_EXACT_MG", "GFRS_FP4_KERNEL", "GFRS_FP4_COPY")}}
     rng = np.random.default_rng(5)
     ms = [int(x) for x in sys.argv[1].split(",")] if len(sys.argv) > 1 else [20, 24, 28, 32]
+    if "--scattered" in sys.argv:  # inputs as separate allocations (the row-pointer-table kernels)
+        rows = [data[j].clone() for j in range(k)]
+        del data
+        torch.cuda.empty_cache()
+        data = rows
     for m in ms:
         coeff = rng.integers(1, 256, size=(m, k), dtype=np.uint8)
         out = alloc_rows(m, C, "cuda")
@@ -42,9 +47,10 @@ def main():
                 torch.cuda.synchronize()
                 ts.append(s.elapsed_time(e) * 1e3)
             cols = 1 << 16
-            ok = np.array_equal(out[:, :cols].cpu().numpy(), gf.GF256.gemm(coeff, data[:, :cols].cpu().numpy()))
+            src = torch.stack([r[:cols] for r in data]) if isinstance(data, list) else data[:, :cols]
+            ok = np.array_equal(out[:, :cols].cpu().numpy(), gf.GF256.gemm(coeff, src.cpu().numpy()))
             if ncopy:
-                ok = ok and torch.equal(dst[:ncopy], data[:ncopy])
+                ok = ok and all(torch.equal(dst[j], data[j]) for j in range(ncopy))
             res[f"m{m}_copies{ncopy}"] = {"median_us": round(float(np.median(ts)), 1), "min_us": round(min(ts), 1),
                                           "ok": bool(ok)}
     print(json.dumps(res), flush=True)
