@@ -379,7 +379,7 @@ def test_fp4_staggered_kernel_matches_v1_and_oracle(k, m, variant, monkeypatch):
     assert all(np.array_equal(results[0], r) for r in results[1:])
 
 
-@pytest.mark.parametrize("k,m", [(128, 32), (128, 28), (128, 20), (127, 13), (120, 8), (113, 4), (128, 1)])
+@pytest.mark.parametrize("k,m", [(128, 32), (128, 28), (128, 24), (128, 20), (127, 13), (120, 8), (113, 4), (128, 1)])
 @pytest.mark.parametrize("variant", ["uniform", "scattered", "copy"])
 def test_fp4_a_resident_kernel_matches_oracle(k, m, variant, monkeypatch):
     """The A-resident FP4 kernel (gf_gemm_fp4ar_kernel: A in AGPRs, accumulators in VGPRs, bias as
