@@ -90,3 +90,40 @@ def test_torchrun_dist_cli_windows_world3_and_stale_outputs(tmp_path, gather):
                        text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     assert (d1 / "o.bin").read_bytes() == payload
+
+
+def test_torchrun_dist_cli_bounded_host_memory(tmp_path):
+    """The distributed CLI streams a file much larger than its window without holding it: the peak
+    RSS of any rank stays within a fixed margin of a bare `import torch, gpu_rscode_amd` process
+    (a whole-file read on rank 0 would add the file size, 256 MiB, to it)."""
+    import resource
+
+    size = 256 << 20
+    with open(tmp_path / "f.bin", "wb") as f:
+        block = os.urandom(1 << 20)
+        for i in range(size >> 20):
+            f.write(block[i:] + block[:i])
+    env = dict(os.environ, PYTHONPATH=ROOT, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    r = subprocess.run([sys.executable, "-c", "import torch, gpu_rscode_amd, gpu_rscode_amd._native as n; n.cpu()"],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr
+    base_kib = resource.getrusage(resource.RUSAGE_CHILDREN).ru_maxrss
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_port()}", "-m", "gpu_rscode_amd", "--dist", "--gather", "rccl",
+           "--window", str(4 << 20)]
+    r = subprocess.run(cmd + ["-k", "4", "-n", "6", "-e", "f.bin"], cwd=tmp_path, capture_output=True, text=True,
+                       timeout=600, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    ff.write_conf(str(tmp_path / "conf"), ["_0_f.bin", "_2_f.bin", "_4_f.bin", "_5_f.bin"])
+    cmd[6] = f"--master-port={_port()}"
+    r = subprocess.run(cmd + ["-d", "-i", "f.bin", "-c", "conf", "-o", "o.bin"], cwd=tmp_path, capture_output=True,
+                       text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    peak_kib = resource.getrusage(resource.RUSAGE_CHILDREN).ru_maxrss
+    with open(tmp_path / "f.bin", "rb") as a, open(tmp_path / "o.bin", "rb") as b:
+        while True:
+            x, y = a.read(1 << 24), b.read(1 << 24)
+            assert x == y
+            if not x:
+                break
+    assert peak_kib - base_kib < 160 * 1024, (base_kib, peak_kib)
