@@ -57,3 +57,18 @@ def test_single_rank_record_and_comm_choice():
 def test_world_size_mismatch_is_an_error():
     r = _run(["--device", "cpu", "--gpus", "3", "--steps", "1"], env={"WORLD_SIZE": "2", "RANK": "0"})
     assert r.returncode == 2 and "WORLD_SIZE=2" in r.stderr
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("preset,erased", [("k10n14", 4), ("k128n160", 32)])
+def test_gpu_bench_record_with_worst_case_e2e_decode(preset, erased):
+    """One rank on the MI355X, 64 MiB: the device step verifies, and the e2e block's decode rebuilds
+    the first `erasures` natives (src/unit-test.sh keeps the last k chunks) through the host pipeline."""
+    r = _run(["--preset", preset, "--steps", "3", "--warmup", "1", "--bytes", str(64 << 20)], timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = _record(r.stdout)
+    assert rec["verified"] is True and rec["n_gpus"] == 1 and rec["config"]["device"] == "cuda"
+    assert rec["config"]["engine"] == ("mfma" if preset == "k128n160" else "valu")
+    e2e = rec["e2e"]
+    assert e2e["verified"] is True and e2e["erased"] == erased
+    assert e2e["encode_GBps"] > 0 and e2e["decode_GBps"] > 0
