@@ -30,6 +30,12 @@ def build(target: str = "all", jobs: int | None = None, quiet: bool = True) -> N
         print(res.stdout)
 
 
+def have_sources() -> bool:
+    """False for an installed copy of the package (``pip install``): no ``csrc/`` next to it, the
+    modules were built at install time and are used as they are."""
+    return (CSRC / "Makefile").exists()
+
+
 SOURCE_SUFFIXES = (".hip", ".cpp", ".h", ".hpp")
 
 

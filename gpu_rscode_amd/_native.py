@@ -21,7 +21,7 @@ def _load(name: str, target: str):
     if name in _mods:
         return _mods[name]
     so = _build.artifact(f"_{name}.so")
-    if os.environ.get("GPURS_NO_BUILD") != "1":
+    if os.environ.get("GPURS_NO_BUILD") != "1" and _build.have_sources():
         # incremental: a no-op when the .so is newer than every source
         try:
             _build.build(target)
