@@ -16,6 +16,6 @@ from . import gf
 from .gf import GF, SingularMatrixError
 from .models import ReedSolomon, UnrecoverableError, alloc_rows
 
-__version__ = "0.1.0"
+__version__ = "0.2.0"
 
 __all__ = ["gf", "GF", "SingularMatrixError", "ReedSolomon", "UnrecoverableError", "alloc_rows", "__version__"]
