@@ -3,16 +3,29 @@
 so it never tries to rebuild — plus the `gpu-rscode` entry point and the bin/RS, bin/CPU-RS CLIs
 (the reference installs its RS binary with autotools `make install`)."""
 import os
+import shutil
 import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+def _source_copy(dst):
+    """The installable part of the tree, mtimes kept (copy2) so `make` finds everything up to date and
+    pip's in-tree build files (build/lib, *.egg-info) land in the copy, not in the repository."""
+    ignore = shutil.ignore_patterns("__pycache__", "*.egg-info")
+    for d in ("csrc", "gpu_rscode_amd", "bin", os.path.join("build", "obj")):
+        if os.path.isdir(os.path.join(ROOT, d)):
+            shutil.copytree(os.path.join(ROOT, d), os.path.join(dst, d), ignore=ignore, copy_function=shutil.copy2)
+    for f in ("setup.py", "pyproject.toml", "README.md"):
+        shutil.copy2(os.path.join(ROOT, f), os.path.join(dst, f))
+
+
 def test_pip_install_outside_the_tree(tmp_path):
-    target = tmp_path / "site"
+    src, target = tmp_path / "src", tmp_path / "site"
+    _source_copy(str(src))
     r = subprocess.run([sys.executable, "-m", "pip", "install", "--no-build-isolation", "--no-deps", "--no-index",
-                        "--target", str(target), ROOT], capture_output=True, text=True, timeout=850)
+                        "--target", str(target), str(src)], capture_output=True, text=True, timeout=850)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert (target / "gpu_rscode_amd" / "_cpu.so").exists() and (target / "gpu_rscode_amd" / "_hip.so").exists()
     assert (target / "bin" / "RS").exists() and (target / "bin" / "CPU-RS").exists()
