@@ -20,7 +20,7 @@ struct Args {
   int streams = 1;  // -s
   std::string in_file, conf, out;
   std::string matrix = "vandermonde";
-  std::string mul = "row";
+  std::string mul = "simd";
   int gpus = 0;  // 0 = all visible
   std::vector<int> devices;  // --devices 0,1,...: explicit shard -> device list (entries may repeat)
   int threads = 1;
@@ -62,7 +62,7 @@ inline void usage(const char* prog, bool gpu) {
     std::printf("  --devices I,J,...       explicit column-shard -> device list (a device may repeat)\n");
     std::printf("  --slice BYTES           column slice per stream step (default 16 MiB)\n");
   } else {
-    std::printf("  --mul logexp|logexp0|logexp1|logexp2|logexp3|loop|full|double|perm|row\n");
+    std::printf("  --mul logexp|logexp0|logexp1|logexp2|logexp3|loop|full|double|perm|row|simd\n");
     std::printf("  --threads T             worker threads (default 1, the reference's single thread)\n");
   }
   (void)prog;

@@ -1,6 +1,8 @@
 // CPU GF(2^8) GEMM with the reference's multiply strategies (see gfrs/cpu_codec.h).
 #include "gfrs/cpu_codec.h"
 
+#include <immintrin.h>
+
 #include <algorithm>
 #include <array>
 #include <cstring>
@@ -59,6 +61,35 @@ inline uint8_t m_zeroband(uint8_t a, uint8_t b) { return kTables.exp[kTables.log
 inline uint8_t m_full(uint8_t a, uint8_t b) { return tables().full[a][b]; }
 inline uint8_t m_nibble(uint8_t a, uint8_t b) { return tables().nib_hi[a >> 4][b] ^ tables().nib_lo[a & 15][b]; }
 
+// out ^= c * in, 32 bytes per step: c * x = lo[x & 15] ^ hi[x >> 4] (GF multiply is linear over
+// GF(2), so the two nibbles multiply separately), each 16-entry table one pshufb.
+__attribute__((target("avx2"))) void axpy_avx2(uint8_t c, const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
+                                               int64_t n) {
+  const uint8_t* row = tables().full[c];
+  alignas(16) uint8_t lo[16], hi[16];
+  for (int x = 0; x < 16; ++x) {
+    lo[x] = row[x];
+    hi[x] = row[x << 4];
+  }
+  const __m256i tl = _mm256_broadcastsi128_si256(_mm_load_si128(reinterpret_cast<const __m128i*>(lo)));
+  const __m256i th = _mm256_broadcastsi128_si256(_mm_load_si128(reinterpret_cast<const __m128i*>(hi)));
+  const __m256i mask = _mm256_set1_epi8(0x0f);
+  int64_t x = 0;
+  for (; x + 32 <= n; x += 32) {
+    const __m256i v = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(in + x));
+    const __m256i l = _mm256_shuffle_epi8(tl, _mm256_and_si256(v, mask));
+    const __m256i h = _mm256_shuffle_epi8(th, _mm256_and_si256(_mm256_srli_epi16(v, 4), mask));
+    const __m256i o = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(out + x));
+    _mm256_storeu_si256(reinterpret_cast<__m256i*>(out + x), _mm256_xor_si256(o, _mm256_xor_si256(l, h)));
+  }
+  for (; x < n; ++x) out[x] ^= row[in[x]];
+}
+
+bool host_has_avx2() {
+  static const bool has = __builtin_cpu_supports("avx2");
+  return has;
+}
+
 // Per-row kernel for one coefficient c over bytes [0, n): out ^= c * in.
 template <CpuMul S>
 void axpy(uint8_t c, const uint8_t* __restrict__ in, uint8_t* __restrict__ out, int64_t n) {
@@ -67,7 +98,11 @@ void axpy(uint8_t c, const uint8_t* __restrict__ in, uint8_t* __restrict__ out, 
     for (int64_t x = 0; x < n; ++x) out[x] ^= in[x];
     return;
   }
-  if constexpr (S == CpuMul::kRow || S == CpuMul::kFull) {
+  if constexpr (S == CpuMul::kSimd) {
+    if (host_has_avx2()) return axpy_avx2(c, in, out, n);
+    const uint8_t* row = tables().full[c];
+    for (int64_t x = 0; x < n; ++x) out[x] ^= row[in[x]];
+  } else if constexpr (S == CpuMul::kRow || S == CpuMul::kFull) {
     const uint8_t* row = tables().full[c];
     for (int64_t x = 0; x < n; ++x) out[x] ^= row[in[x]];
   } else if constexpr (S == CpuMul::kPerm) {
@@ -113,16 +148,16 @@ void gemm_threads(const std::vector<const uint8_t*>& in, const std::vector<uint8
 }  // namespace
 
 CpuMul parse_cpu_mul(const std::string& s) {
-  static const std::array<const char*, 10> names = {"logexp", "logexp0", "logexp1", "logexp2", "logexp3",
-                                                    "loop",   "full",    "double",  "perm",    "row"};
+  static const std::array<const char*, 11> names = {"logexp", "logexp0", "logexp1", "logexp2", "logexp3", "loop",
+                                                    "full",   "double",  "perm",    "row",     "simd"};
   for (size_t i = 0; i < names.size(); ++i)
     if (s == names[i]) return CpuMul(i);
   throw std::invalid_argument("unknown CPU multiply strategy: " + s);
 }
 
 const char* cpu_mul_name(CpuMul m) {
-  static const char* names[] = {"logexp", "logexp0", "logexp1", "logexp2", "logexp3",
-                                "loop",   "full",    "double",  "perm",    "row"};
+  static const char* names[] = {"logexp", "logexp0", "logexp1", "logexp2", "logexp3", "loop",
+                                "full",   "double",  "perm",    "row",     "simd"};
   return names[int(m)];
 }
 
@@ -138,6 +173,7 @@ uint8_t cpu_mul(CpuMul s, uint8_t a, uint8_t b) {
     case CpuMul::kNibble: return m_nibble(a, b);
     case CpuMul::kPerm: return perm_apply(perm_for_coeff(b), a);
     case CpuMul::kRow: return m_full(a, b);
+    case CpuMul::kSimd: return m_nibble(a, b);
   }
   return 0;
 }
@@ -158,6 +194,7 @@ void cpu_gemm(const std::vector<const uint8_t*>& in, const std::vector<uint8_t*>
     case CpuMul::kNibble: return gemm_threads<CpuMul::kNibble>(in, out, coeff, ncols, threads);
     case CpuMul::kPerm: return gemm_threads<CpuMul::kPerm>(in, out, coeff, ncols, threads);
     case CpuMul::kRow: return gemm_threads<CpuMul::kRow>(in, out, coeff, ncols, threads);
+    case CpuMul::kSimd: return gemm_threads<CpuMul::kSimd>(in, out, coeff, ncols, threads);
   }
 }
 

@@ -14,7 +14,10 @@
 //   kFull          cpu-rs-full.c      64 KiB gfmul[256][256] table
 //   kNibble        cpu-rs-double.c    L[a>>4][b] ^ R[a&15][b] nibble-split tables
 //   kPerm          (new)              host emulation of the gfx950 v_perm 3-chunk tables
-//   kRow           (new, default)     one 256-byte product row per coefficient, multi-threaded
+//   kRow           (new)              one 256-byte product row per coefficient, multi-threaded
+//   kSimd          (new, default)     cpu-rs-double.c's nibble split, vectorised: the two 16-entry
+//                                     tables of a coefficient in one register each, 32 bytes per
+//                                     pshufb pair (AVX2; kRow where the host lacks it)
 #pragma once
 
 #include <cstdint>
@@ -36,6 +39,7 @@ enum class CpuMul : int {
   kNibble,
   kPerm,
   kRow,
+  kSimd,
 };
 
 CpuMul parse_cpu_mul(const std::string& s);
@@ -43,7 +47,7 @@ const char* cpu_mul_name(CpuMul m);
 
 // out_rows[i][c] = XOR_j coeff[i][j] * in_rows[j][c], c in [0, ncols). threads <= 0: hardware.
 void cpu_gemm(const std::vector<const uint8_t*>& in_rows, const std::vector<uint8_t*>& out_rows, const Mat& coeff,
-              int64_t ncols, CpuMul strategy = CpuMul::kRow, int threads = 1);
+              int64_t ncols, CpuMul strategy = CpuMul::kSimd, int threads = 1);
 
 // Scalar multiply through a given strategy (exposed for the per-strategy unit tests).
 uint8_t cpu_mul(CpuMul strategy, uint8_t a, uint8_t b);

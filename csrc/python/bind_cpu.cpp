@@ -31,7 +31,7 @@ PYBIND11_MODULE(_cpu, m) {
         py::gil_scoped_release nogil;
         cpu_gemm(ip, op, c, ncols, s, threads);
       },
-      py::arg("in_ptrs"), py::arg("out_ptrs"), py::arg("coeff"), py::arg("ncols"), py::arg("strategy") = "row",
+      py::arg("in_ptrs"), py::arg("out_ptrs"), py::arg("coeff"), py::arg("ncols"), py::arg("strategy") = "simd",
       py::arg("threads") = 1);
 
   auto gemm_fn = [](const std::string& strategy, int threads) -> GemmFn {
@@ -52,7 +52,7 @@ PYBIND11_MODULE(_cpu, m) {
         return report(r);
       },
       py::arg("file"), py::arg("k"), py::arg("p"), py::arg("matrix") = "vandermonde", py::arg("cpu_meta") = false,
-      py::arg("strategy") = "row", py::arg("threads") = 1);
+      py::arg("strategy") = "simd", py::arg("threads") = 1);
   m.def(
       "decode_file",
       [gemm_fn](const std::string& file, const std::string& conf, const std::string& out, const std::string& strategy,
@@ -65,7 +65,7 @@ PYBIND11_MODULE(_cpu, m) {
         }
         return report(r);
       },
-      py::arg("file"), py::arg("conf"), py::arg("out") = "", py::arg("strategy") = "row", py::arg("threads") = 1);
+      py::arg("file"), py::arg("conf"), py::arg("out") = "", py::arg("strategy") = "simd", py::arg("threads") = 1);
 
   m.def(
       "encode_file_stream",
@@ -81,7 +81,7 @@ PYBIND11_MODULE(_cpu, m) {
         return stream_report(r);
       },
       py::arg("file"), py::arg("k"), py::arg("p"), py::arg("matrix") = "vandermonde", py::arg("cpu_meta") = false,
-      py::arg("strategy") = "row", py::arg("threads") = 1, py::arg("window") = 0, py::arg("resume") = true,
+      py::arg("strategy") = "simd", py::arg("threads") = 1, py::arg("window") = 0, py::arg("resume") = true,
       py::arg("durable") = true, py::arg("stop_after") = -1);
   m.def(
       "decode_file_stream",
@@ -96,7 +96,7 @@ PYBIND11_MODULE(_cpu, m) {
         }
         return stream_report(r);
       },
-      py::arg("file"), py::arg("conf"), py::arg("out") = "", py::arg("strategy") = "row", py::arg("threads") = 1,
+      py::arg("file"), py::arg("conf"), py::arg("out") = "", py::arg("strategy") = "simd", py::arg("threads") = 1,
       py::arg("window") = 0, py::arg("resume") = true, py::arg("durable") = true, py::arg("stop_after") = -1);
   m.def("progress_path", &progress_path);
 

@@ -52,7 +52,7 @@ class ReedSolomon:
     """
 
     def __init__(self, k: int, n: int, matrix: str = "vandermonde", field: str = "gf256",
-                 cpu_strategy: str = "row", cpu_threads: int = 1):
+                 cpu_strategy: str = "simd", cpu_threads: int = 1):
         if not (1 <= k <= n):
             raise ValueError("need 1 <= k <= n")
         self.k, self.n, self.p = k, n, n - k

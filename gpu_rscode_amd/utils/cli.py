@@ -39,7 +39,7 @@ def _parser() -> argparse.ArgumentParser:
     ap.add_argument("--gpus", type=int, default=0, help="GPUs for the single-process pipeline (0 = all)")
     ap.add_argument("--slice", type=int, default=16 << 20)
     ap.add_argument("--threads", type=int, default=1, help="CPU backend threads")
-    ap.add_argument("--mul", default="row", help="CPU multiply strategy")
+    ap.add_argument("--mul", default="simd", help="CPU multiply strategy (row: the scalar product-row form)")
     ap.add_argument("--dist", action="store_true", help="torch.distributed multi-GPU mode (torchrun)")
     ap.add_argument("--gather", choices=["rccl", "none"], default="rccl")
     ap.add_argument("--window", type=int, default=None,

@@ -22,7 +22,7 @@ from gpu_rscode_amd.ops.gemm import build_desc, desc_layout, pad_m, perm_tables_
 from gpu_rscode_amd.utils import fileformat as ff
 
 FIX = os.path.join(os.path.dirname(__file__), "fixtures", "golden_parity.json")
-STRATEGIES = ["logexp", "logexp0", "logexp1", "logexp2", "logexp3", "loop", "full", "double", "perm", "row"]
+STRATEGIES = ["logexp", "logexp0", "logexp1", "logexp2", "logexp3", "loop", "full", "double", "perm", "row", "simd"]
 
 
 def golden_input(n: int) -> bytes:
