@@ -85,6 +85,58 @@ __attribute__((target("avx2"))) void axpy_avx2(uint8_t c, const uint8_t* __restr
   for (; x < n; ++x) out[x] ^= row[in[x]];
 }
 
+// Register-blocked form for the whole GEMM over columns [a, b): groups of up to 4 output rows stay
+// in ymm accumulators while every input row's 32 bytes are loaded once per group, split into
+// nibbles once, and hit with each coefficient's two table shuffles (the tables sit in L1).
+__attribute__((target("avx2"))) void gemm_avx2(const std::vector<const uint8_t*>& in, const std::vector<uint8_t*>& out,
+                                               const Mat& coeff, int64_t a, int64_t b) {
+  const int k = int(in.size()), m = int(out.size());
+  struct alignas(32) Y {
+    __m256i v;
+  };
+  std::vector<Y> tl(size_t(m) * k), th(size_t(m) * k);  // (C++17 aligned new: 32-byte elements)
+  for (int i = 0; i < m; ++i)
+    for (int j = 0; j < k; ++j) {
+      const uint8_t* row = tables().full[coeff[size_t(i) * k + j]];
+      alignas(16) uint8_t lo[16], hi[16];
+      for (int x = 0; x < 16; ++x) {
+        lo[x] = row[x];
+        hi[x] = row[x << 4];
+      }
+      tl[size_t(i) * k + j].v = _mm256_broadcastsi128_si256(_mm_load_si128(reinterpret_cast<const __m128i*>(lo)));
+      th[size_t(i) * k + j].v = _mm256_broadcastsi128_si256(_mm_load_si128(reinterpret_cast<const __m128i*>(hi)));
+    }
+  const __m256i mask = _mm256_set1_epi8(0x0f);
+  const int64_t vend = a + (b - a) / 32 * 32;
+  constexpr int64_t kTile = 16 << 10;  // column tile: the k input slices stay in L2 across row groups
+  for (int64_t t0 = a; t0 < vend; t0 += kTile)
+  for (int i0 = 0; i0 < m; i0 += 4) {
+    const int g = std::min(4, m - i0);
+    for (int64_t x = t0; x < std::min(vend, t0 + kTile); x += 32) {
+      __m256i acc[4] = {_mm256_setzero_si256(), _mm256_setzero_si256(), _mm256_setzero_si256(),
+                        _mm256_setzero_si256()};
+      for (int j = 0; j < k; ++j) {
+        const __m256i v = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(in[j] + x));
+        const __m256i l = _mm256_and_si256(v, mask);
+        const __m256i h = _mm256_and_si256(_mm256_srli_epi16(v, 4), mask);
+        for (int t = 0; t < g; ++t) {
+          const size_t c = size_t(i0 + t) * k + j;
+          acc[t] = _mm256_xor_si256(acc[t], _mm256_xor_si256(_mm256_shuffle_epi8(tl[c].v, l), _mm256_shuffle_epi8(th[c].v, h)));
+        }
+      }
+      for (int t = 0; t < g; ++t) _mm256_storeu_si256(reinterpret_cast<__m256i*>(out[i0 + t] + x), acc[t]);
+    }
+  }
+  for (int i = 0; i < m && vend < b; ++i) {  // ragged tail, scalar
+    uint8_t* o = out[i];
+    for (int64_t x = vend; x < b; ++x) {
+      uint8_t r = 0;
+      for (int j = 0; j < k; ++j) r ^= tables().full[coeff[size_t(i) * k + j]][in[j][x]];
+      o[x] = r;
+    }
+  }
+}
+
 bool host_has_avx2() {
   static const bool has = __builtin_cpu_supports("avx2");
   return has;
@@ -116,6 +168,9 @@ void axpy(uint8_t c, const uint8_t* __restrict__ in, uint8_t* __restrict__ out, 
 template <CpuMul S>
 void gemm_range(const std::vector<const uint8_t*>& in, const std::vector<uint8_t*>& out, const Mat& coeff, int64_t a,
                 int64_t b) {
+  if constexpr (S == CpuMul::kSimd) {
+    if (host_has_avx2()) return gemm_avx2(in, out, coeff, a, b);
+  }
   const int k = int(in.size()), m = int(out.size());
   constexpr int64_t kTile = 32 << 10;  // keep the k input tiles + m outputs L2-resident
   for (int64_t t = a; t < b; t += kTile) {

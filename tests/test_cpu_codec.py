@@ -71,7 +71,7 @@ def test_every_strategy_matches_oracle(strategy):
 
 
 @pytest.mark.parametrize("strategy", STRATEGIES)
-@pytest.mark.parametrize("k,m,ncols", [(4, 2, 1000), (10, 4, 4099), (3, 3, 1)])
+@pytest.mark.parametrize("k,m,ncols", [(4, 2, 1000), (10, 4, 4099), (3, 3, 1), (7, 9, 16447), (1, 6, 33)])
 def test_cpu_gemm_matches_oracle(strategy, k, m, ncols):
     rng = np.random.default_rng(k * m + ncols)
     coeff = rng.integers(0, 256, size=(m, k), dtype=np.uint8)
@@ -82,14 +82,15 @@ def test_cpu_gemm_matches_oracle(strategy, k, m, ncols):
     assert np.array_equal(out, GF256.gemm(coeff, data))
 
 
-def test_cpu_gemm_multithreaded():
-    k, m, ncols = 10, 4, 3 << 20
+@pytest.mark.parametrize("strategy,m", [("row", 4), ("simd", 4), ("simd", 6)])
+def test_cpu_gemm_multithreaded(strategy, m):
+    k, ncols = 10, (3 << 20) + 13
     rng = np.random.default_rng(5)
     coeff = rng.integers(0, 256, size=(m, k), dtype=np.uint8)
     data = rng.integers(0, 256, size=(k, ncols), dtype=np.uint8)
     out = np.zeros((m, ncols), dtype=np.uint8)
     cpu().gemm([data[j].ctypes.data for j in range(k)], [out[i].ctypes.data for i in range(m)], coeff.tobytes(),
-               ncols, "row", 4)
+               ncols, strategy, 4)
     assert np.array_equal(out, GF256.gemm(coeff, data))
 
 
