@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-2 session AJ: final tree after the CPU-codec change (rebuilt _cpu.so, bin/RS): GPU suite,
 # smoke, default bench.
-O=gpurun_out/r02aj
+O=${O:-gpurun_out/r02aj}
 source "$(dirname "$0")/gpustep.sh"
 export GPURS_NO_BUILD=1
 step pytest_gpu 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread &&
