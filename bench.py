@@ -41,7 +41,7 @@ published point to k=10, n=14 is k=8, n=11 on 1.1 GB (Tesla C2050): encode 695.0
 1.2736 GB/s. Two ratios are reported, labelled:
   vs_baseline      device-resident value / 1.2736 (the driver's field: value / BASELINE number);
   e2e.vs_baseline_e2e  the like-for-like one: pinned host -> H2D -> kernel -> D2H encode and decode
-                   of the same 1 GiB stripe (-s 4 streams, every rank concurrently on its own PCIe
+                   of the same 1 GiB stripe (-s 2 streams, every rank concurrently on its own PCIe
                    link), survivors read from host memory, erased natives rebuilt to host memory.
 """
 from __future__ import annotations
@@ -90,8 +90,10 @@ def parse(argv=None):
     ap.add_argument("--no-compare", action="store_true", help="N > 1: skip timing the other --comm modes")
     ap.add_argument("--no-e2e", action="store_true", help="skip the pinned host->device->host timing")
     ap.add_argument("--e2e", action="store_true", help=argparse.SUPPRESS)  # (on by default now)
-    ap.add_argument("--streams", type=int, default=4, help="e2e: HIP streams (-s) per GPU")
-    ap.add_argument("--slice", type=int, default=32 << 20, help="e2e: column slice per stream step")
+    # e2e -s 2 / 16 MiB: profiles/r02al (52.0 GB/s against 51.2 at -s 4 / 32 MiB; -s 1 reaches 52.3 because each
+    # lane already overlaps H2D, kernel and D2H on its own copy-in + compute streams)
+    ap.add_argument("--streams", type=int, default=2, help="e2e: HIP streams (-s) per GPU")
+    ap.add_argument("--slice", type=int, default=16 << 20, help="e2e: column slice per stream step")
     ap.add_argument("--vec", type=int, default=None, help="kernel variant: 16-byte groups per lane (ablation)")
     ap.add_argument("--pf", type=int, default=2, help="kernel variant: rows in flight (with --vec)")
     ap.add_argument("--nt", action="store_true", help="kernel variant: non-temporal (with --vec)")
