@@ -155,14 +155,15 @@ def table(d: str) -> str:
             return {}
         return {(r["k"], r["p"]): r for r in json.load(open(path))["points"]}
 
-    g, c = load("gpu.json"), load("cpu.json")
+    g, c, cs = load("gpu.json"), load("cpu.json"), load("cpu_simd.json")
     mb = SIZE / 1048576
     lines = ["| n-k | k | ref GPU enc ms | e2e enc ms | dev enc ms | ref GPU dec ms | e2e dec ms | dev dec ms | "
-             "ref CPU enc ms | CPU enc ms (1 thr) | ref CPU dec ms | CPU dec ms (1 thr) | e2e enc+dec MB/s (ref) |",
-             "|---|---|---|---|---|---|---|---|---|---|---|---|---|"]
+             "ref CPU enc ms | CPU enc ms (1 thr) | ref CPU dec ms | CPU dec ms (1 thr) | CPU simd enc / dec ms (1 thr) | "
+             "e2e enc+dec MB/s (ref) |",
+             "|---|---|---|---|---|---|---|---|---|---|---|---|---|---|"]
     for p in PS:
         for i, k in enumerate(KS):
-            gr, cr = g.get((k, p), {}), c.get((k, p), {})
+            gr, cr, sr = g.get((k, p), {}), c.get((k, p), {}), cs.get((k, p), {})
 
             def f(x):
                 return "—" if x is None else (f"{x:,.1f}" if x >= 10 else f"{x:.3f}")
@@ -174,7 +175,8 @@ def table(d: str) -> str:
             lines.append(f"| {p} | {k} | {ref_e:,.2f} | {f(gr.get('e2e_enc_ms'))} | {f(gr.get('gpu_enc_ms'))} | "
                          f"{ref_d:,.2f} | {f(gr.get('e2e_dec_ms'))} | {f(gr.get('gpu_dec_ms'))} | "
                          f"{PUBLISHED[(p, 'cpu_enc')][i]:,.0f} | {f(cr.get('cpu_enc_ms'))} | "
-                         f"{PUBLISHED[(p, 'cpu_dec')][i]:,.0f} | {f(cr.get('cpu_dec_ms'))} | {mbps} |")
+                         f"{PUBLISHED[(p, 'cpu_dec')][i]:,.0f} | {f(cr.get('cpu_dec_ms'))} | "
+                         f"{f(sr.get('cpu_enc_ms'))} / {f(sr.get('cpu_dec_ms'))} | {mbps} |")
     return "\n".join(lines)
 
 
@@ -185,6 +187,7 @@ def main() -> int:
     ap.add_argument("--ks", default=",".join(map(str, KS)))
     ap.add_argument("--ps", default=",".join(map(str, PS)))
     ap.add_argument("--threads", type=int, default=1)
+    ap.add_argument("--strategy", default="row", help="CPU part: multiply strategy (row = the reference-like scalar form)")
     ap.add_argument("--table", metavar="DIR")
     a = ap.parse_args()
     if a.table:
@@ -193,7 +196,7 @@ def main() -> int:
     pts = []
     for p in map(int, a.ps.split(",")):
         for k in map(int, a.ks.split(",")):
-            r = gpu_point(k, p) if a.part == "gpu" else cpu_point(k, p, a.threads)
+            r = gpu_point(k, p) if a.part == "gpu" else cpu_point(k, p, a.threads, a.strategy)
             print(json.dumps(r), flush=True)
             pts.append(r)
     if a.out:
