@@ -109,22 +109,25 @@ __attribute__((target("avx2"))) void gemm_avx2(const std::vector<const uint8_t*>
   const __m256i mask = _mm256_set1_epi8(0x0f);
   const int64_t vend = a + (b - a) / 32 * 32;
   constexpr int64_t kTile = 16 << 10;  // column tile: the k input slices stay in L2 across row groups
-  for (int64_t t0 = a; t0 < vend; t0 += kTile)
-  for (int i0 = 0; i0 < m; i0 += 4) {
-    const int g = std::min(4, m - i0);
-    for (int64_t x = t0; x < std::min(vend, t0 + kTile); x += 32) {
-      __m256i acc[4] = {_mm256_setzero_si256(), _mm256_setzero_si256(), _mm256_setzero_si256(),
-                        _mm256_setzero_si256()};
-      for (int j = 0; j < k; ++j) {
-        const __m256i v = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(in[j] + x));
-        const __m256i l = _mm256_and_si256(v, mask);
-        const __m256i h = _mm256_and_si256(_mm256_srli_epi16(v, 4), mask);
-        for (int t = 0; t < g; ++t) {
-          const size_t c = size_t(i0 + t) * k + j;
-          acc[t] = _mm256_xor_si256(acc[t], _mm256_xor_si256(_mm256_shuffle_epi8(tl[c].v, l), _mm256_shuffle_epi8(th[c].v, h)));
+  for (int64_t t0 = a; t0 < vend; t0 += kTile) {
+    const int64_t t1 = std::min(vend, t0 + kTile);
+    for (int i0 = 0; i0 < m; i0 += 4) {
+      const int g = std::min(4, m - i0);
+      for (int64_t x = t0; x < t1; x += 32) {
+        __m256i acc[4] = {_mm256_setzero_si256(), _mm256_setzero_si256(), _mm256_setzero_si256(),
+                          _mm256_setzero_si256()};
+        for (int j = 0; j < k; ++j) {
+          const __m256i v = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(in[j] + x));
+          const __m256i l = _mm256_and_si256(v, mask);
+          const __m256i h = _mm256_and_si256(_mm256_srli_epi16(v, 4), mask);
+          for (int t = 0; t < g; ++t) {
+            const size_t c = size_t(i0 + t) * k + j;
+            const __m256i prod = _mm256_xor_si256(_mm256_shuffle_epi8(tl[c].v, l), _mm256_shuffle_epi8(th[c].v, h));
+            acc[t] = _mm256_xor_si256(acc[t], prod);
+          }
         }
+        for (int t = 0; t < g; ++t) _mm256_storeu_si256(reinterpret_cast<__m256i*>(out[i0 + t] + x), acc[t]);
       }
-      for (int t = 0; t < g; ++t) _mm256_storeu_si256(reinterpret_cast<__m256i*>(out[i0 + t] + x), acc[t]);
     }
   }
   for (int i = 0; i < m && vend < b; ++i) {  // ragged tail, scalar
