@@ -10,29 +10,41 @@ under torchrun (the driver's launch) every rank checks WORLD_SIZE == --gpus.
 
 One step on every rank:
   1. encode:  parity[4, C] = E . data[10, C]                          (gfx950 v_perm GF-GEMM)
-  2. decode:  4 erasures drawn from a pool of recoverable patterns (natives AND parity erased);
-              the decode system is solved ON DEVICE every step (LDS Gauss-Jordan on the e x (e+k)
-              systematic system [G[P, erased] | B'], on a side stream, one step ahead, beside the
-              previous step's decode GEMM), then the erased natives are rebuilt and surviving
-              natives copied in one fused pass into a fresh [10, C] output.
-  3. N > 1:   the step's parity leaves the GPU over xGMI (parallel/placement.py), asynchronously on
-              RCCL's stream while the next step computes (parity double-buffered):
-              --comm owners (default) places parity chunk-contiguously: one all_to_all in which each
-                rank sends 1/N of its parity to every peer, all 7 links of every GPU busy;
-              --comm root gathers every rank's whole parity into rank 0 (the reference's gather,
-                src/encode.cu:410-429, as grouped point-to-point: one link per peer into rank 0);
-              --comm none: no traffic.
-              The JSON carries the headline (default mode) plus the other two modes, each timed in
-              its own barrier-bracketed loop ("value_by_comm").
-Consecutive steps alternate between two lanes (--lanes 2: a stream, a parity slot and a decode
-output each), so step i+1's encode runs into the launch gap and the tail wave of step i's decode
-instead of after them; every step still encodes and decodes its whole stripe (measured: 0.663 ->
-0.657 ms at k=10, 1.569 -> 1.537 ms at k=128, profiles/r02_lanes).
+  2. decode:  4 erased chunks (natives AND parity) drawn from a pool of recoverable patterns. The
+              pattern lives in device memory: rank 0 writes it and RCCL-broadcasts it to every rank
+              (a lost node takes the same chunk index from every stripe — the reference's one shared
+              decode system, src/decode.cu:375). Each rank then checks it, solves the systematic
+              e x (e+k) decode system and writes the decode plan (row pointers + tables) ON DEVICE
+              (ops.PatternDecoder; on a side stream, one step ahead), and one fused pass rebuilds the
+              erased natives and copies the surviving ones into a fresh [10, C] output.
+Consecutive steps alternate between two lanes (--lanes 2: a stream, a parity slot, a decode output
+and a decode plan each), so step i+1's encode runs into the launch gap and the tail wave of step
+i's decode (every step still encodes and decodes its whole stripe).
 C = ceil(2^30 / 10) = 107374183 bytes (odd, as in the reference, src/encode.cu:317). Data is synthetic
-random bytes generated in HBM; the matrices are the reference Vandermonde, RCCL-broadcast from rank 0
-together with the erasure-pattern pool. Scaling is weak: every GPU encodes and decodes its own 1 GiB.
+random bytes generated in HBM; E and the pattern pool are RCCL-broadcast from rank 0 at setup.
+
+Headline (N > 1): weak scaling, --comm bcast. Every GPU encodes and decodes its own 1 GiB stripe and
+keeps its parity and decoded rows in its own HBM — exactly what the N = 1 number does — and the
+step's RCCL traffic is the pattern broadcast. The same record also carries, each timed in its own
+barrier-bracketed loop:
+  value_by_comm   per-step parity movement on top of the headline step:
+                    owners — one all_to_all placing parity chunk-contiguously (1/N of every block
+                             over every xGMI link); root — every peer's whole parity block into rank 0
+                             (the reference's gather, src/encode.cu:410-429, as grouped send/recv);
+                    none   — no per-step traffic at all (each rank draws the pattern itself)
+  value_strong    the reference's multi-GPU semantics: ONE 1 GiB stripe column-sharded over the N
+                  ranks (src/encode.cu:368-381), every step ending with the gather of parity and
+                  decoded natives into rank 0's full rows (in place, one link per peer)
+  value_no_comm   = value_by_comm.none
+Moving 0.43 GB of parity per step over xGMI costs more than the 0.65 ms step itself (~64 GB/s per
+link direction against ~5 TB/s of HBM), so those numbers measure the links; the headline measures
+the codec the way N = 1 does. --comm / --scaling choose the headline explicitly.
 
 value = (encoded bytes + decoded bytes) over all ranks / max-over-ranks step time, in GB/s (1e9).
+
+--force-pg (or GFRS_FORCE_PG=1) creates a one-rank RCCL process group at N = 1: the broadcast, the
+all_to_all, the grouped send/recv and the strong-scaling gather then run against rank 0 itself, so
+every RCCL code path of the N > 1 run executes on a single MI355X.
 
 Reference comparison. The reference's published MB/s is PCIe-inclusive: H2D + kernel + D2H
 (src/encode.cu:117-119,228-232, src/decode.cu:96-98,186-190, doc/design.tex:482-500). Its nearest
@@ -42,36 +54,46 @@ published point to k=10, n=14 is k=8, n=11 on 1.1 GB (Tesla C2050): encode 695.0
   vs_baseline      device-resident value / 1.2736 (the driver's field: value / BASELINE number);
   e2e.vs_baseline_e2e  the like-for-like one: pinned host -> H2D -> kernel -> D2H encode and decode
                    of the same 1 GiB stripe (-s 2 streams, every rank concurrently on its own PCIe
-                   link), survivors read from host memory, erased natives rebuilt to host memory.
+                   link), survivors read from host memory, erased natives rebuilt to host memory;
+                   e2e.decode_full_GBps is the reference's exact decode shape (the whole k x k
+                   inverse applied, all k natives D2H into one contiguous file image).
 """
 from __future__ import annotations
 
-import argparse
-import json
 import os
-import socket
-import subprocess
-import sys
-import time
 
-import numpy as np
-import torch
-import torch.distributed as dist
+os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on this driver (RCCL peers)
+
+import argparse  # noqa: E402
+import json  # noqa: E402
+import socket  # noqa: E402
+import subprocess  # noqa: E402
+import sys  # noqa: E402
+import time  # noqa: E402
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 from gpu_rscode_amd import gf  # noqa: E402
 from gpu_rscode_amd.models import ReedSolomon, alloc_rows  # noqa: E402
-from gpu_rscode_amd.parallel.placement import MODES, ParityExchange  # noqa: E402
+from gpu_rscode_amd.parallel.dist import shard_range  # noqa: E402
+from gpu_rscode_amd.parallel.placement import ParityExchange, StripeGather  # noqa: E402
 from gpu_rscode_amd.utils.timing import trace_range  # noqa: E402
 
 BASELINE_GBPS = 2 * 1_096_310_784 / 1.72168 / 1e9  # 1.2736 GB/s
 METRIC = "encode+decode throughput (GB/s) at k=10,n=14 on 1 GiB; 1/2/4/8-GPU scaling"
+COMM_MODES = ("bcast", "owners", "root", "none")
 
-# BASELINE.json configs (per-GPU shapes; scaling is weak: every GPU runs one of these)
+# BASELINE.json configs. Weak presets are per GPU; strong presets are the whole job's bytes.
 PRESETS = {
     "k10n14": dict(k=10, n=14, bytes=1 << 30, erasures=4),
     "k16n20_8g": dict(k=16, n=20, bytes=8 << 30, erasures=4),
+    # config #4 as one stripe: 64 GiB column-sharded over the ranks (8 GiB each at N = 8), parity and
+    # decoded natives gathered into rank 0 once after the timed loop (timed on its own)
+    "k16n20_64g": dict(k=16, n=20, bytes=64 << 30, erasures=4, scaling="strong", gather="end", lanes=1),
     "k128n160": dict(k=128, n=160, bytes=1 << 30, erasures=32),
     "k4n6": dict(k=4, n=6, bytes=1_096_310_784, erasures=2),
 }
@@ -84,37 +106,44 @@ def parse(argv=None):
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--k", type=int, default=None)
     ap.add_argument("--n", type=int, default=None)
-    ap.add_argument("--bytes", type=int, default=None, help="input bytes per GPU")
+    ap.add_argument("--bytes", type=int, default=None, help="input bytes per GPU (weak) / in total (strong)")
     ap.add_argument("--erasures", type=int, default=None)
-    ap.add_argument("--comm", default="owners", choices=MODES, help="per-step parity traffic for N > 1")
-    ap.add_argument("--no-compare", action="store_true", help="N > 1: skip timing the other --comm modes")
+    ap.add_argument("--comm", default="bcast", choices=COMM_MODES, help="per-step RCCL traffic (headline mode)")
+    ap.add_argument("--scaling", default=None, choices=["weak", "strong"],
+                    help="weak: a stripe per GPU (default); strong: one stripe column-sharded over all GPUs")
+    ap.add_argument("--gather", default=None, choices=["step", "end", "none"],
+                    help="strong scaling: gather parity + decoded natives into rank 0 every step (default), "
+                         "once after the timed loop, or never")
+    ap.add_argument("--force-pg", action="store_true",
+                    help="N = 1: create a one-rank RCCL process group and run every collective against itself")
+    ap.add_argument("--no-compare", action="store_true", help="skip timing the other --comm / --scaling modes")
     ap.add_argument("--no-e2e", action="store_true", help="skip the pinned host->device->host timing")
-    ap.add_argument("--e2e", action="store_true", help=argparse.SUPPRESS)  # (on by default now)
-    # e2e -s 2 / 16 MiB: profiles/r02al (52.0 GB/s against 51.2 at -s 4 / 32 MiB; -s 1 reaches 52.3 because each
-    # lane already overlaps H2D, kernel and D2H on its own copy-in + compute streams)
+    ap.add_argument("--e2e", action="store_true", help=argparse.SUPPRESS)  # (on by default)
+    # e2e -s 2 / 16 MiB: profiles/r02al (52.0 GB/s against 51.2 at -s 4 / 32 MiB)
     ap.add_argument("--streams", type=int, default=2, help="e2e: HIP streams (-s) per GPU")
     ap.add_argument("--slice", type=int, default=16 << 20, help="e2e: column slice per stream step")
     ap.add_argument("--vec", type=int, default=None, help="kernel variant: 16-byte groups per lane (ablation)")
     ap.add_argument("--pf", type=int, default=2, help="kernel variant: rows in flight (with --vec)")
     ap.add_argument("--nt", action="store_true", help="kernel variant: non-temporal (with --vec)")
-    ap.add_argument("--no-overlap", action="store_true", help="invert on the main stream (no side stream)")
-    ap.add_argument("--lanes", type=int, default=2,
+    ap.add_argument("--no-overlap", action="store_true", help="solve on the main stream (no side stream)")
+    ap.add_argument("--lanes", type=int, default=None,
                     help="streams that consecutive steps alternate between (own parity slot + decode output)")
     ap.add_argument("--preset", default="k10n14", choices=sorted(PRESETS),
-                    help="BASELINE.json config: k10n14 (headline, #2/#3), k16n20_8g (#4 per GPU), k128n160 (#5), "
-                         "k4n6 (the reference's published shape)")
+                    help="BASELINE.json config: k10n14 (headline, #2/#3), k16n20_8g (#4 per GPU), k16n20_64g "
+                         "(#4 as one 64 GiB stripe), k128n160 (#5), k4n6 (the reference's published shape)")
     ap.add_argument("--engine", default="auto", choices=["auto", "valu", "mfma"],
                     help="encode GEMM engine (auto: FP4 matrix cores for wide stripes, v_perm otherwise)")
     ap.add_argument("--graph", action="store_true", help="replay each step from a captured hipGraph (N = 1)")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu: the C++ CPU codec over gloo (launcher / communication plumbing on a host)")
     a = ap.parse_args(argv)
-    pr = PRESETS[a.preset]
+    pr = dict(scaling="weak", gather="step", lanes=2, **PRESETS[a.preset])
     for key, val in pr.items():
         if getattr(a, key) is None:
             setattr(a, key, val)
     if a.device == "cpu" and "--bytes" not in " ".join(argv if argv is not None else sys.argv):
         a.bytes = 1 << 20  # plumbing runs: 1 MiB per rank
+    a.force_pg = a.force_pg or os.environ.get("GFRS_FORCE_PG") == "1"
     return a
 
 
@@ -130,81 +159,74 @@ def launch(gpus: int, argv: list[str]) -> int:
     process has not touched a GPU and never execs) and return its exit status."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__), *argv]
-    env = dict(os.environ)
-    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on this driver (RCCL peer mapping)
-    return subprocess.run(cmd, env=env).returncode
+    return subprocess.run(cmd, env=dict(os.environ)).returncode
 
 
 # ---- workloads -------------------------------------------------------------------------------
 def erasure_pool(k: int, n: int, erasures: int, rs: ReedSolomon, size: int = 16) -> list[list[int]]:
-    """Recoverable survivor lists with `erasures` chunks lost, at least one native among them."""
+    """Recoverable survivor lists with `erasures` of the n chunks lost. Every pattern loses the same
+    number of natives — ceil(erasures * k / n), the expected share rounded up (3 of 4 at k=10, n=14;
+    26 of 32 at k=128, n=160) — so one device-built decode plan shape serves the whole pool; the
+    rest of the erasures hit parity chunks."""
     rng = np.random.default_rng(1234)
+    e_nat = min(k, erasures, max(erasures - (n - k), -(-erasures * k // n)))
     pool = []
     while len(pool) < size:
-        erased = sorted(rng.choice(n, size=erasures, replace=False).tolist())
+        nat = rng.choice(k, size=e_nat, replace=False).tolist()
+        par = (k + rng.choice(n - k, size=erasures - e_nat, replace=False)).tolist()
+        erased = set(nat + par)
         rows = [r for r in range(n) if r not in erased]
-        if any(e < k for e in erased) and rs.is_recoverable(rows):
+        if rs.is_recoverable(rows):
             pool.append(rows)
     return pool
 
 
-class GpuWorkload:
-    """Encode + on-device decode solve + fused decode on one MI355X (the HIP kernels)."""
+def _check_windows(C: int, width: int = 1 << 16) -> list[tuple[int, int]]:
+    """Head, middle and ragged-tail column windows used to check full parity rows."""
+    wins = {(0, min(C, width)), (max(0, C // 2 - width // 2), min(C, C // 2 + width // 2)), (max(0, C - width), C)}
+    return sorted(wins)
 
-    def __init__(self, a, k, n, C, e_mat, g, pool, rank, dev, slots):
-        from gpu_rscode_amd.ops import GemmPlan, fill_random_
+
+class GpuWorkload:
+    """Encode + device-built decode plan + fused decode on one MI355X (the HIP kernels)."""
+
+    def __init__(self, a, k, n, C, e_mat, g, pool_dev, rank, dev, slots, parity_bufs=None, out_bufs=None, seed=None):
         from gpu_rscode_amd._native import hip
+        from gpu_rscode_amd.ops import GemmPlan, PatternDecoder, fill_random_
 
         hip()  # fail loudly if the native extension is missing
-        self.a, self.k, self.p = a, k, n - k
-        # lanes: consecutive steps alternate between `lanes` streams, each with its own parity slot
-        # and decode output, so step i+1's encode fills the launch gap and the tail of step i's
-        # decode (every step still encodes and decodes its whole 1 GiB)
+        self.a, self.k, self.p, self.C, self.rank = a, k, n - k, C, rank
         self.lanes = 1 if a.graph else max(1, a.lanes)
         slots = max(slots, self.lanes)
         self.data = alloc_rows(k, C, dev)
-        fill_random_(self.data.as_strided((self.data.untyped_storage().nbytes(),), (1,)), seed=rank + 1)
-        self.parity = [alloc_rows(self.p, C, dev) for _ in range(slots)]
-        self.outs = [alloc_rows(k, C, dev) for _ in range(self.lanes)]
-        self.out = self.outs[0]
+        fill_random_(self.data.as_strided((self.data.untyped_storage().nbytes(),), (1,)),
+                     seed=rank + 1 if seed is None else seed)
+        self.parity = parity_bufs or [alloc_rows(self.p, C, dev) for _ in range(slots)]
+        self.outs = out_bufs or [alloc_rows(k, C, dev) for _ in range(self.lanes)]
         self.g_dev = torch.from_numpy(np.ascontiguousarray(g)).to(dev)
         self.e_mat = e_mat
+        self.pool_dev = pool_dev
+        self.e = k - sum(1 for r in pool_dev[0].tolist() if r < k)
         self.enc = [GemmPlan(self.data, par, e_mat, engine=a.engine) for par in self.parity]
-        self.dec = []
-        for si, par in enumerate(self.parity):
-            stripe = [self.data[i] for i in range(k)] + [par[i] for i in range(self.p)]
-            out = self.outs[si % self.lanes]
-            plans = []
-            for rows in pool:
-                erased = [i for i in range(k) if i not in rows]
-                copies = [out[r] if r < k else None for r in rows]
-                plan = GemmPlan([stripe[r] for r in rows], [out[i] for i in erased], copies=copies,
-                                device_tables=True)
-                plan.rows_dev = torch.tensor(rows, dtype=torch.int32, device=dev)
-                plan.erased_dev = torch.tensor(erased, dtype=torch.int32, device=dev)
-                plan.status = torch.zeros(1, dtype=torch.int32, device=dev)
-                plans.append(plan)
-            self.dec.append(plans)
+        self.dec = [PatternDecoder(self.g_dev, [self.data[i] for i in range(k)] + [par[i] for i in range(self.p)],
+                                   [self.outs[s % self.lanes][i] for i in range(k)], self.e)
+                    for s, par in enumerate(self.parity)]
         self.streams = [torch.cuda.Stream(dev) for _ in range(self.lanes)]  # non-default (hipGraph capture)
         self.stream = self.streams[0]
         torch.cuda.set_stream(self.stream)
-        self.side = torch.cuda.Stream(dev)  # decode-system solve overlaps the encode GEMM
+        self.side = torch.cuda.Stream(dev)  # pattern + decode-system solve overlap the encode GEMM
         self.inv_done = torch.cuda.Event()
         self.kv = dict(vec=a.vec, pf=a.pf, nt=a.nt)
-        self.last = None
         self.graph_mode = False
+        self.bcast = False  # rank 0 RCCL-broadcasts each step's pattern (set per timed mode)
 
     def flat_parity(self, slot: int) -> torch.Tensor:
         par = self.parity[slot]
         return par.as_strided((par.untyped_storage().nbytes(),), (1,))
 
-    def _plan(self, i: int, slot: int):
-        return self.dec[slot][i % len(self.dec[slot])]
-
-    def _solve(self, plan, stream) -> None:
-        from gpu_rscode_amd.ops import decode_system_into_plan
-
-        decode_system_into_plan(self.g_dev, plan.rows_dev, plan.erased_dev, plan, status=plan.status, stream=stream)
+    def piece_rows(self, slot: int) -> list[torch.Tensor]:
+        """The rows a strong-scaling gather moves for `slot`: parity, then the decoded natives."""
+        return [self.parity[slot][i] for i in range(self.p)] + [self.outs[slot % self.lanes][i] for i in range(self.k)]
 
     def lane_stream(self, slot: int):
         """The stream of the lane that owns parity slot `slot`."""
@@ -216,90 +238,109 @@ class GpuWorkload:
         self.stream = self.lane_stream(slot)
         torch.cuda.set_stream(self.stream)
 
-    def step(self, i: int, slot: int) -> None:
-        """One encode + one on-device decode solve + one decode GEMM.
+    def _prepare(self, i: int, dec, stream) -> None:
+        """Step i's pattern into dec.rows (rank 0 writes it; with bcast every rank receives it over
+        RCCL), then the on-device check + solve + plan build — all ordered on `stream`."""
+        with torch.cuda.stream(stream):
+            if self.rank == 0 or not self.bcast:
+                dec.rows.copy_(self.pool_dev[i % self.pool_dev.shape[0]], non_blocking=True)
+            if self.bcast:
+                dist.broadcast(dec.rows, 0)
+            dec.solve(stream)
 
-        Default schedule: the decode system of step i+1 is solved on a side stream right after step
-        i's decode GEMM is queued, so the one-workgroup solve runs beside that GEMM (whose register
-        use leaves room for it; the staggered FP4 encode kernel of wide stripes does not). Each
-        plan's solve waits for the previous decode that read the same tables (event per plan)."""
-        plan = self._plan(i, slot)
-        self.last = plan
-        if self.a.no_overlap:  # everything on one stream, solve first
-            self._solve(plan, self.stream)
+    def step(self, i: int, slot: int) -> None:
+        """One encode + one device-built decode plan + one decode GEMM.
+
+        Default schedule: the plan of step i+1 is built on a side stream right after step i's decode
+        GEMM is queued, so the one-workgroup solve runs beside that GEMM. Each lane's decoder waits
+        for the previous decode that read its descriptor (event per decoder)."""
+        dec = self.dec[slot]
+        if self.a.no_overlap:  # everything on one stream, plan first
+            self._prepare(i, dec, self.stream)
             self.enc[slot].run(**self.kv)
-            plan.run(**self.kv)
+            dec.run(**self.kv)
             return
-        if self.graph_mode:  # captured per pattern: solve under this step's encode
+        if self.graph_mode:  # captured per pattern: plan built under this step's encode
             self.side.wait_stream(self.stream)
-            self._solve(plan, self.side)
+            self._prepare(i, dec, self.side)
             self.inv_done.record(self.side)
             self.enc[slot].run(**self.kv)
             self.stream.wait_event(self.inv_done)
-            plan.run(**self.kv)
+            dec.run(**self.kv)
             return
-        if not getattr(plan, "pending", False):  # (first step of a loop)
-            self._issue_solve(plan)
+        if not getattr(dec, "pending", False):  # (first step of a loop)
+            self._issue(i, dec)
         self.enc[slot].run(**self.kv)
-        self.stream.wait_event(plan.solved)
-        plan.run(**self.kv)
-        plan.used.record(self.stream)
-        plan.pending = False
+        self.stream.wait_event(dec.solved)
+        dec.run(**self.kv)
+        dec.used.record(self.stream)
+        dec.pending = False
         nxt_slot = (i + 1) % len(self.dec)
-        nxt = self._plan(i + 1, nxt_slot)
-        self._issue_solve(nxt, self.lane_stream(nxt_slot))
+        self._issue(i + 1, self.dec[nxt_slot], self.lane_stream(nxt_slot))
 
     def reset(self) -> None:
-        """Start a loop with no solve in flight: its first step solves its own system (so a timed
-        loop of K steps runs K + 1 solves — one more than it needs)."""
-        for plans in self.dec:
-            for plan in plans:
-                plan.pending = False
+        """Start a loop with no plan in flight: its first step builds its own (so a timed loop of K
+        steps builds K + 1 plans — one more than it needs)."""
+        for dec in self.dec:
+            dec.pending = False
 
-    def _issue_solve(self, plan, stream=None) -> None:
-        if not hasattr(plan, "solved"):
-            plan.solved, plan.used = torch.cuda.Event(), torch.cuda.Event()
-            plan.used.record(stream or self.stream)
-        self.side.wait_event(plan.used)  # the last decode that read these tables is done
-        self._solve(plan, self.side)
-        plan.solved.record(self.side)
-        plan.pending = True
+    def _issue(self, i: int, dec, stream=None) -> None:
+        if not hasattr(dec, "solved"):
+            dec.solved, dec.used = torch.cuda.Event(), torch.cuda.Event()
+            dec.used.record(stream or self.stream)
+        self.side.wait_event(dec.used)  # the last decode that read this descriptor is done
+        self._prepare(i, dec, self.side)
+        dec.solved.record(self.side)
+        dec.pending = True
 
     def sync(self) -> None:
         torch.cuda.synchronize()
 
     def verify(self) -> bool:
-        ok = self.last is not None and int(self.last.status.item()) == 0
+        """Every decoder's last pattern solved (status 0), every decoded output equals the data in
+        full, and every parity slot matches the numpy oracle at its head, middle and ragged tail."""
+        ok = all(int(d.status.item()) == 0 for d in self.dec)
         ok = ok and all(torch.equal(out, self.data) for out in self.outs)
-        cols = min(self.data.shape[1], 1 << 16)
-        want = gf.GF256.gemm(self.e_mat, self.data[:, :cols].cpu().numpy())
-        return bool(ok and all(np.array_equal(par[:, :cols].cpu().numpy(), want) for par in self.parity))
+        for a, b in _check_windows(self.C):
+            want = gf.GF256.gemm(self.e_mat, self.data[:, a:b].cpu().numpy())
+            ok = ok and all(np.array_equal(par[:, a:b].cpu().numpy(), want) for par in self.parity)
+        return bool(ok)
 
 
 class CpuWorkload:
     """The same step on host tensors through the C++ CPU codec (gloo plumbing runs)."""
 
-    def __init__(self, a, k, n, C, e_mat, g, pool, rank, slots):
-        self.k, self.p = k, n - k
+    def __init__(self, a, k, n, C, e_mat, g, pool_dev, rank, slots, parity_bufs=None, out_bufs=None, seed=None):
+        self.k, self.p, self.C, self.rank = k, n - k, C, rank
         self.rs = ReedSolomon(k, n)
         self.rs.E, self.rs.G = e_mat, g
-        gen = torch.Generator().manual_seed(rank + 1)
+        gen = torch.Generator().manual_seed(rank + 1 if seed is None else seed)
         self.data = torch.randint(0, 256, (k, C), dtype=torch.uint8, generator=gen)
-        self.parity = [torch.zeros((self.p, C), dtype=torch.uint8) for _ in range(slots)]
-        self.out = torch.zeros((k, C), dtype=torch.uint8)
-        self.pool = pool
+        self.parity = parity_bufs or [torch.zeros((self.p, C), dtype=torch.uint8) for _ in range(slots)]
+        self.lanes = len(self.parity)
+        self.outs = out_bufs or [torch.zeros((k, C), dtype=torch.uint8) for _ in range(self.lanes)]
+        self.pool_dev = pool_dev
+        self.bcast = False
 
     def flat_parity(self, slot: int) -> torch.Tensor:
-        return self.parity[slot].view(-1)
+        return self.parity[slot].reshape(-1)
+
+    def piece_rows(self, slot: int) -> list[torch.Tensor]:
+        return [self.parity[slot][i] for i in range(self.p)] + [self.outs[slot % self.lanes][i] for i in range(self.k)]
 
     def use_lane(self, slot: int) -> None:
         pass
 
     def step(self, i: int, slot: int) -> None:
         self.rs.encode(self.data, self.parity[slot])
-        rows = self.pool[i % len(self.pool)]
+        rows_t = self.pool_dev[i % self.pool_dev.shape[0]].clone()
+        if self.bcast:  # the pattern comes from rank 0, as on the GPU path
+            if self.rank != 0:
+                rows_t.fill_(-1)
+            dist.broadcast(rows_t, 0)
+        rows = rows_t.tolist()
         stripe = [self.data[r] if r < self.k else self.parity[slot][r - self.k] for r in rows]
-        self.rs.decode(stripe, rows, out=self.out)
+        self.rs.decode(stripe, rows, out=self.outs[slot % self.lanes])
 
     def sync(self) -> None:
         pass
@@ -309,56 +350,76 @@ class CpuWorkload:
 
     def verify(self) -> bool:
         want = gf.GF256.gemm(self.rs.E, self.data.numpy())
-        return torch.equal(self.out, self.data) and all(np.array_equal(par.numpy(), want) for par in self.parity)
+        return all(torch.equal(o, self.data) for o in self.outs) and all(
+            np.array_equal(par.numpy(), want) for par in self.parity)
+
+
+def make_work(a, k, n, C, e_mat, g, pool_dev, rank, dev, slots, **kw):
+    if dev.type == "cuda":
+        return GpuWorkload(a, k, n, C, e_mat, g, pool_dev, rank, dev, slots, **kw)
+    return CpuWorkload(a, k, n, C, e_mat, g, pool_dev, rank, slots, **kw)
 
 
 # ---- timing ----------------------------------------------------------------------------------
-def timed_loop(work, xchg: ParityExchange, steps: int, world: int, dev, label: str) -> float:
-    """Seconds for `steps` steps, bracketed by barrier + synchronize on both sides, max over ranks."""
-    slots = len(xchg.sources)
-
-    def one(i):
+def _run_steps(work, xchg, steps: int) -> None:
+    slots = len(work.parity)
+    for i in range(steps):
         slot = i % slots
         work.use_lane(slot)
-        xchg.wait(slot)  # the exchange that last read this parity buffer is done
+        xchg.wait(slot)  # the exchange that last read this slot's buffers is done
         work.step(i, slot)
         xchg.start(slot)
+    xchg.drain()
 
+
+def timed_loop(work, xchg, steps: int, world: int, dev, label: str) -> float:
+    """Seconds for `steps` steps, bracketed by barrier + synchronize on both sides, max over ranks."""
     work.reset()
     with trace_range(f"bench/{label}"):
         if world > 1:
             dist.barrier()
         work.sync()
         t0 = time.perf_counter()
-        for i in range(steps):
-            one(i)
-        xchg.drain()
+        _run_steps(work, xchg, steps)
         work.sync()
         if world > 1:
             dist.barrier()
         work.sync()
         elapsed = time.perf_counter() - t0
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    return max_over_ranks(elapsed, dev, world)
+
+
+def max_over_ranks(x: float, dev, world: int) -> float:
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
 
-def warm(work, xchg: ParityExchange, steps: int) -> None:
+def warm(work, xchg, steps: int) -> None:
     work.reset()
-    slots = len(xchg.sources)
-    for i in range(steps):
-        work.use_lane(i % slots)
-        xchg.wait(i % slots)
-        work.step(i, i % slots)
-        xchg.start(i % slots)
-    xchg.drain()
+    _run_steps(work, xchg, steps)
     work.sync()
+
+
+class _NoExchange:
+    def start(self, slot):
+        pass
+
+    def wait(self, slot):
+        pass
+
+    def drain(self):
+        pass
+
+    def verify(self, slot):
+        return True
 
 
 def e2e(a, k, n, C, rs: ReedSolomon, rows: list[int], work: GpuWorkload, dev, world: int) -> dict:
     """Reference-comparable timing on every rank at once: pinned host rows -> H2D -> GF-GEMM -> D2H
-    (the native streaming pipeline, -s `a.streams`), encode then a 4-erasure decode."""
+    (the native streaming pipeline, -s `a.streams`): encode, a decode that rebuilds the erased
+    natives, and the reference's full decode (k x k inverse, all k natives into a [k, C] image)."""
     from gpu_rscode_amd._native import hip
 
     h = hip()
@@ -368,51 +429,141 @@ def e2e(a, k, n, C, rs: ReedSolomon, rows: list[int], work: GpuWorkload, dev, wo
     par = torch.empty((p, C), dtype=torch.uint8, pin_memory=True)
     erased = [i for i in range(k) if i not in rows]
     rec = torch.empty((len(erased), C), dtype=torch.uint8, pin_memory=True)
-    dm = rs.decode_matrix(rows)[erased]
+    image = torch.empty((k, C), dtype=torch.uint8, pin_memory=True)  # the decoded file, contiguous
+    dm_full = rs.decode_matrix(rows)
     enc_in = [host[j].data_ptr() for j in range(k)]
     enc_out = [par[i].data_ptr() for i in range(p)]
     dec_in = [host[r].data_ptr() if r < k else par[r - k].data_ptr() for r in rows]
     dec_out = [rec[i].data_ptr() for i in range(len(erased))]
+    full_out = [image[i].data_ptr() for i in range(k)]
     emat = np.ascontiguousarray(rs.E).tobytes()
-    dmat = np.ascontiguousarray(dm).tobytes()
-    h.prepare_pipeline([dev.index], k, max(p, len(erased)), C, a.streams, a.slice)
+    dmat = np.ascontiguousarray(dm_full[erased]).tobytes()
+    fmat = np.ascontiguousarray(dm_full).tobytes()
+    h.prepare_pipeline([dev.index], k, max(p, k), C, a.streams, a.slice)
 
     def run(ins, outs, mat):
         return h.gemm_host([dev.index], ins, outs, mat, C, a.streams, a.slice, 0, False)["devices"][0]
 
     res = {}
-    for name, ins, outs, mat in (("encode", enc_in, enc_out, emat), ("decode", dec_in, dec_out, dmat)):
+    for name, ins, outs, mat in (("encode", enc_in, enc_out, emat), ("decode", dec_in, dec_out, dmat),
+                                 ("decode_full", dec_in, full_out, fmat)):
         run(ins, outs, mat)  # warm (first DMA of fresh pinned pages)
         best = None
         for _ in range(3):
             if world > 1:
                 dist.barrier()
             st = run(ins, outs, mat)
-            t = torch.tensor([st["ms_total"]], dtype=torch.float64, device=dev)
-            if world > 1:
-                dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            if best is None or float(t.item()) < best[0]:
-                best = (float(t.item()), st)
+            t = max_over_ranks(st["ms_total"], dev, world)
+            if best is None or t < best[0]:
+                best = (t, st)
         res[name] = best
-    cols = min(C, 1 << 16)
-    ok = np.array_equal(par[:, :cols].numpy(), work.parity[0][:, :cols].cpu().numpy())
-    ok = ok and torch.equal(rec, host[erased])
+    ok = True
+    for a0, b0 in _check_windows(C):
+        ok = ok and np.array_equal(par[:, a0:b0].numpy(), work.parity[0][:, a0:b0].cpu().numpy())
+    ok = ok and torch.equal(rec, host[erased]) and torch.equal(image, host)
     stripe_bytes = k * C * world
-    enc_ms, dec_ms = res["encode"][0], res["decode"][0]
+    enc_ms, dec_ms, full_ms = res["encode"][0], res["decode"][0], res["decode_full"][0]
     both = 2 * stripe_bytes / ((enc_ms + dec_ms) / 1e3) / 1e9
     return {
         "encode_GBps": round(stripe_bytes / (enc_ms / 1e3) / 1e9, 3),
         "decode_GBps": round(stripe_bytes / (dec_ms / 1e3) / 1e9, 3),
+        "decode_full_GBps": round(stripe_bytes / (full_ms / 1e3) / 1e9, 3),
         "encode_decode_GBps": round(both, 3),
         "vs_baseline_e2e": round(both / BASELINE_GBPS, 1),
-        "encode_ms": round(enc_ms, 3), "decode_ms": round(dec_ms, 3),
+        "encode_ms": round(enc_ms, 3), "decode_ms": round(dec_ms, 3), "decode_full_ms": round(full_ms, 3),
         "encode_ms_stream": round(res["encode"][1]["ms_stream"], 3),
         "decode_ms_stream": round(res["decode"][1]["ms_stream"], 3),
         "streams": a.streams, "slice_bytes": a.slice, "erased": len(erased), "verified": bool(ok),
         "what": "pinned host -> H2D -> GF-GEMM -> D2H per rank (own PCIe link), max over ranks; decode erases the "
-                "first `erased` natives (src/unit-test.sh pattern), reads the k survivors, writes the rebuilt "
-                "natives (surviving natives stay in host memory)",
+                "first `erased` natives (src/unit-test.sh pattern) and reads the k survivors: decode writes the "
+                "rebuilt natives (surviving natives stay in host memory), decode_full is the reference's shape "
+                "(src/decode.cu:149-176: the whole k x k inverse, all k natives D2H into one contiguous image)",
     }
+
+
+# ---- runs ------------------------------------------------------------------------------------
+def run_weak(a, k, n, e_mat, g, pool_dev, rank, world, dev, has_pg, modes):
+    """Weak scaling: every rank encodes and decodes its own a.bytes stripe."""
+    C = (a.bytes + k - 1) // k
+    slots = 2 if has_pg else 1  # parity double-buffered while its exchange is in flight
+    work = make_work(a, k, n, C, e_mat, g, pool_dev, rank, dev, slots)
+    slots = len(work.parity)
+    flats = [work.flat_parity(s) for s in range(slots)]
+    results = {}
+    for mi, mode in enumerate(modes):
+        xchg = ParityExchange(flats, mode if mode in ("owners", "root") else "none")
+        work.bcast = has_pg and mode != "none"
+        steps = a.steps if mi == 0 else min(a.steps, 20)
+        warm(work, xchg, a.warmup if mi == 0 else 2)
+        if a.graph and mi == 0:
+            work.graph_mode = True
+            graphs = []
+            for i in range(len(pool_dev)):
+                gph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gph, stream=work.stream):
+                    work.step(i, 0)
+                graphs.append(gph)
+            torch.cuda.synchronize()
+            step_fn = work.step
+            work.step = lambda i, slot: graphs[i % len(graphs)].replay()  # noqa: E731
+            elapsed = timed_loop(work, xchg, steps, world, dev, f"timed/weak/{mode}")
+            work.step = step_fn
+            work.graph_mode = False
+        else:
+            elapsed = timed_loop(work, xchg, steps, world, dev, f"timed/weak/{mode}")
+        ok = all(xchg.verify(s) for s in range(slots))
+        results[mode] = dict(elapsed=elapsed, steps=steps, ok=ok, sent=xchg.bytes_sent, recv=xchg.bytes_received,
+                             link=xchg.bytes_per_link, bytes=2 * k * C * world)
+        del xchg
+    return work, C, results
+
+
+def run_strong(a, k, n, e_mat, g, pool_dev, rank, world, dev, has_pg, steps, warmup):
+    """Strong scaling: ONE stripe of a.bytes column-sharded over the ranks (shard_range, the
+    reference's split, src/encode.cu:368-381). Rank 0's shard computes in place inside its full
+    rows, so the gather moves only the peers' pieces."""
+    Ct = (a.bytes + k - 1) // k
+    p = n - k
+    lo, hi = shard_range(Ct, world, rank)
+    widths = [b - a_ for a_, b in (shard_range(Ct, world, r) for r in range(world))]
+    lanes = 1 if a.graph else max(1, a.lanes)
+    slots = max(2 if (has_pg and a.gather == "step") else 1, lanes)
+    fulls = None
+    par_bufs = out_bufs = None
+    if rank == 0 and a.gather != "none":
+        mk = (lambda r: alloc_rows(r, Ct, dev)) if dev.type == "cuda" else (lambda r: torch.zeros((r, Ct), dtype=torch.uint8))
+        full_par = [mk(p) for _ in range(slots)]
+        full_out = [mk(k) for _ in range(lanes)]
+        fulls = [[full_par[s][i] for i in range(p)] + [full_out[s % lanes][i] for i in range(k)] for s in range(slots)]
+        par_bufs = [fp[:, :hi - lo] for fp in full_par]
+        out_bufs = [fo[:, :hi - lo] for fo in full_out]
+    work = make_work(a, k, n, hi - lo, e_mat, g, pool_dev, rank, dev, slots, parity_bufs=par_bufs,
+                     out_bufs=out_bufs, seed=1000 + rank)
+    slots = len(work.parity)
+    gather = None
+    if a.gather != "none":
+        gather = StripeGather([work.piece_rows(s) for s in range(slots)], fulls, widths)
+    xchg = gather if (gather is not None and a.gather == "step") else _NoExchange()
+    work.bcast = has_pg
+    warm(work, xchg, warmup)
+    elapsed = timed_loop(work, xchg, steps, world, dev, f"timed/strong/{a.gather}")
+    ok = all(xchg.verify(s) for s in range(slots))
+    out = dict(elapsed=elapsed, steps=steps, ok=ok, bytes=2 * k * Ct, total_cols=Ct, widths=widths,
+               gather=a.gather, link=gather.bytes_per_link if gather else 0,
+               recv=gather.bytes_received if (gather and rank == 0) else 0)
+    if a.gather == "end":
+        if world > 1:
+            dist.barrier()
+        work.sync()
+        t0 = time.perf_counter()
+        gather.start(0)
+        gather.drain()
+        work.sync()
+        gt = max_over_ranks(time.perf_counter() - t0, dev, world)
+        out.update(gather_ms=round(gt * 1e3, 3), gather_ok=gather.verify(0),
+                   gather_GBps=round(gather.bytes_per_link * max(1, world - 1) / gt / 1e9, 3) if world > 1 else None)
+        out["ok"] = out["ok"] and out["gather_ok"]
+    return work, out
 
 
 # ---- main ------------------------------------------------------------------------------------
@@ -433,86 +584,80 @@ def main(argv=None) -> int:
         dev = torch.device("cuda", local)
     else:
         dev = torch.device("cpu")
-    if world > 1:
+    has_pg = world > 1 or a.force_pg
+    if has_pg:
         kw = {"device_id": dev} if dev.type == "cuda" else {}
+        if world == 1 and "MASTER_PORT" not in os.environ:
+            kw.update(init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1)
         dist.init_process_group("nccl" if dev.type == "cuda" else "gloo", **kw)
         if dist.get_world_size() != world:
             raise SystemExit("process group size does not match WORLD_SIZE")
+    if a.graph and has_pg:
+        raise SystemExit("--graph is single-GPU only, without a process group (per-step RCCL traffic)")
 
     k, n = a.k, a.n
-    p = n - k
-    C = (a.bytes + k - 1) // k
 
     # ---- setup: E and the erasure-pattern pool come from rank 0 (RCCL broadcast) -------------
     rs = ReedSolomon(k, n)
     pool = erasure_pool(k, n, a.erasures, rs)
     e_t = torch.from_numpy(rs.E.copy()).to(dev)
     pool_t = torch.tensor(pool, dtype=torch.int32, device=dev)
-    if world > 1:
+    if has_pg:
         dist.broadcast(e_t, 0)
         dist.broadcast(pool_t, 0)
     e_mat = e_t.cpu().numpy()
-    pool = pool_t.cpu().tolist()
     rs.E, rs.G = e_mat, gf.GF256.generator(e_mat)
 
-    modes = [a.comm] if world == 1 or a.no_compare else [a.comm] + [m for m in MODES if m != a.comm]
-    slots = 2 if world > 1 else 1  # parity double-buffered while its exchange is in flight
-    if a.graph and world > 1:
-        raise SystemExit("--graph is single-GPU only (per-step RCCL exchange)")
-    if dev.type == "cuda":
-        work = GpuWorkload(a, k, n, C, e_mat, rs.G, pool, rank, dev, slots)
-    else:
-        work = CpuWorkload(a, k, n, C, e_mat, rs.G, pool, rank, slots)
-    slots = len(work.parity)  # (the GPU workload gives every lane its own slot)
-    flats = [work.flat_parity(s) for s in range(slots)]
-
-    results = {}
-    verified = True
-    for mi, mode in enumerate(modes):
-        xchg = ParityExchange(flats, mode)
-        steps = a.steps if mi == 0 else min(a.steps, 20)
-        warm(work, xchg, a.warmup if mi == 0 else 2)
-        if a.graph and mode == a.comm:
-            work.graph_mode = True
-            graphs = []
-            for i in range(len(work.dec[0])):
-                gph = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(gph, stream=work.stream):
-                    work.step(i, 0)
-                graphs.append(gph)
-            torch.cuda.synchronize()
-            step_fn = work.step
-            work.step = lambda i, slot: graphs[i % len(graphs)].replay()  # noqa: E731
-            elapsed = timed_loop(work, xchg, steps, world, dev, f"timed/{mode}")
-            work.step = step_fn
+    compare = has_pg and not a.no_compare
+    head_strong = a.scaling == "strong"
+    weak_modes = [a.comm] + ([m for m in COMM_MODES if m != a.comm] if compare else [])
+    results, strong = {}, None
+    work = None
+    if not head_strong:
+        work, C, results = run_weak(a, k, n, e_mat, rs.G, pool_t, rank, world, dev, has_pg, weak_modes)
+    if head_strong or compare:
+        steps = a.steps if head_strong else min(a.steps, 20)
+        swork, strong = run_strong(a, k, n, e_mat, rs.G, pool_t, rank, world, dev, has_pg, steps,
+                                   a.warmup if head_strong else 2)
+        if work is None:
+            work, C = swork, swork.C
         else:
-            elapsed = timed_loop(work, xchg, steps, world, dev, f"timed/{mode}")
-        ok = xchg.verify((steps - 1) % slots)
-        results[mode] = dict(elapsed=elapsed, steps=steps, ok=ok, sent=xchg.bytes_sent, recv=xchg.bytes_received,
-                             link=xchg.bytes_per_link)
-        verified = verified and ok
-        del xchg
+            sw_ok = swork.verify()
+            strong["ok"] = strong["ok"] and sw_ok
+            del swork
 
     # ---- verification (outside the timed regions) ---------------------------------------------
-    ok = work.verify()
-    okt = torch.tensor([1 if (ok and verified) else 0], device=dev)
+    ok = work.verify() and all(r["ok"] for r in results.values()) and (strong is None or strong["ok"])
+    okt = torch.tensor([1 if ok else 0], device=dev)
     if world > 1:
         dist.all_reduce(okt, op=dist.ReduceOp.MIN)
     ok = bool(okt.item())
 
-    bytes_per_step = 2 * k * C * world  # encoded input + decoded output, all ranks
-
     def gbps(r):
-        return bytes_per_step / (r["elapsed"] / r["steps"]) / 1e9
+        return r["bytes"] / (r["elapsed"] / r["steps"]) / 1e9
 
-    head = results[a.comm]
+    head = strong if head_strong else results[a.comm]
     ms = head["elapsed"] / head["steps"] * 1e3
     value = gbps(head)
     metric = METRIC
-    if a.preset != "k10n14" or a.bytes != PRESETS["k10n14"]["bytes"]:
-        metric = f"encode+decode throughput (GB/s) at k={k},n={n} on {a.bytes / 2**30:.3g} GiB per GPU"
-    comm_desc = {"owners": "parity all_to_all to chunk owners over RCCL/xGMI",
-                 "root": "parity gather to rank 0 over RCCL/xGMI (grouped send/recv)", "none": "no per-step traffic"}
+    if a.preset != "k10n14" or a.bytes != PRESETS["k10n14"]["bytes"] or head_strong:
+        per = "in total, one stripe sharded over the GPUs" if head_strong else "per GPU"
+        metric = f"encode+decode throughput (GB/s) at k={k},n={n} on {a.bytes / 2**30:.3g} GiB {per}"
+    comm_desc = {"bcast": "rank 0 RCCL-broadcasts the step's erasure pattern; parity and decoded rows stay in "
+                          "each GPU's HBM (as at N = 1)",
+                 "owners": "pattern broadcast + parity all_to_all to chunk owners over RCCL/xGMI",
+                 "root": "pattern broadcast + parity gather to rank 0 over RCCL/xGMI (grouped send/recv)",
+                 "none": "no per-step traffic (each rank draws the pattern itself)"}
+    head_mode = a.comm if has_pg else "none"
+    if head_strong:
+        parallelism = f"dp{world} strong (one {k}-row stripe column-sharded, gather {a.gather})"
+        comm_what = {"step": "pattern broadcast + parity and decoded natives gathered into rank 0 every step",
+                     "end": "pattern broadcast; parity and decoded natives gathered into rank 0 once, after the "
+                            "timed loop (timed on its own: strong.gather_ms)",
+                     "none": "pattern broadcast only"}[a.gather] if has_pg else "none (one GPU)"
+    else:
+        parallelism = f"dp{world} weak (stripe per rank, E + pattern pool RCCL-broadcast)"
+        comm_what = comm_desc[head_mode]
     rec = {
         "metric": metric,
         "value": round(value, 3),
@@ -522,25 +667,31 @@ def main(argv=None) -> int:
         "warmup": a.warmup,
         "ms_per_step": round(ms, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if head_strong else "weak",
         "vs_baseline": round(value / BASELINE_GBPS, 1),
         "dtype": "uint8 (GF(2^8) symbols)",
         "data": "synthetic (device-generated random bytes)" if dev.type == "cuda" else "synthetic (host random bytes)",
         "config": {"model": f"RS(k={k},n={n}) reference Vandermonde, GF(2^8) poly 0x11D",
-                   "global_batch": f"{a.bytes} B per GPU ({k} x {C} B chunks)", "seq_len": C,
-                   "parallelism": f"dp{world} (stripe per rank, E + erasure pool RCCL-broadcast)",
-                   "comm": a.comm if world > 1 else "none", "comm_what": comm_desc[a.comm if world > 1 else "none"],
+                   "global_batch": (f"{a.bytes} B in total ({k} x {C} B columns per rank shard)" if head_strong
+                                    else f"{a.bytes} B per GPU ({k} x {C} B chunks)"),
+                   "seq_len": C, "parallelism": parallelism,
+                   "comm": ("strong/" + a.gather) if head_strong else head_mode, "comm_what": comm_what,
                    "erasures": a.erasures,
-                   "decode_invert": ("device Gauss-Jordan (systematic e x (e+k) system) per step" if dev.type == "cuda"
+                   "decode_invert": ("device-built plan per step: pattern check + systematic e x (e+k) Gauss-Jordan "
+                                     "+ descriptor rows/tables" if dev.type == "cuda"
                                      else "host row-pivoted Gauss-Jordan (cached per pattern)"),
                    "engine": getattr(getattr(work, "enc", [None])[0], "engine", "cpu"), "graph": bool(a.graph),
-                   "preset": a.preset, "device": dev.type},
+                   "preset": a.preset, "device": dev.type, "process_group": bool(has_pg)},
         "verified": ok,
         "vs_baseline_what": "device-resident value / reference nearest published PCIe-inclusive point; "
                             "the like-for-like ratio is e2e.vs_baseline_e2e",
         "baseline": {"gbps": round(BASELINE_GBPS, 4), "source": "k=8,n=11 1.1 GB Tesla C2050 (nearest published)"},
     }
-    if world > 1:
+    if has_pg and not head_strong:
+        rec["headline_why"] = ("weak scaling with the parity left in each GPU's HBM, as the N = 1 number does; the "
+                               "per-step parity movement over xGMI (value_by_comm.owners / .root) and the "
+                               "reference's one-stripe strong scaling (value_strong) are timed alongside")
+    if results and (has_pg or len(results) > 1):
         # busiest xGMI link: bytes it carries per step, and the rate the measured step implies for
         # it (a lower bound on what the link sustained; when the step is link-bound, its rate)
         rec["value_by_comm"] = {m: {"GBps": round(gbps(r), 3), "ms_per_step": round(r["elapsed"] / r["steps"] * 1e3, 4),
@@ -552,14 +703,21 @@ def main(argv=None) -> int:
                                 for m, r in results.items()}
         if "none" in results:
             rec["value_no_comm"] = round(gbps(results["none"]), 3)
-    if dev.type == "cuda" and not a.no_e2e:
+    if strong is not None:
+        rec["value_strong"] = round(gbps(strong), 3)
+        rec["strong"] = {"GBps": round(gbps(strong), 3), "ms_per_step": round(strong["elapsed"] / strong["steps"] * 1e3, 4),
+                         "steps": strong["steps"], "stripe_bytes": a.bytes, "shard_cols": strong["widths"],
+                         "gather": strong["gather"], "busiest_link_bytes_per_step": strong["link"],
+                         "bytes_recv_rank0": strong["recv"] if rank == 0 else None, "verified": strong["ok"],
+                         **{kk: strong[kk] for kk in ("gather_ms", "gather_GBps") if kk in strong}}
+    if dev.type == "cuda" and not a.no_e2e and not head_strong:
         # the reference's worst case (src/unit-test.sh: keep the last k chunks): the first
         # `erasures` natives are lost, so every one of them is rebuilt and copied back to the host
         e = min(a.erasures, k, n - k)
         rec["e2e"] = e2e(a, k, n, C, rs, list(range(e, k)) + list(range(k, k + e)), work, dev, world)
     if rank == 0:
         print(json.dumps(rec), flush=True)
-    if world > 1:
+    if has_pg:
         dist.destroy_process_group()
     return 0 if ok else 1
 

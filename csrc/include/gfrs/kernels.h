@@ -36,8 +36,12 @@ hipError_t launch_gf_gemm_variant(const void* desc, int k, int m_pad, int64_t co
 // ids, erased = the e erased native ids (device int32). Writes X (e x k, decode coefficients of the
 // erased natives in survivor order) to dm (optional), status (1 = unrecoverable), and the v_perm
 // tables tab[j][b] into desc (k inputs, m_pad >= e outputs) when given.
-hipError_t launch_gf_decode_system(const uint8_t* g, int k, const int* rows, const int* erased, int e, uint8_t* dm,
-                                   int* status, void* desc, int m_pad, hipStream_t stream);
+// Device-built plan (ptrs != null, desc required): `erased` becomes an OUTPUT (derived from rows on
+// the device) and the descriptor's row pointers are written from ptrs = {chunk row 0..n_chunks-1,
+// output row 0..k-1} (uint64 device addresses); status 2 = invalid pattern.
+hipError_t launch_gf_decode_system(const uint8_t* g, int k, const int* rows, int* erased, int e, uint8_t* dm,
+                                   int* status, void* desc, int m_pad, hipStream_t stream,
+                                   const uint64_t* ptrs = nullptr, int n_chunks = 0);
 hipError_t launch_gf_invert(const uint8_t* a, uint8_t* a_inv, int n, int batch, int* status,
                             void* desc, const int* sel_rows, int m, int m_pad, hipStream_t stream);
 

@@ -190,25 +190,34 @@ __global__ __launch_bounds__(B) void gf_invert_kernel(const uint8_t* __restrict_
 // [rows_j == P_a] for a parity survivor j. Gauss-Jordan on [M | B'] (e x (e+k)) yields X directly:
 // O(e^2 (e+k)) instead of inverting the whole k x k system (k=128, e=32: ~40x less work, and the
 // wide decode no longer waits ~1 ms for a 128x128 inverse — profiles/r01_p128).
-// LDS carve of the decode-system kernel before M: exp 1024 | log 512 | pivot-search slots + count 16 |
-// pivot rows 256 | parity survivors 256 | rows 256 | erased 256 | pivot inverses 256 (ids are
-// bytes). Kept small so the solve fits next to a full-LDS persistent GEMM block (k=128, e=32:
-// 7.9 KiB; gf_mfma_fp4.hip kSideReserve).
-constexpr size_t kDecSysFixed = 1552 + 5 * 256;
+// LDS carve of the decode-system kernel before M: exp 1024 | log 512 | pivot-search slots, parity
+// count, pattern-error flag 32 | pivot rows 256 | parity survivors 256 | rows 256 | erased 256 |
+// pivot inverses 256 (ids are bytes). Kept small so the solve fits next to a full-LDS persistent
+// GEMM block (k=128, e=32: 7.9 KiB; gf_mfma_fp4.hip kSideReserve).
+constexpr size_t kDecSysFixed = 1568 + 5 * 256;
 
+// Device-built decode plans (`ptrs` != null): the survivor list `rows` is the only input — e.g. an
+// erasure pattern just RCCL-broadcast into device memory by a coordinator rank. The kernel checks
+// it (k distinct chunk ids < n_chunks, exactly e natives missing; else status 2), derives the erased
+// natives (written back to `erased`, ascending) and, besides the tables, writes the descriptor's
+// row pointers from the stripe's pointer table ptrs = {chunk row 0..n_chunks-1, output row 0..k-1}:
+// in[j] = chunk[rows[j]], copy[j] = out[rows[j]] for a native survivor, out[i] = out[erased[i]].
+// A singular or invalid pattern leaves no output pointer (the GEMM then stores nothing).
 template <int B>
 __global__ __launch_bounds__(B) void gf_decode_system_kernel(const uint8_t* __restrict__ g, int k,
                                                              const int* __restrict__ rows,
-                                                             const int* __restrict__ erased, int e,
+                                                             int* __restrict__ erased, int e,
                                                              uint8_t* __restrict__ dm, int* __restrict__ status,
-                                                             uint32_t* __restrict__ tab, int m_pad) {
+                                                             uint32_t* __restrict__ tab, int m_pad,
+                                                             const uint64_t* __restrict__ ptrs, int n_chunks,
+                                                             uint64_t* __restrict__ dptr) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int W = e + k;
   const int PW = (((W + 3) / 4) | 1);
   uint8_t* exp_s = smem;
   uint16_t* log_s = reinterpret_cast<uint16_t*>(smem + 1024);
-  int* piv_s = reinterpret_cast<int*>(smem + 1536);  // [0..2] pivot-search slots, [3] parity count
-  uint8_t* perm_s = smem + 1552;  // perm_s[c] = pivot row of column c
+  int* piv_s = reinterpret_cast<int*>(smem + 1536);  // [0..2] pivot-search slots, [3] parity count, [4] bad
+  uint8_t* perm_s = smem + 1568;  // perm_s[c] = pivot row of column c
   uint8_t* prow = perm_s + 256;   // parity survivors (e of them), survivor order (ids < 256)
   uint8_t* rows_s = prow + 256;
   uint8_t* erased_s = rows_s + 256;
@@ -222,10 +231,49 @@ __global__ __launch_bounds__(B) void gf_decode_system_kernel(const uint8_t* __re
   for (int i = kExpLen + tid; i < 1024; i += B) exp_s[i] = 0;
   for (int i = tid; i < 256; i += B) log_s[i] = d_gf_tables.log[i];
   for (int i = tid; i < e * PW; i += B) M[i] = 0;
-  for (int i = tid; i < k; i += B) rows_s[i] = uint8_t(rows[i]);
-  for (int i = tid; i < e; i += B) erased_s[i] = uint8_t(erased[i]);
   if (tid < 3) piv_s[tid] = e;
+  if (tid == 4) piv_s[4] = 0;
   __syncthreads();
+  if (ptrs) {
+    for (int i = tid; i < k; i += B) {
+      const int r = rows[i];
+      const bool ok = r >= 0 && r < n_chunks;
+      rows_s[i] = uint8_t(ok ? r : 0);
+      if (!ok) piv_s[4] = 1;
+    }
+  } else {
+    for (int i = tid; i < k; i += B) rows_s[i] = uint8_t(rows[i]);
+    for (int i = tid; i < e; i += B) erased_s[i] = uint8_t(erased[i]);
+  }
+  __syncthreads();
+  if (ptrs) {
+    // chunk i (one lane each, n_chunks <= 256 = B) counts its occurrences among the survivors
+    // (broadcast LDS reads); missing natives are flagged in perm_s, which the solve reuses later
+    for (int i = tid; i < n_chunks; i += B) {
+      int cnt = 0;
+      for (int j = 0; j < k; ++j) cnt += rows_s[j] == i;
+      if (cnt > 1) piv_s[4] = 1;
+      if (i < k) perm_s[i] = uint8_t(cnt == 0);
+    }
+    __syncthreads();
+    if (tid < 64) {  // erased natives in ascending order: ballot prefix sum in wave 0
+      int base = 0;
+      for (int i0 = 0; i0 < k; i0 += 64) {
+        const int i = i0 + tid;
+        const bool miss = i < k && perm_s[i];
+        const unsigned long long bal = __ballot(miss);
+        const int a = base + __popcll(bal & ((1ull << tid) - 1ull));
+        if (miss && a < e) {
+          erased_s[a] = uint8_t(i);
+          erased[a] = i;
+        }
+        base += __popcll(bal);
+      }
+      if (tid == 0 && base != e) piv_s[4] = 1;
+    }
+    __syncthreads();
+  }
+  const int bad = piv_s[4];
   // parity survivors in survivor order: a ballot prefix sum in wave 0 (a one-lane scan of the
   // global ids was k dependent HBM round trips: ~130 us of the k=128 solve)
   if (tid < 64) {
@@ -241,7 +289,7 @@ __global__ __launch_bounds__(B) void gf_decode_system_kernel(const uint8_t* __re
     if (tid == 0) piv_s[3] = base < e ? base : e;
   }
   __syncthreads();
-  int singular = piv_s[3] != e;  // not exactly e parity survivors: inconsistent pattern
+  int singular = (bad || piv_s[3] != e) ? 1 : 0;  // not exactly e parity survivors: inconsistent pattern
   if (!singular) {
     // the e x (e+k) system, 8 independent global loads in flight per lane
     for (int i0 = tid; i0 < e * W; i0 += 8 * B) {
@@ -320,10 +368,19 @@ __global__ __launch_bounds__(B) void gf_decode_system_kernel(const uint8_t* __re
     __syncthreads();
   }
 
-  if (tid == 0 && status) *status = singular;
+  if (tid == 0 && status) *status = bad ? 2 : singular;
   if (!singular) {
     for (int b = tid; b < e; b += B) pinv_s[b] = exp_s[255 - log_s[byte_at(perm_s[b], b)]];
     __syncthreads();
+  }
+  if (dptr) {  // descriptor row pointers: in[k] | copy[k] | out[m_pad] (desc.h)
+    const uint64_t* outp = ptrs + n_chunks;
+    for (int j = tid; j < k; j += B) {
+      const int r = rows_s[j];
+      dptr[j] = ptrs[r];
+      dptr[k + j] = (!singular && r < k) ? outp[r] : 0;
+    }
+    for (int i = tid; i < m_pad; i += B) dptr[2 * k + i] = (!singular && i < e) ? outp[erased_s[i]] : 0;
   }
   // X[b][j] = M[perm_s[b]][e + j] / M[perm_s[b]][b]
   auto x_at = [&](int b, int j) -> uint32_t {
@@ -348,9 +405,13 @@ __global__ __launch_bounds__(B) void gf_decode_system_kernel(const uint8_t* __re
 
 }  // namespace
 
-hipError_t launch_gf_decode_system(const uint8_t* g, int k, const int* rows, const int* erased, int e, uint8_t* dm,
-                                   int* status, void* desc, int m_pad, hipStream_t stream) {
+hipError_t launch_gf_decode_system(const uint8_t* g, int k, const int* rows, int* erased, int e, uint8_t* dm,
+                                   int* status, void* desc, int m_pad, hipStream_t stream, const uint64_t* ptrs,
+                                   int n_chunks) {
   if (k <= 0 || k > 256 || e <= 0 || e > k || (desc && e > m_pad)) return hipErrorInvalidValue;
+  if (ptrs && (!desc || !erased || n_chunks < k + e || n_chunks > 256)) return hipErrorInvalidValue;
+  uint64_t* dptr = nullptr;
+  if (ptrs) dptr = reinterpret_cast<uint64_t*>(static_cast<char*>(desc) + desc_layout(k, m_pad).in_off);
   const int W = e + k;
   const int PW = (((W + 3) / 4) | 1);
   const size_t lds = kDecSysFixed + 4 * size_t(e) * PW;
@@ -362,7 +423,8 @@ hipError_t launch_gf_decode_system(const uint8_t* g, int k, const int* rows, con
     const hipError_t err = ensure_lds_optin(reinterpret_cast<const void*>(&gf_decode_system_kernel<256>));
     if (err != hipSuccess) return err;
   }
-  gf_decode_system_kernel<256><<<1, 256, lds, stream>>>(g, k, rows, erased, e, dm, status, tab, m_pad);
+  gf_decode_system_kernel<256><<<1, 256, lds, stream>>>(g, k, rows, erased, e, dm, status, tab, m_pad, ptrs,
+                                                        n_chunks, dptr);
   return hipGetLastError();
 }
 

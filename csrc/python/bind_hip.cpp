@@ -116,14 +116,18 @@ PYBIND11_MODULE(_hip, m) {
                             as_stream(stream)),
           "fp4_bitmat");
   });
-  m.def("decode_system", [](uint64_t g, int k, uint64_t rows, uint64_t erased, int e, uint64_t dm, uint64_t status,
-                            uint64_t desc, int m_pad, uint64_t stream) {
-    check(launch_gf_decode_system(reinterpret_cast<const uint8_t*>(g), k, reinterpret_cast<const int*>(rows),
-                                  reinterpret_cast<const int*>(erased), e, reinterpret_cast<uint8_t*>(dm),
-                                  reinterpret_cast<int*>(status), reinterpret_cast<void*>(desc), m_pad,
-                                  as_stream(stream)),
-          "decode_system");
-  });
+  m.def(
+      "decode_system",
+      [](uint64_t g, int k, uint64_t rows, uint64_t erased, int e, uint64_t dm, uint64_t status, uint64_t desc,
+         int m_pad, uint64_t stream, uint64_t ptrs, int n_chunks) {
+        check(launch_gf_decode_system(reinterpret_cast<const uint8_t*>(g), k, reinterpret_cast<const int*>(rows),
+                                      reinterpret_cast<int*>(erased), e, reinterpret_cast<uint8_t*>(dm),
+                                      reinterpret_cast<int*>(status), reinterpret_cast<void*>(desc), m_pad,
+                                      as_stream(stream), reinterpret_cast<const uint64_t*>(ptrs), n_chunks),
+              "decode_system");
+      },
+      py::arg("g"), py::arg("k"), py::arg("rows"), py::arg("erased"), py::arg("e"), py::arg("dm"), py::arg("status"),
+      py::arg("desc"), py::arg("m_pad"), py::arg("stream"), py::arg("ptrs") = 0, py::arg("n_chunks") = 0);
   m.def("fp4_bitmat_sel", [](uint64_t coeff, int ld, uint64_t sel, int mm, int k, uint64_t bitmat, int mg_cap,
                              uint64_t stream) {
     check(launch_fp4_bitmat_sel(reinterpret_cast<const uint8_t*>(coeff), ld, reinterpret_cast<const int*>(sel), mm, k,

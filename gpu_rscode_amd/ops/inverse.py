@@ -73,14 +73,17 @@ def invert_into_plan(a: torch.Tensor, plan: GemmPlan, sel_rows, *, status: torch
 
 
 def decode_system_into_plan(g: torch.Tensor, rows: torch.Tensor, erased: torch.Tensor, plan: GemmPlan, *,
-                            status: torch.Tensor | None = None,
-                            stream: torch.cuda.Stream | None = None) -> torch.Tensor:
+                            status: torch.Tensor | None = None, stream: torch.cuda.Stream | None = None,
+                            ptrs: torch.Tensor | None = None) -> torch.Tensor:
     """Systematic decode with no k x k inverse: solve [G[P, erased] | B'] (e x (e+k)) on device and
     write the decode tables (and, on the matrix-core engine, the bit-matrix) into ``plan``.
 
     ``g``: the (n, k) generator [I; E] on device; ``rows``: the k survivor ids (device int32, the
     plan's input order); ``erased``: the e erased native ids (device int32, the plan's output
     order, e = plan.m). Graph-capturable (no host copies). Returns the device status word.
+    With ``ptrs`` (device int64 [n + k]: every chunk row's address, then every output row's) the plan
+    is built on the device from ``rows`` alone: ``erased`` is derived and written by the kernel, and
+    so are the descriptor's row pointers (see :class:`PatternDecoder`); status 2 = invalid pattern.
     (csrc/kernels/gf_invert.hip::gf_decode_system_kernel.)
     """
     k = g.shape[1]
@@ -98,8 +101,69 @@ def decode_system_into_plan(g: torch.Tensor, rows: torch.Tensor, erased: torch.T
         if getattr(plan, "_dm_buf", None) is None or plan._dm_buf.shape != (plan.m, k):
             plan._dm_buf = torch.empty((plan.m, k), dtype=torch.uint8, device=g.device)
         dm = plan._dm_buf.data_ptr()
+    n_chunks = 0
+    if ptrs is not None:
+        n_chunks = g.shape[0]
+        if ptrs.dtype != torch.int64 or ptrs.device != g.device or ptrs.numel() != n_chunks + k:
+            raise ValueError("ptrs must be a device int64 tensor of n chunk + k output row addresses")
     hip().decode_system(g.data_ptr(), k, rows.data_ptr(), erased.data_ptr(), plan.m, dm, status.data_ptr(),
-                        plan.desc.data_ptr(), plan.m_pad, st.cuda_stream)
+                        plan.desc.data_ptr(), plan.m_pad, st.cuda_stream, 0 if ptrs is None else ptrs.data_ptr(),
+                        n_chunks)
     if plan.engine == "mfma":
         plan.set_device_coeff(plan._dm_buf, stream=st)
     return status
+
+
+class PatternDecoder:
+    """A decode whose erasure pattern lives in DEVICE memory: one plan serves every pattern with
+    ``e`` erased natives, and nothing about the pattern passes through the host.
+
+    ``rows`` (device int32 [k]) holds the survivor chunk ids; it may be written by a kernel, a
+    device copy, or an RCCL broadcast from a coordinator rank (bench.py: rank 0 picks the step's
+    failed chunks — a lost node takes the same chunk index from every stripe, so one pattern per
+    step). :meth:`solve` checks the pattern, solves the systematic decode system and writes the
+    descriptor (row pointers and tables) on the device; :meth:`run` rebuilds the erased natives
+    into ``out`` and copies the surviving natives in the same pass. Both are graph-capturable.
+
+    Args:
+        g: (n, k) generator [I; E] on the device.
+        chunks: the stripe's n rows (k natives then the parity rows), 16-byte aligned.
+        out: k output rows, 16-byte aligned.
+        e: erased natives per pattern (1..min(k, n-k)).
+        engine: GEMM engine ("auto": FP4 matrix cores for wide stripes).
+    """
+
+    def __init__(self, g: torch.Tensor, chunks, out, e: int, engine: str = "auto"):
+        chunks, out = list(chunks), list(out)
+        n, k = g.shape
+        if len(chunks) != n or len(out) != k:
+            raise ValueError(f"need the stripe's {n} chunk rows and {k} output rows")
+        if not 1 <= e <= min(k, n - k):
+            raise ValueError(f"e must be in [1, {min(k, n - k)}]")
+        rows_all = chunks + out
+        if any(r.dtype != torch.uint8 or r.dim() != 1 or r.device != g.device or r.data_ptr() % 16 for r in rows_all):
+            raise ValueError("chunk / output rows must be 16-byte aligned uint8 rows on the generator's device")
+        self.g, self.k, self.n, self.e = g, k, n, e
+        # placeholders until the first solve: inputs = the natives, outputs = the first e output rows
+        self.plan = GemmPlan(chunks[:k], out[:e], copies=out, device_tables=True, engine=engine)
+        self.plan.ncols = min(r.numel() for r in rows_all)
+        if self.plan.engine == "mfma":
+            self.plan.in_stride = 0  # survivors are not equally spaced: DMA row pointers come from the descriptor
+        dev = g.device
+        self.ptrs = torch.tensor([int(r.data_ptr()) for r in rows_all], dtype=torch.int64, device=dev)
+        self.rows = torch.zeros(k, dtype=torch.int32, device=dev)
+        self.erased = torch.zeros(e, dtype=torch.int32, device=dev)
+        self.status = torch.zeros(1, dtype=torch.int32, device=dev)
+        self._keep = rows_all  # the rows the pointer table names stay alive with the decoder
+
+    @property
+    def engine(self) -> str:
+        return self.plan.engine
+
+    def solve(self, stream: torch.cuda.Stream | None = None) -> torch.Tensor:
+        """Build the plan for the pattern now in :attr:`rows` (device work on ``stream``)."""
+        return decode_system_into_plan(self.g, self.rows, self.erased, self.plan, status=self.status, stream=stream,
+                                       ptrs=self.ptrs)
+
+    def run(self, stream: torch.cuda.Stream | None = None, **kw) -> None:
+        self.plan.run(stream, **kw)

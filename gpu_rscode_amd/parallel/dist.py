@@ -24,6 +24,7 @@ link-bound. Shards are 4 KiB-aligned column ranges so every rank's rows stay 16-
 from __future__ import annotations
 
 import os
+import socket
 from dataclasses import dataclass
 
 import numpy as np
@@ -48,15 +49,19 @@ class DistContext:
         return self.rank == 0
 
 
-def init_distributed(backend: str | None = None) -> DistContext:
+def init_distributed(backend: str | None = None, force_pg: bool | None = None) -> DistContext:
     """Initialise from torchrun's environment (RANK, WORLD_SIZE, LOCAL_RANK, MASTER_*).
 
     Backend defaults to ``nccl`` (RCCL) when a GPU is visible, else ``gloo``. Safe to call when a
-    process group already exists.
+    process group already exists. At world 1 no process group is created unless ``force_pg`` (or
+    ``GFRS_FORCE_PG=1``): then a one-rank group runs every collective against rank 0 itself, which
+    is how the RCCL code paths execute on a single MI355X (tests, ``bench.py --force-pg``).
     """
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if force_pg is None:
+        force_pg = os.environ.get("GFRS_FORCE_PG") == "1"
     use_gpu = torch.cuda.is_available() and torch.cuda.device_count() > 0 and backend != "gloo"
     if use_gpu:
         torch.cuda.set_device(local)
@@ -64,14 +69,28 @@ def init_distributed(backend: str | None = None) -> DistContext:
     else:
         device = torch.device("cpu")
     backend = backend or ("nccl" if use_gpu else "gloo")
-    if world > 1 and not dist.is_initialized():
+    if (world > 1 or force_pg) and not dist.is_initialized():
         kw = {"device_id": device} if device.type == "cuda" else {}
+        if world == 1 and "MASTER_PORT" not in os.environ:
+            kw.update(init_method=f"tcp://127.0.0.1:{free_port()}", rank=0, world_size=1)
         dist.init_process_group(backend, **kw)
     return DistContext(rank, world, local, device, backend)
 
 
+def free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
 def _world() -> int:
     return dist.get_world_size() if dist.is_initialized() else 1
+
+
+def _self_p2p() -> bool:
+    """A one-rank process group: a rank's own piece moves through RCCL send/recv to itself, so the
+    grouped point-to-point path of N > 1 runs unchanged at world 1 (--force-pg)."""
+    return dist.is_initialized() and dist.get_world_size() == 1 and dist.get_backend() == "nccl"
 
 
 def _rank() -> int:
@@ -89,7 +108,7 @@ def shard_range(ncols: int, world: int, rank: int, align: int = SHARD_ALIGN) -> 
 
 def broadcast_matrix(mat: np.ndarray | None, device: torch.device, src: int = 0) -> np.ndarray:
     """Broadcast a small uint8 matrix (E, or a decode inverse) from ``src`` to every rank."""
-    if _world() == 1:
+    if not dist.is_initialized():
         return np.asarray(mat, dtype=np.uint8)
     shape = torch.zeros(2, dtype=torch.int64, device=device)
     if _rank() == src:
@@ -104,24 +123,38 @@ def broadcast_matrix(mat: np.ndarray | None, device: torch.device, src: int = 0)
     return buf.cpu().numpy()
 
 
+def _aligned_rows(t: torch.Tensor) -> bool:
+    return t.stride(1) == 1 and t.data_ptr() % 16 == 0 and (t.shape[0] <= 1 or t.stride(0) % 16 == 0)
+
+
 def scatter_columns(full: torch.Tensor | None, rows: int, ncols: int, device: torch.device, src: int = 0,
                     align: int = SHARD_ALIGN) -> torch.Tensor:
     """Rank ``src`` holds ``full`` [rows, ncols] (unit column stride); every rank gets its column
-    shard [rows, b - a].
+    shard [rows, b - a] on ``device``.
 
     Point-to-point, one message per (peer, row): every row piece travels straight from its place in
     ``full`` into the receiver's pitched shard (256-byte row pitch, 16-byte aligned rows for the GEMM
     kernels) — no staging copies on either side. Rank ``src`` returns a view of its own shard inside
-    ``full`` (nothing moves)."""
+    ``full`` when that is already on ``device`` with 16-byte aligned rows (nothing moves); otherwise
+    its shard is copied into pitched rows on ``device`` (through RCCL send/recv to itself on a
+    one-rank group), so no rank falls back to the bytewise kernel for an odd C."""
     world, rank = _world(), _rank()
     a, b = shard_range(ncols, world, rank, align)
+    own_p2p = False
     if rank == src:
         if full is None or full.dim() != 2 or full.stride(1) != 1 or full.shape[0] != rows or full.shape[1] < ncols:
             raise ValueError("scatter_columns: rank src needs full [rows, >= ncols] with unit column stride")
-        local = full[:, a:b]
+        view = full[:, a:b]
+        if full.device == device and _aligned_rows(view):
+            local = view
+        else:
+            local = alloc_rows(rows, b - a, device)
+            own_p2p = _self_p2p() and full.device == device and device.type == "cuda"
+            if not own_p2p:
+                local.copy_(view)
     else:
         local = alloc_rows(rows, b - a, device)
-    if world == 1:
+    if not dist.is_initialized():
         return local
     ops = []
     if rank == src:
@@ -129,6 +162,9 @@ def scatter_columns(full: torch.Tensor | None, rows: int, ncols: int, device: to
             ra, rb = shard_range(ncols, world, r, align)
             if r != src and rb > ra:
                 ops += [dist.P2POp(dist.isend, full[i, ra:rb], r) for i in range(rows)]
+        if own_p2p and b > a:
+            for i in range(rows):
+                ops += [dist.P2POp(dist.isend, full[i, a:b], src), dist.P2POp(dist.irecv, local[i], src)]
     elif b > a:
         ops += [dist.P2POp(dist.irecv, local[i], src) for i in range(rows)]
     if ops:
@@ -137,27 +173,41 @@ def scatter_columns(full: torch.Tensor | None, rows: int, ncols: int, device: to
     return local
 
 
-def gather_pieces(local: torch.Tensor, widths: list[int], dst: int = 0) -> torch.Tensor | None:
+def gather_pieces(local: torch.Tensor, widths: list[int], dst: int = 0,
+                  out: torch.Tensor | None = None) -> torch.Tensor | None:
     """Rank r contributes ``local`` [rows, widths[r]] (rows 1-D contiguous); rank ``dst`` returns the
-    pieces side by side in rank order as one pitched [rows, sum(widths)] tensor, others None.
+    pieces side by side in rank order as one [rows, sum(widths)] tensor (``out`` if given, else a new
+    pitched one), others None.
 
     One point-to-point message per (peer, row), received in place into the destination's column
-    slice — each peer drives its own xGMI link into ``dst``; the only copy is dst's own piece."""
+    slice — each peer drives its own xGMI link into ``dst``. dst's own piece is not moved when
+    ``local`` already is that slice of ``out``; otherwise it is copied (RCCL send/recv to itself on a
+    one-rank group)."""
     world, rank = _world(), _rank()
     rows = local.shape[0]
     if len(widths) != world or local.shape[1] != widths[rank]:
         raise ValueError("gather_pieces: widths must list every rank's piece width (this rank's = local.shape[1])")
-    if world == 1:
-        return local
+    if out is None and not dist.is_initialized():
+        return local  # one process, no group: the piece is the whole
     ops = []
     full = None
     if rank == dst:
         offs = [0]
         for w in widths:
             offs.append(offs[-1] + w)
-        full = alloc_rows(rows, offs[-1], local.device)
-        if widths[dst]:
-            full[:, offs[dst]:offs[dst + 1]].copy_(local)
+        if out is None:
+            full = alloc_rows(rows, offs[-1], local.device)
+        else:
+            if out.dim() != 2 or out.shape[0] != rows or out.shape[1] < offs[-1] or out.stride(1) != 1:
+                raise ValueError("gather_pieces: out must be [rows, >= sum(widths)] with unit column stride")
+            full = out
+        mine = full[:, offs[dst]:offs[dst + 1]]
+        if widths[dst] and mine.data_ptr() != local.data_ptr():
+            if _self_p2p() and local.device.type == "cuda":
+                for i in range(rows):
+                    ops += [dist.P2POp(dist.isend, local[i], dst), dist.P2POp(dist.irecv, mine[i], dst)]
+            else:
+                mine.copy_(local)
         for r in range(world):
             if r != dst and widths[r]:
                 ops += [dist.P2POp(dist.irecv, full[i, offs[r]:offs[r + 1]], r) for i in range(rows)]

@@ -1,4 +1,4 @@
-"""Per-step parity placement over torch.distributed (RCCL over xGMI on MI355X, gloo on CPU).
+"""Per-step placement of coded bytes over torch.distributed (RCCL over xGMI on MI355X, gloo on CPU).
 
 After every rank has encoded its own stripe, its parity has to leave the GPU for where it is
 stored. The reference gathers every device's parity slices into one host buffer after the worker
@@ -8,17 +8,26 @@ decides which links carry it:
 
 ``root``   every peer sends its whole parity block to rank 0 (the reference's pattern, as grouped
            point-to-point send/recv: each peer drives its own link into rank 0). Rank 0's inbound
-           links carry (N-1) blocks per step; the other 6·N links of the mesh idle.
+           links carry (N-1) blocks per step; the other links of the mesh idle.
 ``owners`` parity is placed chunk-contiguously: the concatenation of every rank's parity bytes is
            cut into N equal contiguous pieces and rank o owns piece o (it receives 1/N of every
            rank's block). That is one ``all_to_all_single`` in which every link of the mesh carries
-           1/N of a block instead of a whole one — the xGMI-native placement: N× less traffic on the
-           busiest link than ``root``, spread over all N-1 links of every GPU.
+           1/N of a block instead of a whole one — N× less traffic on the busiest link than
+           ``root``, spread over all N-1 links of every GPU.
 ``none``   no traffic (compute-only reference point).
 
+:class:`StripeGather` is the strong-scaling form (one stripe column-sharded over all ranks, the
+reference's multi-GPU semantics, ``src/encode.cu:368-381``): every rank's column piece of the
+parity and decoded rows lands in place in rank 0's full rows.
+
 Exchanges run asynchronously on the process group's own stream (RCCL's internal stream on GPU) so
-the next step's encode/decode overlaps them; :meth:`ParityExchange.wait` orders a later overwrite
-of a source buffer after the exchange that reads it (double-buffered sources).
+the next step's encode/decode overlaps them. Every slot has its own receive storage, so exchanges
+of consecutive slots never share a destination; :meth:`wait` orders a later overwrite of a source
+buffer after the exchange that reads it (double-buffered sources).
+
+With a one-rank RCCL process group (``bench.py --force-pg``, ``GFRS_FORCE_PG=1``) the same calls run
+against rank 0 itself: ``owners`` is an ``all_to_all_single`` to self and ``root`` a grouped
+send/recv to self, so every RCCL code path executes on a single MI355X.
 """
 from __future__ import annotations
 
@@ -34,11 +43,29 @@ def even_splits(nbytes: int, world: int) -> list[int]:
     return [base + (1 if r < rem else 0) for r in range(world)]
 
 
-def _checksum(x: torch.Tensor) -> torch.Tensor:
-    """Two int64 digests of a flat uint8 tensor: byte sum and a position-weighted sum of a prefix."""
-    n = min(x.numel(), 1 << 16)
-    w = torch.arange(1, n + 1, dtype=torch.int64, device=x.device)
-    return torch.stack([x.sum(dtype=torch.int64), (x[:n].to(torch.int64) * w).sum()])
+def _checksum(x: torch.Tensor, chunk: int = 1 << 26) -> torch.Tensor:
+    """Two int64 digests of a flat uint8 tensor: byte sum and a position-weighted sum of all bytes
+    (weights cycle through 1..65536, so a moved or swapped byte changes it). Chunked, so a GiB-sized
+    row needs only 2 x 512 MiB of int64 temporaries."""
+    out = torch.zeros(2, dtype=torch.int64, device=x.device)
+    for a in range(0, x.numel(), chunk):
+        c = x[a:a + chunk].to(torch.int64)
+        w = torch.arange(a, a + c.numel(), dtype=torch.int64, device=x.device).remainder_(1 << 16).add_(1)
+        out[0] += c.sum()
+        out[1] += (c * w).sum()
+    return out
+
+
+def _pg_world_rank() -> tuple[int, int, bool]:
+    if dist.is_initialized():
+        return dist.get_world_size(), dist.get_rank(), True
+    return 1, 0, False
+
+
+def _self_loop() -> bool:
+    """A one-rank RCCL group: a rank's own block travels through send/recv to itself (gloo has no
+    self point-to-point; there the own block simply stays put)."""
+    return dist.is_initialized() and dist.get_world_size() == 1 and dist.get_backend() == "nccl"
 
 
 class ParityExchange:
@@ -49,6 +76,9 @@ class ParityExchange:
             one per pipeline slot. Every rank must pass the same sizes.
         mode: ``"owners"``, ``"root"`` or ``"none"`` (see module docstring).
         root: destination rank of ``"root"``.
+
+    Receive storage is per slot: ``recvs[slot]`` (owners: the pieces this rank owns, in source-rank
+    order) and ``recv_lists[slot][r]`` (root, on the root: rank r's block).
     """
 
     def __init__(self, sources: list[torch.Tensor], mode: str = "owners", root: int = 0):
@@ -59,23 +89,26 @@ class ParityExchange:
         if len({s.numel() for s in sources}) != 1:
             raise ValueError("every source buffer must have the same size")
         self.sources = sources
-        self.world = dist.get_world_size() if dist.is_initialized() else 1
-        self.rank = dist.get_rank() if dist.is_initialized() else 0
-        self.mode = mode if self.world > 1 else "none"
+        self.world, self.rank, has_pg = _pg_world_rank()
+        # a one-rank process group still runs the exchange (against itself): --force-pg
+        self.mode = mode if has_pg else "none"
+        self.self_loop = _self_loop()
         self.root = root
         self.nbytes = sources[0].numel()
         dev = sources[0].device
-        self.recv: torch.Tensor | None = None
-        self.recv_list: list[torch.Tensor | None] = []
+        slots = len(sources)
+        self.recvs: list[torch.Tensor | None] = [None] * slots
+        self.recv_lists: list[list[torch.Tensor | None]] = [[] for _ in range(slots)]
         if self.mode == "owners":
             self.in_splits = even_splits(self.nbytes, self.world)
             mine = self.in_splits[self.rank]
             self.out_splits = [mine] * self.world  # every source sends me its piece `rank`
-            self.recv = torch.empty(mine * self.world, dtype=torch.uint8, device=dev)
+            self.recvs = [torch.empty(mine * self.world, dtype=torch.uint8, device=dev) for _ in range(slots)]
         elif self.mode == "root" and self.rank == root:
-            self.recv_list = [torch.empty(self.nbytes, dtype=torch.uint8, device=dev) if r != root else None
-                              for r in range(self.world)]
-        self.pending: list[list | None] = [None] * len(sources)
+            self.recv_lists = [[torch.empty(self.nbytes, dtype=torch.uint8, device=dev)
+                                if (r != root or self.self_loop) else None for r in range(self.world)]
+                               for _ in range(slots)]
+        self.pending: list[list | None] = [None] * slots
 
     # ---- traffic accounting (per step) ---------------------------------------------------------
     @property
@@ -99,7 +132,9 @@ class ParityExchange:
     def bytes_per_link(self) -> int:
         """Bytes the busiest point-to-point link carries per step (one direction): owners — one
         rank's piece (every ordered pair of ranks exchanges one piece over its direct xGMI link);
-        root — a whole block into the root."""
+        root — a whole block into the root. Zero at world 1 (nothing crosses a link)."""
+        if self.world == 1:
+            return 0
         if self.mode == "owners":
             return max(self.in_splits)
         if self.mode == "root":
@@ -115,15 +150,15 @@ class ParityExchange:
         self.wait(slot)
         src = self.sources[slot]
         if self.mode == "owners":
-            w = dist.all_to_all_single(self.recv, src, self.out_splits, self.in_splits, async_op=True)
+            w = dist.all_to_all_single(self.recvs[slot], src, self.out_splits, self.in_splits, async_op=True)
             self.pending[slot] = [w]
             return
         ops = []
         if self.rank == self.root:
             for r in range(self.world):
-                if r != self.root:
-                    ops.append(dist.P2POp(dist.irecv, self.recv_list[r], r))
-        else:
+                if r != self.root or self.self_loop:
+                    ops.append(dist.P2POp(dist.irecv, self.recv_lists[slot][r], r))
+        if self.rank != self.root or self.self_loop:
             ops.append(dist.P2POp(dist.isend, src, self.root))
         self.pending[slot] = dist.batch_isend_irecv(ops) if ops else None
 
@@ -141,8 +176,9 @@ class ParityExchange:
 
     # ---- verification (outside timed regions) ---------------------------------------------------
     def verify(self, slot: int) -> bool:
-        """True when what the last exchange delivered equals the senders' ``sources[slot]`` pieces
-        (checksums exchanged with the same pattern). Collective: every rank must call it."""
+        """True when what slot ``slot``'s last exchange delivered equals the senders' ``sources[slot]``
+        pieces (checksums of every byte, exchanged with the same pattern). Collective: every rank
+        must call it."""
         if self.mode == "none":
             return True
         self.drain()
@@ -156,8 +192,8 @@ class ParityExchange:
             expect = torch.empty_like(send)
             dist.all_to_all_single(expect, send)
             mine = self.in_splits[self.rank]
-            got = torch.stack([_checksum(self.recv[r * mine:(r + 1) * mine]) for r in range(self.world)])
-            # my own piece never travels: it is compared against itself (recv holds a copy of it)
+            recv = self.recvs[slot]
+            got = torch.stack([_checksum(recv[r * mine:(r + 1) * mine]) for r in range(self.world)])
             ok = torch.equal(got, expect)
         else:
             mine = _checksum(src)
@@ -165,8 +201,117 @@ class ParityExchange:
             dist.gather(mine, allsum, dst=self.root)
             ok = True
             if self.rank == self.root:
-                ok = all(torch.equal(_checksum(self.recv_list[r]), allsum[r])
-                         for r in range(self.world) if r != self.root)
+                ok = all(torch.equal(_checksum(self.recv_lists[slot][r]), allsum[r])
+                         for r in range(self.world) if r != self.root or self.self_loop)
+        flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        return bool(flag.item())
+
+
+class StripeGather:
+    """Strong scaling's per-step gather: rank r's column piece ``[offs[r], offs[r+1])`` of every row
+    lands in place in rank ``dst``'s full rows (the reference's H2H gather of parity and decoded
+    slices after its device threads join, ``src/encode.cu:410-429``, ``src/decode.cu:380-405``, as
+    grouped point-to-point — one message per (peer, row), each peer on its own xGMI link).
+
+    Args:
+        pieces: per slot, this rank's 1-D piece rows (same row count on every rank and slot).
+        fulls: per slot, on ``dst`` only: the full rows (``sum(widths)`` bytes each). When dst's
+            piece rows are views of the full rows at offset 0 (it computed in place) nothing moves
+            for its own piece; otherwise it is copied (or, on a one-rank RCCL group, sent to self).
+        widths: every rank's piece width in bytes.
+    """
+
+    def __init__(self, pieces: list[list[torch.Tensor]], fulls: list[list[torch.Tensor]] | None,
+                 widths: list[int], dst: int = 0):
+        self.world, self.rank, self.has_pg = _pg_world_rank()
+        if len(widths) != self.world:
+            raise ValueError("widths must list every rank's piece width")
+        self.pieces, self.fulls, self.widths, self.dst = pieces, fulls, widths, dst
+        self.offs = [0]
+        for w in widths:
+            self.offs.append(self.offs[-1] + w)
+        if any(len(p) != len(pieces[0]) for p in pieces) or any(r.numel() < widths[self.rank] for p in pieces for r in p):
+            raise ValueError("every slot needs the same number of piece rows, each widths[rank] bytes")
+        if self.rank == dst:
+            if fulls is None or len(fulls) != len(pieces) or any(len(f) != len(pieces[0]) for f in fulls):
+                raise ValueError("rank dst needs full rows for every slot")
+            if any(r.numel() < self.offs[-1] for f in fulls for r in f):
+                raise ValueError("full rows must hold sum(widths) bytes")
+        self.self_loop = _self_loop()
+        self.pending: list[list | None] = [None] * len(pieces)
+
+    def _in_place(self, slot: int) -> bool:
+        w = self.widths[self.dst]
+        return all(p.data_ptr() == f.data_ptr() for p, f in zip(self.pieces[slot], self.fulls[slot])) or w == 0
+
+    @property
+    def bytes_per_link(self) -> int:
+        """Bytes the busiest link into dst carries per step (one peer's piece of every row)."""
+        rows = len(self.pieces[0])
+        peers = [self.widths[r] for r in range(self.world) if r != self.dst]
+        return rows * max(peers) if peers else 0
+
+    @property
+    def bytes_received(self) -> int:
+        rows = len(self.pieces[0])
+        return rows * (self.offs[-1] - self.widths[self.dst]) if self.rank == self.dst else 0
+
+    def start(self, slot: int) -> None:
+        self.wait(slot)
+        w_mine = self.widths[self.rank]
+        ops = []
+        if self.rank == self.dst:
+            full, mine = self.fulls[slot], self.pieces[slot]
+            own_moves = w_mine and not self._in_place(slot)
+            for r in range(self.world):
+                if r == self.dst or not self.widths[r]:
+                    continue
+                a, b = self.offs[r], self.offs[r + 1]
+                ops += [dist.P2POp(dist.irecv, row[a:b], r) for row in full]
+            if own_moves:
+                a, b = self.offs[self.dst], self.offs[self.dst + 1]
+                if self.self_loop:
+                    for row, src in zip(full, mine):
+                        ops += [dist.P2POp(dist.irecv, row[a:b], self.dst), dist.P2POp(dist.isend, src[:w_mine],
+                                                                                        self.dst)]
+                else:
+                    for row, src in zip(full, mine):
+                        row[a:b].copy_(src[:w_mine], non_blocking=True)
+        elif w_mine:
+            ops += [dist.P2POp(dist.isend, row[:w_mine], self.dst) for row in self.pieces[slot]]
+        self.pending[slot] = dist.batch_isend_irecv(ops) if ops else None
+
+    def wait(self, slot: int) -> None:
+        works = self.pending[slot]
+        if works:
+            for w in works:
+                w.wait()
+        self.pending[slot] = None
+
+    def drain(self) -> None:
+        for s in range(len(self.pieces)):
+            self.wait(s)
+
+    def verify(self, slot: int) -> bool:
+        """dst's full rows equal every rank's pieces (checksums of every byte). Collective."""
+        self.drain()
+        dev = self.pieces[slot][0].device
+        w_mine = self.widths[self.rank]
+        mine = torch.stack([_checksum(r[:w_mine]) for r in self.pieces[slot]])  # [rows, 2]
+        if self.world == 1 and not self.has_pg:
+            allsum = [mine]
+        else:
+            allsum = [torch.empty_like(mine) for _ in range(self.world)] if self.rank == self.dst else None
+            dist.gather(mine, allsum, dst=self.dst)
+        ok = True
+        if self.rank == self.dst:
+            for r in range(self.world):
+                a, b = self.offs[r], self.offs[r + 1]
+                got = torch.stack([_checksum(row[a:b]) for row in self.fulls[slot]])
+                ok = ok and torch.equal(got, allsum[r])
+        if not self.has_pg:
+            return bool(ok)
         flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
         dist.all_reduce(flag, op=dist.ReduceOp.MIN)
         return bool(flag.item())

@@ -32,17 +32,43 @@ def test_launcher_runs_world_ranks_and_reports_every_comm_mode(gpus):
     assert r.returncode == 0, r.stderr[-3000:]
     rec = _record(r.stdout)
     assert rec["n_gpus"] == gpus and rec["steps"] == 3 and rec["warmup"] == 1
-    assert rec["verified"] is True
-    assert rec["config"]["comm"] == "owners" and rec["config"]["parallelism"].startswith(f"dp{gpus}")
+    assert rec["verified"] is True and rec["scaling"] == "weak" and "headline_why" in rec
+    assert rec["config"]["comm"] == "bcast" and rec["config"]["parallelism"].startswith(f"dp{gpus}")
     by = rec["value_by_comm"]
-    assert set(by) == {"owners", "root", "none"} and all(v["verified"] for v in by.values())
+    assert set(by) == {"bcast", "owners", "root", "none"} and all(v["verified"] for v in by.values())
     par_bytes = by["owners"]["bytes_sent_per_rank_step"]
     assert par_bytes > 0 and by["none"]["bytes_sent_per_rank_step"] == 0
+    assert by["bcast"]["bytes_sent_per_rank_step"] == 0  # the headline keeps parity in place
     assert by["root"]["bytes_recv_rank0_step"] > par_bytes  # rank 0 takes whole blocks from every peer
-    assert rec["value"] == by["owners"]["GBps"] and rec["value_no_comm"] == by["none"]["GBps"]
+    assert rec["value"] == by["bcast"]["GBps"] and rec["value_no_comm"] == by["none"]["GBps"]
     # busiest link: one piece per ordered pair (owners) vs a whole block into rank 0 (root)
     assert by["root"]["busiest_link_bytes_per_step"] > by["owners"]["busiest_link_bytes_per_step"] > 0
     assert by["none"]["busiest_link_bytes_per_step"] == 0 and by["owners"]["busiest_link_GBps_implied"] > 0
+    # the reference's strong scaling: one stripe sharded over the ranks, gathered into rank 0 per step
+    st = rec["strong"]
+    assert st["verified"] is True and rec["value_strong"] == st["GBps"] and len(st["shard_cols"]) == gpus
+    assert sum(st["shard_cols"]) == (300_001 + 9) // 10 and st["gather"] == "step"
+    assert st["bytes_recv_rank0"] == 14 * (sum(st["shard_cols"]) - st["shard_cols"][0])
+
+
+@pytest.mark.parametrize("gather", ["step", "end"])
+def test_strong_scaling_headline(gather):
+    r = _run(["--device", "cpu", "--gpus", "2", "--scaling", "strong", "--gather", gather, "--steps", "2",
+              "--warmup", "1", "--bytes", str(200_003)])
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = _record(r.stdout)
+    assert rec["scaling"] == "strong" and rec["verified"] is True and rec["value"] == rec["value_strong"]
+    assert rec["config"]["comm"] == f"strong/{gather}" and "value_by_comm" not in rec
+    if gather == "end":
+        assert rec["strong"]["gather_ms"] > 0
+
+
+def test_forced_one_rank_group_runs_every_mode():
+    r = _run(["--device", "cpu", "--force-pg", "--steps", "2", "--warmup", "1", "--bytes", str(100_000)])
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = _record(r.stdout)
+    assert rec["n_gpus"] == 1 and rec["config"]["process_group"] is True and rec["verified"] is True
+    assert set(rec["value_by_comm"]) == {"bcast", "owners", "root", "none"} and rec["strong"]["verified"]
 
 
 def test_single_rank_record_and_comm_choice():
@@ -63,7 +89,8 @@ def test_world_size_mismatch_is_an_error():
 @pytest.mark.parametrize("preset,erased", [("k10n14", 4), ("k128n160", 32)])
 def test_gpu_bench_record_with_worst_case_e2e_decode(preset, erased):
     """One rank on the MI355X, 64 MiB: the device step verifies, and the e2e block's decode rebuilds
-    the first `erasures` natives (src/unit-test.sh keeps the last k chunks) through the host pipeline."""
+    the first `erasures` natives (src/unit-test.sh keeps the last k chunks) through the host pipeline,
+    and its reference-shaped decode writes all k natives into one pinned file image."""
     r = _run(["--preset", preset, "--steps", "3", "--warmup", "1", "--bytes", str(64 << 20)], timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]
     rec = _record(r.stdout)
@@ -71,4 +98,26 @@ def test_gpu_bench_record_with_worst_case_e2e_decode(preset, erased):
     assert rec["config"]["engine"] == ("mfma" if preset == "k128n160" else "valu")
     e2e = rec["e2e"]
     assert e2e["verified"] is True and e2e["erased"] == erased
-    assert e2e["encode_GBps"] > 0 and e2e["decode_GBps"] > 0
+    assert e2e["encode_GBps"] > 0 and e2e["decode_GBps"] > 0 and e2e["decode_full_GBps"] > 0
+
+
+@pytest.mark.gpu
+def test_gpu_bench_forced_rccl_group_every_mode():
+    """--force-pg on one MI355X: a one-rank RCCL group runs the per-step pattern broadcast, the owners
+    all_to_all (to self), the root grouped send/recv (to self) and the strong-scaling gather — every
+    RCCL path of the N > 1 run — and each mode verifies."""
+    r = _run(["--force-pg", "--steps", "4", "--warmup", "1", "--bytes", str(64 << 20), "--no-e2e"], timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = _record(r.stdout)
+    assert rec["verified"] is True and rec["config"]["process_group"] is True
+    assert set(rec["value_by_comm"]) == {"bcast", "owners", "root", "none"}
+    assert all(v["verified"] for v in rec["value_by_comm"].values()) and rec["strong"]["verified"] is True
+
+
+@pytest.mark.gpu
+def test_gpu_bench_strong_gather_end_one_rank_group():
+    r = _run(["--force-pg", "--scaling", "strong", "--gather", "end", "--steps", "3", "--warmup", "1",
+              "--bytes", str(32 << 20)], timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = _record(r.stdout)
+    assert rec["verified"] is True and rec["scaling"] == "strong" and rec["strong"]["gather_ms"] >= 0

@@ -83,7 +83,8 @@ def _case_distributed_codec(ctx):
 
 def _case_parity_exchange(ctx):
     """ParityExchange delivers exactly the senders' bytes: owners = piece `rank` of every rank's
-    block, in source order; root = every peer's whole block on rank 0. Two alternating slots."""
+    block, in source order; root = every peer's whole block on rank 0. Two alternating slots, each
+    with its own receive storage."""
     from gpu_rscode_amd.parallel.placement import ParityExchange, even_splits
 
     nbytes = 3 * 4096 + 17  # not divisible by the world size: uneven pieces
@@ -91,28 +92,88 @@ def _case_parity_exchange(ctx):
     def block(r, slot):
         return torch.arange(nbytes, dtype=torch.int64).add(7 * r + 131 * slot).remainder(251).to(torch.uint8)
 
+    def check(x, mode, slot):
+        if mode == "owners":
+            sp = even_splits(nbytes, ctx.world)
+            off = sum(sp[: ctx.rank])
+            mine = sp[ctx.rank]
+            want = torch.cat([block(r, slot)[off:off + mine] for r in range(ctx.world)])
+            assert torch.equal(x.recvs[slot], want), (mode, slot)
+            assert x.bytes_sent == nbytes - mine and x.bytes_received == mine * (ctx.world - 1)
+        elif mode == "root" and ctx.rank == 0:
+            for r in range(1, ctx.world):
+                assert torch.equal(x.recv_lists[slot][r], block(r, slot)), (mode, slot, r)
+
     srcs = [block(ctx.rank, s) for s in range(2)]
     for mode in ("owners", "root", "none"):
         x = ParityExchange(srcs, mode)
         for slot in (0, 1, 0):
             x.start(slot)
             x.wait(slot)
-            if mode == "owners":
-                sp = even_splits(nbytes, ctx.world)
-                off = sum(sp[: ctx.rank])
-                mine = sp[ctx.rank]
-                want = torch.cat([block(r, slot)[off:off + mine] for r in range(ctx.world)])
-                assert torch.equal(x.recv, want), (mode, slot)
-                assert x.bytes_sent == nbytes - mine and x.bytes_received == mine * (ctx.world - 1)
-            elif mode == "root" and ctx.rank == 0:
-                for r in range(1, ctx.world):
-                    assert torch.equal(x.recv_list[r], block(r, slot)), (mode, slot, r)
+            check(x, mode, slot)
+            assert x.verify(slot)
+        # both slots in flight at once: start(0), start(1), wait(0), wait(1) — neither slot's
+        # delivery may be torn by the other's
+        x.start(0)
+        x.start(1)
+        x.wait(0)
+        x.wait(1)
+        for slot in (0, 1):
+            check(x, mode, slot)
             assert x.verify(slot)
         x.drain()
 
 
+def _case_stripe_gather(ctx):
+    """StripeGather: every rank's column piece of each slot's rows lands in rank 0's full rows; rank
+    0's own piece is computed in place (a view of its full rows) and never moves."""
+    from gpu_rscode_amd.parallel.placement import StripeGather
+
+    ncols, rows, slots = 3 * 4096 + 77, 3, 2
+    widths = [b - a for a, b in (pdist.shard_range(ncols, ctx.world, r) for r in range(ctx.world))]
+    a, b = pdist.shard_range(ncols, ctx.world, ctx.rank)
+
+    def content(slot):
+        return (torch.arange(rows * ncols, dtype=torch.int64).view(rows, ncols) * 3 + 17 * slot).remainder(251).to(
+            torch.uint8)
+
+    fulls = None
+    if ctx.rank == 0:
+        full_t = [torch.zeros((rows, ncols), dtype=torch.uint8) for _ in range(slots)]
+        fulls = [[f[i] for i in range(rows)] for f in full_t]
+        pieces_t = [f[:, : b - a] for f in full_t]
+    else:
+        pieces_t = [torch.zeros((rows, b - a), dtype=torch.uint8) for _ in range(slots)]
+    for s in range(slots):
+        pieces_t[s].copy_(content(s)[:, a:b])
+    g = StripeGather([[p[i] for i in range(rows)] for p in pieces_t], fulls, widths)
+    g.start(0)
+    g.start(1)
+    g.wait(0)
+    g.wait(1)
+    for s in range(slots):
+        assert g.verify(s)
+        if ctx.rank == 0:
+            assert torch.equal(full_t[s], content(s))
+    if ctx.rank == 0:
+        assert g.bytes_received == rows * (ncols - widths[0])
+
+
+def _case_scatter_odd_c_alignment(ctx):
+    """An odd C in a plain contiguous [k, C] tensor: row i starts at i*C, so rank 0's shard cannot be
+    a view — it gets a pitched, 16-byte aligned copy like every other rank."""
+    C = 2 * 4096 + 4095
+    full = torch.arange(4 * C, dtype=torch.int64).remainder(253).to(torch.uint8).view(4, C)
+    shard = pdist.scatter_columns(full if ctx.rank == 0 else None, 4, C, ctx.device)
+    a, b = pdist.shard_range(C, ctx.world, ctx.rank)
+    assert torch.equal(shard, full[:, a:b])
+    assert all(shard[i].data_ptr() % 16 == 0 for i in range(4))
+    if ctx.rank == 0:
+        assert shard.data_ptr() != full.data_ptr()
+
+
 @pytest.mark.parametrize("case", ["_case_broadcast", "_case_scatter_gather", "_case_distributed_codec",
-                                  "_case_parity_exchange"])
+                                  "_case_parity_exchange", "_case_stripe_gather", "_case_scatter_odd_c_alignment"])
 def test_distributed_world2(case):
     _run(case, 2)
 
@@ -123,3 +184,25 @@ def test_distributed_codec_world3():
 
 def test_parity_exchange_world3():
     _run("_case_parity_exchange", 3)
+
+
+def test_stripe_gather_world3():
+    _run("_case_stripe_gather", 3)
+
+
+def _forced_worker(rank, fn_name):
+    for v in ("MASTER_PORT", "WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        os.environ.pop(v, None)
+    ctx = pdist.init_distributed(backend="gloo", force_pg=True)
+    assert dist.is_initialized() and dist.get_world_size() == 1
+    try:
+        globals()[fn_name](ctx)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("case", ["_case_broadcast", "_case_distributed_codec", "_case_parity_exchange",
+                                  "_case_stripe_gather"])
+def test_forced_one_rank_group(case):
+    """--force-pg: a one-rank process group runs the same collectives against itself."""
+    mp.spawn(_forced_worker, args=(case,), nprocs=1, join=True)

@@ -286,3 +286,103 @@ def test_rs_cli_device_list_shards(tmp_path, devices):
                        capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     assert (tmp_path / "out.bin").read_bytes() == payload
+
+
+@pytest.mark.parametrize("k,n,e,C", [(10, 14, 3, 1_000_003), (4, 6, 2, 65537), (128, 160, 26, 1 << 20)])
+def test_pattern_decoder_device_built_plans(k, n, e, C):
+    """One PatternDecoder serves every pattern with e erased natives: the survivor list is written
+    into device memory only, the kernel derives the erased natives, the row pointers and the tables
+    (no host involvement), and the fused pass rebuilds + copies every native. k=128 runs the FP4
+    matrix-core decode from descriptor row pointers."""
+    from gpu_rscode_amd.ops import PatternDecoder
+
+    rs = ReedSolomon(k, n)
+    host, data = _data(k, C, 5)
+    parity = rs.encode(data)
+    out = alloc_rows(k, C, "cuda", fill=0)
+    g = torch.from_numpy(rs.G).cuda()
+    dec = PatternDecoder(g, [data[i] for i in range(k)] + [parity[i] for i in range(n - k)], [out[i] for i in range(k)], e)
+    assert dec.engine == ("mfma" if k >= 64 else "valu")
+    rng = np.random.default_rng(9)
+    tested = 0
+    while tested < 4:
+        nat = rng.choice(k, size=e, replace=False).tolist()
+        extra = rng.choice(n - k, size=min(n - k - e, 1) if n - k > e else 0, replace=False).tolist()
+        erased = set(nat) | {k + x for x in extra}
+        rows = [r for r in range(n) if r not in erased][:k]
+        if not rs.is_recoverable(rows):
+            continue
+        out.zero_()
+        dec.rows.copy_(torch.tensor(rows, dtype=torch.int32))
+        dec.solve()
+        dec.run()
+        torch.cuda.synchronize()
+        assert int(dec.status.item()) == 0, rows
+        assert sorted(dec.erased.cpu().tolist()) == sorted(nat)
+        assert np.array_equal(out.cpu().numpy(), host), rows
+        tested += 1
+
+
+def test_pattern_decoder_rejects_bad_patterns_without_writing():
+    """Invalid survivor lists (duplicate id, id out of range, wrong number of erased natives) report
+    status 2; a non-MDS singular pattern reports 1. Neither writes any output row."""
+    from gpu_rscode_amd.ops import PatternDecoder
+
+    k, n, C = 10, 14, 4099
+    rs = ReedSolomon(k, n)
+    host, data = _data(k, C, 6)
+    parity = rs.encode(data)
+    out = alloc_rows(k, C, "cuda", fill=0x5A)
+    g = torch.from_numpy(rs.G).cuda()
+    dec = PatternDecoder(g, [data[i] for i in range(k)] + [parity[i] for i in range(n - k)], [out[i] for i in range(k)], 4)
+    # {4,5,9,11} is one of the reference Vandermonde's 12 singular 4-erasure sets (SURVEY §2.2): it
+    # erases natives 4, 5, 9 and parity 11, so it runs on a 3-native plan
+    singular = [r for r in range(n) if r not in (4, 5, 9, 11)]
+    assert not rs.is_recoverable(singular)
+    cases = {2: [[0, 0, 2, 3, 6, 7, 8, 10, 11, 12],  # duplicate id
+                 [0, 1, 2, 3, 6, 7, 8, 10, 11, 99],  # id out of range
+                 [0, 1, 2, 3, 4, 6, 7, 8, 10, 11]],  # 2 natives missing, the plan rebuilds 4
+             1: [singular]}
+    dec3 = PatternDecoder(g, [data[i] for i in range(k)] + [parity[i] for i in range(n - k)], [out[i] for i in range(k)], 3)
+    for want, pats in cases.items():
+        for rows in pats:
+            d = dec3 if want == 1 else dec
+            d.rows.copy_(torch.tensor(rows, dtype=torch.int32))
+            d.solve()
+            d.run()
+            torch.cuda.synchronize()
+            assert int(d.status.item()) == want, rows
+            assert bool((out == 0x5A).all()), rows  # nothing stored: no output or copy pointer
+
+
+def test_distributed_rs_on_a_one_rank_rccl_group():
+    """DistributedRS with a forced one-rank RCCL ("nccl") group on the MI355X: broadcast_matrix, the
+    scatter (odd C: rank 0's shard is re-pitched through send/recv to itself) and the in-place gather
+    all execute as RCCL calls."""
+    code = r'''
+import os, numpy as np, torch, torch.distributed as dist
+from gpu_rscode_amd.parallel import dist as pdist
+from gpu_rscode_amd.gf import GF256
+ctx = pdist.init_distributed(force_pg=True)
+assert dist.get_backend() == "nccl" and dist.get_world_size() == 1
+k, n, C = 10, 14, 5 * 4096 + 77
+drs = pdist.DistributedRS(k, n, ctx)
+host = np.random.default_rng(0).integers(0, 256, size=(k, C), dtype=np.uint8)
+data = torch.from_numpy(host).cuda()
+parity = drs.encode_global(data, C)
+torch.cuda.synchronize()
+assert np.array_equal(parity.cpu().numpy(), GF256.gemm(GF256.vandermonde_ref(k, n - k), host))
+stripe = torch.cat([data, parity.contiguous()])
+rows = [0, 1, 3, 5, 6, 8, 10, 11, 12, 13]
+out = drs.decode_global(stripe[rows].contiguous(), rows, C)
+torch.cuda.synchronize()
+assert np.array_equal(out.cpu().numpy(), host)
+dist.destroy_process_group()
+print("DRS-RCCL-OK")
+'''
+    env = dict(os.environ)
+    for v in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(v, None)
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run(["python", "-c", code], capture_output=True, text=True, timeout=180, env=env, cwd=root)
+    assert r.returncode == 0 and "DRS-RCCL-OK" in r.stdout, (r.stdout[-2000:], r.stderr[-3000:])
