@@ -5,15 +5,19 @@
 // each device streaming pinned host rows through `-s` HIP streams (gfrs/pipeline.h).
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <exception>
 #include <memory>
 #include <stdexcept>
+#include <string>
 
 #include "cli_common.h"
 #include "gfrs/async_prepare.h"
 #include "gfrs/codec_file.h"
 #include "gfrs/format.h"
+#include "gfrs/host_alloc.h"
 #include "gfrs/pipeline.h"
 #include "gfrs/stream_codec.h"
 
@@ -23,7 +27,11 @@ void check(hipError_t e, const char* what) {
   if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
 }
 
+// Pinned host buffers: huge-page anonymous memory + hipHostRegister (gfrs/host_alloc.h, ~25x
+// cheaper than hipHostMalloc); GFRS_HOST_ALLOC=hipHostMalloc selects the plain allocator.
 gfrs::HostAlloc pinned_alloc() {
+  const char* env = std::getenv("GFRS_HOST_ALLOC");
+  if (!env || std::string(env) != "hipHostMalloc") return gfrs::thp_pinned_host_alloc();
   return {[](size_t n) -> uint8_t* {
             void* p = nullptr;
             if (hipHostMalloc(&p, n, hipHostMallocDefault) != hipSuccess) return nullptr;
@@ -45,7 +53,10 @@ int main(int argc, char** argv) {
       return 0;
     }
     int ndev = 0;
-    check(hipGetDeviceCount(&ndev), "hipGetDeviceCount");
+    const auto t_init = std::chrono::steady_clock::now();
+    check(hipGetDeviceCount(&ndev), "hipGetDeviceCount");  // first HIP call: runtime + device discovery
+    const double ms_init =
+        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_init).count();
     if (ndev <= 0) throw std::runtime_error("no GPU visible (use bin/CPU-RS for the CPU codec)");
     if (a.gpus > 0 && a.gpus < ndev) ndev = a.gpus;
     std::vector<int> devices(ndev);
@@ -70,18 +81,46 @@ int main(int argc, char** argv) {
     so.resume = a.resume;
     so.durable = a.sync;
     const StreamOptions* sop = a.streaming() ? &so : nullptr;
-    double gpu_ms = 0;  // the reference's "Total GPU ... time" (transfers + kernels, all devices)
+    double gpu_ms = 0;  // stream-loop time: transfers + kernels + frees, all devices (setup excluded)
+    double setup_ms = 0, setup_past_ms = 0;  // helper-thread device setup, and the part the GEMM waited for
     std::unique_ptr<AsyncPrepare> prep = enc ? prepare_for_encode(devices, opt, a.in_file, a.k, a.n - a.k, sop)
                                              : prepare_for_decode(devices, opt, a.in_file, sop);
+    // GFRS_SETUP=serial (measurement aid): finish the device setup before the host buffers are
+    // allocated and the file is read, so each phase's uncontended cost shows
+    if (prep && std::getenv("GFRS_SETUP") && std::string(std::getenv("GFRS_SETUP")) == "serial") {
+      const double ms = prep->wait();
+      if (!a.quiet) {
+        std::printf("GPU pipeline setup (serial): %fms\n", ms);
+        for (size_t d = 0; d < prep->stats().size(); ++d) {
+          const PrepareStats& ps = prep->stats()[d];
+          std::printf("Device%zu: setup breakdown: device bring-up %fms, streams+buffers %fms, kernel load %fms, "
+                      "DMA warm-up %fms\n",
+                      d, ps.ms_device, ps.ms_lanes, ps.ms_kernel, ps.ms_dma);
+        }
+      }
+      setup_ms += ms;
+      prep.reset();
+    }
     const GemmFn gemm = [&](const std::vector<const uint8_t*>& in, const std::vector<uint8_t*>& out,
                             const Mat& coeff, int64_t ncols) {
       if (prep) {
         const auto t0 = std::chrono::steady_clock::now();
+        const double since_start = prep->ms_until(t0);
         const double ms = prep->wait();
         const double waited = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-        if (!a.quiet)
-          std::printf("GPU pipeline setup: %fms on a helper thread during the file reads (%fms of it past them)\n", ms,
-                      waited);
+        setup_ms += ms;
+        setup_past_ms += waited;
+        if (!a.quiet) {
+          std::printf("GPU pipeline setup: %fms on a helper thread started %fms before the GEMM was ready to run "
+                      "(%fms of it past the file reads)\n",
+                      ms, since_start, waited);
+          for (size_t d = 0; d < prep->stats().size(); ++d) {
+            const PrepareStats& ps = prep->stats()[d];
+            std::printf("Device%zu: setup breakdown: device bring-up %fms, streams+buffers %fms, kernel load %fms, "
+                        "DMA warm-up %fms\n",
+                        d, ps.ms_device, ps.ms_lanes, ps.ms_kernel, ps.ms_dma);
+          }
+        }
         prep.reset();
       }
       std::vector<PipelineStats> st;
@@ -108,11 +147,21 @@ int main(int argc, char** argv) {
       r = enc ? encode_file(a.in_file, a.k, a.n - a.k, parse_matrix_kind(a.matrix), gemm, pinned_alloc(), a.cpu_meta)
               : decode_file(a.in_file, a.conf, a.out, gemm, pinned_alloc());
     }
-    if (!a.quiet)
-      std::printf("GPU %s bandwidth: %.3f MB/s (%lld bytes in %.3f ms of GPU time, k=%d, p=%d, %zu device "
-                  "shard(s), %d stream(s))\n",
-                  verb, r.total_size / 1048576.0 / (std::max(gpu_ms, 1e-9) / 1e3), static_cast<long long>(r.total_size),
-                  gpu_ms, r.k, r.p, devices.size(), a.streams);
+    if (!a.quiet) {
+      const double mb = r.total_size / 1048576.0;
+      std::printf("Host: HIP runtime init %fms, pinned buffers %fms, file read %fms\n", ms_init, r.ms_alloc,
+                  r.ms_read);
+      std::printf("GPU %s bandwidth: %.3f MB/s (%lld bytes in %.3f ms of GPU time: transfers + kernels, device "
+                  "setup excluded; k=%d, p=%d, %zu device shard(s), %d stream(s))\n",
+                  verb, mb / (std::max(gpu_ms, 1e-9) / 1e3), static_cast<long long>(r.total_size), gpu_ms, r.k, r.p,
+                  devices.size(), a.streams);
+      // the reference's "Total GPU ... time" window starts before its cudaMalloc/cudaStreamCreate
+      // (src/encode.cu:117-119,168-232): setup on the critical path counts, overlapped setup does not
+      std::printf("GPU %s bandwidth, reference window (setup on the critical path + transfers + kernels): %.3f MB/s "
+                  "(%.3f ms); with the whole setup serialised: %.3f MB/s (%.3f ms)\n",
+                  verb, mb / (std::max(gpu_ms + setup_past_ms, 1e-9) / 1e3), gpu_ms + setup_past_ms,
+                  mb / (std::max(gpu_ms + setup_ms, 1e-9) / 1e3), gpu_ms + setup_ms);
+    }
   } catch (const std::exception& e) {
     std::fprintf(stderr, "RS: %s\n", e.what());
     return 1;

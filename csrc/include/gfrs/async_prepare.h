@@ -24,10 +24,9 @@ namespace gfrs {
 class AsyncPrepare {
  public:
   AsyncPrepare(std::vector<int> devices, PipelineOptions opt, int k, int m, int64_t ncols)
-      : th_([this, devices = std::move(devices), opt, k, m, ncols] {
-          const auto t0 = std::chrono::steady_clock::now();
-          err_ = prepare_pipeline_multi(devices, k, m, ncols, opt);
-          ms_ = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+      : t0_(std::chrono::steady_clock::now()), th_([this, devices = std::move(devices), opt, k, m, ncols] {
+          err_ = prepare_pipeline_multi(devices, k, m, ncols, opt, &stats_);
+          ms_ = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0_).count();
         }) {}
   AsyncPrepare(const AsyncPrepare&) = delete;
   AsyncPrepare& operator=(const AsyncPrepare&) = delete;
@@ -41,11 +40,19 @@ class AsyncPrepare {
     if (err_ != hipSuccess) throw std::runtime_error(std::string("GPU pipeline setup: ") + hipGetErrorString(err_));
     return ms_;
   }
+  // Per-device breakdown (valid after wait()).
+  const std::vector<PrepareStats>& stats() const { return stats_; }
+  // Milliseconds from this object's creation to `t` (e.g. when the file reads finished).
+  double ms_until(std::chrono::steady_clock::time_point t) const {
+    return std::chrono::duration<double, std::milli>(t - t0_).count();
+  }
 
  private:
   hipError_t err_ = hipSuccess;
   double ms_ = 0;
-  std::thread th_;  // last member: starts after err_/ms_ exist
+  std::vector<PrepareStats> stats_;
+  std::chrono::steady_clock::time_point t0_;
+  std::thread th_;  // last member: starts after everything above exists
 };
 
 // Encode of `file` with k natives and p parity rows: k x C in, p x C out (or, streamed, k x W

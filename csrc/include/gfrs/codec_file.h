@@ -28,6 +28,7 @@ struct FileReport {
   int64_t total_size = 0, chunk_size = 0;
   int k = 0, p = 0, erased = 0;
   int rejected = 0;  // chunks skipped because their CRC-32 did not match METADATA
+  double ms_alloc = 0;  // host buffer allocation (pinned hipHostMalloc on the GPU path), all buffers
   double ms_read = 0, ms_matrix = 0, ms_compute = 0, ms_write = 0;
 };
 

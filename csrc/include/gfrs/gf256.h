@@ -133,6 +133,29 @@ constexpr PermTable perm_for_coeff(uint8_t c) {
   return perm_from_basis(basis);
 }
 
+// GF(16) (poly x^4 + x + 1 = 0x13, src/gf16.h / src/galoisfield.cu:22) multiply.
+constexpr uint8_t gf16_mul(uint8_t a, uint8_t b) {
+  unsigned r = 0, x = a & 15u;
+  for (int i = 0; i < 4; ++i) {
+    if (b & (1u << i)) r ^= x;
+    x <<= 1;
+    if (x & 0x10u) x ^= 0x13u;
+  }
+  return static_cast<uint8_t>(r & 15u);
+}
+
+// Perm table of the design doc's "GF(16) method" (doc/design.tex:190-209): each byte is two
+// independent GF(16) symbols, both multiplied by c (c < 16) — a GF(2)-linear byte map like any other,
+// so the GF(256) kernels run it unchanged.
+constexpr PermTable perm_for_coeff_gf16(uint8_t c) {
+  uint8_t basis[8]{};
+  for (int b = 0; b < 4; ++b) {
+    basis[b] = gf16_mul(c, static_cast<uint8_t>(1u << b));
+    basis[b + 4] = static_cast<uint8_t>(gf16_mul(c, static_cast<uint8_t>(1u << b)) << 4);
+  }
+  return perm_from_basis(basis);
+}
+
 // Evaluate a perm table on the host (byte-exact emulation of the device v_perm path).
 constexpr uint8_t perm_apply(const PermTable& t, uint8_t x) {
   const unsigned s0 = x & 7u, s1 = (x >> 3) & 7u, s2 = x >> 6;

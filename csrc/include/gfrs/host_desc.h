@@ -10,11 +10,12 @@
 
 namespace gfrs {
 
-// coeff: m x k row-major, or empty to leave the table block zeroed (filled later on device by
+// coeff: m x k row-major (GF(2^8), or GF(16) nibble-method coefficients with field_w = 4), or empty
+// to leave the table block zeroed (filled later on device by
 // launch_perm_tables / launch_gf_invert). copy may be empty (no fused copies).
 inline std::vector<uint8_t> build_desc(int k, int m, const std::vector<uint64_t>& in,
                                        const std::vector<uint64_t>& copy, const std::vector<uint64_t>& out,
-                                       const Mat& coeff) {
+                                       const Mat& coeff, int field_w = 8) {
   if (k <= 0 || m <= 0 || k > 256 || m > 256) throw std::invalid_argument("build_desc: 1 <= k,m <= 256");
   if (int(in.size()) != k) throw std::invalid_argument("build_desc: need k input pointers");
   if (int(out.size()) != m) throw std::invalid_argument("build_desc: need m output pointers");
@@ -29,7 +30,8 @@ inline std::vector<uint8_t> build_desc(int k, int m, const std::vector<uint64_t>
   if (!copy.empty()) std::memcpy(d.data() + l.copy_off, copy.data(), 8 * size_t(k));
   std::memcpy(d.data() + l.out_off, out.data(), 8 * size_t(m));
   if (!coeff.empty()) {
-    const std::vector<PermTable> t = perm_tables_kmajor(coeff, m, k);
+    if (field_w != 8 && field_w != 4) throw std::invalid_argument("build_desc: field_w must be 8 or 4");
+    const std::vector<PermTable> t = perm_tables_kmajor(coeff, m, k, field_w);
     for (int j = 0; j < k; ++j)
       std::memcpy(d.data() + l.tab_off + (size_t(j) * m_pad) * sizeof(PermTable), &t[size_t(j) * m],
                   sizeof(PermTable) * size_t(m));

@@ -140,10 +140,14 @@ inline bool decode_matrix(const Mat& g, int k, const std::vector<int>& rows, Mat
 
 // Perm tables for an m x k coefficient matrix, laid out [k][m] (row j of the input stream
 // first) so a kernel walking the k inputs reads one contiguous m-record slab per input row.
-inline std::vector<PermTable> perm_tables_kmajor(const Mat& coeff, int m, int k) {
+// field_w = 8: GF(2^8) multiply by each coefficient; 4: the GF(16) nibble method (coefficients < 16).
+inline std::vector<PermTable> perm_tables_kmajor(const Mat& coeff, int m, int k, int field_w = 8) {
   std::vector<PermTable> t(size_t(k) * m);
   for (int j = 0; j < k; ++j)
-    for (int i = 0; i < m; ++i) t[size_t(j) * m + i] = perm_for_coeff(coeff[size_t(i) * k + j]);
+    for (int i = 0; i < m; ++i) {
+      const uint8_t c = coeff[size_t(i) * k + j];
+      t[size_t(j) * m + i] = field_w == 4 ? perm_for_coeff_gf16(c) : perm_for_coeff(c);
+    }
   return t;
 }
 

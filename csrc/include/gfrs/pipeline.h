@@ -34,6 +34,7 @@ struct PipelineOptions {
   bool persistent = true;          // keep streams/buffers/descriptor per device for the next call
   int copy_streams = 1;            // 1: H2D on a per-lane copy-in stream; 0: everything on one stream
   bool rect = true;                // equally spaced host rows: one 2-D copy per slice instead of k / m
+  int field_w = 8;                 // 8: GF(2^8) coefficients; 4: the GF(16) nibble method (doc/design.tex:190-209)
 };
 
 struct PipelineStats {
@@ -50,13 +51,23 @@ struct PipelineStats {
 hipError_t gemm_host(int device, const std::vector<const uint8_t*>& in_rows, const std::vector<uint8_t*>& out_rows,
                      const Mat& coeff, int64_t c0, int64_t c1, const PipelineOptions& opt, PipelineStats* stats);
 
+// Where a prepare_pipeline call spends its time (bin/RS prints it; roctx ranges of the same names).
+struct PrepareStats {
+  double ms_device = 0;  // hipSetDevice: the runtime's device/context bring-up on this thread
+  double ms_lanes = 0;   // streams, events, hipMalloc of the slice buffers, descriptor uploads
+  double ms_kernel = 0;  // first GEMM launch + completion: code-object load
+  double ms_dma = 0;     // first H2D / D2H (1-D and 2-D) per lane: copy engines and blit kernels
+  double ms_total = 0;
+};
+
 // Creates the device's streams, events and slice buffers for a later gemm_host over `ncols` columns
 // of k inputs / m outputs with `opt` (persistent workspace), and loads the kernels — so a caller can
 // overlap device setup with its file reads and keep it out of the timed GPU region.
-hipError_t prepare_pipeline(int device, int k, int m, int64_t ncols, const PipelineOptions& opt);
-// prepare_pipeline on every device for the shards gemm_host_multi will give it.
+hipError_t prepare_pipeline(int device, int k, int m, int64_t ncols, const PipelineOptions& opt,
+                            PrepareStats* stats = nullptr);
+// prepare_pipeline on every device for the shards gemm_host_multi will give it (stats per device).
 hipError_t prepare_pipeline_multi(const std::vector<int>& devices, int k, int m, int64_t ncols,
-                                  const PipelineOptions& opt);
+                                  const PipelineOptions& opt, std::vector<PrepareStats>* stats = nullptr);
 
 // Column shard [first, second) of device index d of `devices` (4 KiB aligned, remainder last).
 std::pair<int64_t, int64_t> device_shard(int64_t ncols, int devices, int d);

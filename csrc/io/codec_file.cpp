@@ -52,7 +52,16 @@ FileReport encode_file(const std::string& file, int k, int p, MatrixKind kind, c
   r.total_size = file_size(file);
   r.chunk_size = std::max<int64_t>(1, chunk_size(r.total_size, k));
   const int64_t C = r.chunk_size;
-  Buf data(alloc, size_t(k) * C), parity(alloc, size_t(std::max(p, 1)) * C);
+  std::unique_ptr<Buf> data_b, parity_b;
+  {
+    TraceRange tr("encode/alloc");
+    data_b = std::make_unique<Buf>(alloc, size_t(k) * C);
+    parity_b = std::make_unique<Buf>(alloc, size_t(std::max(p, 1)) * C);
+  }
+  Buf& data = *data_b;
+  Buf& parity = *parity_b;
+  r.ms_alloc = ms_since(t);
+  t = Clock::now();
   {
     TraceRange tr("encode/read");
     read_into(file, 0, data.p, int64_t(k) * C);
@@ -124,7 +133,16 @@ FileReport decode_file(const std::string& file, const std::string& conf, const s
     cand_idx.push_back(idx);
     cand_path.push_back(resolve_chunk(nm, file));
   }
-  Buf surv(alloc, size_t(k) * C);
+  double ms_meta = ms_since(t);
+  t = Clock::now();
+  std::unique_ptr<Buf> surv_b;
+  {
+    TraceRange tr("decode/alloc");
+    surv_b = std::make_unique<Buf>(alloc, size_t(k) * C);
+  }
+  Buf& surv = *surv_b;
+  r.ms_alloc = ms_since(t);
+  t = Clock::now();
   std::vector<int> rows;
   std::vector<std::vector<uint8_t>> spare;  // verified chunks beyond the first k (rarely needed)
   auto row_ok = [&](int ci, uint8_t* dst) -> bool {
@@ -184,7 +202,7 @@ FileReport decode_file(const std::string& file, const std::string& conf, const s
     std::memcpy(surv.p + size_t(i) * C, src, size_t(C));  // pick is increasing: slot i <= pos, no clobber of later picks
   }
   rows = rows_of(pick);
-  r.ms_read = ms_since(t);
+  r.ms_read = ms_meta + ms_since(t);
 
   t = Clock::now();
   Mat dm;
@@ -198,10 +216,12 @@ FileReport decode_file(const std::string& file, const std::string& conf, const s
   for (int i = 0; i < k; ++i)
     if (pos_of_native[i] < 0) erased.push_back(i);
   r.erased = int(erased.size());
-  // (the output rows are allocated outside the timed GEMM region, like encode's parity buffer:
-  // a pinned hipHostMalloc of ~GBs takes tens of ms)
-  Buf rec(alloc, size_t(std::max<size_t>(erased.size(), 1)) * C);
   r.ms_matrix = ms_since(t);
+  // (the output rows are allocated outside the timed GEMM region and outside the matrix time, like
+  // encode's parity buffer: a pinned hipHostMalloc of ~GBs takes tens of ms)
+  t = Clock::now();
+  Buf rec(alloc, size_t(std::max<size_t>(erased.size(), 1)) * C);
+  r.ms_alloc += ms_since(t);
 
   t = Clock::now();
   if (!erased.empty()) {

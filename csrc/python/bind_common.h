@@ -41,6 +41,7 @@ inline py::dict report(const gfrs::FileReport& r) {
   d["p"] = r.p;
   d["erased"] = r.erased;
   d["rejected"] = r.rejected;
+  d["ms_alloc"] = r.ms_alloc;
   d["ms_read"] = r.ms_read;
   d["ms_matrix"] = r.ms_matrix;
   d["ms_compute"] = r.ms_compute;

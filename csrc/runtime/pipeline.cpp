@@ -3,6 +3,7 @@
 #include "gfrs/trace.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <chrono>
 #include <map>
 #include <memory>
@@ -129,7 +130,8 @@ Geometry geometry(int64_t ncols, const PipelineOptions& opt) {
 
 // Streams, events and buffers for `lanes` lanes of k x slice in / m x slice out, descriptors built
 // from `coeff` (zeros when empty). Caller holds ws.mu and has set the device.
-hipError_t setup_lanes(Workspace& ws, int lanes, int k, int m, int64_t slice, const Mat& coeff, bool split) {
+hipError_t setup_lanes(Workspace& ws, int lanes, int k, int m, int64_t slice, const Mat& coeff, bool split,
+                       int field_w = 8) {
   if (int(ws.lane.size()) < lanes) ws.lane.resize(size_t(lanes));
   const Mat zero = coeff.empty() ? Mat(size_t(m) * k, 0) : Mat{};
   const Mat& c = coeff.empty() ? zero : coeff;
@@ -147,7 +149,7 @@ hipError_t setup_lanes(Workspace& ws, int lanes, int k, int m, int64_t slice, co
       std::vector<uint64_t> ip(k), op(m);
       for (int j = 0; j < k; ++j) ip[j] = reinterpret_cast<uint64_t>(S.in + size_t(j) * slice);
       for (int i = 0; i < m; ++i) op[i] = reinterpret_cast<uint64_t>(S.out + size_t(i) * slice);
-      std::vector<uint8_t> d = build_desc(k, m, ip, {}, op, c);
+      std::vector<uint8_t> d = build_desc(k, m, ip, {}, op, c, field_w);
       if (d != S.desc_host) {
         GFRS_TRY(ensure(&S.desc, S.desc_cap, d.size()));
         // every lane was drained before the previous call returned, so no kernel still reads it
@@ -165,7 +167,24 @@ struct Run {
   int64_t pitch = 0;
 };
 
-// Maximal runs of equally spaced rows with spacing >= min_pitch (min_pitch 0: every row alone).
+// Largest host row pitch a 2-D copy is given. hipMemcpy2DAsync's pitches are size_t, but the DMA
+// engines' pitch fields are narrower than that; beyond 2^31 - 1 (a non-streamed bin/RS run of a big
+// file with small k: C of several GiB) rows are copied one by one. GFRS_MAX_RECT_PITCH lowers the
+// cap (tests exercise the fallback with small rows).
+int64_t max_rect_pitch() {
+  static const int64_t cap = [] {
+    int64_t c = (int64_t(1) << 31) - 1;
+    if (const char* e = std::getenv("GFRS_MAX_RECT_PITCH")) {
+      const long long v = std::atoll(e);
+      if (v > 0 && v < c) c = v;
+    }
+    return c;
+  }();
+  return cap;
+}
+
+// Maximal runs of equally spaced rows with spacing in [min_pitch, max_rect_pitch()] (min_pitch 0:
+// every row alone).
 template <class Ptr>
 std::vector<Run> row_runs(const std::vector<Ptr>& rows, int64_t min_pitch) {
   std::vector<Run> runs;
@@ -174,7 +193,7 @@ std::vector<Run> row_runs(const std::vector<Ptr>& rows, int64_t min_pitch) {
     Run r{int(i), 1, 0};
     if (min_pitch > 0 && i + 1 < rows.size()) {
       const int64_t d = at(i + 1) - at(i);
-      if (d >= min_pitch) {
+      if (d >= min_pitch && d <= max_rect_pitch()) {
         r.pitch = d;
         while (i + r.count < rows.size() && at(i + r.count) - at(i + r.count - 1) == d) ++r.count;
       }
@@ -215,15 +234,29 @@ hipError_t release_workspaces() {
   return hipSuccess;
 }
 
-hipError_t prepare_pipeline(int device, int k, int m, int64_t ncols, const PipelineOptions& opt) {
+hipError_t prepare_pipeline(int device, int k, int m, int64_t ncols, const PipelineOptions& opt,
+                            PrepareStats* stats) {
   if (!valid(k, m, 0, 0, ncols, opt)) return hipErrorInvalidValue;
   if (ncols == 0) return hipSuccess;
-  GFRS_TRY(hipSetDevice(device));
+  PrepareStats ps;
+  const auto t_all = Clock::now();
+  auto t = t_all;
+  {
+    TraceRange tr("pipeline/prepare/device");
+    GFRS_TRY(hipSetDevice(device));
+    GFRS_TRY(hipFree(nullptr));  // forces the device's context into existence on this thread
+  }
+  ps.ms_device = ms_since(t);
   const Geometry g = geometry(ncols, opt);
   Workspace& ws = workspace(device);
   std::lock_guard<std::mutex> guard(ws.mu);
   TraceRange tr("pipeline/prepare");
-  GFRS_TRY(setup_lanes(ws, g.lanes, k, m, g.slice, {}, opt.copy_streams > 0));
+  t = Clock::now();
+  {
+    TraceRange tl("pipeline/prepare/lanes");
+    GFRS_TRY(setup_lanes(ws, g.lanes, k, m, g.slice, {}, opt.copy_streams > 0));
+  }
+  ps.ms_lanes = ms_since(t);
   // Before anyone's clock starts, run every path the stream loop will take once, on a few columns:
   // the kernel launch (code-object load), and H2D / D2H copies in both the 1-D and the 2-D form
   // on the streams that will issue them. The first DMA of a process sets up its copy engines and
@@ -234,6 +267,17 @@ hipError_t prepare_pipeline(int device, int k, int m, int64_t ncols, const Pipel
   GFRS_TRY(hipHostMalloc(&host, 2 * kProbe, hipHostMallocDefault));
   auto* h = static_cast<uint8_t*>(host);
   hipError_t err = hipSuccess;
+  t = Clock::now();
+  {  // kernel first (code-object load), alone, so its cost is separable from the copies'
+    TraceRange tk("pipeline/prepare/kernel");
+    Lane& L = ws.lane[0];
+    err = launch_gf_gemm(L.slot[0].desc, k, pad_m(m), 0, std::min<int64_t>(g.slice, int64_t(probe)), opt.bytewise, 0,
+                         L.compute);
+    if (err == hipSuccess) err = hipStreamSynchronize(L.compute);
+  }
+  ps.ms_kernel = ms_since(t);
+  t = Clock::now();
+  TraceRange td("pipeline/prepare/dma");
   for (int l = 0; l < g.lanes && err == hipSuccess; ++l) {
     Lane& L = ws.lane[size_t(l)];
     hipStream_t cin = L.copy_in ? L.copy_in : L.compute;
@@ -254,22 +298,27 @@ hipError_t prepare_pipeline(int device, int k, int m, int64_t ncols, const Pipel
   }
   const hipError_t e2 = drain(ws.lane);
   const hipError_t e3 = hipHostFree(host);
+  ps.ms_dma = ms_since(t);
+  ps.ms_total = ms_since(t_all);
+  if (stats) *stats = ps;
   if (err != hipSuccess) return err;
   if (e2 != hipSuccess) return e2;
   return e3;
 }
 
 hipError_t prepare_pipeline_multi(const std::vector<int>& devices, int k, int m, int64_t ncols,
-                                  const PipelineOptions& opt) {
+                                  const PipelineOptions& opt, std::vector<PrepareStats>* stats) {
   const int D = int(devices.size());
   if (D <= 0) return hipErrorInvalidValue;
   std::vector<hipError_t> err(D, hipSuccess);
+  std::vector<PrepareStats> ps(static_cast<size_t>(D));
   std::vector<std::thread> th;
   for (int d = 0; d < D; ++d) {
     const auto [a, b] = device_shard(ncols, D, d);
-    th.emplace_back([&, d, a = a, b = b] { err[d] = prepare_pipeline(devices[d], k, m, b - a, opt); });
+    th.emplace_back([&, d, a = a, b = b] { err[d] = prepare_pipeline(devices[d], k, m, b - a, opt, &ps[size_t(d)]); });
   }
   for (auto& t : th) t.join();
+  if (stats) *stats = ps;
   for (auto e : err)
     if (e != hipSuccess) return e;
   return hipSuccess;
@@ -297,7 +346,7 @@ hipError_t gemm_host(int device, const std::vector<const uint8_t*>& in_rows, con
   std::lock_guard<std::mutex> guard(ws.mu);
   {
     TraceRange tr("pipeline/setup");
-    const hipError_t e = setup_lanes(ws, lanes, k, m, slice, coeff, opt.copy_streams > 0);
+    const hipError_t e = setup_lanes(ws, lanes, k, m, slice, coeff, opt.copy_streams > 0, opt.field_w);
     if (e != hipSuccess) {
       (void)drain(ws.lane);
       return e;

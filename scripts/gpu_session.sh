@@ -11,6 +11,8 @@
 #   presets    bench.py on every BASELINE preset (k128n160, k16n20_8g, k4n6, k16n20_64g)
 #   rccl       scripts/rccl_probe.py at world 1 + bench.py --force-pg in every --comm / --scaling mode
 #   files      bin/RS on a 1 GiB file: in-memory and streamed encode + 4-erasure decode, cmp
+#   rcclprof   rocprofv3 kernel timelines of the one-rank RCCL group (owners/root/bcast) + no group
+#   setup      bin/RS device-setup breakdown (slice sizes, serial vs overlapped)
 #   prof       rocprofv3 --kernel-trace --stats of the headline and wide-stripe benches
 #   pmc        PMC passes (counters only, kernel-trace) of the encode / decode / wide kernels
 #   sweep      the reference's published k-sweep (scripts/sweep.py)
@@ -66,9 +68,36 @@ r_files() {
   step stream_decode 300 bin/RS -d -i $F -c /tmp/rs_conf -o /tmp/rs_out2.bin --window 0 --no-sync -s 4 &&
   step cmp_stream 60 cmp $F /tmp/rs_out2.bin
 }
+r_setup() {  # bin/RS device + host setup breakdown, 1 GiB encode + decode (THP-pinned vs hipHostMalloc)
+  local F=/tmp/rs_in.bin
+  step mkfile2 120 $PY -c "import os; open('$F','wb').write(os.urandom((1<<30)+12345))" &&
+  step conf2 30 bash -c "printf '/tmp/_%d_rs_in.bin\\n' 4 5 6 7 8 9 10 11 12 13 > /tmp/rs_conf" &&
+  step setup_enc 120 bin/RS -k 10 -n 14 -e $F -s 2 &&
+  step setup_dec 120 bin/RS -d -i $F -c /tmp/rs_conf -o /tmp/rs_out.bin -s 2 &&
+  step setup_cmp 60 cmp $F /tmp/rs_out.bin &&
+  step setup_enc2 120 bin/RS -k 10 -n 14 -e $F -s 2 &&
+  step setup_dec2 120 bin/RS -d -i $F -c /tmp/rs_conf -o /tmp/rs_out.bin -s 2 &&
+  step setup_enc_hhm 120 env GFRS_HOST_ALLOC=hipHostMalloc bin/RS -k 10 -n 14 -e $F -s 2 &&
+  step setup_dec_hhm 120 env GFRS_HOST_ALLOC=hipHostMalloc bin/RS -d -i $F -c /tmp/rs_conf -o /tmp/rs_out.bin -s 2 &&
+  step setup_enc_serial 120 env GFRS_SETUP=serial bin/RS -k 10 -n 14 -e $F -s 2 &&
+  step setup_stream_enc 120 bin/RS -k 10 -n 14 -e $F --window 0 --no-sync -s 4 &&
+  step setup_stream_dec 120 bin/RS -d -i $F -c /tmp/rs_conf -o /tmp/rs_out2.bin --window 0 --no-sync -s 4 &&
+  step setup_cmp2 60 cmp $F /tmp/rs_out2.bin
+}
 r_prof() {
   step prof_k10 300 $PROF -d $O/prof_k10 -- python3 bench.py --steps 20 --no-e2e &&
   step prof_k128 300 $PROF -d $O/prof_k128 -- python3 bench.py --preset k128n160 --steps 20 --no-e2e
+}
+r_rcclprof() {  # kernel timelines: RCCL kernels on their own stream beside the GEMMs (one-rank group)
+  local m
+  for m in owners root bcast; do
+    step trace_pg_$m 300 rocprofv3 --kernel-trace --output-format csv -o run -d $O/trace_pg_$m -- \
+      python3 bench.py --force-pg --comm $m --no-compare --no-e2e --steps 20 --warmup 3 &&
+    $PY scripts/trace_overlap.py $O/trace_pg_$m --last 60 --out $O/timeline_pg_$m.txt > /dev/null || return 1
+  done
+  step trace_nopg 300 rocprofv3 --kernel-trace --output-format csv -o run -d $O/trace_nopg -- \
+    python3 bench.py --no-e2e --steps 20 --warmup 3 &&
+  $PY scripts/trace_overlap.py $O/trace_nopg --last 60 --out $O/timeline_nopg.txt > /dev/null
 }
 r_pmc() {
   local C1="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_MFMA SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR"
