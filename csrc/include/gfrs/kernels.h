@@ -26,6 +26,11 @@ hipError_t launch_gf_gemm_batched(const void* desc, int k, int m_pad, int batch,
 hipError_t launch_gf_gemm_variant(const void* desc, int k, int m_pad, int64_t col0, int64_t ncols,
                                   int vec, int pf, bool nt, int max_blocks, hipStream_t stream);
 
+// LDS-LUT ablation (gf_gemm_lut.hip): the same GEMM with per-coefficient 4-bit nibble tables in LDS
+// (two ds_read_u8 per byte product), built from the descriptor's tables; 16-byte aligned columns,
+// the < 16-byte tail on the byte kernel.
+hipError_t launch_gf_gemm_lut(const void* desc, int k, int m_pad, int64_t col0, int64_t ncols, hipStream_t stream);
+
 // ---- Gauss-Jordan inverse (csrc/kernels/gf_invert.hip) ---------------------------------------
 // Inverts `batch` n x n matrices (row-major, contiguous) with row pivoting, one workgroup each,
 // [A|I] resident in LDS. status[b] = 0 ok, 1 singular. n <= 256.

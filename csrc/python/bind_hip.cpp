@@ -107,6 +107,10 @@ PYBIND11_MODULE(_hip, m) {
       },
       py::arg("a"), py::arg("a_inv"), py::arg("n"), py::arg("batch") = 1, py::arg("status") = 0, py::arg("desc") = 0,
       py::arg("sel_rows") = 0, py::arg("m") = 0, py::arg("m_pad") = 0, py::arg("stream") = 0);
+  m.def("gemm_lut", [](uint64_t desc, int k, int m_pad, int64_t col0, int64_t ncols, uint64_t stream) {
+    check(launch_gf_gemm_lut(reinterpret_cast<const void*>(desc), k, m_pad, col0, ncols, as_stream(stream)),
+          "gf_gemm_lut");
+  });
   m.def("mfma_bitmat_bytes", &mfma_bitmat_bytes);
   m.def("mfma_bitmat", [](uint64_t coeff, int mm, int k, uint64_t bitmat, uint64_t stream) {
     check(launch_mfma_bitmat(reinterpret_cast<const uint8_t*>(coeff), mm, k, reinterpret_cast<void*>(bitmat),

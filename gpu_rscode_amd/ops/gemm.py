@@ -235,6 +235,9 @@ class GemmPlan:
             else:  # filled on device later (set_device_coeff / invert_into_plan)
                 self.bitmat = torch.zeros(hip().fp4_bitmat_bytes(self.k, self.m, self.mfma_mg), dtype=torch.uint8,
                                           device=self.device)
+        elif engine == "lut":  # LDS nibble-table ablation (csrc/kernels/gf_gemm_lut.hip)
+            if self.bytewise or self.batch > 1:
+                raise ValueError("engine='lut' needs 16-byte aligned rows and one stripe")
         elif engine != "valu":
             raise ValueError(f"unknown engine {engine!r}")
         self._mark_ready()
@@ -325,6 +328,8 @@ class GemmPlan:
         elif self.engine == "mfma" and vec is None and col0 % 2 == 0:
             h.gemm_fp4(int(self.bitmat.data_ptr()), int(self.desc.data_ptr()), self.k, self.m, col0, ncols,
                        self.mfma_mg, self.in_stride, self.copies is not None, s)
+        elif self.engine == "lut" and vec is None and col0 % 16 == 0:
+            h.gemm_lut(int(self.desc.data_ptr()), self.k, self.m_pad, col0, ncols, s)
         elif self.engine == "mfma_i8" and vec is None and col0 % 2 == 0:
             h.gemm_mfma(int(self.bitmat.data_ptr()), int(self.desc.data_ptr()), self.k, self.m, col0, ncols, s)
         elif self.bytewise:

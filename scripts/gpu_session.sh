@@ -16,6 +16,9 @@
 #   prof       rocprofv3 --kernel-trace --stats of the headline and wide-stripe benches
 #   pmc        PMC passes (counters only, kernel-trace) of the encode / decode / wide kernels
 #   sweep      the reference's published k-sweep (scripts/sweep.py)
+#   gf16       the design doc's GF(16)-method point (k=4, n=6, 1.1 GB; device + e2e)
+#   lut        kbench: v_perm vs FP4 / int8 MFMA vs the LDS nibble-table kernel on every shape
+#   wide       FP4 wide-stripe shapes: default kernels vs A-resident (plain / XCD-paired chunks)
 #   ad hoc:    CMD="..." scripts/gpu_session.sh NAME cmd   (one step, 600 s)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -117,6 +120,18 @@ r_pmc() {
   done
 }
 r_sweep() { step sweep 1200 $PY scripts/sweep.py --part gpu --out $O/sweep_gpu.json; }
+r_gf16() { step gf16 300 $PY scripts/sweep.py --part gf16 --out $O/gf16.json; }
+r_lut() {  # LDS nibble-table ablation next to v_perm and the matrix-core kernels (kbench, interleaved rounds)
+  step kbench_lut 600 $PY scripts/kbench.py --rounds 3 --reps 5 --variants "None;mfma;mfma_i8;lut" --out $O/kbench_lut.json
+}
+r_wide() {  # wide-stripe FP4 kernel shapes (k=128, m rebuilt rows, with / without fused copies): A/B of kernel choices
+  local i
+  for i in 1 2; do
+    step wide_default_$i 300 $PY scripts/fp4_shapes.py ${WIDE_MS:-20,24,26,28,32} &&
+    step wide_ar_$i 300 env GFRS_FP4_KERNEL=ar GFRS_AR_PAIR=0 $PY scripts/fp4_shapes.py ${WIDE_MS:-20,24,26,28,32} &&
+    step wide_ar_pair_$i 300 env GFRS_FP4_KERNEL=ar GFRS_AR_PAIR=1 $PY scripts/fp4_shapes.py ${WIDE_MS:-20,24,26,28,32} || return 1
+  done
+}
 r_cmd() { step cmd 600 bash -c "$CMD"; }
 
 rc=0

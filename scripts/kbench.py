@@ -22,7 +22,7 @@ from gpu_rscode_amd.models import alloc_rows  # noqa: E402
 from gpu_rscode_amd.ops import GemmPlan, fill_random_, gf_invert  # noqa: E402
 
 VARIANTS = [None, (1, 1, False), (1, 2, False), (1, 4, False), (1, 2, True), (1, 4, True), (2, 1, False),
-            (2, 2, False), (2, 2, True), "mfma", "mfma_mg4", "mfma_mg2", "mfma_i8"]
+            (2, 2, False), (2, 2, True), "mfma", "mfma_mg4", "mfma_mg2", "mfma_i8", "lut"]
 
 
 def timed(fn, reps):
@@ -51,6 +51,7 @@ def make_case(name, k, m, ncopy, total_bytes):
              "mfma_mg2": GemmPlan(data, out, coeff, copies=copies, engine="mfma", mfma_mg=2)}
     if not ncopy:
         mplan["mfma_i8"] = GemmPlan(data, out, coeff, engine="mfma_i8")
+    mplan["lut"] = GemmPlan(data, out, coeff, copies=copies, engine="lut")  # LDS nibble tables (ablation)
     traffic = (k + m + ncopy) * C
     return {"name": name, "k": k, "m": m, "copies": ncopy, "C": C, "plan": plan, "mplan": mplan,
             "traffic": traffic, "keep": (data, out, copies)}
@@ -88,7 +89,7 @@ def main():
         for tok in a.variants.split(";"):
             if tok == "None":
                 variants.append(None)
-            elif tok.startswith("mfma"):
+            elif tok.startswith("mfma") or tok == "lut":
                 variants.append(tok)
             else:
                 v, pf, nt = (int(x) for x in tok.split(","))

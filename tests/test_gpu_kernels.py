@@ -411,3 +411,42 @@ def test_fp4_a_resident_kernel_matches_oracle(k, m, variant, monkeypatch):
         c = cdst.cpu().numpy()
         for j in range(k):
             assert np.array_equal(c[j], want_in[j] if j % 3 else np.full(ncols, 0x44, np.uint8)), j
+
+
+@pytest.mark.parametrize("k,m,ncols,ncopy", [(10, 4, 1000003, 0), (10, 4, 65536 + 5, 6), (128, 32, 70000, 0),
+                                              (16, 20, 4096, 0), (3, 1, 15, 0), (256, 16, 33333, 0)])
+def test_lds_lut_kernel_matches_oracle(k, m, ncols, ncopy):
+    """The LDS nibble-table ablation (engine='lut', csrc/kernels/gf_gemm_lut.hip): tables built on
+    device from the descriptor, any tile (m_pad 1..32), fused copies, the ragged tail on the byte kernel."""
+    _native_loaded()
+    rng = np.random.default_rng(k * 31 + m)
+    coeff = rng.integers(0, 256, size=(m, k), dtype=np.uint8)
+    host, dev = _rand_rows(k, ncols, k + 2 * m)
+    out = alloc_rows(m, ncols, "cuda", fill=0x3C)
+    copies = None
+    if ncopy:
+        dst = alloc_rows(k, ncols, "cuda", fill=0)
+        copies = [dst[j] if j < ncopy else None for j in range(k)]
+    plan = GemmPlan(dev, out, coeff, copies=copies, engine="lut")
+    plan.run()
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), GF256.gemm(coeff, host))
+    if ncopy:
+        assert np.array_equal(dst.cpu().numpy()[:ncopy], host[:ncopy])
+
+
+def test_lds_lut_kernel_gf16_maps():
+    _native_loaded()
+    k, m, ncols = 4, 2, 100000
+    f = gf.field(4)
+    coeff = f.vandermonde_ref(k, m)
+    maps = np.stack([np.stack([gf.byte_map_gf16_nibbles(int(coeff[i, j])) for j in range(k)]) for i in range(m)])
+    host, dev = _rand_rows(k, ncols, 22)
+    out = alloc_rows(m, ncols, "cuda", fill=0)
+    GemmPlan(dev, out, maps=maps, engine="lut").run()
+    torch.cuda.synchronize()
+    want = np.zeros((m, ncols), np.uint8)
+    for i in range(m):
+        for j in range(k):
+            want[i] ^= maps[i, j][host[j]]
+    assert np.array_equal(out.cpu().numpy(), want)
