@@ -86,6 +86,12 @@ hipError_t launch_fp4_bitmat_sel(const uint8_t* coeff, int ld, const int* sel, i
 hipError_t launch_mfma_bitmat(const uint8_t* coeff, int m, int k, void* bitmat,
                               hipStream_t stream);
 
+// FP4 kernels: the bit-matrix allocation ends with a write-only sink of kFp4SinkSlots 1-KiB slots;
+// each wave stores its dummy / destination-less bytes into slot (4 * block + wave) % slots, so the
+// sink writes of concurrent waves land on different L2 lines (one shared 1-KiB sink made every CU of
+// an XCD queue on the same L2 channel). Nothing reads it.
+constexpr int kFp4SinkSlots = 256;
+
 // ---- FP4 A-resident form (csrc/kernels/gf_mfma_fp4ar.hip; called by launch_gf_gemm_fp4) ---------
 // k in (112, 128], one bitmat group of mg <= 8 M-tiles (the layout launch_fp4_bitmat builds).
 // Processes the leading whole chunks of [col0, col0 + ncols) and reports how many columns in

@@ -130,11 +130,16 @@ __device__ __forceinline__ int bias_scale_of_lane(int lane) { return 127 + 23 - 
 // empty asm statements so no use can be scheduled above the wait; the compiler's own alias
 // tracking would otherwise put a vmcnt(0)/lgkmcnt(0) in front of every read.
 constexpr int kSlotBytes = 1024;
-// The bit-matrix allocation ends with a 1-KiB sink: output rows past m (padding of the last
-// M-tile group) and fused copies with no destination are stored there, so neither the epilogue
-// nor the K loop branches — one basic block the scheduler can interleave (MFMAs and conditional
-// stores in separate blocks serialise). Nothing reads the sink.
-constexpr int kSinkBytes = 1024;
+// The bit-matrix allocation ends with a sink: output rows past m (padding of the last M-tile group)
+// and fused copies with no destination are stored there, so neither the epilogue nor the K loop
+// branches — one basic block the scheduler can interleave (MFMAs and conditional stores in
+// separate blocks serialise). Nothing reads the sink. One 1-KiB slot per wave, spread over
+// kFp4SinkSlots (kernels.h): GFRS_FP4_SINK=1 restores the single shared slot (A/B measurements).
+constexpr int kSinkBytes = 1024 * kFp4SinkSlots;
+__device__ __forceinline__ uint64_t sink_slot(uint64_t base, int spread) {
+  const unsigned slot = spread ? (blockIdx.x * 4u + (threadIdx.x >> 6)) % unsigned(kFp4SinkSlots) : 0u;
+  return base + uint64_t(slot) * 1024u + 16u * (threadIdx.x & 63u);
+}
 // LDS the launcher tries to leave free next to a persistent block, so a side-stream kernel (the
 // decode-system solve, gf_invert.hip: 8.4 KiB at k=128, e=32) can co-reside instead of waiting
 // for the whole GEMM.
@@ -172,7 +177,7 @@ template <int MG, bool UNI, bool COPY, int kRing, int KS>
 __global__ __launch_bounds__(256, 1) void gf_gemm_fp4_kernel(cptr<uint64_t> in, cptr<uint64_t> out, cptr<uint64_t> copy,
                                                              const i32x4* __restrict__ bitmat, int k, int m,
                                                              int ksteps, int groups, int64_t col0, int64_t nchunks,
-                                                             int64_t chunk_slots, int64_t in_stride) {
+                                                             int64_t chunk_slots, int64_t in_stride, int sink_spread) {
   constexpr int NTW = kNTW;              // N-tiles (32 columns each) per wave
   constexpr int kWaves = 4, kThreads = 256;
   constexpr int kCW = 32 * NTW;          // columns per wave
@@ -201,7 +206,7 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4_kernel(cptr<uint64_t> in, 
   uint64_t* outptr = rowptr + 256;  // this group's 4*MG output rows
   const i32x4* src = bitmat + size_t(g) * MG * ksteps * 64;
   // this lane's 16 bytes of the sink past the bit-matrix (kSinkBytes)
-  const uint64_t sink = uint64_t(bitmat + size_t(groups) * MG * ksteps * 64) + 16 * (threadIdx.x & 63);
+  const uint64_t sink = sink_slot(uint64_t(bitmat + size_t(groups) * MG * ksteps * 64), sink_spread);
   for (int i = threadIdx.x; i < MG * ksteps * 64; i += kThreads) afrag[i] = src[i];
   if (!UNI)
     for (int i = threadIdx.x; i < k; i += kThreads) rowptr[i] = in[i];
@@ -561,7 +566,7 @@ template <int MG, bool UNI, bool COPY, int R, int KS, int ABL = 0>
 __global__ __launch_bounds__(256, 1) void gf_gemm_fp4sk_kernel(cptr<uint64_t> in, cptr<uint64_t> out,
                                                                cptr<uint64_t> copy, const i32x4* __restrict__ bitmat,
                                                                int k, int m, int groups, int64_t col0, int64_t nchunks,
-                                                               int64_t chunk_slots, int64_t in_stride) {
+                                                               int64_t chunk_slots, int64_t in_stride, int sink_spread) {
   constexpr int NTW = kNTW;              // N-tiles (32 columns each) per wave
   constexpr int kWaves = 4, kThreads = 256;
   constexpr int kCW = 32 * NTW;          // columns per wave (64)
@@ -586,7 +591,7 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4sk_kernel(cptr<uint64_t> in
   uint64_t* outptr = rowptr + 256;
   uint64_t* copyptr = rowptr + 256 + 32;
   const i32x4* src = bitmat + size_t(g) * MG * NS * 64;
-  const uint64_t sink = uint64_t(bitmat + size_t(groups) * MG * NS * 64) + 16 * (threadIdx.x & 63);
+  const uint64_t sink = sink_slot(uint64_t(bitmat + size_t(groups) * MG * NS * 64), sink_spread);
   for (int i = threadIdx.x; i < MG * NS * 64; i += kThreads) afrag[i] = src[i];
   if (!UNI)
     for (int i = threadIdx.x; i < k; i += kThreads) rowptr[i] = in[i];
@@ -1064,6 +1069,15 @@ int fp4_occupancy(size_t fixed) {
   return occ;
 }
 
+// GFRS_FP4_SINK=1: every wave's sink stores share one 1-KiB slot (the round-2 layout, A/B only)
+int fp4_sink_spread() {
+  static const int v = [] {
+    const char* e = std::getenv("GFRS_FP4_SINK");
+    return (e && std::atoi(e) == 1) ? 0 : 1;
+  }();
+  return v;
+}
+
 struct Fp4Args {
   cptr<uint64_t> in, out, copy;
   const void* bitmat;
@@ -1082,7 +1096,7 @@ hipError_t launch_fp4(const Fp4Geometry& geo, int occ, const Fp4Args& a, hipStre
   const unsigned blocks = unsigned(slots * geo.groups);
   gf_gemm_fp4_kernel<MG, UNI, COPY, R, KS><<<blocks, 256, lds, stream>>>(
       a.in, a.out, a.copy, static_cast<const i32x4*>(a.bitmat), a.k, a.m, geo.ksteps, geo.groups, a.col0, a.nchunks,
-      slots, a.in_stride);
+      slots, a.in_stride, fp4_sink_spread());
   return hipGetLastError();
 }
 
@@ -1174,7 +1188,7 @@ hipError_t launch_fp4sk(const Fp4Geometry& geo, const Fp4Args& a, hipStream_t st
   const unsigned blocks = unsigned(slots * geo.groups);
   gf_gemm_fp4sk_kernel<MG, UNI, COPY, R, KS, ABL><<<blocks, 256, lds, stream>>>(
       a.in, a.out, a.copy, static_cast<const i32x4*>(a.bitmat), a.k, a.m, geo.groups, a.col0, a.nchunks, slots,
-      a.in_stride);
+      a.in_stride, fp4_sink_spread());
   return hipGetLastError();
 }
 

@@ -103,7 +103,8 @@ template <int MGW, int WPG, bool UNI, bool COPY, int R>
 __global__ __launch_bounds__(256, 1) void gf_gemm_fp4ar_kernel(cptr<uint64_t> in, cptr<uint64_t> out,
                                                                cptr<uint64_t> copy, const i32x4* __restrict__ bitmat,
                                                                int k, int m, int mg, int64_t col0, int64_t nchunks,
-                                                               int64_t chunk_slots, int64_t in_stride, int pair) {
+                                                               int64_t chunk_slots, int64_t in_stride, int pair,
+                                                               int sink_spread) {
   constexpr int CG = 4 / WPG;               // column groups per block
   constexpr int kBC = CG * kCW;             // block columns per chunk
   constexpr int WN = MGW == 3 ? 4 : MGW;    // B window (a power of two dividing kNS, >= MGW)
@@ -148,7 +149,9 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4ar_kernel(cptr<uint64_t> in
   const uint32_t optr_addr = lds0 + 8u * 256u + uint32_t(32 * mh * MGW + 16 * h);
   const uint32_t rowptr_addr = lds0;
   const uint32_t cptr_addr = lds0 + 8u * (256u + 32u);
-  const uint64_t sink = uint64_t(bitmat + size_t(mg) * kNS * 64) + 16 * lane;
+  // this wave's 1-KiB slot of the sink past the bit-matrix (kFp4SinkSlots, kernels.h)
+  const unsigned sslot = sink_spread ? (blockIdx.x * 4u + unsigned(wave)) % unsigned(kFp4SinkSlots) : 0u;
+  const uint64_t sink = uint64_t(bitmat + size_t(mg) * kNS * 64) + uint64_t(sslot) * 1024u + 16 * lane;
   const int scale = 0x7F7F7F7F;  // E8M0 1.0 for every block of 32
   const uint64_t in0 = UNI ? in[0] : 0;
   const int drow = lane >> 2;                      // this lane's row within a DMA'd slot
@@ -442,12 +445,16 @@ hipError_t launch_ar(const Fp4ArLaunch& a, int64_t* done, hipStream_t stream) {
     return e ? std::atoi(e) : 0;
   }();
   const int pair = (WPG == 2 && pair_env) ? 1 : 0;
+  static const int sink_spread = [] {  // GFRS_FP4_SINK=1: one shared sink slot (A/B only)
+    const char* e = std::getenv("GFRS_FP4_SINK");
+    return (e && std::atoi(e) == 1) ? 0 : 1;
+  }();
   const int64_t q = pair ? 16 : 8;
   int64_t slots = std::max<int64_t>(q, (int64_t(device_cu_count()) * occ) / q * q);
   slots = std::min<int64_t>(slots, (nchunks + q - 1) / q * q);
   gf_gemm_fp4ar_kernel<MGW, WPG, UNI, COPY, R><<<unsigned(slots), 256, lds, stream>>>(
       (cptr<uint64_t>)a.in, (cptr<uint64_t>)a.out, (cptr<uint64_t>)a.copy, static_cast<const i32x4*>(a.bitmat), a.k,
-      a.m, a.mg, a.col0, nchunks, slots, a.in_stride, pair);
+      a.m, a.mg, a.col0, nchunks, slots, a.in_stride, pair, sink_spread);
   return hipGetLastError();
 }
 

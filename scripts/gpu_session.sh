@@ -18,7 +18,7 @@
 #   sweep      the reference's published k-sweep (scripts/sweep.py)
 #   gf16       the design doc's GF(16)-method point (k=4, n=6, 1.1 GB; device + e2e)
 #   lut        kbench: v_perm vs FP4 / int8 MFMA vs the LDS nibble-table kernel on every shape
-#   wide       FP4 wide-stripe shapes: default kernels vs A-resident (plain / XCD-paired chunks)
+#   wide       FP4 wide-stripe shapes: default kernels vs A-resident, spread vs single sink slot
 #   ad hoc:    CMD="..." scripts/gpu_session.sh NAME cmd   (one step, 600 s)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -128,8 +128,9 @@ r_wide() {  # wide-stripe FP4 kernel shapes (k=128, m rebuilt rows, with / witho
   local i
   for i in 1 2; do
     step wide_default_$i 300 $PY scripts/fp4_shapes.py ${WIDE_MS:-20,24,26,28,32} &&
-    step wide_ar_$i 300 env GFRS_FP4_KERNEL=ar GFRS_AR_PAIR=0 $PY scripts/fp4_shapes.py ${WIDE_MS:-20,24,26,28,32} &&
-    step wide_ar_pair_$i 300 env GFRS_FP4_KERNEL=ar GFRS_AR_PAIR=1 $PY scripts/fp4_shapes.py ${WIDE_MS:-20,24,26,28,32} || return 1
+    step wide_default_sink1_$i 300 env GFRS_FP4_SINK=1 $PY scripts/fp4_shapes.py ${WIDE_MS:-20,24,26,28,32} &&
+    step wide_ar_$i 300 env GFRS_FP4_KERNEL=ar $PY scripts/fp4_shapes.py ${WIDE_MS:-20,24,26,28,32} &&
+    step wide_ar_sink1_$i 300 env GFRS_FP4_KERNEL=ar GFRS_FP4_SINK=1 $PY scripts/fp4_shapes.py ${WIDE_MS:-20,24,26,28,32} || return 1
   done
 }
 r_cmd() { step cmd 600 bash -c "$CMD"; }
