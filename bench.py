@@ -137,7 +137,7 @@ def parse(argv=None):
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu: the C++ CPU codec over gloo (launcher / communication plumbing on a host)")
     a = ap.parse_args(argv)
-    pr = dict(scaling="weak", gather="step", lanes=2, **PRESETS[a.preset])
+    pr = {"scaling": "weak", "gather": "step", "lanes": 2, **PRESETS[a.preset]}
     for key, val in pr.items():
         if getattr(a, key) is None:
             setattr(a, key, val)

@@ -103,7 +103,7 @@ template <int MGW, int WPG, bool UNI, bool COPY, int R>
 __global__ __launch_bounds__(256, 1) void gf_gemm_fp4ar_kernel(cptr<uint64_t> in, cptr<uint64_t> out,
                                                                cptr<uint64_t> copy, const i32x4* __restrict__ bitmat,
                                                                int k, int m, int mg, int64_t col0, int64_t nchunks,
-                                                               int64_t chunk_slots, int64_t in_stride, int pair,
+                                                               int64_t chunk_slots, int64_t in_stride,
                                                                int sink_spread) {
   constexpr int CG = 4 / WPG;               // column groups per block
   constexpr int kBC = CG * kCW;             // block columns per chunk
@@ -116,11 +116,7 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4ar_kernel(cptr<uint64_t> in
   uint64_t* outptr = rowptr + 256;
   uint64_t* copyptr = outptr + 32;
   const int bid = blockIdx.x;
-  // slot -> column chunk. Blocks are dealt to the 8 XCDs round-robin (bid & 7). pair: blocks b and
-  // b + 8 (one XCD) take ADJACENT chunks, so a two-row-half block's 128-column chunk and its
-  // neighbour (256 contiguous columns, as one 4-column-group block writes) leave through one L2.
-  const int64_t slot0 = pair ? int64_t(bid >> 4) * 16 + 2 * (bid & 7) + ((bid >> 3) & 1)
-                             : int64_t(bid >> 3) * 8 + (bid & 7);
+  const int64_t slot0 = int64_t(bid >> 3) * 8 + (bid & 7);  // slot -> one XCD (blocks round-robin)
   if (slot0 >= chunk_slots) return;
   const int my_chunks = int((nchunks - slot0 + chunk_slots - 1) / chunk_slots);
   if (my_chunks <= 0) return;
@@ -439,22 +435,15 @@ hipError_t launch_ar(const Fp4ArLaunch& a, int64_t* done, hipStream_t stream) {
   const int64_t nchunks = a.ncols / kBC;
   *done = nchunks * kBC;
   if (nchunks == 0) return hipSuccess;
-  // GFRS_AR_PAIR: 1 = adjacent chunks per XCD pair for two-row-half blocks (default off until measured)
-  static const int pair_env = [] {
-    const char* e = std::getenv("GFRS_AR_PAIR");
-    return e ? std::atoi(e) : 0;
-  }();
-  const int pair = (WPG == 2 && pair_env) ? 1 : 0;
   static const int sink_spread = [] {  // GFRS_FP4_SINK=1: one shared sink slot (A/B only)
     const char* e = std::getenv("GFRS_FP4_SINK");
     return (e && std::atoi(e) == 1) ? 0 : 1;
   }();
-  const int64_t q = pair ? 16 : 8;
-  int64_t slots = std::max<int64_t>(q, (int64_t(device_cu_count()) * occ) / q * q);
-  slots = std::min<int64_t>(slots, (nchunks + q - 1) / q * q);
+  int64_t slots = std::max<int64_t>(8, (int64_t(device_cu_count()) * occ) / 8 * 8);
+  slots = std::min<int64_t>(slots, (nchunks + 7) / 8 * 8);
   gf_gemm_fp4ar_kernel<MGW, WPG, UNI, COPY, R><<<unsigned(slots), 256, lds, stream>>>(
       (cptr<uint64_t>)a.in, (cptr<uint64_t>)a.out, (cptr<uint64_t>)a.copy, static_cast<const i32x4*>(a.bitmat), a.k,
-      a.m, a.mg, a.col0, nchunks, slots, a.in_stride, pair, sink_spread);
+      a.m, a.mg, a.col0, nchunks, slots, a.in_stride, sink_spread);
   return hipGetLastError();
 }
 

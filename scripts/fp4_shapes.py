@@ -22,7 +22,7 @@ def main():
     data = alloc_rows(k, C, "cuda")
     fill_random_(data.as_strided((data.untyped_storage().nbytes(),), (1,)), seed=3)
     dst = alloc_rows(k, C, "cuda")
-    res = {"env": {x: os.environ.get(x) for x in ("GFRS_FP4_EXACT_MG", "GFRS_FP4_KERNEL", "GFRS_FP4_COPY", "GFRS_AR_PAIR", "GFRS_FP4_SINK")}}
+    res = {"env": {x: os.environ.get(x) for x in ("GFRS_FP4_EXACT_MG", "GFRS_FP4_KERNEL", "GFRS_FP4_COPY", "GFRS_FP4_SINK")}}
     rng = np.random.default_rng(5)
     ms = [int(x) for x in sys.argv[1].split(",")] if len(sys.argv) > 1 else [20, 24, 28, 32]
     if "--scattered" in sys.argv:  # inputs as separate allocations (the row-pointer-table kernels)

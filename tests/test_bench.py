@@ -80,6 +80,20 @@ def test_single_rank_record_and_comm_choice():
         assert key in rec
 
 
+def test_every_preset_parses():
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    for name, pr in bench.PRESETS.items():
+        a = bench.parse(["--preset", name])
+        assert (a.k, a.n, a.bytes, a.erasures) == (pr["k"], pr["n"], pr["bytes"], pr["erasures"])
+        assert a.scaling == pr.get("scaling", "weak") and a.lanes == pr.get("lanes", 2)
+    a = bench.parse(["--preset", "k16n20_64g", "--scaling", "weak", "--lanes", "2"])
+    assert a.scaling == "weak" and a.lanes == 2  # explicit flags win over the preset
+
+
 def test_world_size_mismatch_is_an_error():
     r = _run(["--device", "cpu", "--gpus", "3", "--steps", "1"], env={"WORLD_SIZE": "2", "RANK": "0"})
     assert r.returncode == 2 and "WORLD_SIZE=2" in r.stderr
