@@ -53,8 +53,14 @@ inline uint8_t* thp_pinned_alloc(size_t n, int touch_threads = 8) {
     });
   for (auto& t : th) t.join();
   if (hipHostRegister(p, len, hipHostRegisterDefault) != hipSuccess) {
+    // registration refused (e.g. a locked-memory limit): fall back to the runtime's own pinned
+    // allocator rather than failing the codec
     munmap(p, len);
-    return nullptr;
+    void* q = nullptr;
+    if (hipHostMalloc(&q, n ? n : 1, hipHostMallocDefault) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> g(host_alloc_detail::mu());
+    host_alloc_detail::sizes()[static_cast<uint8_t*>(q)] = 0;  // 0: hipHostFree on release
+    return static_cast<uint8_t*>(q);
   }
   std::lock_guard<std::mutex> g(host_alloc_detail::mu());
   host_alloc_detail::sizes()[p] = len;
@@ -69,6 +75,10 @@ inline void thp_pinned_free(uint8_t* p) {
     if (it == host_alloc_detail::sizes().end()) return;
     len = it->second;
     host_alloc_detail::sizes().erase(it);
+  }
+  if (len == 0) {  // the hipHostMalloc fallback
+    (void)hipHostFree(p);
+    return;
   }
   (void)hipHostUnregister(p);
   munmap(p, len);

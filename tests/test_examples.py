@@ -13,6 +13,7 @@ CASES = [
     (["bash", os.path.join(EX, "encode_decode.sh")], "identity decode OK"),
     (["bash", os.path.join(EX, "streaming_resume.sh")], "streamed round trip OK"),
     ([sys.executable, os.path.join(EX, "python_api.py")], "python API tour OK"),
+    ([sys.executable, os.path.join(EX, "distributed.py")], "distributed tour OK"),
 ]
 
 
@@ -21,7 +22,7 @@ def _run(cmd, cwd, env_extra=None):
     return subprocess.run(cmd, cwd=cwd, env=env, capture_output=True, text=True, timeout=300)
 
 
-@pytest.mark.parametrize("cmd,expect", CASES, ids=["encode_decode", "streaming_resume", "python_api"])
+@pytest.mark.parametrize("cmd,expect", CASES, ids=["encode_decode", "streaming_resume", "python_api", "distributed"])
 def test_example_cpu(cmd, expect, tmp_path):
     r = _run(cmd, tmp_path, {"HIP_VISIBLE_DEVICES": "", "CUDA_VISIBLE_DEVICES": ""})
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
@@ -31,7 +32,7 @@ def test_example_cpu(cmd, expect, tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("cmd,expect", CASES, ids=["encode_decode", "streaming_resume", "python_api"])
+@pytest.mark.parametrize("cmd,expect", CASES, ids=["encode_decode", "streaming_resume", "python_api", "distributed"])
 def test_example_gpu(cmd, expect, tmp_path):
     r = _run(cmd, tmp_path)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
