@@ -19,6 +19,7 @@
 #   gf16       the design doc's GF(16)-method point (k=4, n=6, 1.1 GB; device + e2e)
 #   lut        kbench: v_perm vs FP4 / int8 MFMA vs the LDS nibble-table kernel on every shape
 #   wide       FP4 wide-stripe shapes: default kernels vs A-resident, spread vs single sink slot
+#   e2efull    host pipeline sweep (streams x slice) for the full-decode and encode shapes
 #   ad hoc:    CMD="..." scripts/gpu_session.sh NAME cmd   (one step, 600 s)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -132,6 +133,11 @@ r_wide() {  # wide-stripe FP4 kernel shapes (k=128, m rebuilt rows, with / witho
     step wide_ar_$i 300 env GFRS_FP4_KERNEL=ar $PY scripts/fp4_shapes.py ${WIDE_MS:-20,24,26,28,32} &&
     step wide_ar_sink1_$i 300 env GFRS_FP4_KERNEL=ar GFRS_FP4_SINK=1 $PY scripts/fp4_shapes.py ${WIDE_MS:-20,24,26,28,32} || return 1
   done
+}
+r_e2efull() {  # host pipeline, the reference's decode shape (k=10 in, all 10 natives out) and the encode shape
+  step pipe_full 300 $PY scripts/pipe_bench.py --m 10 --streams 1,2,3,4 --split 1 --rect 1 \
+    --slices 8388608,16777216,33554432 &&
+  step pipe_enc 300 $PY scripts/pipe_bench.py --m 4 --streams 1,2,3,4 --split 1 --rect 1 --slices 8388608,16777216,33554432
 }
 r_cmd() { step cmd 600 bash -c "$CMD"; }
 
