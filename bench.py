@@ -239,14 +239,14 @@ class GpuWorkload:
         torch.cuda.set_stream(self.stream)
 
     def _prepare(self, i: int, dec, stream) -> None:
-        """Step i's pattern into dec.rows (rank 0 writes it; with bcast every rank receives it over
-        RCCL), then the on-device check + solve + plan build — all ordered on `stream`."""
+        """Step i's pattern (rank 0 takes it from the device-resident pool; with bcast every other
+        rank receives it over RCCL into its decoder's rows), then the on-device check + solve + plan
+        build — all ordered on `stream`, no copies."""
         with torch.cuda.stream(stream):
-            if self.rank == 0 or not self.bcast:
-                dec.rows.copy_(self.pool_dev[i % self.pool_dev.shape[0]], non_blocking=True)
+            src = self.pool_dev[i % self.pool_dev.shape[0]] if (self.rank == 0 or not self.bcast) else dec.rows
             if self.bcast:
-                dist.broadcast(dec.rows, 0)
-            dec.solve(stream)
+                dist.broadcast(src, 0)
+            dec.solve(stream, rows=src)
 
     def step(self, i: int, slot: int) -> None:
         """One encode + one device-built decode plan + one decode GEMM.

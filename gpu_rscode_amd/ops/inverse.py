@@ -160,9 +160,13 @@ class PatternDecoder:
     def engine(self) -> str:
         return self.plan.engine
 
-    def solve(self, stream: torch.cuda.Stream | None = None) -> torch.Tensor:
-        """Build the plan for the pattern now in :attr:`rows` (device work on ``stream``)."""
-        return decode_system_into_plan(self.g, self.rows, self.erased, self.plan, status=self.status, stream=stream,
+    def solve(self, stream: torch.cuda.Stream | None = None, rows: torch.Tensor | None = None) -> torch.Tensor:
+        """Build the plan for the pattern now in :attr:`rows` — or in ``rows`` (any device int32 [k]
+        tensor, e.g. a row of a device-resident pattern pool: no copy) — as device work on ``stream``."""
+        rows = self.rows if rows is None else rows
+        if rows.dtype != torch.int32 or rows.device != self.g.device or rows.numel() != self.k or not rows.is_contiguous():
+            raise ValueError("rows must be a contiguous int32 [k] tensor on the decoder's device")
+        return decode_system_into_plan(self.g, rows, self.erased, self.plan, status=self.status, stream=stream,
                                        ptrs=self.ptrs)
 
     def run(self, stream: torch.cuda.Stream | None = None, **kw) -> None:
