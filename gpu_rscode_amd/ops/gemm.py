@@ -340,7 +340,7 @@ class GemmPlan:
             h.gemm_variant(int(self.desc.data_ptr()), self.k, self.m_pad, col0, ncols, vec, pf, nt, max_blocks, s)
 
 
-# wide stripes go to the FP4 matrix-core kernel: measured on MI355X (profiles/r01_kbench5) it wins
+# wide stripes go to the FP4 matrix-core kernel: measured on MI355X (profiles/archive/r01_kbench5) it wins
 # from k*m ~ 2k coefficients (k=128, p=32: 1.10 ms vs 1.45 ms per GiB); narrow codes stay on the
 # v_perm kernel, which is at the HBM roofline there (k=10, p=4: 0.27 ms vs 0.87 ms).
 _MFMA_MIN_K, _MFMA_MIN_M = 64, 16
