@@ -10,10 +10,11 @@ under torchrun (the driver's launch) every rank checks WORLD_SIZE == --gpus.
 
 One step on every rank:
   1. encode:  parity[4, C] = E . data[10, C]                          (gfx950 v_perm GF-GEMM)
-  2. decode:  4 erased chunks (natives AND parity) drawn from a pool of recoverable patterns. The
-              pattern lives in device memory: rank 0 writes it and RCCL-broadcasts it to every rank
-              (a lost node takes the same chunk index from every stripe — the reference's one shared
-              decode system, src/decode.cu:375). Each rank then checks it, solves the systematic
+  2. decode:  4 random erased chunks (natives AND parity, at least one native) drawn from a pool
+              of recoverable patterns. The pattern lives in device memory: rank 0 takes it from the
+              device-resident pool and RCCL-broadcasts it to every rank (a lost node takes the same
+              chunk index from every stripe — the reference's one shared decode system,
+              src/decode.cu:375). Each rank then checks it, solves the systematic
               e x (e+k) decode system and writes the decode plan (row pointers + tables) ON DEVICE
               (ops.PatternDecoder; on a side stream, one step ahead), and one fused pass rebuilds the
               erased natives and copies the surviving ones into a fresh [10, C] output.
@@ -164,19 +165,15 @@ def launch(gpus: int, argv: list[str]) -> int:
 
 # ---- workloads -------------------------------------------------------------------------------
 def erasure_pool(k: int, n: int, erasures: int, rs: ReedSolomon, size: int = 16) -> list[list[int]]:
-    """Recoverable survivor lists with `erasures` of the n chunks lost. Every pattern loses the same
-    number of natives — ceil(erasures * k / n), the expected share rounded up (3 of 4 at k=10, n=14;
-    26 of 32 at k=128, n=160) — so one device-built decode plan shape serves the whole pool; the
-    rest of the erasures hit parity chunks."""
+    """Recoverable survivor lists with `erasures` random chunks of the n lost (natives and parity
+    alike), at least one native among them — BASELINE config #3's "4 random erasures". Patterns
+    with the same number of erased natives share one device-built decode plan."""
     rng = np.random.default_rng(1234)
-    e_nat = min(k, erasures, max(erasures - (n - k), -(-erasures * k // n)))
     pool = []
     while len(pool) < size:
-        nat = rng.choice(k, size=e_nat, replace=False).tolist()
-        par = (k + rng.choice(n - k, size=erasures - e_nat, replace=False)).tolist()
-        erased = set(nat + par)
+        erased = set(rng.choice(n, size=erasures, replace=False).tolist())
         rows = [r for r in range(n) if r not in erased]
-        if rs.is_recoverable(rows):
+        if any(e < k for e in erased) and rs.is_recoverable(rows):
             pool.append(rows)
     return pool
 
@@ -206,10 +203,14 @@ class GpuWorkload:
         self.g_dev = torch.from_numpy(np.ascontiguousarray(g)).to(dev)
         self.e_mat = e_mat
         self.pool_dev = pool_dev
-        self.e = k - sum(1 for r in pool_dev[0].tolist() if r < k)
+        # erased natives per pool pattern (known on the host: it picks the plan shape, the pattern
+        # itself only ever travels on the device)
+        self.e_of = [k - sum(1 for r in rows if r < k) for rows in pool_dev.tolist()]
         self.enc = [GemmPlan(self.data, par, e_mat, engine=a.engine) for par in self.parity]
-        self.dec = [PatternDecoder(self.g_dev, [self.data[i] for i in range(k)] + [par[i] for i in range(self.p)],
-                                   [self.outs[s % self.lanes][i] for i in range(k)], self.e)
+        # one device-built decode plan per (slot, number of erased natives)
+        self.dec = [{e: PatternDecoder(self.g_dev, [self.data[i] for i in range(k)] + [par[i] for i in range(self.p)],
+                                       [self.outs[s % self.lanes][i] for i in range(k)], e)
+                     for e in sorted(set(self.e_of))}
                     for s, par in enumerate(self.parity)]
         self.streams = [torch.cuda.Stream(dev) for _ in range(self.lanes)]  # non-default (hipGraph capture)
         self.stream = self.streams[0]
@@ -254,7 +255,7 @@ class GpuWorkload:
         Default schedule: the plan of step i+1 is built on a side stream right after step i's decode
         GEMM is queued, so the one-workgroup solve runs beside that GEMM. Each lane's decoder waits
         for the previous decode that read its descriptor (event per decoder)."""
-        dec = self.dec[slot]
+        dec = self._dec(i, slot)
         if self.a.no_overlap:  # everything on one stream, plan first
             self._prepare(i, dec, self.stream)
             self.enc[slot].run(**self.kv)
@@ -276,13 +277,17 @@ class GpuWorkload:
         dec.used.record(self.stream)
         dec.pending = False
         nxt_slot = (i + 1) % len(self.dec)
-        self._issue(i + 1, self.dec[nxt_slot], self.lane_stream(nxt_slot))
+        self._issue(i + 1, self._dec(i + 1, nxt_slot), self.lane_stream(nxt_slot))
+
+    def _dec(self, i: int, slot: int):
+        return self.dec[slot][self.e_of[i % len(self.e_of)]]
 
     def reset(self) -> None:
         """Start a loop with no plan in flight: its first step builds its own (so a timed loop of K
         steps builds K + 1 plans — one more than it needs)."""
-        for dec in self.dec:
-            dec.pending = False
+        for decs in self.dec:
+            for dec in decs.values():
+                dec.pending = False
 
     def _issue(self, i: int, dec, stream=None) -> None:
         if not hasattr(dec, "solved"):
@@ -299,7 +304,7 @@ class GpuWorkload:
     def verify(self) -> bool:
         """Every decoder's last pattern solved (status 0), every decoded output equals the data in
         full, and every parity slot matches the numpy oracle at its head, middle and ragged tail."""
-        ok = all(int(d.status.item()) == 0 for d in self.dec)
+        ok = all(int(d.status.item()) == 0 for decs in self.dec for d in decs.values())
         ok = ok and all(torch.equal(out, self.data) for out in self.outs)
         for a, b in _check_windows(self.C):
             want = gf.GF256.gemm(self.e_mat, self.data[:, a:b].cpu().numpy())
