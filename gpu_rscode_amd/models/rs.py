@@ -160,7 +160,9 @@ class ReedSolomon:
     def decode_batch(self, survivors: torch.Tensor, rows: Sequence[int], out: torch.Tensor | None = None,
                      stream: torch.cuda.Stream | None = None) -> torch.Tensor:
         """Rebuild the erased natives of B stripes that lost the same chunks (one launch):
-        ``survivors`` [B, k, C] (chunk ids ``rows``) -> ``out`` [B, k, C] natives."""
+        ``survivors`` [B, k, C] (chunk ids ``rows``) -> ``out`` [B, k, C] natives. On the GPU the
+        surviving natives are copied in the same pass (batched fused copy) and the plan is cached
+        per (buffers, pattern), so a repeated call is one kernel launch."""
         rows = [int(r) for r in rows]
         B, k, C = survivors.shape
         if k != self.k:
@@ -170,21 +172,31 @@ class ReedSolomon:
             base = torch.empty(B * self.k * pitch, dtype=torch.uint8, device=survivors.device)
             out = base.as_strided((B, self.k, C), (self.k * pitch, pitch, 1))
         pos = {r: j for j, r in enumerate(rows)}
-        for r, j in pos.items():
-            if r < self.k:
-                out[:, r].copy_(survivors[:, j])
         erased = [i for i in range(self.k) if i not in pos]
-        if not erased:
-            return out
-        dm = self.decode_matrix(rows)[erased]
-        if survivors.device.type != "cuda":
+        if survivors.device.type != "cuda" or not erased:
+            for r, j in pos.items():
+                if r < self.k:
+                    out[:, r].copy_(survivors[:, j])
+            if not erased:
+                return out
+            dm = self.decode_matrix(rows)[erased]
             for b in range(B):
                 self._cpu_gemm(dm, _rows(survivors[b]), [out[b, i] for i in erased])
             return out
-        outs = [[out[b, i] for i in erased] for b in range(B)]
-        ins = [[survivors[b, j] for j in range(self.k)] for b in range(B)]
-        maps = self._maps(dm)
-        GemmPlan(ins, outs, None if maps is not None else dm, maps=maps).run(stream)
+        key = ("decb", tuple(rows), int(survivors.data_ptr()), tuple(survivors.stride()), tuple(survivors.shape),
+               int(out.data_ptr()), tuple(out.stride()))
+        plan = self._plans.get(key)
+        if plan is None:
+            dm = self.decode_matrix(rows)[erased]
+            maps = self._maps(dm)
+            outs = [[out[b, i] for i in erased] for b in range(B)]
+            ins = [[survivors[b, j] for j in range(self.k)] for b in range(B)]
+            copies = [[out[b, r] if r < self.k else None for r in rows] for b in range(B)]
+            plan = GemmPlan(ins, outs, None if maps is not None else dm, maps=maps, copies=copies)
+            if len(self._plans) > 64:
+                self._plans.clear()
+            self._plans[key] = plan
+        plan.run(stream)
         return out
 
     # ---- decode ------------------------------------------------------------------------------

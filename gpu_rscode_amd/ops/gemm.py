@@ -164,11 +164,16 @@ class GemmPlan:
             # batched: B stripes of identical shape, one launch (grid.y = stripe)
             if len(bi) != len(bo) or len(bi) < 1 or len(bi) > 65535:
                 raise ValueError("batched plan needs 1..65535 stripes in inputs and outputs")
-            if copies is not None or engine not in ("valu", "auto"):
-                raise ValueError("batched plans support neither fused copies nor engine='mfma'")
+            if engine not in ("valu", "auto"):
+                raise ValueError("batched plans run on the v_perm kernel (engine='valu')")
             self.batch = len(bi)
             self._stripes_in, self._stripes_out = bi, bo
             inputs, outputs = bi[0], bo[0]
+            if copies is not None:  # per stripe: k destination rows (or None entries)
+                if len(copies) != self.batch or any(len(c) != len(bi[0]) for c in copies):
+                    raise ValueError("batched copies need one list of k destinations per stripe")
+                self._stripes_copy = [list(c) for c in copies]
+                copies = copies[0]
         self.inputs = _rows(inputs)
         self.outputs = _rows(outputs)
         self.copies = None if copies is None else [c for c in copies]
@@ -190,7 +195,11 @@ class GemmPlan:
             _check_rows(all_out, "output", dev)
             if any(len(st) != self.k for st in self._stripes_in) or any(len(st) != self.m for st in self._stripes_out):
                 raise ValueError("every stripe needs the same number of input / output rows")
-        lens = [r.numel() for r in all_in + all_out + [c for c in (self.copies or []) if c is not None]]
+        all_copy = ([c for st in self._stripes_copy for c in st] if self.batch > 1 and self.copies is not None
+                    else (self.copies or []))
+        if self.batch > 1 and self.copies is not None:
+            _check_rows([c for c in all_copy if c is not None], "copy", dev)
+        lens = [r.numel() for r in all_in + all_out + [c for c in all_copy if c is not None]]
         self.ncols = min(lens) if lens else 0
         if coeff is not None:
             tables = perm_tables_from_coeff(np.asarray(coeff).reshape(self.m, self.k))
@@ -202,9 +211,9 @@ class GemmPlan:
             raise ValueError("need coeff, maps or device_tables=True")
         ptr = lambda t: int(t.data_ptr())  # noqa: E731
         self.bytewise = any(ptr(r) % 16 for r in all_in + all_out) or any(
-            c is not None and ptr(c) % 16 for c in (self.copies or []))
+            c is not None and ptr(c) % 16 for c in all_copy)
         host = build_desc([ptr(r) for r in all_in], [ptr(r) for r in all_out],
-                          None if self.copies is None else [ptr(c) if c is not None else 0 for c in self.copies],
+                          None if self.copies is None else [ptr(c) if c is not None else 0 for c in all_copy],
                           tables, self.batch)
         self.desc = torch.from_numpy(host).to(self.device)
         self.layout = desc_layout(self.k, self.m_pad, self.batch)

@@ -20,6 +20,7 @@
 #   lut        kbench: v_perm vs FP4 / int8 MFMA vs the LDS nibble-table kernel on every shape
 #   wide       FP4 wide-stripe shapes: default kernels vs A-resident, spread vs single sink slot
 #   e2efull    host pipeline sweep (streams x slice) for the full-decode and encode shapes
+#   serve      small-object serving throughput: batched vs per-object launches vs hipGraph
 #   ad hoc:    CMD="..." scripts/gpu_session.sh NAME cmd   (one step, 600 s)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -139,6 +140,7 @@ r_e2efull() {  # host pipeline, the reference's decode shape (k=10 in, all 10 na
     --slices 8388608,16777216,33554432 &&
   step pipe_enc 300 $PY scripts/pipe_bench.py --m 4 --streams 1,2,3,4 --split 1 --rect 1 --slices 8388608,16777216,33554432
 }
+r_serve() { step serve 600 $PY scripts/serve_bench.py --out $O/serve.json; }
 r_cmd() { step cmd 600 bash -c "$CMD"; }
 
 rc=0
