@@ -408,3 +408,20 @@ print("PITCH-CAP-OK")
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     r = subprocess.run(["python", "-c", code], capture_output=True, text=True, timeout=180, env=env, cwd=root)
     assert r.returncode == 0 and "PITCH-CAP-OK" in r.stdout, (r.stdout[-2000:], r.stderr[-3000:])
+
+
+def test_host_pipeline_gf16_nibble_method():
+    """gemm_host(field_w=4): the GF(16) method (doc/design.tex:190-209) through the pinned streaming
+    pipeline, checked against the numpy GF(16) nibble maps."""
+    k, p, C = 4, 2, 1_000_003
+    rs = ReedSolomon(k, k + p, field="gf16")
+    host = torch.from_numpy(np.random.default_rng(16).integers(0, 256, size=(k, C), dtype=np.uint8)).pin_memory()
+    par = torch.zeros((p, C), dtype=torch.uint8).pin_memory()
+    hip().gemm_host([0], [host[j].data_ptr() for j in range(k)], [par[i].data_ptr() for i in range(p)],
+                    np.ascontiguousarray(rs.E).tobytes(), C, 2, 1 << 18, 0, False, field_w=4)
+    maps = rs._maps(rs.E)
+    want = np.zeros((p, C), np.uint8)
+    for i in range(p):
+        for j in range(k):
+            want[i] ^= maps[i, j][host[j].numpy()]
+    assert np.array_equal(par.numpy(), want)
