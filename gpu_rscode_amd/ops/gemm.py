@@ -322,13 +322,18 @@ class GemmPlan:
         ncols = self.ncols - col0 if ncols is None else ncols
         if col0 < 0 or ncols < 0 or col0 + ncols > self.ncols:
             raise ValueError(f"column range [{col0}, {col0 + ncols}) outside rows of {self.ncols} bytes")
-        st = stream or torch.cuda.current_stream(self.device)
-        if self._ready is not None:
-            st.wait_event(self._ready)
-            self._ready = None
-        if stream is not None:
+        if stream is None:
+            if self._ready is not None:
+                torch.cuda.current_stream(self.device).wait_event(self._ready)
+                self._ready = None
+            # the raw handle: no Stream object per launch (small-object serving is launch-bound)
+            s = torch._C._cuda_getCurrentRawStream(self.device.index)
+        else:
+            if self._ready is not None:
+                stream.wait_event(self._ready)
+                self._ready = None
             self.desc.record_stream(stream)
-        s = st.cuda_stream
+            s = stream.cuda_stream
         h = hip()
         if self.batch > 1:
             if vec is not None:
