@@ -17,7 +17,9 @@ One step on every rank:
               src/decode.cu:375). Each rank then checks it, solves the systematic
               e x (e+k) decode system and writes the decode plan (row pointers + tables) ON DEVICE
               (ops.PatternDecoder; on a side stream, one step ahead), and one fused pass rebuilds the
-              erased natives and copies the surviving ones into a fresh [10, C] output.
+              erased natives and copies the surviving ones into a fresh [10, C] output. The
+              broadcast itself runs --bcast-ahead (2) steps ahead on a stream of its own, into a
+              ring of pattern slots, so a late RCCL kernel never delays a solve.
 Consecutive steps alternate between two lanes (--lanes 2: a stream, a parity slot, a decode output
 and a decode plan each), so step i+1's encode runs into the launch gap and the tail wave of step
 i's decode (every step still encodes and decodes its whole stripe).
@@ -127,6 +129,8 @@ def parse(argv=None):
     ap.add_argument("--pf", type=int, default=2, help="kernel variant: rows in flight (with --vec)")
     ap.add_argument("--nt", action="store_true", help="kernel variant: non-temporal (with --vec)")
     ap.add_argument("--no-overlap", action="store_true", help="solve on the main stream (no side stream)")
+    ap.add_argument("--bcast-ahead", type=int, default=2,
+                    help="bcast: steps a pattern's broadcast runs ahead of the step that solves it (0: in line)")
     ap.add_argument("--lanes", type=int, default=None,
                     help="streams that consecutive steps alternate between (own parity slot + decode output)")
     ap.add_argument("--preset", default="k10n14", choices=sorted(PRESETS),
@@ -220,6 +224,17 @@ class GpuWorkload:
         self.kv = dict(vec=a.vec, pf=a.pf, nt=a.nt)
         self.graph_mode = False
         self.bcast = False  # rank 0 RCCL-broadcasts each step's pattern (set per timed mode)
+        # Look-ahead broadcast: step j's pattern is broadcast on its own stream while step j - ahead
+        # is issued, into ring slot j % R; the solve of step j waits for that one broadcast only. An
+        # RCCL kernel can sit queued behind a GEMM's workgroups for hundreds of microseconds (a small
+        # copy kernel on another queue waited 150-600 us in profiles/r03_rccl), and its peers hold
+        # theirs until it starts, so in-line broadcasting would put that wait on the solve's path.
+        self.ahead = max(0, a.bcast_ahead)
+        self.ring = torch.empty((self.ahead + 2, k), dtype=torch.int32, device=dev)
+        self.pat_stream = torch.cuda.Stream(dev)
+        self.pat_ready = [torch.cuda.Event() for _ in range(self.ahead + 2)]
+        self.pat_free = [torch.cuda.Event() for _ in range(self.ahead + 2)]
+        self.bcast_next = None
 
     def flat_parity(self, slot: int) -> torch.Tensor:
         par = self.parity[slot]
@@ -288,13 +303,39 @@ class GpuWorkload:
         for decs in self.dec:
             for dec in decs.values():
                 dec.pending = False
+        self.bcast_next = None  # every rank restarts the broadcast sequence at the loop's first step
+
+    def _bcast_until(self, j: int) -> None:
+        """Issue the pattern broadcasts of every step up to j (same sequence on every rank)."""
+        R, P = len(self.ring), self.pool_dev.shape[0]
+        while self.bcast_next <= j:
+            t, s = self.bcast_next, self.bcast_next % R
+            with torch.cuda.stream(self.pat_stream):
+                # every rank, rank 0 included, solves from the ring (one code path: a one-rank RCCL
+                # group on one GPU runs the same slots and events as the peers of an 8-GPU job)
+                self.pat_stream.wait_event(self.pat_free[s])  # the solve that last read slot s
+                if self.rank == 0:
+                    self.ring[s].copy_(self.pool_dev[t % P])
+                dist.broadcast(self.ring[s], 0)
+                self.pat_ready[s].record(self.pat_stream)
+            self.bcast_next += 1
 
     def _issue(self, i: int, dec, stream=None) -> None:
         if not hasattr(dec, "solved"):
             dec.solved, dec.used = torch.cuda.Event(), torch.cuda.Event()
             dec.used.record(stream or self.stream)
         self.side.wait_event(dec.used)  # the last decode that read this descriptor is done
-        self._prepare(i, dec, self.side)
+        if self.bcast and self.ahead > 0:
+            if self.bcast_next is None:
+                self.bcast_next = i
+            self._bcast_until(i + self.ahead)
+            s = i % len(self.ring)
+            self.side.wait_event(self.pat_ready[s])
+            with torch.cuda.stream(self.side):
+                dec.solve(self.side, rows=self.ring[s])
+            self.pat_free[s].record(self.side)
+        else:
+            self._prepare(i, dec, self.side)
         dec.solved.record(self.side)
         dec.pending = True
 
@@ -686,7 +727,8 @@ def main(argv=None) -> int:
                                      "+ descriptor rows/tables" if dev.type == "cuda"
                                      else "host row-pivoted Gauss-Jordan (cached per pattern)"),
                    "engine": getattr(getattr(work, "enc", [None])[0], "engine", "cpu"), "graph": bool(a.graph),
-                   "preset": a.preset, "device": dev.type, "process_group": bool(has_pg)},
+                   "preset": a.preset, "device": dev.type, "process_group": bool(has_pg),
+                   "bcast_ahead": a.bcast_ahead if (has_pg and dev.type == "cuda") else None},
         "verified": ok,
         "vs_baseline_what": "device-resident value / reference nearest published PCIe-inclusive point; "
                             "the like-for-like ratio is e2e.vs_baseline_e2e",
