@@ -139,6 +139,10 @@ def parse(argv=None):
     ap.add_argument("--engine", default="auto", choices=["auto", "valu", "mfma"],
                     help="encode GEMM engine (auto: FP4 matrix cores for wide stripes, v_perm otherwise)")
     ap.add_argument("--graph", action="store_true", help="replay each step from a captured hipGraph (N = 1)")
+    ap.add_argument("--pg-backend", default=None, choices=["nccl", "gloo"],
+                    help="process-group backend (default: nccl = RCCL on cuda, gloo on cpu). gloo on cuda "
+                         "rehearses N ranks on fewer GPUs: ranks wrap round the visible devices (RCCL refuses two "
+                         "ranks on one GPU); weak bcast / owners / none only")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu: the C++ CPU codec over gloo (launcher / communication plumbing on a host)")
     a = ap.parse_args(argv)
@@ -149,6 +153,14 @@ def parse(argv=None):
     if a.device == "cpu" and "--bytes" not in " ".join(argv if argv is not None else sys.argv):
         a.bytes = 1 << 20  # plumbing runs: 1 MiB per rank
     a.force_pg = a.force_pg or os.environ.get("GFRS_FORCE_PG") == "1"
+    if a.pg_backend is None:
+        a.pg_backend = "nccl" if a.device == "cuda" else "gloo"
+    if a.device == "cpu" and a.pg_backend != "gloo":
+        ap.error("--device cpu runs over gloo")
+    a.rehearsal = a.device == "cuda" and a.pg_backend == "gloo"
+    if a.rehearsal and (a.scaling == "strong" or a.comm == "root" or a.graph):
+        ap.error("--pg-backend gloo on cuda: weak scaling with --comm bcast / owners / none only "
+                 "(the point-to-point gathers need RCCL)")
     return a
 
 
@@ -263,6 +275,7 @@ class GpuWorkload:
             if self.bcast:
                 dist.broadcast(src, 0)
             dec.solve(stream, rows=src)
+        dec.last_i = i
 
     def step(self, i: int, slot: int) -> None:
         """One encode + one device-built decode plan + one decode GEMM.
@@ -334,6 +347,7 @@ class GpuWorkload:
             with torch.cuda.stream(self.side):
                 dec.solve(self.side, rows=self.ring[s])
             self.pat_free[s].record(self.side)
+            dec.last_i = i
         else:
             self._prepare(i, dec, self.side)
         dec.solved.record(self.side)
@@ -346,6 +360,14 @@ class GpuWorkload:
         """Every decoder's last pattern solved (status 0), every decoded output equals the data in
         full, and every parity slot matches the numpy oracle at its head, middle and ragged tail."""
         ok = all(int(d.status.item()) == 0 for decs in self.dec for d in decs.values())
+        # each decoder's last plan was built for the pattern of the step it was issued for (on a
+        # rank other than 0 that pattern only ever arrived by the step's broadcast)
+        pool = self.pool_dev.tolist()
+        for decs in self.dec:
+            for d in decs.values():
+                if hasattr(d, "last_i"):
+                    want = sorted(set(range(self.k)) - set(pool[d.last_i % len(pool)]))
+                    ok = ok and sorted(d.erased.tolist()) == want
         ok = ok and all(torch.equal(out, self.data) for out in self.outs)
         for a, b in _check_windows(self.C):
             want = gf.GF256.gemm(self.e_mat, self.data[:, a:b].cpu().numpy())
@@ -626,16 +648,18 @@ def main(argv=None) -> int:
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if a.device == "cuda":
+        if a.rehearsal:  # (device_count does not initialise the GPU)
+            local %= max(1, torch.cuda.device_count())
         torch.cuda.set_device(local)
         dev = torch.device("cuda", local)
     else:
         dev = torch.device("cpu")
     has_pg = world > 1 or a.force_pg
     if has_pg:
-        kw = {"device_id": dev} if dev.type == "cuda" else {}
+        kw = {"device_id": dev} if a.pg_backend == "nccl" else {}
         if world == 1 and "MASTER_PORT" not in os.environ:
             kw.update(init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1)
-        dist.init_process_group("nccl" if dev.type == "cuda" else "gloo", **kw)
+        dist.init_process_group(a.pg_backend, **kw)
         if dist.get_world_size() != world:
             raise SystemExit("process group size does not match WORLD_SIZE")
     if a.graph and has_pg:
@@ -656,12 +680,13 @@ def main(argv=None) -> int:
 
     compare = has_pg and not a.no_compare
     head_strong = a.scaling == "strong"
-    weak_modes = [a.comm] + ([m for m in COMM_MODES if m != a.comm] if compare else [])
+    weak_modes = [a.comm] + ([m for m in COMM_MODES if m != a.comm and not (a.rehearsal and m == "root")]
+                             if compare else [])
     results, strong = {}, None
     work = None
     if not head_strong:
         work, C, results = run_weak(a, k, n, e_mat, rs.G, pool_t, rank, world, dev, has_pg, weak_modes)
-    if head_strong or compare:
+    if head_strong or (compare and not a.rehearsal):
         steps = a.steps if head_strong else min(a.steps, 20)
         swork, strong = run_strong(a, k, n, e_mat, rs.G, pool_t, rank, world, dev, has_pg, steps,
                                    a.warmup if head_strong else 2)
@@ -728,6 +753,9 @@ def main(argv=None) -> int:
                                      else "host row-pivoted Gauss-Jordan (cached per pattern)"),
                    "engine": getattr(getattr(work, "enc", [None])[0], "engine", "cpu"), "graph": bool(a.graph),
                    "preset": a.preset, "device": dev.type, "process_group": bool(has_pg),
+                   "pg_backend": a.pg_backend if has_pg else None,
+                   "rehearsal": (f"{world} ranks sharing {torch.cuda.device_count()} GPU(s) over gloo: a code-path "
+                                 "check, not a scaling number") if (a.rehearsal and has_pg) else None,
                    "bcast_ahead": a.bcast_ahead if (has_pg and dev.type == "cuda") else None},
         "verified": ok,
         "vs_baseline_what": "device-resident value / reference nearest published PCIe-inclusive point; "

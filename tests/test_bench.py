@@ -135,3 +135,17 @@ def test_gpu_bench_strong_gather_end_one_rank_group():
     assert r.returncode == 0, r.stderr[-3000:]
     rec = _record(r.stdout)
     assert rec["verified"] is True and rec["scaling"] == "strong" and rec["strong"]["gather_ms"] >= 0
+
+
+@pytest.mark.gpu
+def test_gpu_bench_three_ranks_rehearsed_on_one_gpu():
+    """Three ranks share the one MI355X over gloo (RCCL refuses two ranks on one GPU): ranks 1 and 2
+    take every step's pattern only from rank 0's look-ahead broadcast into their ring slots, and each
+    decoder's last plan must match the pattern of the step it was built for; owners all_to_all too."""
+    r = _run(["--gpus", "3", "--pg-backend", "gloo", "--steps", "6", "--warmup", "2", "--bytes", str(32 << 20),
+              "--no-e2e"], timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = _record(r.stdout)
+    assert rec["verified"] is True and rec["n_gpus"] == 3 and rec["config"]["pg_backend"] == "gloo"
+    assert rec["config"]["rehearsal"] and set(rec["value_by_comm"]) == {"bcast", "owners", "none"}
+    assert all(v["verified"] for v in rec["value_by_comm"].values()) and "strong" not in rec
