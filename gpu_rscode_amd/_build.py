@@ -2,7 +2,8 @@
 
 Artifacts are built next to the sources so they travel with the repository snapshot to the GPU
 box: ``gpu_rscode_amd/_hip.so`` (gfx950 kernels + runtime), ``gpu_rscode_amd/_cpu.so`` (CPU codec),
-``bin/RS`` and ``bin/CPU-RS`` (CLIs). ``make`` is incremental, so calling :func:`build` when
+``bin/RS`` and ``bin/CPU-RS`` (CLIs), ``lib/libgfrs.so`` (the C API, ``csrc/include/gfrs.h``) and
+``bin/gfrs_capi_demo``. ``make`` is incremental, so calling :func:`build` when
 everything is up to date costs a few milliseconds.
 """
 from __future__ import annotations
@@ -19,7 +20,7 @@ _lock = threading.Lock()
 
 
 def build(target: str = "all", jobs: int | None = None, quiet: bool = True) -> None:
-    """Run ``make -C csrc <target>``. Targets: ``all``, ``hip``, ``cpu``."""
+    """Run ``make -C csrc <target>``. Targets: ``all``, ``hip``, ``cpu``, ``capi``."""
     jobs = jobs or min(8, os.cpu_count() or 4)
     cmd = ["make", "-C", str(CSRC), f"-j{jobs}", target]
     with _lock:
