@@ -11,7 +11,7 @@
  * Every function returning int returns GFRS_OK (0) or a negative GFRS_E* code; the message of the
  * last failure on the calling thread is gfrs_last_error(). Launch functions are asynchronous on
  * their stream, like the kernels under them. Build: `make -C csrc capi` -> lib/libgfrs.so;
- * example: examples/capi_demo.c.
+ * example: csrc/capi/demo.c.
  */
 #ifndef GFRS_H
 #define GFRS_H

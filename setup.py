@@ -1,6 +1,7 @@
 """``pip install --no-build-isolation .`` — builds the native modules and CLIs for gfx950 with
 ``make -C csrc`` (hipcc + g++) before packaging; The bin/RS and
-bin/CPU-RS CLIs install into the environment's bin directory next to the ``gpu-rscode`` entry point.
+bin/CPU-RS CLIs install into the environment's bin directory next to the ``gpu-rscode`` entry point,
+the C API (lib/libgfrs.so, include/gfrs.h) into its lib and include directories.
 No network is needed: --no-build-isolation uses the setuptools, wheel and pybind11 already installed."""
 import os
 import subprocess
@@ -29,6 +30,6 @@ setup(
               "gpu_rscode_amd.utils"],
     package_data={"gpu_rscode_amd": ["_hip.so", "_cpu.so"]},
     entry_points={"console_scripts": ["gpu-rscode = gpu_rscode_amd.utils.cli:main"]},
-    data_files=[("bin", ["bin/RS", "bin/CPU-RS"])],
+    data_files=[("bin", ["bin/RS", "bin/CPU-RS"]), ("lib", ["lib/libgfrs.so"]), ("include", ["csrc/include/gfrs.h"])],
     cmdclass={"build_py": BuildNative},
 )

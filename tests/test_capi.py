@@ -86,7 +86,7 @@ def test_bad_arguments_are_reported_not_crashed(lib):
 
 @pytest.mark.gpu
 def test_gpu_capi_demo(lib):
-    """examples/capi_demo.c: encode plan, device-built decoder (valid, invalid, singular patterns),
+    """csrc/capi/demo.c: encode plan, device-built decoder (valid, invalid, singular patterns),
     a k=128 p=32 stripe on the FP4 matrix-core engine and the host pipeline, all from C."""
     r = subprocess.run([DEMO], capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stdout + r.stderr

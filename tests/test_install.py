@@ -14,7 +14,7 @@ def _source_copy(dst):
     """The installable part of the tree, mtimes kept (copy2) so `make` finds everything up to date and
     pip's in-tree build files (build/lib, *.egg-info) land in the copy, not in the repository."""
     ignore = shutil.ignore_patterns("__pycache__", "*.egg-info")
-    for d in ("csrc", "gpu_rscode_amd", "bin", os.path.join("build", "obj")):
+    for d in ("csrc", "gpu_rscode_amd", "bin", "lib", os.path.join("build", "obj")):
         if os.path.isdir(os.path.join(ROOT, d)):
             shutil.copytree(os.path.join(ROOT, d), os.path.join(dst, d), ignore=ignore, copy_function=shutil.copy2)
     for f in ("setup.py", "pyproject.toml", "README.md"):
@@ -29,6 +29,11 @@ def test_pip_install_outside_the_tree(tmp_path):
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert (target / "gpu_rscode_amd" / "_cpu.so").exists() and (target / "gpu_rscode_amd" / "_hip.so").exists()
     assert (target / "bin" / "RS").exists() and (target / "bin" / "CPU-RS").exists()
+    # the C API: header into <prefix>/include, library into <prefix>/lib (pip's --target keeps only
+    # the package part of lib/, so the library is checked in the wheel's RECORD)
+    assert (target / "include" / "gfrs.h").exists()
+    record = (target / "gpu_rscode_amd-0.2.0.dist-info" / "RECORD").read_text()
+    assert "libgfrs.so," in record
     env = dict(os.environ, PYTHONPATH=str(target))
     code = ("import numpy as np, torch, gpu_rscode_amd\n"
             "from gpu_rscode_amd import ReedSolomon, gf\n"
