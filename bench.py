@@ -577,6 +577,8 @@ def run_weak(a, k, n, e_mat, g, pool_dev, rank, world, dev, has_pg, modes):
             elapsed = timed_loop(work, xchg, steps, world, dev, f"timed/weak/{mode}")
             work.step = step_fn
             work.graph_mode = False
+            for j in range(steps):  # which pattern each decoder last solved (capture order differs)
+                work._dec(j, 0).last_i = j
         else:
             elapsed = timed_loop(work, xchg, steps, world, dev, f"timed/weak/{mode}")
         ok = all(xchg.verify(s) for s in range(slots))

@@ -149,3 +149,13 @@ def test_gpu_bench_three_ranks_rehearsed_on_one_gpu():
     assert rec["verified"] is True and rec["n_gpus"] == 3 and rec["config"]["pg_backend"] == "gloo"
     assert rec["config"]["rehearsal"] and set(rec["value_by_comm"]) == {"bcast", "owners", "none"}
     assert all(v["verified"] for v in rec["value_by_comm"].values()) and "strong" not in rec
+
+
+@pytest.mark.gpu
+def test_gpu_bench_graph_replay_verifies():
+    """--graph: every pattern's step captured once, replayed in the pool's order for more steps than
+    the pool holds; the record must still verify each decoder against the last pattern it ran."""
+    r = _run(["--graph", "--no-e2e", "--steps", "21", "--warmup", "2", "--bytes", str(64 << 20)], timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    rec = _record(r.stdout)
+    assert rec["verified"] is True and rec["config"]["graph"] is True
