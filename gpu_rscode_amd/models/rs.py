@@ -12,6 +12,7 @@ or a list of 1-D tensors. CUDA tensors run the gfx950 kernels; CPU tensors run t
 """
 from __future__ import annotations
 
+from collections import OrderedDict
 from typing import Sequence
 
 import numpy as np
@@ -37,6 +38,30 @@ def alloc_rows(rows: int, ncols: int, device="cuda", fill: int | None = None) ->
 
 class UnrecoverableError(gf.SingularMatrixError):
     """The surviving chunks do not determine the data (singular decode system)."""
+
+
+class _PlanCache(OrderedDict):
+    """Plans keyed by (op, buffers, pattern), least recently used evicted past ``capacity``. A hit
+    must never turn into a rebuild while a caller relies on the plan: a hipGraph capture of
+    ``encode_batch`` after 64 per-object ``encode`` calls used to miss because the old cache was
+    cleared wholesale past 64 entries (and building a plan uploads a descriptor, which a capturing
+    stream refuses)."""
+
+    def __init__(self, capacity: int = 512):
+        super().__init__()
+        self.capacity = capacity
+
+    def get(self, key, default=None):
+        if key in self:
+            self.move_to_end(key)
+            return self[key]
+        return default
+
+    def __setitem__(self, key, value):
+        super().__setitem__(key, value)
+        self.move_to_end(key)
+        while len(self) > self.capacity:
+            self.popitem(last=False)
 
 
 class ReedSolomon:
@@ -71,7 +96,7 @@ class ReedSolomon:
         else:
             raise ValueError(f"unknown field {field!r}")
         self.G = np.vstack([np.eye(k, dtype=np.uint8), self.E]).astype(np.uint8)
-        self._plans: dict = {}
+        self._plans = _PlanCache()
         self._dm: dict = {}
         self._g_dev: dict = {}  # (device, id(G)) -> G on device, for the on-device decode system
 
@@ -87,8 +112,6 @@ class ReedSolomon:
         if plan is None:
             maps = self._maps(coeff)
             plan = GemmPlan(inputs, outputs, None if maps is not None else coeff, maps=maps, copies=copies)
-            if len(self._plans) > 64:
-                self._plans.clear()
             self._plans[key] = plan
         return plan
 
@@ -193,8 +216,6 @@ class ReedSolomon:
             ins = [[survivors[b, j] for j in range(self.k)] for b in range(B)]
             copies = [[out[b, r] if r < self.k else None for r in rows] for b in range(B)]
             plan = GemmPlan(ins, outs, None if maps is not None else dm, maps=maps, copies=copies)
-            if len(self._plans) > 64:
-                self._plans.clear()
             self._plans[key] = plan
         plan.run(stream)
         return out

@@ -299,3 +299,14 @@ def test_aggressive_read_skips_missing_and_singular_subsets(tmp_path):
     ff.write_conf(str(tmp_path / "conf"), [ff.chunk_path(str(f), r) for r in bad + rest])
     cpu().decode_file(str(f), str(tmp_path / "conf"), str(tmp_path / "o"))
     assert (tmp_path / "o").read_bytes() == payload
+
+
+def test_plan_cache_is_lru():
+    from gpu_rscode_amd.models.rs import _PlanCache
+
+    c = _PlanCache(capacity=3)
+    for i in range(3):
+        c[i] = i
+    assert c.get(0) == 0  # 0 becomes the most recent
+    c[3] = 3  # evicts 1, the least recently used
+    assert list(c) == [2, 0, 3] and c.get(1) is None

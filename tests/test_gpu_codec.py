@@ -196,6 +196,39 @@ def test_batched_encode_decode_small_objects():
     assert torch.equal(out, data)
 
 
+def test_batched_plans_survive_many_per_object_plans_into_a_graph_capture():
+    """A captured hipGraph of encode_batch / decode_batch must find their cached plans even after
+    more than 64 other plans were built (per-object encodes): a miss during capture would build a
+    plan, whose descriptor upload a capturing stream refuses (scripts/serve_bench.py hit this)."""
+    k, n, B, C = 10, 14, 70, 8_192
+    rs = ReedSolomon(k, n)
+    host = np.random.default_rng(4).integers(0, 256, size=(B, k, C), dtype=np.uint8)
+    data = torch.from_numpy(host).cuda()
+    parity = torch.empty((B, n - k, C), dtype=torch.uint8, device="cuda")
+    rows = [0, 2, 3, 4, 6, 7, 9, 10, 11, 13]
+    surv = torch.empty((B, k, C), dtype=torch.uint8, device="cuda")
+    out = torch.empty((B, k, C), dtype=torch.uint8, device="cuda")
+    st = torch.cuda.Stream()
+    with torch.cuda.stream(st):
+        rs.encode_batch(data, parity)
+        for j, r in enumerate(rows):
+            surv[:, j].copy_(data[:, r] if r < k else parity[:, r - k])
+        rs.decode_batch(surv, rows, out)
+        for b in range(B):  # 70 per-object plans on top of the two batched ones
+            rs.encode(data[b], parity[b])
+    torch.cuda.synchronize()
+    parity.zero_()
+    out.zero_()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=st):
+        rs.encode_batch(data, parity)
+        rs.decode_batch(surv, rows, out)
+    g.replay()
+    torch.cuda.synchronize()
+    assert np.array_equal(parity[B - 1].cpu().numpy(), GF256.gemm(rs.E, host[B - 1]))
+    assert torch.equal(out, data)
+
+
 def test_stream_file_codec_gpu_equals_cpu_and_resumes(tmp_path):
     payload = os.urandom(5_000_011)
     g, c = tmp_path / "g", tmp_path / "c"
