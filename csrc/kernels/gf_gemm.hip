@@ -13,8 +13,9 @@
 //     redundantly re-stores the coefficient and data tiles, src/matrix.cu:250-292).
 //   * 16-byte vector loads/stores per lane (global_load_dwordx4), one-row software prefetch,
 //     no barriers at all (the reference has divergent __syncthreads on ragged tails,
-//     src/matrix.cu:269-322). Ragged byte tails go to a byte kernel instead of the reference's
-//     all-or-nothing `C % 8` switch to its slow byte path (src/matrix.cu:796).
+//     src/matrix.cu:269-322). Ragged byte tails take one extra lane per byte in the same launch
+//     instead of the reference's all-or-nothing `C % 8` switch to its slow byte path
+//     (src/matrix.cu:796).
 //   * XCD-aware block mapping: output tiles of the same column block are dealt to one XCD so the
 //     re-read of the input rows by tile > 0 hits that XCD's L2 (cdna_hip_programming.md §5.5 T1).
 //   * Fused survivor copy: decode streams every survivor row once and, when asked, writes it to
@@ -120,31 +121,43 @@ __device__ __forceinline__ void st16(gptr<u32x4> p, u32x4 v) {
   else *p = v;
 }
 
-// Byte-granular GEMM of `nbytes` columns starting at `off` for one lane (ragged tail).
+// One byte column of the ragged tail (< 16 V bytes past the last full group), one lane per byte.
+// The row bytes are loaded 8 at a time before any of them is used: a copy store may alias the
+// next row's input as far as the compiler knows, so a plain load-use-store loop serialises every
+// load behind the previous store. One lane walking the whole tail that way cost ~20 us per launch
+// (k=10, 10-byte tail: 100 dependent HBM loads), the whole kernel time of a 1 MiB object
+// (scripts/tail_probe.py, profiles/r04_tail).
 template <int MT>
-__device__ void tail_bytes(const DescView& d, int k, int m_pad, int i0, bool do_copy, int64_t off, int nbytes) {
-  for (int b = 0; b < nbytes; ++b) {
-    uint32_t acc[MT];
+__device__ void tail_byte(const DescView& d, int k, int m_pad, int i0, bool do_copy, int64_t off) {
+  constexpr int kB = 8;
+  uint32_t acc[MT];
 #pragma unroll
-    for (int i = 0; i < MT; ++i) acc[i] = 0;
-    for (int j = 0; j < k; ++j) {
-      const uint8_t x = ((gptr<const uint8_t>)d.in[j])[off + b];
-      if (do_copy && d.copy[j]) ((gptr<uint8_t>)d.copy[j])[off + b] = x;
-      const Sel s = make_sel(x);
-      const auto t = d.tab + (size_t(j) * m_pad + i0) * kPermStride;
+  for (int i = 0; i < MT; ++i) acc[i] = 0;
+  for (int j0 = 0; j0 < k; j0 += kB) {
+    uint8_t x[kB];
 #pragma unroll
-      for (int i = 0; i < MT; ++i) acc[i] = mac_map(acc[i], t + i * kPermStride, s);
+    for (int u = 0; u < kB; ++u) x[u] = j0 + u < k ? ((gptr<const uint8_t>)d.in[j0 + u])[off] : uint8_t(0);
+#pragma unroll
+    for (int u = 0; u < kB; ++u) {
+      const int j = j0 + u;
+      if (j < k) {
+        if (do_copy && d.copy[j]) ((gptr<uint8_t>)d.copy[j])[off] = x[u];
+        const Sel s = make_sel(x[u]);
+        const auto t = d.tab + (size_t(j) * m_pad + i0) * kPermStride;
+#pragma unroll
+        for (int i = 0; i < MT; ++i) acc[i] = mac_map(acc[i], t + i * kPermStride, s);
+      }
     }
-#pragma unroll
-    for (int i = 0; i < MT; ++i)
-      if (d.out[i0 + i]) ((gptr<uint8_t>)d.out[i0 + i])[off + b] = uint8_t(acc[i]);
   }
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+    if (d.out[i0 + i]) ((gptr<uint8_t>)d.out[i0 + i])[off] = uint8_t(acc[i]);
 }
 
 // Vector kernel: each lane owns V consecutive 16-byte groups of every row and keeps PF input rows
 // in flight (a static register ring: the ring slot of row j is j % PF, resolved at compile time by
-// unrolling the row loop PF-fold). Lane `ngroups` (one past the last full group) also processes the
-// < 16*V ragged tail bytes, so no second launch is needed for odd chunk sizes.
+// unrolling the row loop PF-fold). Lanes ngroups .. ngroups + tail - 1 (past the last full group)
+// take one ragged tail byte each, so no second launch is needed for odd chunk sizes.
 // Stripe b of a batched descriptor (blockIdx.y): its own row pointers, the shared table block.
 __device__ __forceinline__ DescView stripe(DescView d, int k, int m_pad) {
   const int b = blockIdx.y;
@@ -167,7 +180,7 @@ __global__ __launch_bounds__(kBlock) void gf_gemm_vec_kernel(DescView d, int k, 
   for (int64_t cb = tm.cb0; cb < nblk; cb += ncb) {
     const int64_t g = cb * kBlock + threadIdx.x;
     if (g >= ngroups) {
-      if (g == ngroups && tail > 0) tail_bytes<MT>(d, k, m_pad, i0, do_copy, col0 + g * (16 * V), tail);
+      if (g - ngroups < tail) tail_byte<MT>(d, k, m_pad, i0, do_copy, col0 + ngroups * (16 * V) + (g - ngroups));
       continue;
     }
     const int64_t off = col0 + g * (16 * V);
@@ -337,8 +350,8 @@ template <int MT, int V, int PF, bool NT>
 hipError_t launch_vec_cfg(const DescView& d, int k, int m_pad, int batch, int64_t col0, int64_t ngroups, int tail,
                           int max_blocks, hipStream_t stream) {
   const int ntiles = m_pad / MT;
-  // one extra lane past the last group handles the ragged tail
-  const Grid g = make_grid(ngroups + (tail > 0 ? 1 : 0), ntiles, max_blocks);
+  // one extra lane per ragged tail byte past the last group
+  const Grid g = make_grid(ngroups + tail, ntiles, max_blocks);
   if (g.nblk == 0) return hipSuccess;
   gf_gemm_vec_kernel<MT, V, PF, NT>
       <<<dim3(g.blocks, batch), kBlock, 0, stream>>>(d, k, m_pad, ntiles, col0, ngroups, g.nblk, g.ncb, tail);
