@@ -137,6 +137,16 @@ class ReedSolomon:
     # ---- encode ------------------------------------------------------------------------------
     def encode(self, data, parity=None, stream: torch.cuda.Stream | None = None):
         """parity = E . data. ``data``: [k, C] tensor or k rows. Returns the parity rows."""
+        fast = None
+        if isinstance(data, torch.Tensor) and isinstance(parity, torch.Tensor) and data.is_cuda:
+            # repeat calls on the same 2-D buffers: one dict lookup, no per-row views (a small-object
+            # encode is launch-bound; building 14 row views and their key took longer than the kernel)
+            fast = ("enc2d", data.data_ptr(), data.shape, data.stride(), parity.data_ptr(), parity.shape,
+                    parity.stride())
+            plan = self._plans.get(fast)
+            if plan is not None:
+                plan.run(stream)
+                return parity
         ins = _rows(data)
         if len(ins) != self.k:
             raise ValueError(f"expected {self.k} data rows, got {len(ins)}")
@@ -147,7 +157,10 @@ class ReedSolomon:
         if self.p == 0:
             return parity
         if ins[0].device.type == "cuda":
-            self._plan(self._key("enc", ins, outs), ins, outs, self.E).run(stream)
+            plan = self._plan(self._key("enc", ins, outs), ins, outs, self.E)
+            if fast is not None:
+                self._plans[fast] = plan
+            plan.run(stream)
         else:
             self._cpu_gemm(self.E, ins, outs)
         return parity
@@ -257,6 +270,16 @@ class ReedSolomon:
                 a singular pattern then yields zeros and a nonzero ``self.last_status`` instead of an
                 exception (checked lazily, no host sync on the hot path).
         """
+        fast = None
+        if (not device_invert and isinstance(survivors, torch.Tensor) and isinstance(out, torch.Tensor)
+                and survivors.is_cuda):
+            # repeat calls on the same 2-D buffers and pattern: one dict lookup (see encode)
+            fast = ("dec2d", tuple(int(r) for r in rows), survivors.data_ptr(), survivors.shape, survivors.stride(),
+                    out.data_ptr(), out.shape, out.stride())
+            plan = self._plans.get(fast)
+            if plan is not None:
+                plan.run(stream)
+                return out
         ins = _rows(survivors)
         rows = [int(r) for r in rows]
         if len(ins) != self.k or len(rows) != self.k:
@@ -300,6 +323,8 @@ class ReedSolomon:
         else:
             dm = self.decode_matrix(rows)
             plan = self._plan(key, ins, [outs[i] for i in erased], dm[erased], copies=copies)
+            if fast is not None:
+                self._plans[fast] = plan
         plan.run(stream)
         return out
 
