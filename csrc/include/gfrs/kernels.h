@@ -21,7 +21,8 @@ hipError_t launch_gf_gemm(const void* desc, int k, int m_pad, int64_t col0, int6
 hipError_t launch_gf_gemm_batched(const void* desc, int k, int m_pad, int batch, int64_t col0, int64_t ncols,
                                   bool force_bytewise, hipStream_t stream);
 
-// Variant selector for benchmarks/ablation: vec = 16-byte groups per lane (0 = byte kernel),
+// Variant selector for benchmarks/ablation: vec = 16-byte groups per lane (0 = byte kernel, -1 = the
+// byte kernel's serial round-3 form),
 // pf = input rows kept in flight per lane, nt = non-temporal loads/stores.
 hipError_t launch_gf_gemm_variant(const void* desc, int k, int m_pad, int64_t col0, int64_t ncols,
                                   int vec, int pf, bool nt, int max_blocks, hipStream_t stream);

@@ -295,8 +295,11 @@ __global__ __launch_bounds__(kBlock) void gf_gemm_vec_kernel(DescView d, int k, 
   }
 }
 
-// Byte kernel: one lane per byte column; any alignment. Used for ragged tails and unaligned rows.
-template <int MT>
+// Byte kernel: one lane per byte column; any alignment (unaligned rows, column starts off a 16-byte
+// boundary). Each lane runs tail_byte: its k row bytes are loaded 8 at a time before use. SERIAL =
+// the round-3 form (load, copy-store, use, one row at a time: every load waits for the previous
+// store), kept as an ablation (gemm_variant vec = -1).
+template <int MT, bool SERIAL>
 __global__ __launch_bounds__(kBlock) void gf_gemm_byte_kernel(DescView d, int k, int m_pad, int ntiles,
                                                               int64_t col0, int64_t ncols, int64_t nblk,
                                                               int64_t ncb) {
@@ -309,6 +312,10 @@ __global__ __launch_bounds__(kBlock) void gf_gemm_byte_kernel(DescView d, int k,
     const int64_t c = cb * kBlock + threadIdx.x;
     if (c >= ncols) continue;
     const int64_t off = col0 + c;
+    if constexpr (!SERIAL) {
+      tail_byte<MT>(d, k, m_pad, i0, do_copy, off);
+      continue;
+    }
     uint32_t acc[MT];
 #pragma unroll
     for (int i = 0; i < MT; ++i) acc[i] = 0;
@@ -360,12 +367,16 @@ hipError_t launch_vec_cfg(const DescView& d, int k, int m_pad, int batch, int64_
 
 template <int MT>
 hipError_t launch_byte(const DescView& d, int k, int m_pad, int batch, int64_t col0, int64_t ncols, int max_blocks,
-                       hipStream_t stream) {
+                       hipStream_t stream, bool serial = false) {
   if (ncols <= 0) return hipSuccess;
   const int ntiles = m_pad / MT;
   const Grid g = make_grid(ncols, ntiles, max_blocks);
-  gf_gemm_byte_kernel<MT>
-      <<<dim3(g.blocks, batch), kBlock, 0, stream>>>(d, k, m_pad, ntiles, col0, ncols, g.nblk, g.ncb);
+  if (serial)
+    gf_gemm_byte_kernel<MT, true>
+        <<<dim3(g.blocks, batch), kBlock, 0, stream>>>(d, k, m_pad, ntiles, col0, ncols, g.nblk, g.ncb);
+  else
+    gf_gemm_byte_kernel<MT, false>
+        <<<dim3(g.blocks, batch), kBlock, 0, stream>>>(d, k, m_pad, ntiles, col0, ncols, g.nblk, g.ncb);
   return hipGetLastError();
 }
 
@@ -431,7 +442,8 @@ hipError_t run(const void* desc, int k, int m_pad, int batch, int64_t col0, int6
   const DescView d = view(desc, k, m_pad, batch);
   return dispatch_tile(m_pad, [&](auto mt) -> hipError_t {
     constexpr int MT = decltype(mt)::value;
-    if (bytewise || (col0 & 15)) return launch_byte<MT>(d, k, m_pad, batch, col0, ncols, max_blocks, stream);
+    if (bytewise || (col0 & 15) || (cfg && cfg->vec < 0))
+      return launch_byte<MT>(d, k, m_pad, batch, col0, ncols, max_blocks, stream, cfg && cfg->vec < 0);
     return launch_vec<MT>(d, k, m_pad, batch, col0, ncols, cfg ? *cfg : default_cfg(MT), max_blocks, stream);
   });
 }
@@ -452,7 +464,8 @@ hipError_t launch_gf_gemm_variant(const void* desc, int k, int m_pad, int64_t co
                                   bool nt, int max_blocks, hipStream_t stream) {
   if (vec == 0) return run(desc, k, m_pad, 1, col0, ncols, true, nullptr, max_blocks, stream);
   Cfg c;
-  c.vec = vec;
+  c.vec = vec;  // vec < 0: the serial byte kernel (ablation)
+  if (vec < 0) return run(desc, k, m_pad, 1, col0, ncols, true, &c, max_blocks, stream);
   c.pf = pf;
   c.nt = nt;
   return run(desc, k, m_pad, 1, col0, ncols, false, &c, max_blocks, stream);

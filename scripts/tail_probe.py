@@ -1,6 +1,8 @@
 #!/usr/bin/env python3
 """Ragged-tail cost of the v_perm GF-GEMM: the same encode (k=10, p=4) and 4-erasure decode with
-fused copies on C with and without a < 16-byte tail, median kernel time per shape (one JSON line)."""
+fused copies on C with and without a < 16-byte tail, median kernel time per shape (one JSON line).
+--byte: also time the byte kernel (any alignment; run(vec=0)) and its serial round-3 form
+(run(vec=-1)) on the same shapes."""
 from __future__ import annotations
 
 import json
@@ -33,7 +35,8 @@ def med(fn, reps=25):
 def main():
     rs = ReedSolomon(10, 14)
     res = {}
-    for C in [int(x) for x in (sys.argv[1] if len(sys.argv) > 1 else "107374183,107374176,104858,104848").split(",")]:
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    for C in [int(x) for x in (args[0] if args else "107374183,107374176,104858,104848").split(",")]:
         data = alloc_rows(10, C, "cuda")
         fill_random_(data.as_strided((data.untyped_storage().nbytes(),), (1,)), seed=1)
         par = alloc_rows(4, C, "cuda")
@@ -46,6 +49,15 @@ def main():
         copies = [out[r] if r < 10 else None for r in rows]
         dec = GemmPlan(surv, [out[i] for i in erased], dm, copies=copies)
         res[f"C{C}_tail{C % 16}"] = {"enc_us": med(enc.run), "dec_us": med(dec.run)}
+        if "--byte" in sys.argv:
+            res[f"C{C}_tail{C % 16}"].update(byte_enc_us=med(lambda: enc.run(vec=0), 5),
+                                             byte_dec_us=med(lambda: dec.run(vec=0), 5),
+                                             serial_byte_enc_us=med(lambda: enc.run(vec=-1), 5),
+                                             serial_byte_dec_us=med(lambda: dec.run(vec=-1), 5))
+            out.zero_()
+            dec.run(vec=0)
+            torch.cuda.synchronize()
+            assert torch.equal(out, data), "byte kernel decode mismatch"
         torch.cuda.synchronize()
         assert torch.equal(out, data)
         del data, par, out, enc, dec, surv, copies
