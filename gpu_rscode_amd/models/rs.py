@@ -41,7 +41,10 @@ class UnrecoverableError(gf.SingularMatrixError):
 
 
 class _PlanCache(OrderedDict):
-    """Plans keyed by (op, buffers, pattern), least recently used evicted past ``capacity``. A hit
+    """Plans keyed by (op, buffers, pattern), least recently used evicted past ``capacity``. The
+    plans hold no references to the buffers (``hold_buffers=False``): a key names the exact row
+    pointers, so a hit only happens for the caller's live tensors, and a loop over fresh buffers
+    does not keep up to ``capacity`` generations of them allocated. A hit
     must never turn into a rebuild while a caller relies on the plan: a hipGraph capture of
     ``encode_batch`` after 64 per-object ``encode`` calls used to miss because the old cache was
     cleared wholesale past 64 entries (and building a plan uploads a descriptor, which a capturing
@@ -111,7 +114,8 @@ class ReedSolomon:
         plan = self._plans.get(key)
         if plan is None:
             maps = self._maps(coeff)
-            plan = GemmPlan(inputs, outputs, None if maps is not None else coeff, maps=maps, copies=copies)
+            plan = GemmPlan(inputs, outputs, None if maps is not None else coeff, maps=maps, copies=copies,
+                            hold_buffers=False)
             self._plans[key] = plan
         return plan
 
@@ -188,7 +192,7 @@ class ReedSolomon:
         plan = self._plans.get(key)
         if plan is None:
             maps = self._maps(self.E)
-            plan = GemmPlan(data, parity, None if maps is not None else self.E, maps=maps)
+            plan = GemmPlan(data, parity, None if maps is not None else self.E, maps=maps, hold_buffers=False)
             self._plans[key] = plan
         plan.run(stream)
         return parity
@@ -228,7 +232,7 @@ class ReedSolomon:
             outs = [[out[b, i] for i in erased] for b in range(B)]
             ins = [[survivors[b, j] for j in range(self.k)] for b in range(B)]
             copies = [[out[b, r] if r < self.k else None for r in rows] for b in range(B)]
-            plan = GemmPlan(ins, outs, None if maps is not None else dm, maps=maps, copies=copies)
+            plan = GemmPlan(ins, outs, None if maps is not None else dm, maps=maps, copies=copies, hold_buffers=False)
             self._plans[key] = plan
         plan.run(stream)
         return out
@@ -308,7 +312,7 @@ class ReedSolomon:
         if device_invert and self.field == "gf256":
             plan = self._plans.get(key)
             if plan is None:
-                plan = GemmPlan(ins, [outs[i] for i in erased], copies=copies, device_tables=True)
+                plan = GemmPlan(ins, [outs[i] for i in erased], copies=copies, device_tables=True, hold_buffers=False)
                 self._plans[key] = plan
                 plan.rows_dev = torch.tensor(rows, dtype=torch.int32, device=dev)
                 plan.erased_dev = torch.tensor(erased, dtype=torch.int32, device=dev)

@@ -152,10 +152,14 @@ class GemmPlan:
             :func:`gpu_rscode_amd.ops.inverse.invert_into_plan`).
         copies: optional k destination rows (or None entries): input j is copied there in the same
             pass (the fused survivor copy of decode).
+        hold_buffers: keep references to the row tensors (default). A plan only stores raw
+            pointers in its descriptor, so a cache that hands a plan out only for the exact pointers
+            of live tensors (``ReedSolomon``'s plan cache) passes False: otherwise every cached plan
+            pins its caller's buffers and a loop over fresh buffers keeps all of them alive.
     """
 
     def __init__(self, inputs, outputs, coeff=None, *, maps=None, copies=None, device_tables: bool = False,
-                 engine: str = "auto", mfma_mg: int = 8):
+                 engine: str = "auto", mfma_mg: int = 8, hold_buffers: bool = True):
         bi, bo = _batched_rows(inputs), _batched_rows(outputs)
         if (bi is None) != (bo is None):
             raise ValueError("inputs and outputs must both be batched ([B, rows, C]) or both not")
@@ -249,6 +253,10 @@ class GemmPlan:
                 raise ValueError("engine='lut' needs 16-byte aligned rows and one stripe")
         elif engine != "valu":
             raise ValueError(f"unknown engine {engine!r}")
+        self.has_copies = self.copies is not None
+        if not hold_buffers:
+            self.inputs = self.outputs = self.copies = None
+            self._stripes_in = self._stripes_out = self._stripes_copy = None
         self._mark_ready()
 
     def _build_bitmat(self, coeff) -> None:
@@ -341,7 +349,7 @@ class GemmPlan:
             h.gemm_batched(int(self.desc.data_ptr()), self.k, self.m_pad, self.batch, col0, ncols, self.bytewise, s)
         elif self.engine == "mfma" and vec is None and col0 % 2 == 0:
             h.gemm_fp4(int(self.bitmat.data_ptr()), int(self.desc.data_ptr()), self.k, self.m, col0, ncols,
-                       self.mfma_mg, self.in_stride, self.copies is not None, s)
+                       self.mfma_mg, self.in_stride, self.has_copies, s)
         elif self.engine == "lut" and vec is None and col0 % 16 == 0:
             h.gemm_lut(int(self.desc.data_ptr()), self.k, self.m_pad, col0, ncols, s)
         elif self.engine == "mfma_i8" and vec is None and col0 % 2 == 0:

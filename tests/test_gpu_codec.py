@@ -229,6 +229,34 @@ def test_batched_plans_survive_many_per_object_plans_into_a_graph_capture():
     assert torch.equal(out, data)
 
 
+def test_cached_plans_do_not_pin_the_callers_buffers():
+    """Encoding / decoding fresh buffers in a loop must not keep the old ones allocated: the plan
+    cache keys plans by row pointers and its plans hold no tensor references (a cache that pinned
+    its buffers would keep up to 512 generations of 1-GiB stripes alive)."""
+    k, n, C = 10, 14, 1 << 20
+    rs = ReedSolomon(k, n)
+    rows = [0, 1, 2, 5, 6, 8, 10, 11, 12, 13]
+    torch.cuda.synchronize()
+    base = torch.cuda.memory_allocated()
+    for it in range(12):
+        data = alloc_rows(k, C, "cuda", fill=it)
+        parity = rs.encode(data)
+        par2 = alloc_rows(n - k, C, "cuda")
+        rs.encode(data, par2)  # the 2-D fast-path key
+        stripe = [data[i] for i in range(k)] + [parity[i] for i in range(n - k)]
+        out = rs.decode([stripe[r] for r in rows], rows)
+        out2 = rs.decode([stripe[r] for r in rows], rows, device_invert=True)
+        batch = rs.encode_batch(data.unsqueeze(0))
+        torch.cuda.synchronize()
+        assert torch.equal(out, data) and torch.equal(out2, data) and torch.equal(par2, parity)
+        assert torch.equal(batch[0], parity)
+        del data, parity, par2, stripe, out, out2, batch
+    torch.cuda.synchronize()
+    # only descriptors and status words may stay: far below one generation of buffers (42 MiB)
+    assert torch.cuda.memory_allocated() - base < 4 << 20
+    assert len(rs._plans) >= 12
+
+
 def test_stream_file_codec_gpu_equals_cpu_and_resumes(tmp_path):
     payload = os.urandom(5_000_011)
     g, c = tmp_path / "g", tmp_path / "c"
