@@ -3,9 +3,11 @@
 // the GF-GEMM kernels can be priced against it rather than against a 1-in/1-out copy.
 //
 // Build: hipcc -O3 --offload-arch=gfx950 -o build/membench scripts/membench.hip
-// Run:   build/membench            (prints one JSON object)
+// Run:   build/membench [REPS]     (prints one JSON object)
+//        build/membench sdma [ROWS WIDTH]   (copy engines vs blit copies, one JSON line per case)
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <string>
@@ -89,7 +91,7 @@ Case mk(const char* tag) {
   return c;
 }
 
-int main(int argc, char** argv) {
+int pattern_main(int argc, char** argv) {
   const int64_t C = 107374183;            // the headline chunk size (1 GiB / 10)
   const int64_t pitch = (C + 255) / 256 * 256;
   const int reps = argc > 1 ? atoi(argv[1]) : 20;
@@ -151,4 +153,139 @@ int main(int argc, char** argv) {
   }
   printf("}\n");
   return 0;
+}
+
+// ---- copy engines: `membench sdma [ROWS WIDTH]` -----------------------------------------------
+// Device-to-device bandwidth of hipMemcpyDeviceToDeviceNoCU (SDMA, no compute units) against the
+// blit-kernel copy, alone and beside a compute-bound kernel that holds every CU. Question it
+// answers: can the wide decode's survivor copy (102 rows x 8 MiB at k=128) run on the copy engines
+// under the MFMA-bound GEMM instead of inside it? (profiles/r05_sdma: no, ~0.12 TB/s per engine.)
+// ALU-bound spin: every lane runs `iters` dependent FMAs; the result is stored so it is kept.
+__global__ void spin_kernel(float* out, int iters) {
+  float a = threadIdx.x * 1e-3f, b = 1.0001f;
+  for (int i = 0; i < iters; ++i) a = __builtin_fmaf(a, b, 1e-7f);
+  if (a == 12345.0f) out[blockIdx.x * blockDim.x + threadIdx.x] = a;
+}
+
+static float elapsed(hipEvent_t a, hipEvent_t b) {
+  float ms = 0;
+  CHECK(hipEventElapsedTime(&ms, a, b));
+  return ms;
+}
+
+int sdma_main(int argc, char** argv) {
+  const size_t rows = argc > 1 ? std::atoll(argv[1]) : 102;
+  const size_t width = argc > 2 ? std::atoll(argv[2]) : 8388608;  // 1 GiB / 128
+  const size_t pitch_src = width + 256, pitch_dst = width + 512;   // pitched rows, as the codec's
+  const size_t bytes = rows * width;
+  char *src, *dst;
+  float* sink;
+  CHECK(hipMalloc(&src, rows * pitch_src));
+  CHECK(hipMalloc(&dst, rows * pitch_dst));
+  CHECK(hipMalloc(&sink, 1 << 24));
+  CHECK(hipMemset(src, 7, rows * pitch_src));
+  CHECK(hipDeviceSynchronize());
+  hipEvent_t e0, e1, e2;
+  CHECK(hipEventCreate(&e0));
+  CHECK(hipEventCreate(&e1));
+  CHECK(hipEventCreate(&e2));
+  std::vector<hipStream_t> st(9);
+  for (auto& s : st) CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  int cus = 0;
+  CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+
+  // mode 0: one 2-D copy per stream; mode 1: one 1-D copy per row; mode 2: one 1-D copy of the
+  // stream's whole span (contiguous bytes, pitches included)
+  int mode = 0;
+  auto copy2d = [&](hipStream_t s, size_t r0, size_t r1, hipMemcpyKind kind) {
+    if (mode == 0) {
+      CHECK(hipMemcpy2DAsync(dst + r0 * pitch_dst, pitch_dst, src + r0 * pitch_src, pitch_src, width, r1 - r0, kind, s));
+    } else if (mode == 1) {
+      for (size_t r = r0; r < r1; ++r) CHECK(hipMemcpyAsync(dst + r * pitch_dst, src + r * pitch_src, width, kind, s));
+    } else {
+      CHECK(hipMemcpyAsync(dst + r0 * pitch_src, src + r0 * pitch_src, (r1 - r0) * pitch_src, kind, s));
+    }
+  };
+  // split the rows over `ns` streams, all joined into st[0] via events
+  auto copy_split = [&](int ns, hipMemcpyKind kind) {
+    std::vector<hipEvent_t> done(ns);
+    CHECK(hipEventRecord(e0, st[0]));
+    for (int i = 0; i < ns; ++i) {
+      CHECK(hipStreamWaitEvent(st[1 + i], e0, 0));
+      copy2d(st[1 + i], rows * i / ns, rows * (i + 1) / ns, kind);
+      CHECK(hipEventCreateWithFlags(&done[i], hipEventDisableTiming));
+      CHECK(hipEventRecord(done[i], st[1 + i]));
+      CHECK(hipStreamWaitEvent(st[0], done[i], 0));
+    }
+    CHECK(hipEventRecord(e1, st[0]));
+    CHECK(hipStreamSynchronize(st[0]));
+    for (auto& d : done) CHECK(hipEventDestroy(d));
+    return elapsed(e0, e1);
+  };
+
+  // calibrate the spin kernel to ~1 ms on every CU (4 waves per CU)
+  int iters = 1 << 14;
+  for (int t = 0; t < 3; ++t) {
+    CHECK(hipEventRecord(e0, st[0]));
+    spin_kernel<<<cus, 256, 0, st[0]>>>(sink, iters);
+    CHECK(hipEventRecord(e1, st[0]));
+    CHECK(hipStreamSynchronize(st[0]));
+    float ms = elapsed(e0, e1);
+    iters = int(iters * (1.0f / ms));
+  }
+
+  std::printf("{\"rows\": %zu, \"width\": %zu, \"bytes\": %zu, \"cus\": %d}\n", rows, width, bytes, cus);
+  const struct {
+    const char* name;
+    hipMemcpyKind kind;
+  } kinds[] = {{"blit", hipMemcpyDeviceToDevice}, {"nocu", hipMemcpyDeviceToDeviceNoCU}};
+  for (mode = 0; mode < 3; ++mode)
+  for (auto& kd : kinds) {
+    for (int ns : {1, 2, 4, 8}) {
+      copy_split(ns, kd.kind);  // warm
+      float best = 1e9f;
+      for (int r = 0; r < 3; ++r) best = std::min(best, copy_split(ns, kd.kind));
+      std::printf("{\"mode\": %d, \"copy\": \"%s\", \"streams\": %d, \"ms\": %.3f, \"GBps\": %.1f}\n", mode, kd.name, ns, best,
+                  2.0 * bytes / best / 1e6);
+    }
+  }
+  // overlap: spin on st[0] (every CU, ~1 ms) while the copy runs on st[1..ns]
+  for (mode = 0; mode < 3; ++mode)
+  for (auto& kd : kinds) {
+    for (int ns : {1, 4}) {
+      float best_spin = 1e9f, best_both = 1e9f;
+      for (int r = 0; r < 3; ++r) {
+        CHECK(hipEventRecord(e0, st[0]));
+        spin_kernel<<<cus, 256, 0, st[0]>>>(sink, iters);
+        CHECK(hipEventRecord(e1, st[0]));
+        CHECK(hipStreamSynchronize(st[0]));
+        best_spin = std::min(best_spin, elapsed(e0, e1));
+        std::vector<hipEvent_t> done(ns);
+        CHECK(hipEventRecord(e0, st[0]));
+        for (int i = 0; i < ns; ++i) {
+          CHECK(hipStreamWaitEvent(st[1 + i], e0, 0));
+          copy2d(st[1 + i], rows * i / ns, rows * (i + 1) / ns, kd.kind);
+          CHECK(hipEventCreateWithFlags(&done[i], hipEventDisableTiming));
+          CHECK(hipEventRecord(done[i], st[1 + i]));
+        }
+        spin_kernel<<<cus, 256, 0, st[0]>>>(sink, iters);
+        for (int i = 0; i < ns; ++i) CHECK(hipStreamWaitEvent(st[0], done[i], 0));
+        CHECK(hipEventRecord(e2, st[0]));
+        CHECK(hipStreamSynchronize(st[0]));
+        best_both = std::min(best_both, elapsed(e0, e2));
+        for (auto& d : done) CHECK(hipEventDestroy(d));
+      }
+      std::printf("{\"mode\": %d, \"overlap\": \"%s\", \"streams\": %d, \"spin_ms\": %.3f, \"spin_plus_copy_ms\": %.3f}\n", mode, kd.name, ns,
+                  best_spin, best_both);
+    }
+  }
+  CHECK(hipFree(src));
+  CHECK(hipFree(dst));
+  CHECK(hipFree(sink));
+  return 0;
+}
+
+int main(int argc, char** argv) {
+  if (argc > 1 && std::string(argv[1]) == "sdma") return sdma_main(argc - 1, argv + 1);
+  return pattern_main(argc, argv);
 }
