@@ -147,7 +147,7 @@ struct gfrs_plan {
       hip_check(gfrs::launch_gf_gemm_fp4(bitmat.p, desc.p, k, m, 0, ncols, kMgCap, copies ? 0 : in_stride, copies, s),
                 "gf_gemm_fp4");
     else
-      hip_check(gfrs::launch_gf_gemm(desc.p, k, m_pad, 0, ncols, bytewise, 0, s), "gf_gemm");
+      hip_check(gfrs::launch_gf_gemm(desc.p, k, m_pad, 0, ncols, bytewise, 0, s, copies), "gf_gemm");
   }
 };
 

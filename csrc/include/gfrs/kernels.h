@@ -13,8 +13,10 @@ namespace gfrs {
 // [col0, col0 + ncols). Uses the 16-byte v_perm kernel for the aligned body and a byte kernel for
 // the ragged tail; `force_bytewise` routes everything through the byte kernel (unaligned rows).
 // max_blocks caps grid.x (the reference's -p gridDim knob, src/main.c:74-77); 0 = uncapped.
+// copies = false promises the descriptor has no fused-copy rows (an encode): k = 10 with 4-row
+// output tiles then runs the rows-in-flight kernel (all k loads issued before the first multiply).
 hipError_t launch_gf_gemm(const void* desc, int k, int m_pad, int64_t col0, int64_t ncols,
-                          bool force_bytewise, int max_blocks, hipStream_t stream);
+                          bool force_bytewise, int max_blocks, hipStream_t stream, bool copies = true);
 
 // Batched form: `batch` stripes of identical shape share the coefficient tables (small-object
 // serving: one launch for many objects). desc built with desc_layout(k, m_pad, batch).

@@ -295,6 +295,78 @@ __global__ __launch_bounds__(kBlock) void gf_gemm_vec_kernel(DescView d, int k, 
   }
 }
 
+// Rows-in-flight kernel (narrow codes, compile-time K): each lane issues the loads of all K rows of
+// its 16-byte group before the first multiply, so a wave keeps K KiB in flight instead of the vec
+// kernel's PF KiB, and each row is consumed as it lands (the compiler counts vmcnt exactly: the
+// loop is fully unrolled and every load unconditional). This is the access form that reaches the
+// pattern ceiling with no math at all (scripts/membench.hip: 252 us for 10 rows in and 4 out,
+// against 292 us for the PF = 2 vec kernel on the same box, profiles/r05_rows). Fused copies (tile
+// 0 of a decode) are stored as their row lands.
+template <int MT, int K>
+__global__ __launch_bounds__(kBlock) void gf_gemm_rows_kernel(DescView d, int k_tail, int m_pad, int ntiles,
+                                                              int64_t col0, int64_t ngroups, int tail) {
+  // One group per lane and no grid-stride loop: around a loop, every table word (K x MT x 5, all
+  // loop-invariant) would be hoisted into SGPRs ahead of it and spilled (162 VGPRs at K = 10,
+  // MT = 4); straight-line code keeps only one row pair's tables live (80-ish VGPRs).
+  d = stripe(d, K, m_pad);
+  const TileMap tm = map_block(ntiles);
+  const int i0 = tm.tile * MT;
+  const bool do_copy = (tm.tile == 0);
+  const int64_t g = tm.cb0 * kBlock + threadIdx.x;
+  if (g >= ngroups) {
+    // (k_tail == K, passed at run time: a compile-time K would unroll the tail's row loop too)
+    if (g - ngroups < tail) tail_byte<MT>(d, k_tail, m_pad, i0, do_copy, col0 + ngroups * 16 + (g - ngroups));
+    return;
+  }
+  const int64_t off = col0 + g * 16;
+  u32x4 x[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) x[j] = ld16<true>(row_vec(d.in[j], off));
+  uint32_t acc[MT][4];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int w = 0; w < 4; ++w) acc[i][w] = 0;
+#pragma unroll
+  for (int j = 0; j < K; j += 2) {
+    if (do_copy) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+        if (j + u < K) {
+          const uint64_t cp = d.copy[j + u];
+          if (cp) st16<true>(row_vec_w(cp, off), x[j + u]);
+        }
+    }
+    const auto t0 = d.tab + (size_t(j) * m_pad + i0) * kPermStride;
+    if (j + 1 < K) {
+      const auto t1 = t0 + size_t(m_pad) * kPermStride;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        const Sel s0 = make_sel(x[j][w]);
+        const Sel s1 = make_sel(x[j + 1][w]);
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+          acc[i][w] = mac_pair(acc[i][w], t0 + i * kPermStride, s0, t1 + i * kPermStride, s1);
+      }
+    } else {
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        const Sel s = make_sel(x[j][w]);
+#pragma unroll
+        for (int i = 0; i < MT; ++i) acc[i][w] = mac_map(acc[i][w], t0 + i * kPermStride, s);
+      }
+    }
+    // one row pair at a time: the scheduler would otherwise compute every row's selectors (and
+    // load every pair's tables) as soon as the rows land, 12 VGPRs + 2 MT x 5 SGPRs per row
+    __builtin_amdgcn_sched_barrier(0);
+  }
+#pragma unroll
+  for (int i = 0; i < MT; ++i) {
+    const uint64_t op = d.out[i0 + i];
+    if (op) st16<true>(row_vec_w(op, off), u32x4{acc[i][0], acc[i][1], acc[i][2], acc[i][3]});
+  }
+}
+
 // Byte kernel: one lane per byte column; any alignment (unaligned rows, column starts off a 16-byte
 // boundary). Each lane runs tail_byte: its k row bytes are loaded 8 at a time before use. SERIAL =
 // the round-3 form (load, copy-store, use, one row at a time: every load waits for the previous
@@ -398,12 +470,51 @@ struct Cfg {
   bool nt = false;
 };
 
+template <int MT, int K>
+hipError_t launch_rows_k(const DescView& d, int m_pad, int batch, int64_t col0, int64_t ngroups, int tail,
+                         hipStream_t stream) {
+  const int ntiles = m_pad / MT;
+  const Grid g = make_grid(ngroups + tail, ntiles, 0);  // one group per lane: the whole grid
+  if (g.nblk == 0) return hipSuccess;
+  gf_gemm_rows_kernel<MT, K><<<dim3(g.blocks, batch), kBlock, 0, stream>>>(d, K, m_pad, ntiles, col0, ngroups, tail);
+  return hipGetLastError();
+}
+
+// the rows-in-flight kernel exists for the BASELINE codes' k (4, 10, 16) and k = 8, with tiles of at
+// most 4 outputs (its K x 4 VGPRs of loads plus 4 MT accumulators stay near the vec kernel's count)
+bool rows_supported(int k, int mt) { return mt <= 4 && (k == 4 || k == 8 || k == 10 || k == 16); }
+
+template <int MT>
+hipError_t launch_rows(const DescView& d, int k, int m_pad, int batch, int64_t col0, int64_t ngroups, int tail,
+                       hipStream_t stream) {
+  if constexpr (MT <= 4) {
+    switch (k) {
+      case 4: return launch_rows_k<MT, 4>(d, m_pad, batch, col0, ngroups, tail, stream);
+      case 8: return launch_rows_k<MT, 8>(d, m_pad, batch, col0, ngroups, tail, stream);
+      case 10: return launch_rows_k<MT, 10>(d, m_pad, batch, col0, ngroups, tail, stream);
+      case 16: return launch_rows_k<MT, 16>(d, m_pad, batch, col0, ngroups, tail, stream);
+      default: break;
+    }
+  }
+  return hipErrorInvalidValue;
+}
+
 template <int MT>
 hipError_t launch_vec(const DescView& d, int k, int m_pad, int batch, int64_t col0, int64_t ncols, Cfg c,
                       int max_blocks, hipStream_t stream) {
   const int gbytes = 16 * c.vec;
   const int64_t ngroups = ncols / gbytes;
   const int tail = int(ncols - ngroups * gbytes);
+  if (c.pf <= 0) {  // all rows in flight (vec = 1 only); pf = -t: output tiles of t rows instead of MT
+    const int mt = c.pf == 0 ? MT : -c.pf;
+    if (c.vec != 1 || max_blocks > 0 || m_pad % mt != 0 || !rows_supported(k, mt)) return hipErrorInvalidValue;
+    switch (mt) {
+      case 1: return launch_rows<1>(d, k, m_pad, batch, col0, ngroups, tail, stream);
+      case 2: return launch_rows<2>(d, k, m_pad, batch, col0, ngroups, tail, stream);
+      case 4: return launch_rows<4>(d, k, m_pad, batch, col0, ngroups, tail, stream);
+      default: return hipErrorInvalidValue;
+    }
+  }
 #define GFRS_CFG(V, PF, NT)                                                                             \
   if (c.vec == V && c.pf == PF && c.nt == NT)                                                           \
     return launch_vec_cfg<MT, V, PF, NT>(d, k, m_pad, batch, col0, ngroups, tail, max_blocks, stream);
@@ -435,8 +546,14 @@ Cfg default_cfg(int mt) {
   return c;
 }
 
+// Where the rows-in-flight kernel is the default (copy-free descriptors, uncapped grid): measured
+// on the encode shapes (scripts/kbench.py, profiles/r05_rows) it wins only at k = 10 with 4-row
+// tiles (262.6 vs 278.5 us per GiB); at k = 4 and 16 and in the decode (fused copies) the vec kernel
+// is faster.
+bool rows_default(int k, int mt) { return k == 10 && mt == 4; }
+
 hipError_t run(const void* desc, int k, int m_pad, int batch, int64_t col0, int64_t ncols, bool bytewise,
-               const Cfg* cfg, int max_blocks, hipStream_t stream) {
+               const Cfg* cfg, int max_blocks, hipStream_t stream, bool copies = true) {
   if (k <= 0 || m_pad <= 0 || ncols <= 0 || batch <= 0) return batch < 0 ? hipErrorInvalidValue : hipSuccess;
   if (m_pad % tile_for(m_pad) != 0 || batch > 65535) return hipErrorInvalidValue;
   const DescView d = view(desc, k, m_pad, batch);
@@ -444,6 +561,8 @@ hipError_t run(const void* desc, int k, int m_pad, int batch, int64_t col0, int6
     constexpr int MT = decltype(mt)::value;
     if (bytewise || (col0 & 15) || (cfg && cfg->vec < 0))
       return launch_byte<MT>(d, k, m_pad, batch, col0, ncols, max_blocks, stream, cfg && cfg->vec < 0);
+    if (!cfg && !copies && max_blocks == 0 && rows_default(k, MT))
+      return launch_rows<MT>(d, k, m_pad, batch, col0, ncols / 16, int(ncols % 16), stream);
     return launch_vec<MT>(d, k, m_pad, batch, col0, ncols, cfg ? *cfg : default_cfg(MT), max_blocks, stream);
   });
 }
@@ -451,8 +570,8 @@ hipError_t run(const void* desc, int k, int m_pad, int batch, int64_t col0, int6
 }  // namespace
 
 hipError_t launch_gf_gemm(const void* desc, int k, int m_pad, int64_t col0, int64_t ncols, bool force_bytewise,
-                          int max_blocks, hipStream_t stream) {
-  return run(desc, k, m_pad, 1, col0, ncols, force_bytewise, nullptr, max_blocks, stream);
+                          int max_blocks, hipStream_t stream, bool copies) {
+  return run(desc, k, m_pad, 1, col0, ncols, force_bytewise, nullptr, max_blocks, stream, copies);
 }
 
 hipError_t launch_gf_gemm_batched(const void* desc, int k, int m_pad, int batch, int64_t col0, int64_t ncols,

@@ -70,13 +70,14 @@ PYBIND11_MODULE(_hip, m) {
   });
   m.def(
       "gemm",
-      [](uint64_t desc, int k, int m_pad, int64_t col0, int64_t ncols, bool bytewise, int max_blocks, uint64_t stream) {
+      [](uint64_t desc, int k, int m_pad, int64_t col0, int64_t ncols, bool bytewise, int max_blocks, uint64_t stream,
+         bool copies) {
         check(launch_gf_gemm(reinterpret_cast<const void*>(desc), k, m_pad, col0, ncols, bytewise, max_blocks,
-                             as_stream(stream)),
+                             as_stream(stream), copies),
               "gf_gemm");
       },
       py::arg("desc"), py::arg("k"), py::arg("m_pad"), py::arg("col0"), py::arg("ncols"), py::arg("bytewise") = false,
-      py::arg("max_blocks") = 0, py::arg("stream") = 0);
+      py::arg("max_blocks") = 0, py::arg("stream") = 0, py::arg("copies") = true);
   m.def(
       "gemm_batched",
       [](uint64_t desc, int k, int m_pad, int batch, int64_t col0, int64_t ncols, bool bytewise, uint64_t stream) {

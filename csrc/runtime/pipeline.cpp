@@ -272,7 +272,7 @@ hipError_t prepare_pipeline(int device, int k, int m, int64_t ncols, const Pipel
     TraceRange tk("pipeline/prepare/kernel");
     Lane& L = ws.lane[0];
     err = launch_gf_gemm(L.slot[0].desc, k, pad_m(m), 0, std::min<int64_t>(g.slice, int64_t(probe)), opt.bytewise, 0,
-                         L.compute);
+                         L.compute, /*copies=*/false);
     if (err == hipSuccess) err = hipStreamSynchronize(L.compute);
   }
   ps.ms_kernel = ms_since(t);
@@ -288,7 +288,7 @@ hipError_t prepare_pipeline(int device, int k, int m, int64_t ncols, const Pipel
       GFRS_TRY(hipMemcpy2DAsync(L.slot[1].in, size_t(g.slice), h, probe, probe, 1, hipMemcpyHostToDevice, cin));
       GFRS_TRY(hipStreamSynchronize(cin));
       GFRS_TRY(launch_gf_gemm(L.slot[0].desc, k, pad_m(m), 0, std::min<int64_t>(g.slice, int64_t(probe)),
-                              opt.bytewise, 0, L.compute));
+                              opt.bytewise, 0, L.compute, /*copies=*/false));
       GFRS_TRY(hipMemcpyAsync(h + kProbe, L.slot[0].out, probe, hipMemcpyDeviceToHost, L.compute));
       GFRS_TRY(hipMemcpy2DAsync(h + kProbe, probe, L.slot[1].out, size_t(g.slice), probe, 1, hipMemcpyDeviceToHost,
                                 L.compute));
@@ -381,7 +381,8 @@ hipError_t gemm_host(int device, const std::vector<const uint8_t*>& in_rows, con
           GFRS_TRY(hipEventRecord(S.loaded, cin));
           GFRS_TRY(hipStreamWaitEvent(L.compute, S.loaded, 0));
         }
-        GFRS_TRY(launch_gf_gemm(S.desc, k, m_pad, 0, w, opt.bytewise, opt.max_blocks, L.compute));
+        // (pipeline descriptors never carry fused copies)
+        GFRS_TRY(launch_gf_gemm(S.desc, k, m_pad, 0, w, opt.bytewise, opt.max_blocks, L.compute, /*copies=*/false));
         for (const Run& r : out_runs)
           GFRS_TRY(copy_run(out_rows[r.first] + a, size_t(slice), S.out + size_t(r.first) * slice, r, w,
                             hipMemcpyDeviceToHost, L.compute));

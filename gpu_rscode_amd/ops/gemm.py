@@ -357,7 +357,7 @@ class GemmPlan:
         elif self.bytewise:
             h.gemm(int(self.desc.data_ptr()), self.k, self.m_pad, col0, ncols, True, max_blocks, s)
         elif vec is None:
-            h.gemm(int(self.desc.data_ptr()), self.k, self.m_pad, col0, ncols, False, max_blocks, s)
+            h.gemm(int(self.desc.data_ptr()), self.k, self.m_pad, col0, ncols, False, max_blocks, s, self.has_copies)
         else:
             h.gemm_variant(int(self.desc.data_ptr()), self.k, self.m_pad, col0, ncols, vec, pf, nt, max_blocks, s)
 

@@ -57,6 +57,29 @@ def test_gemm_variants_agree(vec, pf, nt):
     assert np.array_equal(out.cpu().numpy(), GF256.gemm(coeff, host))
 
 
+@pytest.mark.parametrize("k", [4, 8, 10, 16])
+@pytest.mark.parametrize("m,pf", [(4, 0), (4, -1), (4, -2), (2, 0), (3, 0), (1, 0)])
+def test_gemm_rows_in_flight_kernel(k, m, pf):
+    """The rows-in-flight kernel (gf_gemm_rows_kernel: all k row loads issued before the first
+    multiply, compile-time k) at every k it is built for, with its own output tile size (pf = 0) or
+    1- / 2-row tiles (pf = -1 / -2), fused copies of every other input row, and a ragged tail:
+    bit-exact against the oracle."""
+    _native_loaded()
+    ncols = 16 * 40000 + 11
+    rng = np.random.default_rng(k * 100 + m)
+    coeff = rng.integers(0, 256, size=(m, k), dtype=np.uint8)
+    host, dev = _rand_rows(k, ncols, k + m + 5)
+    out = alloc_rows(m, ncols, "cuda", fill=0)
+    cdst = alloc_rows(k, ncols, "cuda", fill=0x44)
+    copies = [cdst[j] if j % 2 else None for j in range(k)]
+    GemmPlan(dev, out, coeff, copies=copies).run(vec=1, pf=pf, nt=True)
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), GF256.gemm(coeff, host))
+    c = cdst.cpu().numpy()
+    for j in range(k):
+        assert np.array_equal(c[j], host[j] if j % 2 else np.full(ncols, 0x44, np.uint8)), j
+
+
 def test_gemm_grid_cap_and_column_window():
     _native_loaded()
     k, m, ncols = 6, 3, 200000
