@@ -22,6 +22,8 @@
 //     its destination row in the same pass (saves a full re-read of the survivors).
 #include <hip/hip_runtime.h>
 
+#include <cstdint>
+
 #include "gfrs/desc.h"
 #include "gfrs/kernels.h"
 
@@ -415,11 +417,17 @@ struct Grid {
   unsigned blocks;
 };
 
+// A launch holds at most 2^32 - 1 work-items along x: past that the column blocks are capped (the
+// vec and byte kernels stride over the rest; the rows kernel has no stride loop and is not used).
+constexpr int64_t kMaxGridBlocks = int64_t(UINT32_MAX) / kBlock;
+inline int64_t grid_cap(int ntiles) { return kMaxGridBlocks / ntiles / 8 * 8; }
+
 inline Grid make_grid(int64_t items, int ntiles, int max_blocks) {
   Grid g{};
   g.nblk = (items + kBlock - 1) / kBlock;
   g.ncb = g.nblk;
   if (max_blocks > 0 && g.ncb > max_blocks) g.ncb = max_blocks;
+  if (g.ncb > grid_cap(ntiles)) g.ncb = grid_cap(ntiles);
   const int64_t ncb8 = (g.ncb + 7) / 8 * 8;
   g.blocks = static_cast<unsigned>(ncb8 * ntiles);
   return g;
@@ -476,6 +484,7 @@ hipError_t launch_rows_k(const DescView& d, int m_pad, int batch, int64_t col0, 
   const int ntiles = m_pad / MT;
   const Grid g = make_grid(ngroups + tail, ntiles, 0);  // one group per lane: the whole grid
   if (g.nblk == 0) return hipSuccess;
+  if (g.ncb < g.nblk) return hipErrorInvalidValue;  // beyond one launch's work-items
   gf_gemm_rows_kernel<MT, K><<<dim3(g.blocks, batch), kBlock, 0, stream>>>(d, K, m_pad, ntiles, col0, ngroups, tail);
   return hipGetLastError();
 }
@@ -561,7 +570,8 @@ hipError_t run(const void* desc, int k, int m_pad, int batch, int64_t col0, int6
     constexpr int MT = decltype(mt)::value;
     if (bytewise || (col0 & 15) || (cfg && cfg->vec < 0))
       return launch_byte<MT>(d, k, m_pad, batch, col0, ncols, max_blocks, stream, cfg && cfg->vec < 0);
-    if (!cfg && !copies && max_blocks == 0 && rows_default(k, MT))
+    if (!cfg && !copies && max_blocks == 0 && rows_default(k, MT) &&
+        (ncols / 16 + kBlock) / kBlock <= grid_cap(m_pad / MT))
       return launch_rows<MT>(d, k, m_pad, batch, col0, ncols / 16, int(ncols % 16), stream);
     return launch_vec<MT>(d, k, m_pad, batch, col0, ncols, cfg ? *cfg : default_cfg(MT), max_blocks, stream);
   });
