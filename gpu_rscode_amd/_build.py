@@ -8,6 +8,8 @@ everything is up to date costs a few milliseconds.
 """
 from __future__ import annotations
 
+import contextlib
+import fcntl
 import os
 import subprocess
 import threading
@@ -27,8 +29,27 @@ def build(target: str = "all", jobs: int | None = None, quiet: bool = True) -> N
         res = subprocess.run(cmd, capture_output=True, text=True)
     if res.returncode != 0:
         raise RuntimeError(f"native build failed ({' '.join(cmd)}):\n{res.stdout[-4000:]}\n{res.stderr[-4000:]}")
+    # make left these current with respect to their own dependencies; stamp them so that a source
+    # they do not depend on (a kernel edit for _cpu.so) does not mark them stale to the loader
+    for p in TARGET_OUTPUTS.get(target, ()):
+        if p.exists():
+            os.utime(p)
     if not quiet:
         print(res.stdout)
+
+
+@contextlib.contextmanager
+def file_lock():
+    """Exclusive lock across processes (``flock`` on ``build/.lock``): ranks started together by
+    torchrun serialise their rebuilds instead of overwriting one module concurrently."""
+    path = ROOT / "build" / ".lock"
+    path.parent.mkdir(parents=True, exist_ok=True)
+    with open(path, "a") as f:
+        fcntl.flock(f, fcntl.LOCK_EX)
+        try:
+            yield
+        finally:
+            fcntl.flock(f, fcntl.LOCK_UN)
 
 
 def have_sources() -> bool:
@@ -38,6 +59,9 @@ def have_sources() -> bool:
 
 
 SOURCE_SUFFIXES = (".hip", ".cpp", ".h", ".hpp")
+_HIP_OUT = (PKG / "_hip.so", ROOT / "bin" / "RS")
+_CPU_OUT = (PKG / "_cpu.so", ROOT / "bin" / "CPU-RS")
+TARGET_OUTPUTS = {"hip": _HIP_OUT, "cpu": _CPU_OUT, "all": _HIP_OUT + _CPU_OUT}
 
 
 def newest_source_mtime() -> float:

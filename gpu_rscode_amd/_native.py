@@ -15,21 +15,28 @@ import torch  # noqa: F401  (must precede the _hip import, see module docstring)
 from . import _build
 
 _mods: dict[str, object] = {}
+_CLI = {"cpu": "CPU-RS", "hip": "RS"}  # the CLI each make target links beside its module
 
 
 def _load(name: str, target: str):
     if name in _mods:
         return _mods[name]
     so = _build.artifact(f"_{name}.so")
-    if os.environ.get("GPURS_NO_BUILD") != "1" and _build.have_sources():
-        # incremental: a no-op when the .so is newer than every source
-        try:
-            _build.build(target)
-        except (RuntimeError, OSError):
-            # a failed rebuild is only tolerable when the existing module is up to date with every
-            # source (e.g. no toolchain on this machine); a stale .so would silently run old code
-            if not so.exists() or _build.stale(so):
-                raise
+    # make runs only for a module older than some source. An up-to-date module is imported as it is
+    # even when make's intermediate objects are absent (a snapshot without build/): otherwise every
+    # rank of a torchrun job would relink it while its peers import it. The rebuild itself holds a
+    # cross-process lock and re-checks after acquiring it, so concurrent ranks build once.
+    outs = (so, _build.binary(_CLI[name]))  # what make's target produces
+    if os.environ.get("GPURS_NO_BUILD") != "1" and _build.have_sources() and any(map(_build.stale, outs)):
+        with _build.file_lock():
+            if any(map(_build.stale, outs)):
+                try:
+                    _build.build(target)
+                except (RuntimeError, OSError):
+                    # a failed rebuild is only tolerable when the existing module is up to date with
+                    # every source (e.g. no toolchain here); a stale .so would silently run old code
+                    if not so.exists() or _build.stale(so):
+                        raise
     mod = importlib.import_module(f"gpu_rscode_amd._{name}")
     _mods[name] = mod
     return mod
