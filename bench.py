@@ -45,9 +45,20 @@ the codec the way N = 1 does. --comm / --scaling choose the headline explicitly.
 
 value = (encoded bytes + decoded bytes) over all ranks / max-over-ranks step time, in GB/s (1e9).
 
+Failure isolation (N > 1). The headline is timed, verified and reduced FIRST (step_ms_by_rank shows
+every rank's own step time, so a straggler is visible). Only then do the comparison modes run, one
+at a time (e2e, none, owners, strong, root: least collective risk first), each in its own try under
+one watchdog (--compare-budget). A mode that raises is recorded as {"error": ...} and no further
+collective is issued (the group may be out of step); a mode that hangs (an RCCL peer that never
+joins) is cut off by the watchdog, which prints the record held so far. Either way rank 0 prints the
+ONE JSON line with the verified headline. init_process_group gets a bounded timeout (--pg-timeout,
+longer than both budgets). Fault injection: GFRS_FAULT_MODE=owners|root|strong [GFRS_FAULT_RANK=r]
+[GFRS_FAULT_KIND=hang] (gpu_rscode_amd/parallel/placement.py: maybe_fault).
+
 --force-pg (or GFRS_FORCE_PG=1) creates a one-rank RCCL process group at N = 1: the broadcast, the
 all_to_all, the grouped send/recv and the strong-scaling gather then run against rank 0 itself, so
-every RCCL code path of the N > 1 run executes on a single MI355X.
+every RCCL code path of the N > 1 run executes on a single MI355X. --pg-backend gloo rehearses N
+ranks on one GPU (every mode; point-to-point pieces staged through host memory).
 
 Reference comparison. The reference's published MB/s is PCIe-inclusive: H2D + kernel + D2H
 (src/encode.cu:117-119,228-232, src/decode.cu:96-98,186-190, doc/design.tex:482-500). Its nearest
@@ -68,10 +79,12 @@ import os
 os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on this driver (RCCL peers)
 
 import argparse  # noqa: E402
+import datetime  # noqa: E402
 import json  # noqa: E402
 import socket  # noqa: E402
 import subprocess  # noqa: E402
 import sys  # noqa: E402
+import threading  # noqa: E402
 import time  # noqa: E402
 
 import numpy as np  # noqa: E402
@@ -142,7 +155,15 @@ def parse(argv=None):
     ap.add_argument("--pg-backend", default=None, choices=["nccl", "gloo"],
                     help="process-group backend (default: nccl = RCCL on cuda, gloo on cpu). gloo on cuda "
                          "rehearses N ranks on fewer GPUs: ranks wrap round the visible devices (RCCL refuses two "
-                         "ranks on one GPU); weak bcast / owners / none only")
+                         "ranks on one GPU); point-to-point pieces are staged through host memory")
+    ap.add_argument("--headline-budget", type=float, default=float(os.environ.get("GFRS_HEADLINE_BUDGET_S", 600)),
+                    help="seconds for setup + the headline loop + its verification; past it rank 0 prints an "
+                         "error record and every rank exits")
+    ap.add_argument("--compare-budget", type=float, default=float(os.environ.get("GFRS_COMPARE_BUDGET_S", 180)),
+                    help="seconds for all comparison modes (value_by_comm, strong, e2e) after the headline; a "
+                         "mode still running then is recorded as timed out and the headline record printed")
+    ap.add_argument("--pg-timeout", type=float, default=float(os.environ.get("GFRS_PG_TIMEOUT_S", 900)),
+                    help="process-group timeout (init_process_group(timeout=)); longer than both budgets")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu: the C++ CPU codec over gloo (launcher / communication plumbing on a host)")
     a = ap.parse_args(argv)
@@ -158,9 +179,8 @@ def parse(argv=None):
     if a.device == "cpu" and a.pg_backend != "gloo":
         ap.error("--device cpu runs over gloo")
     a.rehearsal = a.device == "cuda" and a.pg_backend == "gloo"
-    if a.rehearsal and (a.scaling == "strong" or a.comm == "root" or a.graph):
-        ap.error("--pg-backend gloo on cuda: weak scaling with --comm bcast / owners / none only "
-                 "(the point-to-point gathers need RCCL)")
+    if a.rehearsal and a.graph:
+        ap.error("--pg-backend gloo on cuda: no --graph (a rehearsal has per-step host staging)")
     return a
 
 
@@ -440,8 +460,9 @@ def _run_steps(work, xchg, steps: int) -> None:
     xchg.drain()
 
 
-def timed_loop(work, xchg, steps: int, world: int, dev, label: str) -> float:
-    """Seconds for `steps` steps, bracketed by barrier + synchronize on both sides, max over ranks."""
+def timed_loop(work, xchg, steps: int, world: int, dev, label: str) -> list[float]:
+    """Seconds for `steps` steps, bracketed by barrier + synchronize on both sides, per rank (the
+    headline takes the max over ranks)."""
     work.reset()
     with trace_range(f"bench/{label}"):
         if world > 1:
@@ -454,14 +475,21 @@ def timed_loop(work, xchg, steps: int, world: int, dev, label: str) -> float:
             dist.barrier()
         work.sync()
         elapsed = time.perf_counter() - t0
-    return max_over_ranks(elapsed, dev, world)
+    return gather_over_ranks(elapsed, dev, world)
+
+
+def gather_over_ranks(x: float, dev, world: int) -> list[float]:
+    """x from every rank, in rank order (all_gather)."""
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    if world == 1:
+        return [float(t.item())]
+    out = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(out, t)
+    return [float(v.item()) for v in out]
 
 
 def max_over_ranks(x: float, dev, world: int) -> float:
-    t = torch.tensor([x], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t.item())
+    return max(gather_over_ranks(x, dev, world))
 
 
 def warm(work, xchg, steps: int) -> None:
@@ -550,42 +578,41 @@ def e2e(a, k, n, C, rs: ReedSolomon, rows: list[int], work: GpuWorkload, dev, wo
 
 
 # ---- runs ------------------------------------------------------------------------------------
-def run_weak(a, k, n, e_mat, g, pool_dev, rank, world, dev, has_pg, modes):
-    """Weak scaling: every rank encodes and decodes its own a.bytes stripe."""
+def weak_work(a, k, n, e_mat, g, pool_dev, rank, dev, has_pg):
+    """The weak-scaling workload: every rank encodes and decodes its own a.bytes stripe."""
     C = (a.bytes + k - 1) // k
     slots = 2 if has_pg else 1  # parity double-buffered while its exchange is in flight
-    work = make_work(a, k, n, C, e_mat, g, pool_dev, rank, dev, slots)
+    return make_work(a, k, n, C, e_mat, g, pool_dev, rank, dev, slots), C
+
+
+def run_weak_mode(a, work, mode, world, dev, has_pg, steps, warmup, graph=False):
+    """One barrier-bracketed timed loop of the weak workload with `mode`'s per-step traffic."""
+    k, C = work.k, work.C
     slots = len(work.parity)
-    flats = [work.flat_parity(s) for s in range(slots)]
-    results = {}
-    for mi, mode in enumerate(modes):
-        xchg = ParityExchange(flats, mode if mode in ("owners", "root") else "none")
-        work.bcast = has_pg and mode != "none"
-        steps = a.steps if mi == 0 else min(a.steps, 20)
-        warm(work, xchg, a.warmup if mi == 0 else 2)
-        if a.graph and mi == 0:
-            work.graph_mode = True
-            graphs = []
-            for i in range(len(pool_dev)):
-                gph = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(gph, stream=work.stream):
-                    work.step(i, 0)
-                graphs.append(gph)
-            torch.cuda.synchronize()
-            step_fn = work.step
-            work.step = lambda i, slot: graphs[i % len(graphs)].replay()  # noqa: E731
-            elapsed = timed_loop(work, xchg, steps, world, dev, f"timed/weak/{mode}")
-            work.step = step_fn
-            work.graph_mode = False
-            for j in range(steps):  # which pattern each decoder last solved (capture order differs)
-                work._dec(j, 0).last_i = j
-        else:
-            elapsed = timed_loop(work, xchg, steps, world, dev, f"timed/weak/{mode}")
-        ok = all(xchg.verify(s) for s in range(slots))
-        results[mode] = dict(elapsed=elapsed, steps=steps, ok=ok, sent=xchg.bytes_sent, recv=xchg.bytes_received,
-                             link=xchg.bytes_per_link, bytes=2 * k * C * world)
-        del xchg
-    return work, C, results
+    xchg = ParityExchange([work.flat_parity(s) for s in range(slots)], mode if mode in ("owners", "root") else "none")
+    work.bcast = has_pg and mode != "none"
+    warm(work, xchg, warmup)
+    if graph:
+        work.graph_mode = True
+        graphs = []
+        for i in range(len(work.pool_dev)):
+            gph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gph, stream=work.stream):
+                work.step(i, 0)
+            graphs.append(gph)
+        torch.cuda.synchronize()
+        step_fn = work.step
+        work.step = lambda i, slot: graphs[i % len(graphs)].replay()  # noqa: E731
+        per_rank = timed_loop(work, xchg, steps, world, dev, f"timed/weak/{mode}")
+        work.step = step_fn
+        work.graph_mode = False
+        for j in range(steps):  # which pattern each decoder last solved (capture order differs)
+            work._dec(j, 0).last_i = j
+    else:
+        per_rank = timed_loop(work, xchg, steps, world, dev, f"timed/weak/{mode}")
+    ok = all(xchg.verify(s) for s in range(slots))
+    return dict(elapsed=max(per_rank), per_rank=per_rank, steps=steps, ok=ok, sent=xchg.bytes_sent,
+                recv=xchg.bytes_received, link=xchg.bytes_per_link, bytes=2 * k * C * world)
 
 
 def run_strong(a, k, n, e_mat, g, pool_dev, rank, world, dev, has_pg, steps, warmup):
@@ -616,10 +643,10 @@ def run_strong(a, k, n, e_mat, g, pool_dev, rank, world, dev, has_pg, steps, war
     xchg = gather if (gather is not None and a.gather == "step") else _NoExchange()
     work.bcast = has_pg
     warm(work, xchg, warmup)
-    elapsed = timed_loop(work, xchg, steps, world, dev, f"timed/strong/{a.gather}")
+    per_rank = timed_loop(work, xchg, steps, world, dev, f"timed/strong/{a.gather}")
     ok = all(xchg.verify(s) for s in range(slots))
-    out = dict(elapsed=elapsed, steps=steps, ok=ok, bytes=2 * k * Ct, total_cols=Ct, widths=widths,
-               gather=a.gather, link=gather.bytes_per_link if gather else 0,
+    out = dict(elapsed=max(per_rank), per_rank=per_rank, steps=steps, ok=ok, bytes=2 * k * Ct, total_cols=Ct,
+               widths=widths, gather=a.gather, link=gather.bytes_per_link if gather else 0,
                recv=gather.bytes_received if (gather and rank == 0) else 0)
     if a.gather == "end":
         if world > 1:
@@ -629,14 +656,101 @@ def run_strong(a, k, n, e_mat, g, pool_dev, rank, world, dev, has_pg, steps, war
         gather.start(0)
         gather.drain()
         work.sync()
-        gt = max_over_ranks(time.perf_counter() - t0, dev, world)
+        gt = max(gather_over_ranks(time.perf_counter() - t0, dev, world))
         out.update(gather_ms=round(gt * 1e3, 3), gather_ok=gather.verify(0),
                    gather_GBps=round(gather.bytes_per_link * max(1, world - 1) / gt / 1e9, 3) if world > 1 else None)
         out["ok"] = out["ok"] and out["gather_ok"]
     return work, out
 
 
+# ---- failure isolation (N > 1) ---------------------------------------------------------------
+class Emitter:
+    """Prints the ONE JSON record exactly once (rank 0), from the main thread or from a watchdog."""
+
+    def __init__(self, rank: int):
+        self.rank = rank
+        self.lock = threading.Lock()
+        self.done = False
+
+    def emit(self, rec: dict) -> bool:
+        with self.lock:
+            if self.done:
+                return False
+            self.done = True
+            if self.rank == 0:
+                sys.stdout.write(json.dumps(rec) + "\n")
+            sys.stdout.flush()
+            sys.stderr.flush()
+            return True
+
+
+class Watchdog:
+    """Deadline for a stretch of collectives that may hang (an RCCL kernel whose peer never joins
+    does not raise). When it expires, `on_expire()` runs on the watchdog thread (rank 0 prints the
+    record it holds, with the stretch marked as timed out) and the process ends with `code` — no
+    re-exec, no further collectives. Every rank runs one with the same budget, so all ranks leave."""
+
+    def __init__(self, budget_s: float, on_expire, code: int = 0):
+        self.budget_s, self.on_expire, self.code = budget_s, on_expire, code
+        self.timer = threading.Timer(budget_s, self._fire)
+        self.timer.daemon = True
+
+    def _fire(self) -> None:
+        try:
+            self.on_expire()
+        finally:
+            os._exit(self.code)
+
+    def __enter__(self):
+        self.timer.start()
+        return self
+
+    def __exit__(self, *exc):
+        self.timer.cancel()
+        return False
+
+
+def _err(e: BaseException) -> str:
+    return f"{type(e).__name__}: {e}"[:500]
+
+
+def agree(ok: bool, dev, world: int) -> list[int]:
+    """Every rank's status after a comparison mode (1 ok, 0 failed verification), in rank order."""
+    if world == 1:
+        return [1 if ok else 0]
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+    out = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(out, t)
+    return [int(x.item()) for x in out]
+
+
 # ---- main ------------------------------------------------------------------------------------
+def gbps_of(r) -> float:
+    return r["bytes"] / (r["elapsed"] / r["steps"]) / 1e9
+
+
+def mode_entry(r, rank) -> dict:
+    """value_by_comm entry of a timed weak mode: rate, the busiest xGMI link's bytes per step and
+    the rate the measured step implies for it (a lower bound on what the link sustained; when the
+    step is link-bound, its rate)."""
+    return {"GBps": round(gbps_of(r), 3), "ms_per_step": round(r["elapsed"] / r["steps"] * 1e3, 4),
+            "steps": r["steps"], "bytes_sent_per_rank_step": r["sent"],
+            "bytes_recv_rank0_step": r["recv"] if rank == 0 else None,
+            "busiest_link_bytes_per_step": r["link"],
+            "busiest_link_GBps_implied": round(r["link"] / (r["elapsed"] / r["steps"]) / 1e9, 2),
+            "step_ms_by_rank": [round(x / r["steps"] * 1e3, 4) for x in r["per_rank"]],
+            "verified": r["ok"]}
+
+
+def strong_entry(a, strong, rank) -> dict:
+    return {"GBps": round(gbps_of(strong), 3), "ms_per_step": round(strong["elapsed"] / strong["steps"] * 1e3, 4),
+            "steps": strong["steps"], "stripe_bytes": a.bytes, "shard_cols": strong["widths"],
+            "gather": strong["gather"], "busiest_link_bytes_per_step": strong["link"],
+            "bytes_recv_rank0": strong["recv"] if rank == 0 else None, "verified": strong["ok"],
+            "step_ms_by_rank": [round(x / strong["steps"] * 1e3, 4) for x in strong["per_rank"]],
+            **{kk: strong[kk] for kk in ("gather_ms", "gather_GBps") if kk in strong}}
+
+
 def main(argv=None) -> int:
     argv = list(sys.argv[1:] if argv is None else argv)
     a = parse(argv)
@@ -657,61 +771,150 @@ def main(argv=None) -> int:
     else:
         dev = torch.device("cpu")
     has_pg = world > 1 or a.force_pg
-    if has_pg:
-        kw = {"device_id": dev} if a.pg_backend == "nccl" else {}
-        if world == 1 and "MASTER_PORT" not in os.environ:
-            kw.update(init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1)
-        dist.init_process_group(a.pg_backend, **kw)
-        if dist.get_world_size() != world:
-            raise SystemExit("process group size does not match WORLD_SIZE")
-    if a.graph and has_pg:
-        raise SystemExit("--graph is single-GPU only, without a process group (per-step RCCL traffic)")
-
+    emitter = Emitter(rank)
     k, n = a.k, a.n
+    # The headline's own deadline: setup + warmup + the timed loop + its verification. A hang here
+    # leaves no number to save; the record says where it stopped instead of the driver's timeout.
+    stage = {"at": "setup"}
 
-    # ---- setup: E and the erasure-pattern pool come from rank 0 (RCCL broadcast) -------------
-    rs = ReedSolomon(k, n)
-    pool = erasure_pool(k, n, a.erasures, rs)
-    e_t = torch.from_numpy(rs.E.copy()).to(dev)
-    pool_t = torch.tensor(pool, dtype=torch.int32, device=dev)
-    if has_pg:
-        dist.broadcast(e_t, 0)
-        dist.broadcast(pool_t, 0)
-    e_mat = e_t.cpu().numpy()
-    rs.E, rs.G = e_mat, gf.GF256.generator(e_mat)
+    def headline_expired():
+        emitter.emit({"metric": METRIC, "value": None, "unit": "GB/s", "n_gpus": world, "steps": a.steps,
+                      "warmup": a.warmup, "higher_is_better": True, "verified": False,
+                      "error": f"headline timed out after {a.headline_budget:g} s during {stage['at']}"})
 
-    compare = has_pg and not a.no_compare
-    head_strong = a.scaling == "strong"
-    weak_modes = [a.comm] + ([m for m in COMM_MODES if m != a.comm and not (a.rehearsal and m == "root")]
-                             if compare else [])
-    results, strong = {}, None
-    work = None
-    if not head_strong:
-        work, C, results = run_weak(a, k, n, e_mat, rs.G, pool_t, rank, world, dev, has_pg, weak_modes)
-    if head_strong or (compare and not a.rehearsal):
-        steps = a.steps if head_strong else min(a.steps, 20)
-        swork, strong = run_strong(a, k, n, e_mat, rs.G, pool_t, rank, world, dev, has_pg, steps,
-                                   a.warmup if head_strong else 2)
-        if work is None:
-            work, C = swork, swork.C
+    with Watchdog(a.headline_budget, headline_expired, code=3):
+        if has_pg:
+            kw = {"device_id": dev} if a.pg_backend == "nccl" else {}
+            if world == 1 and "MASTER_PORT" not in os.environ:
+                kw.update(init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1)
+            # bounded: a lost peer raises (gloo) or is aborted by the RCCL watchdog after this long;
+            # the bench's own watchdogs (shorter) print the record first
+            dist.init_process_group(a.pg_backend, timeout=datetime.timedelta(seconds=a.pg_timeout), **kw)
+            if dist.get_world_size() != world:
+                raise SystemExit("process group size does not match WORLD_SIZE")
+        if a.graph and has_pg:
+            raise SystemExit("--graph is single-GPU only, without a process group (per-step RCCL traffic)")
+
+        # ---- setup: E and the erasure-pattern pool come from rank 0 (RCCL broadcast) ---------
+        rs = ReedSolomon(k, n)
+        pool = erasure_pool(k, n, a.erasures, rs)
+        e_t = torch.from_numpy(rs.E.copy()).to(dev)
+        pool_t = torch.tensor(pool, dtype=torch.int32, device=dev)
+        if has_pg:
+            dist.broadcast(e_t, 0)
+            dist.broadcast(pool_t, 0)
+        e_mat = e_t.cpu().numpy()
+        rs.E, rs.G = e_mat, gf.GF256.generator(e_mat)
+
+        # ---- the headline: timed, verified and reduced before anything else runs --------------
+        head_strong = a.scaling == "strong"
+        head_mode = a.comm if has_pg else "none"
+        if head_strong:
+            stage["at"] = "strong headline"
+            work, head = run_strong(a, k, n, e_mat, rs.G, pool_t, rank, world, dev, has_pg, a.steps, a.warmup)
+            C = work.C
         else:
-            sw_ok = swork.verify()
-            strong["ok"] = strong["ok"] and sw_ok
-            del swork
+            stage["at"] = f"weak/{head_mode} headline"
+            work, C = weak_work(a, k, n, e_mat, rs.G, pool_t, rank, dev, has_pg)
+            head = run_weak_mode(a, work, head_mode, world, dev, has_pg, a.steps, a.warmup, graph=a.graph)
+        stage["at"] = "headline verification"
+        ok = work.verify() and head["ok"]
+        okt = torch.tensor([1 if ok else 0], device=dev)
+        if world > 1:
+            dist.all_reduce(okt, op=dist.ReduceOp.MIN)
+        ok = bool(okt.item())
+        rec = headline_record(a, k, n, C, world, rank, dev, has_pg, work, head, head_strong, head_mode, ok)
 
-    # ---- verification (outside the timed regions) ---------------------------------------------
-    ok = work.verify() and all(r["ok"] for r in results.values()) and (strong is None or strong["ok"])
-    okt = torch.tensor([1 if ok else 0], device=dev)
-    if world > 1:
-        dist.all_reduce(okt, op=dist.ReduceOp.MIN)
-    ok = bool(okt.item())
+    # ---- comparison modes: each on its own, after the headline is safe ----------------------
+    # A mode that raises is recorded as {"error": ...}; a mode that hangs is cut off by the
+    # watchdog, which prints the record held so far. After any failure no further collective is
+    # issued (the group may be out of step): rank 0 prints and every rank leaves.
+    # Order: least collective risk first (e2e: own PCIe link + barriers; none: no traffic; owners:
+    # one all_to_all), the point-to-point gathers (strong, root) last.
+    compare = has_pg and not a.no_compare
+    todo = []
+    if dev.type == "cuda" and not a.no_e2e and not head_strong:
+        todo.append(("e2e", None))
+    if compare and not head_strong:
+        todo += [("weak", m) for m in ("none", "owners", "bcast") if m != head_mode]
+        todo.append(("strong", a.gather))
+        if head_mode != "root":
+            todo.append(("weak", "root"))
+    done = {"n": 0}
 
-    def gbps(r):
-        return r["bytes"] / (r["elapsed"] / r["steps"]) / 1e9
+    def mark_rest(reason: str, start: int, failed: int | None = None):
+        for j in range(start, len(todo)):
+            kind, m = todo[j]
+            _store(rec, kind, m, {"error": reason} if j == failed else {"skipped": reason})
 
-    head = strong if head_strong else results[a.comm]
+    def compare_expired():
+        cur = todo[done["n"]] if done["n"] < len(todo) else None
+        mark_rest(f"timed out ({a.compare_budget:g} s budget for the comparison modes)", done["n"], done["n"])
+        if cur is not None:
+            mark_rest(f"after {cur[0]}/{cur[1]} timed out", done["n"] + 1)
+        rec["comparisons_complete"] = False
+        emitter.emit(rec)
+
+    clean = True
+    with Watchdog(a.compare_budget, compare_expired, code=0):
+        for i, (kind, m) in enumerate(todo):
+            done["n"] = i
+            try:
+                if kind == "weak":
+                    r = run_weak_mode(a, work, m, world, dev, has_pg, min(a.steps, 20), 2)
+                    r["ok"] = r["ok"] and work.verify()
+                    entry = mode_entry(r, rank)
+                elif kind == "strong":
+                    swork, r = run_strong(a, k, n, e_mat, rs.G, pool_t, rank, world, dev, has_pg, min(a.steps, 20), 2)
+                    r["ok"] = r["ok"] and swork.verify()
+                    del swork
+                    entry = strong_entry(a, r, rank)
+                else:
+                    # the reference's worst case (src/unit-test.sh: keep the last k chunks): the first
+                    # `erasures` natives are lost, so every one of them is rebuilt and copied back
+                    e = min(a.erasures, k, n - k)
+                    entry = e2e(a, k, n, C, rs, list(range(e, k)) + list(range(k, k + e)), work, dev, world)
+                    r = {"ok": entry["verified"]}
+                status = agree(r["ok"], dev, world)
+            except Exception as ex:  # noqa: BLE001 — recorded, then this rank stops issuing collectives
+                _store(rec, kind, m, {"error": f"rank {rank}: {_err(ex)}"})
+                print(f"bench.py rank {rank}: {kind}/{m} failed: {_err(ex)}", file=sys.stderr, flush=True)
+                mark_rest(f"after {kind}/{m} failed", i + 1)
+                clean = False
+                break
+            if kind == "weak" or kind == "strong":
+                entry["verified"] = entry["verified"] and min(status) == 1
+                if min(status) == 0:
+                    entry["failed_ranks"] = [r_ for r_, s_ in enumerate(status) if s_ == 0]
+            _store(rec, kind, m, entry)
+        else:
+            done["n"] = len(todo)
+    if compare:
+        rec["comparisons_complete"] = clean
+    emitter.emit(rec)
+    if has_pg and clean:
+        dist.destroy_process_group()
+    if not clean:  # the group may be out of step: leave without another collective
+        os._exit(0 if ok else 1)
+    return 0 if ok else 1
+
+
+def _store(rec: dict, kind: str, m, entry: dict) -> None:
+    if kind == "weak":
+        rec.setdefault("value_by_comm", {})[m] = entry
+        if m == "none" and "GBps" in entry:
+            rec["value_no_comm"] = entry["GBps"]
+    elif kind == "strong":
+        rec["strong"] = entry
+        if "GBps" in entry:
+            rec["value_strong"] = entry["GBps"]
+    else:
+        rec["e2e"] = entry
+
+
+def headline_record(a, k, n, C, world, rank, dev, has_pg, work, head, head_strong, head_mode, ok) -> dict:
     ms = head["elapsed"] / head["steps"] * 1e3
-    value = gbps(head)
+    value = gbps_of(head)
     metric = METRIC
     if a.preset != "k10n14" or a.bytes != PRESETS["k10n14"]["bytes"] or head_strong:
         per = "in total, one stripe sharded over the GPUs" if head_strong else "per GPU"
@@ -721,7 +924,6 @@ def main(argv=None) -> int:
                  "owners": "pattern broadcast + parity all_to_all to chunk owners over RCCL/xGMI",
                  "root": "pattern broadcast + parity gather to rank 0 over RCCL/xGMI (grouped send/recv)",
                  "none": "no per-step traffic (each rank draws the pattern itself)"}
-    head_mode = a.comm if has_pg else "none"
     if head_strong:
         parallelism = f"dp{world} strong (one {k}-row stripe column-sharded, gather {a.gather})"
         comm_what = {"step": "pattern broadcast + parity and decoded natives gathered into rank 0 every step",
@@ -731,6 +933,7 @@ def main(argv=None) -> int:
     else:
         parallelism = f"dp{world} weak (stripe per rank, E + pattern pool RCCL-broadcast)"
         comm_what = comm_desc[head_mode]
+    step_ms = [x / head["steps"] * 1e3 for x in head["per_rank"]]
     rec = {
         "metric": metric,
         "value": round(value, 3),
@@ -760,6 +963,10 @@ def main(argv=None) -> int:
                                  "check, not a scaling number") if (a.rehearsal and has_pg) else None,
                    "bcast_ahead": a.bcast_ahead if (has_pg and dev.type == "cuda") else None},
         "verified": ok,
+        # per-rank step time of the headline loop (each rank's own clock between the barriers): a
+        # straggler shows as the max; the headline uses the max
+        "step_ms_by_rank": {"min": round(min(step_ms), 4), "max": round(max(step_ms), 4),
+                            "per_rank": [round(x, 4) for x in step_ms]},
         "vs_baseline_what": "device-resident value / reference nearest published PCIe-inclusive point; "
                             "the like-for-like ratio is e2e.vs_baseline_e2e",
         "baseline": {"gbps": round(BASELINE_GBPS, 4), "source": "k=8,n=11 1.1 GB Tesla C2050 (nearest published)"},
@@ -767,36 +974,13 @@ def main(argv=None) -> int:
     if has_pg and not head_strong:
         rec["headline_why"] = ("weak scaling with the parity left in each GPU's HBM, as the N = 1 number does; the "
                                "per-step parity movement over xGMI (value_by_comm.owners / .root) and the "
-                               "reference's one-stripe strong scaling (value_strong) are timed alongside")
-    if results and (has_pg or len(results) > 1):
-        # busiest xGMI link: bytes it carries per step, and the rate the measured step implies for
-        # it (a lower bound on what the link sustained; when the step is link-bound, its rate)
-        rec["value_by_comm"] = {m: {"GBps": round(gbps(r), 3), "ms_per_step": round(r["elapsed"] / r["steps"] * 1e3, 4),
-                                    "steps": r["steps"], "bytes_sent_per_rank_step": r["sent"],
-                                    "bytes_recv_rank0_step": r["recv"] if rank == 0 else None,
-                                    "busiest_link_bytes_per_step": r["link"],
-                                    "busiest_link_GBps_implied": round(r["link"] / (r["elapsed"] / r["steps"]) / 1e9, 2),
-                                    "verified": r["ok"]}
-                                for m, r in results.items()}
-        if "none" in results:
-            rec["value_no_comm"] = round(gbps(results["none"]), 3)
-    if strong is not None:
-        rec["value_strong"] = round(gbps(strong), 3)
-        rec["strong"] = {"GBps": round(gbps(strong), 3), "ms_per_step": round(strong["elapsed"] / strong["steps"] * 1e3, 4),
-                         "steps": strong["steps"], "stripe_bytes": a.bytes, "shard_cols": strong["widths"],
-                         "gather": strong["gather"], "busiest_link_bytes_per_step": strong["link"],
-                         "bytes_recv_rank0": strong["recv"] if rank == 0 else None, "verified": strong["ok"],
-                         **{kk: strong[kk] for kk in ("gather_ms", "gather_GBps") if kk in strong}}
-    if dev.type == "cuda" and not a.no_e2e and not head_strong:
-        # the reference's worst case (src/unit-test.sh: keep the last k chunks): the first
-        # `erasures` natives are lost, so every one of them is rebuilt and copied back to the host
-        e = min(a.erasures, k, n - k)
-        rec["e2e"] = e2e(a, k, n, C, rs, list(range(e, k)) + list(range(k, k + e)), work, dev, world)
-    if rank == 0:
-        print(json.dumps(rec), flush=True)
-    if has_pg:
-        dist.destroy_process_group()
-    return 0 if ok else 1
+                               "reference's one-stripe strong scaling (value_strong) are timed after it, each "
+                               "on its own (a failing comparison mode is recorded, never the headline lost)")
+        rec["value_by_comm"] = {head_mode: mode_entry(head, rank)}
+    if head_strong:
+        rec["value_strong"] = round(value, 3)
+        rec["strong"] = strong_entry(a, head, rank)
+    return rec
 
 
 if __name__ == "__main__":

@@ -31,10 +31,79 @@ send/recv to self, so every RCCL code path executes on a single MI355X.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.distributed as dist
 
 MODES = ("owners", "root", "none")
+
+
+class InjectedFault(RuntimeError):
+    """Raised by :func:`maybe_fault` (fault injection for the N > 1 bench's failure isolation)."""
+
+
+def maybe_fault(mode: str) -> None:
+    """Fault injection: ``GFRS_FAULT_MODE=<mode>`` makes the exchange of that mode
+    (``owners``, ``root``, ``strong``) fail when it starts — on every rank, or only on rank
+    ``GFRS_FAULT_RANK``. ``GFRS_FAULT_KIND=hang`` sleeps instead of raising (a peer that never joins
+    its collectives), which is what a stuck xGMI transfer looks like to the other ranks."""
+    if os.environ.get("GFRS_FAULT_MODE") != mode:
+        return
+    want = os.environ.get("GFRS_FAULT_RANK")
+    if want not in (None, "") and dist.is_initialized() and int(want) != dist.get_rank():
+        return
+    if os.environ.get("GFRS_FAULT_KIND", "raise") == "hang":
+        import time
+
+        time.sleep(float(os.environ.get("GFRS_FAULT_HANG_S", "3600")))
+    raise InjectedFault(f"injected fault in {mode} exchange (GFRS_FAULT_MODE)")
+
+
+def _gather_small(t: torch.Tensor, dst: int) -> list[torch.Tensor] | None:
+    """dist.gather of a small tensor (checksums); gloo gets host copies (it gathers host memory)."""
+    if dist.get_backend() == "gloo" and t.is_cuda:
+        t = t.cpu()
+    out = [torch.empty_like(t) for _ in range(dist.get_world_size())] if dist.get_rank() == dst else None
+    dist.gather(t, out, dst=dst)
+    return out
+
+
+class _StagedRecv:
+    """A gloo receive into host memory whose bytes are copied to the device tensor on wait()."""
+
+    def __init__(self, work, host: torch.Tensor, dst: torch.Tensor):
+        self.work, self.host, self.dst = work, host, dst
+
+    def wait(self) -> None:
+        self.work.wait()
+        self.dst.copy_(self.host)
+
+
+def batch_p2p(ops: list[tuple[str, torch.Tensor, int]]) -> list | None:
+    """Grouped point-to-point: ``ops`` is a list of ``("send" | "recv", tensor, peer)``; returns the
+    works to wait on (None when empty).
+
+    RCCL (and gloo on host tensors) move the tensors in place. gloo cannot send device memory, so a
+    gloo group over GPU tensors — the N-ranks-on-one-GPU rehearsal (``bench.py --pg-backend gloo``) —
+    stages through host copies: a send copies its piece to the host first, a receive lands in host
+    memory and is copied to its device destination by ``wait()``. That path exists only to run the
+    rank-0 receive lists and piece bookkeeping of the N > 1 modes on one GPU; it is not timed as a
+    link rate."""
+    if not ops:
+        return None
+    staged = dist.get_backend() == "gloo" and any(t.is_cuda for _, t, _ in ops)
+    if not staged:
+        return dist.batch_isend_irecv([dist.P2POp(dist.isend if kind == "send" else dist.irecv, t, peer)
+                                       for kind, t, peer in ops])
+    works = []
+    for kind, t, peer in ops:
+        if kind == "send":
+            works.append(dist.isend(t.to("cpu"), peer))
+        else:
+            host = torch.empty(t.shape, dtype=t.dtype)
+            works.append(_StagedRecv(dist.irecv(host, peer), host, t))
+    return works
 
 
 def even_splits(nbytes: int, world: int) -> list[int]:
@@ -147,6 +216,7 @@ class ParityExchange:
         far on the current stream)."""
         if self.mode == "none":
             return
+        maybe_fault(self.mode)
         self.wait(slot)
         src = self.sources[slot]
         if self.mode == "owners":
@@ -157,10 +227,10 @@ class ParityExchange:
         if self.rank == self.root:
             for r in range(self.world):
                 if r != self.root or self.self_loop:
-                    ops.append(dist.P2POp(dist.irecv, self.recv_lists[slot][r], r))
+                    ops.append(("recv", self.recv_lists[slot][r], r))
         if self.rank != self.root or self.self_loop:
-            ops.append(dist.P2POp(dist.isend, src, self.root))
-        self.pending[slot] = dist.batch_isend_irecv(ops) if ops else None
+            ops.append(("send", src, self.root))
+        self.pending[slot] = batch_p2p(ops)
 
     def wait(self, slot: int) -> None:
         """Order later work on the current stream after the exchange reading ``sources[slot]``."""
@@ -196,12 +266,10 @@ class ParityExchange:
             got = torch.stack([_checksum(recv[r * mine:(r + 1) * mine]) for r in range(self.world)])
             ok = torch.equal(got, expect)
         else:
-            mine = _checksum(src)
-            allsum = [torch.empty_like(mine) for _ in range(self.world)] if self.rank == self.root else None
-            dist.gather(mine, allsum, dst=self.root)
+            allsum = _gather_small(_checksum(src), self.root)
             ok = True
             if self.rank == self.root:
-                ok = all(torch.equal(_checksum(self.recv_lists[slot][r]), allsum[r])
+                ok = all(torch.equal(_checksum(self.recv_lists[slot][r]).cpu(), allsum[r].cpu())
                          for r in range(self.world) if r != self.root or self.self_loop)
         flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
         dist.all_reduce(flag, op=dist.ReduceOp.MIN)
@@ -242,8 +310,12 @@ class StripeGather:
         self.pending: list[list | None] = [None] * len(pieces)
 
     def _in_place(self, slot: int) -> bool:
-        w = self.widths[self.dst]
-        return all(p.data_ptr() == f.data_ptr() for p, f in zip(self.pieces[slot], self.fulls[slot])) or w == 0
+        """dst computed its own piece inside its full rows: every piece row starts at column
+        offs[dst] of the matching full row."""
+        if self.widths[self.dst] == 0:
+            return True
+        a = self.offs[self.dst]
+        return all(p.data_ptr() == f[a:].data_ptr() for p, f in zip(self.pieces[slot], self.fulls[slot]))
 
     @property
     def bytes_per_link(self) -> int:
@@ -258,6 +330,7 @@ class StripeGather:
         return rows * (self.offs[-1] - self.widths[self.dst]) if self.rank == self.dst else 0
 
     def start(self, slot: int) -> None:
+        maybe_fault("strong")
         self.wait(slot)
         w_mine = self.widths[self.rank]
         ops = []
@@ -268,19 +341,18 @@ class StripeGather:
                 if r == self.dst or not self.widths[r]:
                     continue
                 a, b = self.offs[r], self.offs[r + 1]
-                ops += [dist.P2POp(dist.irecv, row[a:b], r) for row in full]
+                ops += [("recv", row[a:b], r) for row in full]
             if own_moves:
                 a, b = self.offs[self.dst], self.offs[self.dst + 1]
                 if self.self_loop:
                     for row, src in zip(full, mine):
-                        ops += [dist.P2POp(dist.irecv, row[a:b], self.dst), dist.P2POp(dist.isend, src[:w_mine],
-                                                                                        self.dst)]
+                        ops += [("recv", row[a:b], self.dst), ("send", src[:w_mine], self.dst)]
                 else:
                     for row, src in zip(full, mine):
                         row[a:b].copy_(src[:w_mine], non_blocking=True)
         elif w_mine:
-            ops += [dist.P2POp(dist.isend, row[:w_mine], self.dst) for row in self.pieces[slot]]
-        self.pending[slot] = dist.batch_isend_irecv(ops) if ops else None
+            ops += [("send", row[:w_mine], self.dst) for row in self.pieces[slot]]
+        self.pending[slot] = batch_p2p(ops)
 
     def wait(self, slot: int) -> None:
         works = self.pending[slot]
@@ -302,14 +374,13 @@ class StripeGather:
         if self.world == 1 and not self.has_pg:
             allsum = [mine]
         else:
-            allsum = [torch.empty_like(mine) for _ in range(self.world)] if self.rank == self.dst else None
-            dist.gather(mine, allsum, dst=self.dst)
+            allsum = _gather_small(mine, self.dst)
         ok = True
         if self.rank == self.dst:
             for r in range(self.world):
                 a, b = self.offs[r], self.offs[r + 1]
                 got = torch.stack([_checksum(row[a:b]) for row in self.fulls[slot]])
-                ok = ok and torch.equal(got, allsum[r])
+                ok = ok and torch.equal(got.cpu(), allsum[r].cpu())
         if not self.has_pg:
             return bool(ok)
         flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)

@@ -49,6 +49,48 @@ def test_launcher_runs_world_ranks_and_reports_every_comm_mode(gpus):
     assert st["verified"] is True and rec["value_strong"] == st["GBps"] and len(st["shard_cols"]) == gpus
     assert sum(st["shard_cols"]) == (300_001 + 9) // 10 and st["gather"] == "step"
     assert st["bytes_recv_rank0"] == 14 * (sum(st["shard_cols"]) - st["shard_cols"][0])
+    # per-rank step times of the headline loop (a straggler shows as the max)
+    sm = rec["step_ms_by_rank"]
+    assert len(sm["per_rank"]) == gpus and sm["max"] == max(sm["per_rank"]) and sm["max"] == rec["ms_per_step"]
+    assert all(len(v["step_ms_by_rank"]) == gpus for v in by.values()) and rec["comparisons_complete"] is True
+
+
+def _fault_run(mode, env, gpus=3):
+    e = {"GFRS_FAULT_MODE": mode, "GFRS_COMPARE_BUDGET_S": "25", **env}
+    r = _run(["--device", "cpu", "--gpus", str(gpus), "--steps", "3", "--warmup", "1", "--bytes", str(200_003)],
+             env=e, timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    rec = _record(r.stdout)
+    assert rec["verified"] is True and rec["value"] > 0 and rec["comparisons_complete"] is False
+    assert rec["value_by_comm"]["bcast"]["verified"] is True  # the headline survives
+    return rec
+
+
+def test_fault_in_root_mode_on_every_rank_keeps_the_headline():
+    """An exception in the root gather (the last comparison) on every rank: the headline and every
+    earlier mode are in the one record, root carries the error."""
+    rec = _fault_run("root", {})
+    by = rec["value_by_comm"]
+    assert "InjectedFault" in by["root"]["error"]
+    assert by["none"]["verified"] and by["owners"]["verified"] and rec["strong"]["verified"]
+
+
+def test_fault_on_one_rank_stops_later_modes():
+    """Rank 1 alone fails in the owners all_to_all: its peers see the collective break, owners is an
+    error, the modes after it are skipped (no collective is issued on a group that may be out of
+    step) and rank 0 still prints the verified headline."""
+    rec = _fault_run("owners", {"GFRS_FAULT_RANK": "1"})
+    by = rec["value_by_comm"]
+    assert "error" in by["owners"] and by["none"]["verified"] is True
+    assert "skipped" in rec["strong"] and "skipped" in by["root"]
+
+
+def test_hung_peer_is_cut_off_by_the_watchdog():
+    """Rank 2 never joins the strong-scaling gather (it sleeps): no collective raises, the comparison
+    watchdog expires, rank 0 prints the headline with strong marked as timed out, all ranks exit 0."""
+    rec = _fault_run("strong", {"GFRS_FAULT_RANK": "2", "GFRS_FAULT_KIND": "hang", "GFRS_COMPARE_BUDGET_S": "15"})
+    assert "timed out" in rec["strong"]["error"] and "skipped" in rec["value_by_comm"]["root"]
+    assert rec["value_by_comm"]["owners"]["verified"] is True
 
 
 @pytest.mark.parametrize("gather", ["step", "end"])
@@ -141,14 +183,43 @@ def test_gpu_bench_strong_gather_end_one_rank_group():
 def test_gpu_bench_three_ranks_rehearsed_on_one_gpu():
     """Three ranks share the one MI355X over gloo (RCCL refuses two ranks on one GPU): ranks 1 and 2
     take every step's pattern only from rank 0's look-ahead broadcast into their ring slots, and each
-    decoder's last plan must match the pattern of the step it was built for; owners all_to_all too."""
+    decoder's last plan must match the pattern of the step it was built for. Every N > 1 mode runs:
+    owners all_to_all, root's receive lists and strong scaling's per-row gather into rank 0's full
+    rows (point-to-point pieces staged through host memory under gloo)."""
     r = _run(["--gpus", "3", "--pg-backend", "gloo", "--steps", "6", "--warmup", "2", "--bytes", str(32 << 20),
               "--no-e2e"], timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     rec = _record(r.stdout)
     assert rec["verified"] is True and rec["n_gpus"] == 3 and rec["config"]["pg_backend"] == "gloo"
-    assert rec["config"]["rehearsal"] and set(rec["value_by_comm"]) == {"bcast", "owners", "none"}
-    assert all(v["verified"] for v in rec["value_by_comm"].values()) and "strong" not in rec
+    assert rec["config"]["rehearsal"] and set(rec["value_by_comm"]) == {"bcast", "owners", "root", "none"}
+    assert all(v["verified"] for v in rec["value_by_comm"].values()) and rec["comparisons_complete"] is True
+    st = rec["strong"]
+    assert st["verified"] is True and len(st["shard_cols"]) == 3 and st["bytes_recv_rank0"] > 0
+
+
+@pytest.mark.gpu
+def test_gpu_bench_three_ranks_strong_headline_rehearsed():
+    """--scaling strong as the headline with three ranks on the one GPU: one stripe column-sharded,
+    every step's parity and decoded natives gathered into rank 0's full rows."""
+    r = _run(["--gpus", "3", "--pg-backend", "gloo", "--scaling", "strong", "--steps", "4", "--warmup", "1",
+              "--bytes", str(48 << 20)], timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = _record(r.stdout)
+    assert rec["verified"] is True and rec["scaling"] == "strong" and rec["strong"]["verified"] is True
+    assert len(rec["step_ms_by_rank"]["per_rank"]) == 3
+
+
+@pytest.mark.gpu
+def test_gpu_bench_fault_in_root_mode_keeps_headline():
+    """--force-pg on the MI355X with a fault injected into the root gather: one JSON line, the RCCL
+    headline verified, root recorded as an error, the modes before it verified."""
+    r = _run(["--force-pg", "--steps", "4", "--warmup", "1", "--bytes", str(64 << 20), "--no-e2e"],
+             env={"GFRS_FAULT_MODE": "root"}, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = _record(r.stdout)
+    assert rec["verified"] is True and rec["comparisons_complete"] is False
+    by = rec["value_by_comm"]
+    assert "InjectedFault" in by["root"]["error"] and by["owners"]["verified"] and rec["strong"]["verified"]
 
 
 @pytest.mark.gpu
