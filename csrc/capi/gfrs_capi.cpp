@@ -92,6 +92,13 @@ class DeviceGuard {  // restores the calling thread's current device
     hip_check(hipGetDevice(&prev_), "hipGetDevice");
     if (dev != prev_) hip_check(hipSetDevice(dev), "hipSetDevice");
   }
+  // Teardown form (the *_destroy entry points return void and must never throw into C): errors
+  // from hipGetDevice/hipSetDevice are ignored, the frees still run.
+  struct NoThrow {};
+  DeviceGuard(int dev, NoThrow) {
+    if (hipGetDevice(&prev_) != hipSuccess) prev_ = dev;
+    if (dev != prev_) (void)hipSetDevice(dev);
+  }
   ~DeviceGuard() { (void)hipSetDevice(prev_); }
 
  private:
@@ -304,7 +311,7 @@ int gfrs_plan_engine(const gfrs_plan* p) { return p ? p->engine : GFRS_EINVAL; }
 
 void gfrs_plan_destroy(gfrs_plan* p) {
   if (!p) return;
-  DeviceGuard g(p->device);
+  DeviceGuard g(p->device, DeviceGuard::NoThrow{});
   delete p;
 }
 
@@ -391,7 +398,7 @@ int gfrs_decoder_engine(const gfrs_decoder* d) { return d ? d->plan.engine : GFR
 
 void gfrs_decoder_destroy(gfrs_decoder* d) {
   if (!d) return;
-  DeviceGuard g(d->plan.device);
+  DeviceGuard g(d->plan.device, DeviceGuard::NoThrow{});
   delete d;
 }
 

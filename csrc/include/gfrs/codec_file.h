@@ -15,8 +15,10 @@
 
 namespace gfrs {
 
+// coeff: m x k coefficients of field width `field_w` — 8 (GF(2^8), one byte each) or 16 (GF(2^16),
+// little-endian byte pairs, gfrs/host_desc.h pack16; ncols is then an even byte count).
 using GemmFn = std::function<void(const std::vector<const uint8_t*>& in, const std::vector<uint8_t*>& out,
-                                  const Mat& coeff, int64_t ncols)>;
+                                  const Mat& coeff, int64_t ncols, int field_w)>;
 
 struct HostAlloc {
   std::function<uint8_t*(size_t)> alloc;  // e.g. pinned hipHostMalloc for the GPU path
@@ -33,12 +35,13 @@ struct FileReport {
 };
 
 // Writes _0_<file> .. _{n-1}_<file> and <file>.METADATA (full matrix format unless `cpu_meta`).
+// field_w = 16: GF(2^16) symbols (n <= 65535, even chunk size, versioned METADATA — gfrs/format.h).
 FileReport encode_file(const std::string& file, int k, int p, MatrixKind kind, const GemmFn& gemm,
-                       const HostAlloc& alloc, bool cpu_meta = false);
+                       const HostAlloc& alloc, bool cpu_meta = false, int field_w = 8);
 
 // Reads <file>.METADATA and the k chunks named in `conf`, writes `out` (or overwrites `file` when
 // `out` is empty, like the reference, src/decode.cu:410-425). Throws std::runtime_error for an
-// unrecoverable (singular) erasure pattern.
+// unrecoverable (singular) erasure pattern. The field comes from the METADATA.
 FileReport decode_file(const std::string& file, const std::string& conf, const std::string& out,
                        const GemmFn& gemm, const HostAlloc& alloc);
 

@@ -47,6 +47,15 @@ constexpr DescLayout desc_layout(int k, int m_pad, int batch = 1) {
   return l;
 }
 
+// GF(2^16) descriptor (csrc/kernels/gf_gemm16.hip): the same header and pointer arrays (rows are
+// byte rows holding little-endian 16-bit symbols), and FOUR records per coefficient, tab[j][i][q]
+// with q = 2 * src_byte + dst_byte (gfrs/gf65536.h perm_quad).
+constexpr DescLayout desc_layout16(int k, int m_pad) {
+  DescLayout l = desc_layout(k, m_pad, 1);
+  l.bytes = l.tab_off + 4 * sizeof(PermTable) * size_t(k) * size_t(m_pad);
+  return l;
+}
+
 // Output tile (outputs computed per thread). Tiles are powers of two; m is padded to a multiple.
 constexpr int kMaxTile = 16;
 constexpr int tile_for(int m) {

@@ -8,20 +8,31 @@
 //     reference Vandermonde for the short form.
 //   * decode config: whitespace-separated k chunk names; row index = atoi(basename + 1)
 //     (src/decode.cu:302-318). Conf order defines the row order of the decode system.
+//   * GF(2^16) stripes (an extension: the reference's w = 16 code, src/galoisfield.cu:22-32, was
+//     never built, so it defined no file layout) carry an explicit format version as an extra first
+//     line, "GFRS-METADATA 2 16" (format version, field width), then the same lines with 16-bit
+//     matrix values. Chunks hold little-endian 16-bit symbols; C is rounded up to an even byte
+//     count. GF(2^8) METADATA stays exactly the reference's (no version line), so every file the
+//     reference can read is still written the reference's way.
 #pragma once
 
 #include <cstdint>
 #include <string>
 #include <vector>
 
+#include "gfrs/gf65536.h"
 #include "gfrs/matrix.h"
 
 namespace gfrs {
 
+constexpr int kMetadataVersion = 2;  // the versioned (GF(2^16)) form; unversioned = the reference's
+
 struct Metadata {
   int64_t total_size = 0;
   int p = 0, k = 0;
-  Mat g;                    // (k+p) x k generator
+  int w = 8;                // field width: 8 (reference format) or 16 (versioned format)
+  Mat g;                    // (k+p) x k generator (w = 8)
+  gf16w::Mat g16;           // (k+p) x k generator (w = 16)
   bool has_matrix = false;  // false: 2-line CPU format, g regenerated (reference Vandermonde)
   std::vector<uint32_t> crc;  // optional per-chunk CRC-32 (n entries) — extension, see below
 };
@@ -37,12 +48,19 @@ int chunk_index(const std::string& name);  // atoi(basename + 1); -1 if malforme
 
 void write_metadata(const std::string& path, int64_t total_size, int p, int k, const Mat& e, bool with_matrix = true,
                     const std::vector<uint32_t>& crc = {});
+// GF(2^16): the versioned form (always with the matrix).
+void write_metadata16(const std::string& path, int64_t total_size, int p, int k, const gf16w::Mat& e,
+                      const std::vector<uint32_t>& crc = {});
 Metadata read_metadata(const std::string& path);
 std::vector<std::string> read_conf(const std::string& path);
 void write_conf(const std::string& path, const std::vector<std::string>& names);
 
-// Chunk geometry: C = ceil(total / k) (src/encode.cu:317).
+// Chunk geometry: C = ceil(total / k) (src/encode.cu:317); GF(2^16) rounds up to whole symbols.
 inline int64_t chunk_size(int64_t total, int k) { return (total + k - 1) / k; }
+inline int64_t chunk_size(int64_t total, int k, int field_w) {
+  const int64_t c = chunk_size(total, k);
+  return field_w == 16 ? (c + 1) / 2 * 2 : c;
+}
 
 int64_t file_size(const std::string& path);
 // Reads up to `len` bytes at `offset` into dst; zero-fills what the file does not cover.

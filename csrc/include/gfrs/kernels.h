@@ -18,6 +18,12 @@ namespace gfrs {
 hipError_t launch_gf_gemm(const void* desc, int k, int m_pad, int64_t col0, int64_t ncols,
                           bool force_bytewise, int max_blocks, hipStream_t stream, bool copies = true);
 
+// GF(2^16) form (csrc/kernels/gf_gemm16.hip): desc built with desc_layout16 (build_desc field_w =
+// 16); rows hold little-endian 16-bit symbols, col0 and ncols are even byte counts. `symwise`
+// routes every column through the one-symbol-per-lane kernel (rows not 16-byte aligned).
+hipError_t launch_gf_gemm16(const void* desc, int k, int m_pad, int64_t col0, int64_t ncols, bool symwise,
+                            int max_blocks, hipStream_t stream);
+
 // Batched form: `batch` stripes of identical shape share the coefficient tables (small-object
 // serving: one launch for many objects). desc built with desc_layout(k, m_pad, batch).
 hipError_t launch_gf_gemm_batched(const void* desc, int k, int m_pad, int batch, int64_t col0, int64_t ncols,

@@ -101,12 +101,78 @@ void write_metadata(const std::string& path, int64_t total_size, int p, int k, c
   std::fclose(fp);
 }
 
+void write_metadata16(const std::string& path, int64_t total_size, int p, int k, const gf16w::Mat& e,
+                      const std::vector<uint32_t>& crc) {
+  FILE* fp = std::fopen(path.c_str(), "wb");
+  if (!fp) throw std::runtime_error("cannot open metadata file " + path);
+  std::fprintf(fp, "GFRS-METADATA %d 16\n%lld\n%d %d\n", kMetadataVersion, static_cast<long long>(total_size), p, k);
+  for (int i = 0; i < k; ++i) {
+    for (int j = 0; j < k; ++j) std::fprintf(fp, "%d ", i == j ? 1 : 0);
+    std::fprintf(fp, "\n");
+  }
+  for (int i = 0; i < p; ++i) {
+    for (int j = 0; j < k; ++j) std::fprintf(fp, "%d ", int(e[size_t(i) * k + j]));
+    std::fprintf(fp, "\n");
+  }
+  if (!crc.empty()) {
+    std::fprintf(fp, "crc32");
+    for (uint32_t c : crc) std::fprintf(fp, " %08x", c);
+    std::fprintf(fp, "\n");
+  }
+  std::fclose(fp);
+}
+
+namespace {
+
+// The optional crc32 line after the matrix rows.
+void read_crc(std::istream& in, Metadata& md) {
+  std::string tag;
+  if (in >> tag && tag == "crc32") {
+    std::string h;
+    for (int i = 0; i < md.k + md.p && (in >> h); ++i) md.crc.push_back(uint32_t(std::stoul(h, nullptr, 16)));
+    if (int(md.crc.size()) != md.k + md.p) md.crc.clear();
+  }
+}
+
+Metadata read_metadata16(std::istream& in, const std::string& path) {
+  Metadata md;
+  md.w = 16;
+  long long total = 0;
+  if (!(in >> total >> md.p >> md.k)) throw std::runtime_error("malformed metadata " + path);
+  if (md.k <= 0 || md.p < 0 || md.k + md.p > int(gf16w::kMax) || total < 0)
+    throw std::runtime_error("metadata out of range in " + path);
+  md.total_size = total;
+  const size_t n = size_t(md.k + md.p) * md.k;
+  md.g16.resize(n);
+  long v;
+  for (size_t got = 0; got < n; ++got) {
+    if (!(in >> v)) throw std::runtime_error("truncated metadata matrix in " + path);
+    if (v < 0 || v > 65535) throw std::runtime_error("metadata matrix entry out of range in " + path);
+    md.g16[got] = uint16_t(v);
+  }
+  md.has_matrix = true;
+  read_crc(in, md);
+  return md;
+}
+
+}  // namespace
+
 Metadata read_metadata(const std::string& path) {
   std::ifstream in(path);
   if (!in) throw std::runtime_error("cannot open metadata file " + path);
+  std::string first;
+  if (!(in >> first)) throw std::runtime_error("malformed metadata " + path);
+  if (first == "GFRS-METADATA") {  // versioned form (GF(2^16))
+    int version = 0, w = 0;
+    if (!(in >> version >> w) || version != kMetadataVersion || w != 16)
+      throw std::runtime_error("unsupported metadata version/field in " + path + " (this build reads version " +
+                               std::to_string(kMetadataVersion) + ", field width 16)");
+    return read_metadata16(in, path);
+  }
   Metadata md;
-  long long total = 0;
-  if (!(in >> total >> md.p >> md.k)) throw std::runtime_error("malformed metadata " + path);
+  char* end = nullptr;
+  const long long total = std::strtoll(first.c_str(), &end, 10);
+  if (end == first.c_str() || *end || !(in >> md.p >> md.k)) throw std::runtime_error("malformed metadata " + path);
   if (md.k <= 0 || md.p < 0 || md.k + md.p > 256 || total < 0)
     throw std::runtime_error("metadata out of range in " + path);
   md.total_size = total;
@@ -120,12 +186,7 @@ Metadata read_metadata(const std::string& path) {
   }
   if (got == n) {
     md.has_matrix = true;
-    std::string tag;
-    if (in >> tag && tag == "crc32") {
-      std::string h;
-      for (int i = 0; i < md.k + md.p && (in >> h); ++i) md.crc.push_back(uint32_t(std::stoul(h, nullptr, 16)));
-      if (int(md.crc.size()) != md.k + md.p) md.crc.clear();
-    }
+    read_crc(in, md);
   } else if (got == 0) {
     md.g = generator(vandermonde_ref(md.k, md.p), md.k, md.p);  // CPU-format metadata
     md.has_matrix = false;

@@ -1,0 +1,221 @@
+// GF(2^16) GEMM on gfx950 VALU: out[i][s] = XOR_j c[i][j] * in[j][s] over 16-bit symbols.
+//
+// Completes the reference's field family on the device: its generic field code names w = 4, 8 and
+// 16 (/root/reference/src/galoisfield.cu:22-32, poly 0210013 for w = 16) but only GF(2^8) was ever
+// built. A 16-bit field also lifts the n <= 256 chunk limit of GF(2^8) (n <= 65535 here).
+//
+// How it maps to the v_perm engine (gfrs/gf65536.h): multiplying by c is GF(2)-linear on 16 bits,
+// so with a symbol's low byte l and high byte h
+//     c * s = [L_ll(l) ^ L_hl(h)] | [L_lh(l) ^ L_hh(h)] << 8,
+// four ordinary byte maps. A lane loads 16 bytes (8 little-endian symbols) of a row and
+// de-interleaves them with two v_perm_b32 per 8 bytes into a low-byte plane LO and a high-byte
+// plane HI (4 symbols per dword). Accumulators stay de-interleaved for the whole k loop:
+//     acc_lo ^= L_ll(LO) ^ L_hl(HI)      acc_hi ^= L_lh(LO) ^ L_hh(HI)
+// each one mac_pair (6 v_perm + 3 v_bitop3), with the selectors of LO and HI computed once per row
+// and shared by every output of the tile. The planes are re-interleaved (2 v_perm per 8 bytes) only
+// at the final store. Per byte and coefficient that is twice the GF(2^8) kernel's VALU work — the
+// field's 16x16 bit map has four times the terms of the 8x8 one, spread over twice the bytes.
+//
+// Same streaming structure as gf_gemm.hip: 16-byte non-temporal loads, rows kept in flight by a
+// register ring, XCD-aware block mapping, fused survivor copies on output tile 0 (decode), ragged
+// tail symbols on extra lanes of the same launch, and a symbol kernel for rows that are not 16-byte
+// aligned. Rows must be 2-byte aligned and column ranges whole symbols (even byte offsets/counts).
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "gfrs/desc.h"
+#include "gfrs/kernels.h"
+#include "gfrs/perm_device.h"
+
+namespace gfrs {
+namespace {
+
+using namespace permdev;
+
+constexpr int kQuad = 4 * kPermStride;  // words per coefficient: {L_ll, L_lh, L_hl, L_hh}
+
+// byte-plane shuffles (v_perm pool: bytes 0..3 = second operand, 4..7 = first operand)
+constexpr uint32_t kSelLo = 0x06040200u;  // [l0 l1 l2 l3] from [l0 h0 l1 h1][l2 h2 l3 h3]
+constexpr uint32_t kSelHi = 0x07050301u;  // [h0 h1 h2 h3]
+constexpr uint32_t kSelW0 = 0x05010400u;  // [l0 h0 l1 h1] from lo=[l0..l3], hi=[h0..h3]
+constexpr uint32_t kSelW1 = 0x07030602u;  // [l2 h2 l3 h3]
+
+inline DescView view16(const void* desc, int k, int m_pad) {
+  const DescLayout l = desc_layout16(k, m_pad);
+  const char* b = static_cast<const char*>(desc);
+  return {(cptr<uint64_t>)(b + l.in_off), (cptr<uint64_t>)(b + l.copy_off), (cptr<uint64_t>)(b + l.out_off),
+          (cptr<uint32_t>)(b + l.tab_off)};
+}
+
+// One symbol column (2 bytes at `off`), one lane: k symbols loaded 8 at a time before use (see
+// gf_gemm.hip tail_byte: a load-use-store loop would serialise every load behind the copy store).
+template <int MT>
+__device__ void tail_sym(const DescView& d, int k, int m_pad, int i0, bool do_copy, int64_t off) {
+  constexpr int kB = 8;
+  uint32_t lo[MT], hi[MT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i) lo[i] = hi[i] = 0;
+  for (int j0 = 0; j0 < k; j0 += kB) {
+    uint16_t x[kB];
+#pragma unroll
+    for (int u = 0; u < kB; ++u)
+      x[u] = j0 + u < k ? *(gptr<const uint16_t>)(d.in[j0 + u] + uint64_t(off)) : uint16_t(0);
+#pragma unroll
+    for (int u = 0; u < kB; ++u) {
+      const int j = j0 + u;
+      if (j < k) {
+        if (do_copy && d.copy[j]) *(gptr<uint16_t>)(d.copy[j] + uint64_t(off)) = x[u];
+        const Sel sl = make_sel(x[u] & 0xFFu), sh = make_sel(uint32_t(x[u]) >> 8);
+        const auto t = d.tab + (size_t(j) * m_pad + i0) * kQuad;
+#pragma unroll
+        for (int i = 0; i < MT; ++i) {
+          const auto q = t + i * kQuad;
+          lo[i] = mac_pair(lo[i], q, sl, q + 2 * kPermStride, sh);
+          hi[i] = mac_pair(hi[i], q + kPermStride, sl, q + 3 * kPermStride, sh);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+    if (d.out[i0 + i])
+      *(gptr<uint16_t>)(d.out[i0 + i] + uint64_t(off)) = static_cast<uint16_t>((lo[i] & 0xFFu) | ((hi[i] & 0xFFu) << 8));
+}
+
+// Vector kernel: each lane owns one 16-byte group (8 symbols) of every row, PF rows in flight.
+// Lanes ngroups .. ngroups + tail_syms - 1 take one ragged tail symbol each.
+template <int MT, int PF>
+__global__ __launch_bounds__(kBlock) void gf_gemm16_vec_kernel(DescView d, int k, int m_pad, int ntiles, int64_t col0,
+                                                               int64_t ngroups, int64_t nblk, int64_t ncb,
+                                                               int tail_syms) {
+  const TileMap tm = map_block(ntiles);
+  if (tm.cb0 >= ncb) return;
+  const int i0 = tm.tile * MT;
+  const bool do_copy = (tm.tile == 0);
+
+  for (int64_t cb = tm.cb0; cb < nblk; cb += ncb) {
+    const int64_t g = cb * kBlock + threadIdx.x;
+    if (g >= ngroups) {
+      if (g - ngroups < tail_syms) tail_sym<MT>(d, k, m_pad, i0, do_copy, col0 + ngroups * 16 + 2 * (g - ngroups));
+      continue;
+    }
+    const int64_t off = col0 + g * 16;
+    uint32_t lo[MT][2], hi[MT][2];
+#pragma unroll
+    for (int i = 0; i < MT; ++i) lo[i][0] = lo[i][1] = hi[i][0] = hi[i][1] = 0;
+
+    u32x4 ring[PF];
+#pragma unroll
+    for (int u = 0; u < PF; ++u)
+      if (u < k) ring[u] = ld16<true>(row_vec(d.in[u], off));
+
+    for (int j0 = 0; j0 < k; j0 += PF) {
+#pragma unroll
+      for (int u = 0; u < PF; ++u) {
+        const int j = j0 + u;
+        if (j >= k) break;
+        const u32x4 x = ring[u];
+        if (j + PF < k) ring[u] = ld16<true>(row_vec(d.in[j + PF], off));
+        if (do_copy) {
+          const uint64_t cp = d.copy[j];
+          if (cp) st16<true>(row_vec_w(cp, off), x);
+        }
+        const uint32_t L0 = __builtin_amdgcn_perm(x[1], x[0], kSelLo);
+        const uint32_t H0 = __builtin_amdgcn_perm(x[1], x[0], kSelHi);
+        const uint32_t L1 = __builtin_amdgcn_perm(x[3], x[2], kSelLo);
+        const uint32_t H1 = __builtin_amdgcn_perm(x[3], x[2], kSelHi);
+        const Sel sl0 = make_sel(L0), sh0 = make_sel(H0), sl1 = make_sel(L1), sh1 = make_sel(H1);
+        const auto t = d.tab + (size_t(j) * m_pad + i0) * kQuad;
+#pragma unroll
+        for (int i = 0; i < MT; ++i) {
+          const auto q = t + i * kQuad;
+          lo[i][0] = mac_pair(lo[i][0], q, sl0, q + 2 * kPermStride, sh0);
+          hi[i][0] = mac_pair(hi[i][0], q + kPermStride, sl0, q + 3 * kPermStride, sh0);
+          lo[i][1] = mac_pair(lo[i][1], q, sl1, q + 2 * kPermStride, sh1);
+          hi[i][1] = mac_pair(hi[i][1], q + kPermStride, sl1, q + 3 * kPermStride, sh1);
+        }
+      }
+    }
+
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+      const uint64_t op = d.out[i0 + i];
+      if (!op) continue;
+      const u32x4 w{__builtin_amdgcn_perm(hi[i][0], lo[i][0], kSelW0), __builtin_amdgcn_perm(hi[i][0], lo[i][0], kSelW1),
+                    __builtin_amdgcn_perm(hi[i][1], lo[i][1], kSelW0), __builtin_amdgcn_perm(hi[i][1], lo[i][1], kSelW1)};
+      st16<true>(row_vec_w(op, off), w);
+    }
+  }
+}
+
+// Symbol kernel: one lane per symbol, any 2-byte alignment (rows or column start off 16 bytes).
+template <int MT>
+__global__ __launch_bounds__(kBlock) void gf_gemm16_sym_kernel(DescView d, int k, int m_pad, int ntiles, int64_t col0,
+                                                               int64_t nsyms, int64_t nblk, int64_t ncb) {
+  const TileMap tm = map_block(ntiles);
+  if (tm.cb0 >= ncb) return;
+  const int i0 = tm.tile * MT;
+  const bool do_copy = (tm.tile == 0);
+  for (int64_t cb = tm.cb0; cb < nblk; cb += ncb) {
+    const int64_t s = cb * kBlock + threadIdx.x;
+    if (s < nsyms) tail_sym<MT>(d, k, m_pad, i0, do_copy, col0 + 2 * s);
+  }
+}
+
+constexpr int64_t kMaxGridBlocks = int64_t(UINT32_MAX) / kBlock;
+
+struct Grid {
+  int64_t nblk, ncb;
+  unsigned blocks;
+};
+
+inline Grid make_grid(int64_t items, int ntiles, int max_blocks) {
+  Grid g{};
+  g.nblk = (items + kBlock - 1) / kBlock;
+  g.ncb = g.nblk;
+  if (max_blocks > 0 && g.ncb > max_blocks) g.ncb = max_blocks;
+  const int64_t cap = kMaxGridBlocks / ntiles / 8 * 8;
+  if (g.ncb > cap) g.ncb = cap;
+  g.blocks = static_cast<unsigned>((g.ncb + 7) / 8 * 8 * ntiles);
+  return g;
+}
+
+// Output tile of the w = 16 kernel: the GF(2^8) tile (gfrs/desc.h tile_for) capped at 8, since
+// each output holds four accumulator dwords per 16-byte group here (two planes x two dwords).
+template <typename F>
+hipError_t dispatch16(int m_pad, F&& f) {
+  switch (tile_for(m_pad)) {
+    case 1: return f(std::integral_constant<int, 1>{});
+    case 2: return f(std::integral_constant<int, 2>{});
+    case 4: return f(std::integral_constant<int, 4>{});
+    default: return f(std::integral_constant<int, 8>{});
+  }
+}
+
+}  // namespace
+
+hipError_t launch_gf_gemm16(const void* desc, int k, int m_pad, int64_t col0, int64_t ncols, bool symwise,
+                            int max_blocks, hipStream_t stream) {
+  if (k <= 0 || m_pad <= 0 || ncols <= 0) return ncols < 0 ? hipErrorInvalidValue : hipSuccess;
+  if ((col0 | ncols) & 1) return hipErrorInvalidValue;  // whole 16-bit symbols only
+  if (m_pad % tile_for(m_pad) != 0) return hipErrorInvalidValue;
+  const DescView d = view16(desc, k, m_pad);
+  return dispatch16(m_pad, [&](auto mt) -> hipError_t {
+    constexpr int MT = decltype(mt)::value;
+    const int ntiles = m_pad / MT;
+    if (symwise || (col0 & 15)) {
+      const Grid g = make_grid(ncols / 2, ntiles, max_blocks);
+      gf_gemm16_sym_kernel<MT><<<g.blocks, kBlock, 0, stream>>>(d, k, m_pad, ntiles, col0, ncols / 2, g.nblk, g.ncb);
+      return hipGetLastError();
+    }
+    const int64_t ngroups = ncols / 16;
+    const int tail_syms = int((ncols - ngroups * 16) / 2);
+    const Grid g = make_grid(ngroups + tail_syms, ntiles, max_blocks);
+    gf_gemm16_vec_kernel<MT, 2>
+        <<<g.blocks, kBlock, 0, stream>>>(d, k, m_pad, ntiles, col0, ngroups, g.nblk, g.ncb, tail_syms);
+    return hipGetLastError();
+  });
+}
+
+}  // namespace gfrs

@@ -133,7 +133,7 @@ Geometry geometry(int64_t ncols, const PipelineOptions& opt) {
 hipError_t setup_lanes(Workspace& ws, int lanes, int k, int m, int64_t slice, const Mat& coeff, bool split,
                        int field_w = 8) {
   if (int(ws.lane.size()) < lanes) ws.lane.resize(size_t(lanes));
-  const Mat zero = coeff.empty() ? Mat(size_t(m) * k, 0) : Mat{};
+  const Mat zero = coeff.empty() ? Mat(coeff_bytes(m, k, field_w), 0) : Mat{};
   const Mat& c = coeff.empty() ? zero : coeff;
   for (int l = 0; l < lanes; ++l) {
     Lane& L = ws.lane[size_t(l)];
@@ -217,8 +217,16 @@ hipError_t copy_run(Dst* dst, size_t slot_pitch, const Src* src, const Run& r, i
 }
 
 bool valid(int k, int m, size_t coeff_size, int64_t c0, int64_t c1, const PipelineOptions& opt) {
-  return k > 0 && m > 0 && k <= 256 && m <= 256 && (coeff_size == 0 || coeff_size == size_t(m) * k) && c1 >= c0 &&
-         opt.streams > 0;
+  const int cap = max_rows(opt.field_w);
+  const bool whole = opt.field_w != 16 || ((c0 | c1) & 1) == 0;  // GF(2^16): whole symbols
+  return k > 0 && m > 0 && k <= cap && m <= cap && (coeff_size == 0 || coeff_size == coeff_bytes(m, k, opt.field_w)) &&
+         c1 >= c0 && opt.streams > 0 && whole;
+}
+
+// The slice GEMM of the pipeline's field (descriptors never carry fused copies).
+hipError_t launch_slice(const void* desc, int k, int m, int64_t w, const PipelineOptions& opt, hipStream_t s) {
+  if (opt.field_w == 16) return launch_gf_gemm16(desc, k, pad_m(m), 0, w, opt.bytewise, opt.max_blocks, s);
+  return launch_gf_gemm(desc, k, pad_m(m), 0, w, opt.bytewise, opt.max_blocks, s, /*copies=*/false);
 }
 
 }  // namespace
@@ -254,7 +262,7 @@ hipError_t prepare_pipeline(int device, int k, int m, int64_t ncols, const Pipel
   t = Clock::now();
   {
     TraceRange tl("pipeline/prepare/lanes");
-    GFRS_TRY(setup_lanes(ws, g.lanes, k, m, g.slice, {}, opt.copy_streams > 0));
+    GFRS_TRY(setup_lanes(ws, g.lanes, k, m, g.slice, {}, opt.copy_streams > 0, opt.field_w));
   }
   ps.ms_lanes = ms_since(t);
   // Before anyone's clock starts, run every path the stream loop will take once, on a few columns:
@@ -271,8 +279,7 @@ hipError_t prepare_pipeline(int device, int k, int m, int64_t ncols, const Pipel
   {  // kernel first (code-object load), alone, so its cost is separable from the copies'
     TraceRange tk("pipeline/prepare/kernel");
     Lane& L = ws.lane[0];
-    err = launch_gf_gemm(L.slot[0].desc, k, pad_m(m), 0, std::min<int64_t>(g.slice, int64_t(probe)), opt.bytewise, 0,
-                         L.compute, /*copies=*/false);
+    err = launch_slice(L.slot[0].desc, k, m, std::min<int64_t>(g.slice, int64_t(probe)), opt, L.compute);
     if (err == hipSuccess) err = hipStreamSynchronize(L.compute);
   }
   ps.ms_kernel = ms_since(t);
@@ -287,8 +294,7 @@ hipError_t prepare_pipeline(int device, int k, int m, int64_t ncols, const Pipel
       GFRS_TRY(hipMemcpyAsync(L.slot[0].in, h, probe, hipMemcpyHostToDevice, cin));
       GFRS_TRY(hipMemcpy2DAsync(L.slot[1].in, size_t(g.slice), h, probe, probe, 1, hipMemcpyHostToDevice, cin));
       GFRS_TRY(hipStreamSynchronize(cin));
-      GFRS_TRY(launch_gf_gemm(L.slot[0].desc, k, pad_m(m), 0, std::min<int64_t>(g.slice, int64_t(probe)),
-                              opt.bytewise, 0, L.compute, /*copies=*/false));
+      GFRS_TRY(launch_slice(L.slot[0].desc, k, m, std::min<int64_t>(g.slice, int64_t(probe)), opt, L.compute));
       GFRS_TRY(hipMemcpyAsync(h + kProbe, L.slot[0].out, probe, hipMemcpyDeviceToHost, L.compute));
       GFRS_TRY(hipMemcpy2DAsync(h + kProbe, probe, L.slot[1].out, size_t(g.slice), probe, 1, hipMemcpyDeviceToHost,
                                 L.compute));
@@ -340,7 +346,6 @@ hipError_t gemm_host(int device, const std::vector<const uint8_t*>& in_rows, con
   const Geometry g = geometry(ncols, opt);
   const int64_t slice = g.slice;
   const int lanes = g.lanes;
-  const int m_pad = pad_m(m);
 
   Workspace& ws = workspace(device);
   std::lock_guard<std::mutex> guard(ws.mu);
@@ -381,8 +386,7 @@ hipError_t gemm_host(int device, const std::vector<const uint8_t*>& in_rows, con
           GFRS_TRY(hipEventRecord(S.loaded, cin));
           GFRS_TRY(hipStreamWaitEvent(L.compute, S.loaded, 0));
         }
-        // (pipeline descriptors never carry fused copies)
-        GFRS_TRY(launch_gf_gemm(S.desc, k, m_pad, 0, w, opt.bytewise, opt.max_blocks, L.compute, /*copies=*/false));
+        GFRS_TRY(launch_slice(S.desc, k, m, w, opt, L.compute));
         for (const Run& r : out_runs)
           GFRS_TRY(copy_run(out_rows[r.first] + a, size_t(slice), S.out + size_t(r.first) * slice, r, w,
                             hipMemcpyDeviceToHost, L.compute));

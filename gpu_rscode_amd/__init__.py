@@ -10,14 +10,9 @@ Capabilities of zvonkok/GPU-RSCode (the reference), re-designed for CDNA4:
 """
 from __future__ import annotations
 
-import os
-
-# this driver supports only dmabuf IPC: RCCL peer mappings (and CUDA-tensor sharing between ranks)
-# fail with hipIpcGetMemHandle errors without it. Set before torch initialises the HIP runtime, in
-# every rank however it was launched (torchrun directly, bench.py's self-launch, tests).
-os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-
-import torch  # noqa: F401,E402  — load torch's HIP runtime before the native extension
+# (HSA_ENABLE_IPC_MODE_LEGACY=0 — dmabuf IPC, needed by RCCL peers on this driver — is set by the
+# launchers: bench.py, scripts, __graft_entry__; parallel.dist.init_distributed warns without it.)
+import torch  # noqa: F401  — load torch's HIP runtime before the native extension
 
 from . import gf  # noqa: E402
 from .gf import GF, SingularMatrixError

@@ -39,13 +39,14 @@ def build(target: str = "all", jobs: int | None = None, quiet: bool = True) -> N
 
 
 @contextlib.contextmanager
-def file_lock():
-    """Exclusive lock across processes (``flock`` on ``build/.lock``): ranks started together by
-    torchrun serialise their rebuilds instead of overwriting one module concurrently."""
+def file_lock(shared: bool = False):
+    """Lock across processes (``flock`` on ``build/.lock``): ranks started together by torchrun
+    serialise their rebuilds (exclusive) instead of overwriting one module concurrently, and check
+    staleness and import under the shared lock, so no rank reads a module while another links it."""
     path = ROOT / "build" / ".lock"
     path.parent.mkdir(parents=True, exist_ok=True)
     with open(path, "a") as f:
-        fcntl.flock(f, fcntl.LOCK_EX)
+        fcntl.flock(f, fcntl.LOCK_SH if shared else fcntl.LOCK_EX)
         try:
             yield
         finally:

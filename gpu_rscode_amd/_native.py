@@ -27,17 +27,24 @@ def _load(name: str, target: str):
     # rank of a torchrun job would relink it while its peers import it. The rebuild itself holds a
     # cross-process lock and re-checks after acquiring it, so concurrent ranks build once.
     outs = (so, _build.binary(_CLI[name]))  # what make's target produces
-    if os.environ.get("GPURS_NO_BUILD") != "1" and _build.have_sources() and any(map(_build.stale, outs)):
-        with _build.file_lock():
-            if any(map(_build.stale, outs)):
-                try:
-                    _build.build(target)
-                except (RuntimeError, OSError):
-                    # a failed rebuild is only tolerable when the existing module is up to date with
-                    # every source (e.g. no toolchain here); a stale .so would silently run old code
-                    if not so.exists() or _build.stale(so):
-                        raise
-    mod = importlib.import_module(f"gpu_rscode_amd._{name}")
+    check = os.environ.get("GPURS_NO_BUILD") != "1" and _build.have_sources()
+    if check:
+        with _build.file_lock(shared=True):  # no builder is linking while we look
+            need = any(map(_build.stale, outs))
+        if need:
+            with _build.file_lock():  # exclusive: one rank builds, the others wait and re-check
+                if any(map(_build.stale, outs)):
+                    try:
+                        _build.build(target)
+                    except (RuntimeError, OSError):
+                        # a failed rebuild is only tolerable when the existing module is up to date
+                        # with every source (e.g. no toolchain here); a stale .so would run old code
+                        if not so.exists() or _build.stale(so):
+                            raise
+        with _build.file_lock(shared=True):  # (make also links to a temporary and renames it)
+            mod = importlib.import_module(f"gpu_rscode_amd._{name}")
+    else:
+        mod = importlib.import_module(f"gpu_rscode_amd._{name}")
     _mods[name] = mod
     return mod
 

@@ -69,6 +69,11 @@ def init_distributed(backend: str | None = None, force_pg: bool | None = None) -
     else:
         device = torch.device("cpu")
     backend = backend or ("nccl" if use_gpu else "gloo")
+    if backend == "nccl" and world > 1 and os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY") != "0":
+        import warnings
+
+        warnings.warn("RCCL peers need dmabuf IPC on this driver: export HSA_ENABLE_IPC_MODE_LEGACY=0 before "
+                      "the process starts (hipIpcGetMemHandle fails without it)", RuntimeWarning, stacklevel=2)
     if (world > 1 or force_pg) and not dist.is_initialized():
         kw = {"device_id": device} if device.type == "cuda" else {}
         if world == 1 and "MASTER_PORT" not in os.environ:

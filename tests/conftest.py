@@ -4,6 +4,9 @@ import sys
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+# dmabuf IPC only on this driver (RCCL peers, CUDA-tensor sharing between ranks): set by the launcher,
+# before torch initialises HIP
+os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
