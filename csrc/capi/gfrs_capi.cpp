@@ -423,12 +423,14 @@ int gfrs_encode_file(const char* file, int k, int p, int matrix_kind, const int*
     const gfrs::PipelineOptions opt = pipe_opts(streams, 0);
     auto prep = gfrs::prepare_for_encode(devs, opt, file, k, p);  // device setup beside the reads
     const gfrs::GemmFn gemm = [&](const std::vector<const uint8_t*>& in, const std::vector<uint8_t*>& out,
-                                  const gfrs::Mat& coeff, int64_t ncols) {
+                                  const gfrs::Mat& coeff, int64_t ncols, int field_w) {
       if (prep) {
         prep->wait();
         prep.reset();
       }
-      hip_check(gfrs::gemm_host_multi(devs, in, out, coeff, ncols, opt, nullptr, nullptr), "GPU pipeline");
+      gfrs::PipelineOptions o = opt;
+      o.field_w = field_w;
+      hip_check(gfrs::gemm_host_multi(devs, in, out, coeff, ncols, o, nullptr, nullptr), "GPU pipeline");
     };
     fill_report(gfrs::encode_file(file, k, p, static_cast<gfrs::MatrixKind>(matrix_kind), gemm,
                                   gfrs::thp_pinned_host_alloc()),
@@ -444,12 +446,14 @@ int gfrs_decode_file(const char* file, const char* conf, const char* out, const 
     const gfrs::PipelineOptions opt = pipe_opts(streams, 0);
     auto prep = gfrs::prepare_for_decode(devs, opt, file);
     const gfrs::GemmFn gemm = [&](const std::vector<const uint8_t*>& in, const std::vector<uint8_t*>& o,
-                                  const gfrs::Mat& coeff, int64_t ncols) {
+                                  const gfrs::Mat& coeff, int64_t ncols, int field_w) {
       if (prep) {
         prep->wait();
         prep.reset();
       }
-      hip_check(gfrs::gemm_host_multi(devs, in, o, coeff, ncols, opt, nullptr, nullptr), "GPU pipeline");
+      gfrs::PipelineOptions po = opt;
+      po.field_w = field_w;
+      hip_check(gfrs::gemm_host_multi(devs, in, o, coeff, ncols, po, nullptr, nullptr), "GPU pipeline");
     };
     fill_report(gfrs::decode_file(file, conf, out ? out : "", gemm, gfrs::thp_pinned_host_alloc()), report);
   });

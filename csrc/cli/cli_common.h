@@ -30,6 +30,8 @@ struct Args {
   long long window = -1;  // --window: stream in column windows of this many bytes (0 = auto)
   bool resume = true;     // --no-resume: ignore a <target>.PROGRESS checkpoint
   bool sync = true;       // --no-sync: skip fdatasync before each checkpoint
+  int field_w = 8;        // -w 8|16: symbol width (GF(2^8), or GF(2^16) for n up to 65535)
+  bool zero_copy = false;  // --zero-copy: kernels read/write the pinned host rows over PCIe (no staging)
   bool streaming() const { return window >= 0; }
 };
 
@@ -50,6 +52,8 @@ inline void usage(const char* prog, bool gpu) {
   }
   std::printf("Extensions:\n");
   std::printf("  --matrix vandermonde|cauchy|sys_vandermonde  coding matrix (default: reference Vandermonde)\n");
+  std::printf("  -w|-W 8|16              encode: symbol width, GF(2^8) (default) or GF(2^16) (n <= 65535;\n");
+  std::printf("                          src/galoisfield.cu's w = 16 field); decode reads it from the METADATA\n");
   std::printf("  --cpu-meta              write the 2-line CPU-format METADATA\n");
   std::printf("  --make-conf             write conf-<n>-<k>-<file> keeping the last k chunks (unit-test.sh)\n");
   std::printf("  --window BYTES          bounded-memory streaming codec: column windows of BYTES per chunk\n");
@@ -61,6 +65,8 @@ inline void usage(const char* prog, bool gpu) {
     std::printf("  --gpus N                number of GPUs (default: all visible)\n");
     std::printf("  --devices I,J,...       explicit column-shard -> device list (a device may repeat)\n");
     std::printf("  --slice BYTES           column slice per stream step (default 16 MiB)\n");
+    std::printf("  --zero-copy             the GEMM kernel streams the pinned host rows itself over PCIe: no\n");
+    std::printf("                          device slice buffers or copy engines (-s/--slice then unused)\n");
   } else {
     std::printf("  --mul logexp|logexp0|logexp1|logexp2|logexp3|loop|full|double|perm|row|simd\n");
     std::printf("  --threads T             worker threads (default 1, the reference's single thread)\n");
@@ -101,10 +107,12 @@ inline Args parse(int argc, char** argv, bool gpu) {
                                     {"no-resume", no_argument, nullptr, 9},
                                     {"no-sync", no_argument, nullptr, 10},
                                     {"devices", required_argument, nullptr, 11},
+                                    {"field-width", required_argument, nullptr, 'w'},
+                                    {"zero-copy", no_argument, nullptr, 12},
                                     {"help", no_argument, nullptr, 'h'},
                                     {nullptr, 0, nullptr, 0}};
   int c;
-  while ((c = getopt_long(argc, argv, "k:K:n:N:e:E:i:I:c:C:o:O:p:P:s:S:dDhq", longopts, nullptr)) != -1) {
+  while ((c = getopt_long(argc, argv, "k:K:n:N:e:E:i:I:c:C:o:O:p:P:s:S:w:W:dDhq", longopts, nullptr)) != -1) {
     switch (c) {
       case 'k': case 'K': a.k = to_int(optarg, "nativeBlockNum", 1); break;
       case 'n': case 'N': a.n = to_int(optarg, "totalBlockNum", 1); break;
@@ -116,6 +124,13 @@ inline Args parse(int argc, char** argv, bool gpu) {
       case 'p': case 'P': a.grid = to_int(optarg, "grid size", 0); break;
       case 's': case 'S': a.streams = to_int(optarg, "stream number", 1); break;
       case 'q': a.quiet = true; break;
+      case 'w': case 'W':
+        a.field_w = to_int(optarg, "field width", 8);
+        if (a.field_w != 8 && a.field_w != 16) {
+          std::fprintf(stderr, "invalid field width: %s (8 or 16)\n", optarg);
+          std::exit(2);
+        }
+        break;
       case 1: a.matrix = optarg; break;
       case 2: a.cpu_meta = true; break;
       case 3: a.gpus = to_int(optarg, "GPU count", 1); break;
@@ -126,6 +141,7 @@ inline Args parse(int argc, char** argv, bool gpu) {
       case 8: a.window = to_ll(optarg, "window bytes", 0); break;
       case 9: a.resume = false; break;
       case 10: a.sync = false; break;
+      case 12: a.zero_copy = true; break;
       case 11: {
         std::string list = optarg ? optarg : "";
         size_t pos = 0;
@@ -142,8 +158,13 @@ inline Args parse(int argc, char** argv, bool gpu) {
     }
   }
   if (a.op == Args::kEncode) {
-    if (a.k <= 0 || a.n <= a.k - 1 || a.in_file.empty() || a.n > 256) {
-      std::fprintf(stderr, "encode needs -k K -n N -e FILE with 1 <= K <= N <= 256\n");
+    const int cap = a.field_w == 16 ? 65535 : 256;
+    if (a.k <= 0 || a.n <= a.k - 1 || a.in_file.empty() || a.n > cap) {
+      std::fprintf(stderr, "encode needs -k K -n N -e FILE with 1 <= K <= N <= %d\n", cap);
+      std::exit(2);
+    }
+    if (a.field_w == 16 && (a.streaming() || a.cpu_meta)) {
+      std::fprintf(stderr, "-w 16 writes the versioned METADATA without --window / --cpu-meta\n");
       std::exit(2);
     }
   } else if (a.op == Args::kDecode) {

@@ -7,6 +7,7 @@
 #include "gfrs/codec_file.h"
 #include "gfrs/cpu_codec.h"
 #include "gfrs/format.h"
+#include "gfrs/host_desc.h"
 #include "gfrs/stream_codec.h"
 
 int main(int argc, char** argv) {
@@ -15,7 +16,12 @@ int main(int argc, char** argv) {
   try {
     const CpuMul strat = parse_cpu_mul(a.mul);
     const GemmFn gemm = [&](const std::vector<const uint8_t*>& in, const std::vector<uint8_t*>& out,
-                            const Mat& coeff, int64_t ncols) { cpu_gemm(in, out, coeff, ncols, strat, a.threads); };
+                            const Mat& coeff, int64_t ncols, int field_w) {
+      if (field_w == 16)
+        cpu_gemm16(in, out, unpack16(coeff), ncols, a.threads);
+      else
+        cpu_gemm(in, out, coeff, ncols, strat, a.threads);
+    };
     if (a.op == gfrs_cli::Args::kMakeConf) {
       const std::string name = "conf-" + std::to_string(a.n) + "-" + std::to_string(a.k) + "-" + a.in_file;
       write_conf(name, worst_case_conf(a.in_file, a.n, a.k));
@@ -28,7 +34,7 @@ int main(int argc, char** argv) {
       const FileReport r = a.streaming() ? encode_file_stream(a.in_file, a.k, a.n - a.k, parse_matrix_kind(a.matrix),
                                                               gemm, default_host_alloc(), so, a.cpu_meta)
                                          : encode_file(a.in_file, a.k, a.n - a.k, parse_matrix_kind(a.matrix), gemm,
-                                                       default_host_alloc(), a.cpu_meta);
+                                                       default_host_alloc(), a.cpu_meta, a.field_w);
       if (!a.quiet) {
         std::printf("Total CPU encoding time: %fms\n", r.ms_matrix + r.ms_compute);
         std::printf("CPU encoding bandwidth: %.3f MB/s (strategy %s, %d thread(s))\n",

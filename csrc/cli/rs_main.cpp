@@ -72,6 +72,7 @@ int main(int argc, char** argv) {
     opt.streams = a.streams;
     opt.max_blocks = a.grid;
     opt.slice_bytes = a.slice;
+    opt.zero_copy = a.zero_copy;
     const bool enc = a.op == gfrs_cli::Args::kEncode;
     const char* verb = enc ? "encoding" : "decoding";
     // device setup overlapped with the input reads (gfrs/async_prepare.h), sized for the whole
@@ -83,6 +84,7 @@ int main(int argc, char** argv) {
     const StreamOptions* sop = a.streaming() ? &so : nullptr;
     double gpu_ms = 0;  // stream-loop time: transfers + kernels + frees, all devices (setup excluded)
     double setup_ms = 0, setup_past_ms = 0;  // helper-thread device setup, and the part the GEMM waited for
+    opt.field_w = enc ? a.field_w : 8;  // (decode: the field comes from the METADATA)
     std::unique_ptr<AsyncPrepare> prep = enc ? prepare_for_encode(devices, opt, a.in_file, a.k, a.n - a.k, sop)
                                              : prepare_for_decode(devices, opt, a.in_file, sop);
     // GFRS_SETUP=serial (measurement aid): finish the device setup before the host buffers are
@@ -102,7 +104,7 @@ int main(int argc, char** argv) {
       prep.reset();
     }
     const GemmFn gemm = [&](const std::vector<const uint8_t*>& in, const std::vector<uint8_t*>& out,
-                            const Mat& coeff, int64_t ncols) {
+                            const Mat& coeff, int64_t ncols, int field_w) {
       if (prep) {
         const auto t0 = std::chrono::steady_clock::now();
         const double since_start = prep->ms_until(t0);
@@ -125,12 +127,18 @@ int main(int argc, char** argv) {
       }
       std::vector<PipelineStats> st;
       double wall = 0;
-      check(gemm_host_multi(devices, in, out, coeff, ncols, opt, &st, &wall), "GPU pipeline");
+      PipelineOptions o = opt;
+      o.field_w = field_w;
+      check(gemm_host_multi(devices, in, out, coeff, ncols, o, &st, &wall), "GPU pipeline");
       gpu_ms += wall;
       if (!a.quiet) {
         for (size_t d = 0; d < st.size(); ++d)
-          std::printf("Device%zu: Total GPU %s time: %fms (stream loop %fms, %d slices)\n", d, verb, st[d].ms_total,
-                      st[d].ms_stream, st[d].slices);
+          if (st[d].zero_copy)
+            std::printf("Device%zu: Total GPU %s time: %fms (zero-copy kernel %fms)\n", d, verb, st[d].ms_total,
+                        st[d].ms_stream);
+          else
+            std::printf("Device%zu: Total GPU %s time: %fms (stream loop %fms, %d slices)\n", d, verb, st[d].ms_total,
+                        st[d].ms_stream, st[d].slices);
         std::printf("Total GPU %s time using multiple devices: %fms\n", verb, wall);
       }
     };
@@ -144,7 +152,8 @@ int main(int argc, char** argv) {
                     static_cast<long long>(sr.window), static_cast<long long>(sr.resumed_from));
       r = sr;
     } else {
-      r = enc ? encode_file(a.in_file, a.k, a.n - a.k, parse_matrix_kind(a.matrix), gemm, pinned_alloc(), a.cpu_meta)
+      r = enc ? encode_file(a.in_file, a.k, a.n - a.k, parse_matrix_kind(a.matrix), gemm, pinned_alloc(), a.cpu_meta,
+                            a.field_w)
               : decode_file(a.in_file, a.conf, a.out, gemm, pinned_alloc());
     }
     if (!a.quiet) {

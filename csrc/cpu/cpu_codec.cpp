@@ -5,6 +5,7 @@
 
 #include <algorithm>
 #include <array>
+#include <atomic>
 #include <cstring>
 #include <stdexcept>
 #include <thread>
@@ -254,6 +255,58 @@ void cpu_gemm(const std::vector<const uint8_t*>& in, const std::vector<uint8_t*>
     case CpuMul::kRow: return gemm_threads<CpuMul::kRow>(in, out, coeff, ncols, threads);
     case CpuMul::kSimd: return gemm_threads<CpuMul::kSimd>(in, out, coeff, ncols, threads);
   }
+}
+
+}  // namespace gfrs
+
+namespace gfrs {
+namespace {
+
+// Symbols [s0, s1) of every output: per coefficient two 256-entry product tables, c * l and
+// c * (h << 8), built once per (i, j) and applied to the column range in one pass.
+void gemm16_range(const std::vector<const uint8_t*>& in, const std::vector<uint8_t*>& out, const gf16w::Mat& coeff,
+                  int64_t s0, int64_t s1) {
+  const int k = int(in.size()), m = int(out.size());
+  std::vector<uint16_t> acc(size_t(s1 - s0));
+  uint16_t tlo[256], thi[256];
+  for (int i = 0; i < m; ++i) {
+    std::fill(acc.begin(), acc.end(), uint16_t(0));
+    for (int j = 0; j < k; ++j) {
+      const uint16_t c = coeff[size_t(i) * k + j];
+      if (!c) continue;
+      for (int x = 0; x < 256; ++x) {
+        tlo[x] = gf16w::mul(c, static_cast<uint16_t>(x));
+        thi[x] = gf16w::mul(c, static_cast<uint16_t>(x << 8));
+      }
+      const uint8_t* src = in[j] + 2 * s0;
+      for (int64_t s = 0; s < s1 - s0; ++s) acc[size_t(s)] ^= tlo[src[2 * s]] ^ thi[src[2 * s + 1]];
+    }
+    uint8_t* dst = out[i] + 2 * s0;
+    for (int64_t s = 0; s < s1 - s0; ++s) {
+      dst[2 * s] = static_cast<uint8_t>(acc[size_t(s)] & 0xFF);
+      dst[2 * s + 1] = static_cast<uint8_t>(acc[size_t(s)] >> 8);
+    }
+  }
+}
+
+}  // namespace
+
+void cpu_gemm16(const std::vector<const uint8_t*>& in, const std::vector<uint8_t*>& out, const gf16w::Mat& coeff,
+                int64_t ncols, int threads) {
+  const int k = int(in.size()), m = int(out.size());
+  if (coeff.size() != size_t(m) * k) throw std::invalid_argument("cpu_gemm16: coeff must be m x k");
+  if (ncols % 2) throw std::invalid_argument("cpu_gemm16: ncols must be an even byte count (16-bit symbols)");
+  if (threads <= 0) threads = int(std::max(1u, std::thread::hardware_concurrency()));
+  const int64_t nsym = ncols / 2;
+  // chunks of at most 1 Mi symbols keep each thread's accumulator row in cache-friendly size
+  const int64_t per = std::max<int64_t>(1, std::min<int64_t>(1 << 20, (nsym + threads - 1) / threads));
+  std::vector<std::thread> th;
+  std::atomic<int64_t> next{0};
+  for (int t = 0; t < threads; ++t)
+    th.emplace_back([&] {
+      for (int64_t a; (a = next.fetch_add(per)) < nsym;) gemm16_range(in, out, coeff, a, std::min(nsym, a + per));
+    });
+  for (auto& x : th) x.join();
 }
 
 }  // namespace gfrs

@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "gfrs/format.h"
+#include "gfrs/host_desc.h"
 #include "gfrs/pipeline.h"
 #include "gfrs/stream_codec.h"
 
@@ -60,8 +61,8 @@ class AsyncPrepare {
 inline std::unique_ptr<AsyncPrepare> prepare_for_encode(const std::vector<int>& devices, const PipelineOptions& opt,
                                                         const std::string& file, int k, int p,
                                                         const StreamOptions* stream = nullptr) {
-  if (k <= 0 || p <= 0 || k + p > 256) return nullptr;
-  int64_t C = chunk_size(file_size(file), k);
+  if (k <= 0 || p <= 0 || k + p > max_rows(opt.field_w)) return nullptr;
+  int64_t C = chunk_size(file_size(file), k, opt.field_w);
   if (C <= 0) return nullptr;
   if (stream) C = stream_window(*stream, k + p, C);
   return std::make_unique<AsyncPrepare>(devices, opt, k, p, C);
@@ -73,10 +74,12 @@ inline std::unique_ptr<AsyncPrepare> prepare_for_decode(const std::vector<int>& 
                                                         const StreamOptions* stream = nullptr) {
   const Metadata md = read_metadata(metadata_path(file));
   const int m = std::min(md.k, md.p);
-  int64_t C = chunk_size(md.total_size, md.k);
-  if (md.k <= 0 || m <= 0 || C <= 0 || md.k > 256) return nullptr;
+  PipelineOptions o = opt;
+  o.field_w = md.w;
+  int64_t C = chunk_size(md.total_size, md.k, md.w);
+  if (md.k <= 0 || m <= 0 || C <= 0 || md.k > max_rows(md.w)) return nullptr;
   if (stream) C = stream_window(*stream, 2 * md.k, C);
-  return std::make_unique<AsyncPrepare>(devices, opt, md.k, m, C);
+  return std::make_unique<AsyncPrepare>(devices, o, md.k, m, C);
 }
 
 }  // namespace gfrs

@@ -24,6 +24,7 @@
 #include <string>
 #include <vector>
 
+#include "gfrs/gf65536.h"
 #include "gfrs/matrix.h"
 
 namespace gfrs {
@@ -48,6 +49,12 @@ const char* cpu_mul_name(CpuMul m);
 // out_rows[i][c] = XOR_j coeff[i][j] * in_rows[j][c], c in [0, ncols). threads <= 0: hardware.
 void cpu_gemm(const std::vector<const uint8_t*>& in_rows, const std::vector<uint8_t*>& out_rows, const Mat& coeff,
               int64_t ncols, CpuMul strategy = CpuMul::kSimd, int threads = 1);
+
+// GF(2^16) (gfrs/gf65536.h): out_rows[i][s] = XOR_j coeff[i][j] * in_rows[j][s] over little-endian
+// 16-bit symbols; ncols is a byte count (even). Two 256-entry product tables per coefficient (low
+// and high source byte), columns split over `threads` (<= 0: hardware).
+void cpu_gemm16(const std::vector<const uint8_t*>& in_rows, const std::vector<uint8_t*>& out_rows,
+                const gf16w::Mat& coeff, int64_t ncols, int threads = 1);
 
 // Scalar multiply through a given strategy (exposed for the per-strategy unit tests).
 uint8_t cpu_mul(CpuMul strategy, uint8_t a, uint8_t b);

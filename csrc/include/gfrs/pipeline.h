@@ -34,10 +34,17 @@ struct PipelineOptions {
   bool persistent = true;          // keep streams/buffers/descriptor per device for the next call
   int copy_streams = 1;            // 1: H2D on a per-lane copy-in stream; 0: everything on one stream
   bool rect = true;                // equally spaced host rows: one 2-D copy per slice instead of k / m
-  int field_w = 8;                 // 8: GF(2^8) coefficients; 4: the GF(16) nibble method (doc/design.tex:190-209)
+  int field_w = 8;                 // 8: GF(2^8) coefficients; 4: the GF(16) nibble method (doc/design.tex:190-209);
+                                   // 16: GF(2^16), coefficients packed as little-endian pairs (host_desc.h pack16)
+  // Zero-copy: the GEMM kernel reads the k input rows and writes the m output rows straight from/to
+  // pinned, device-mapped host memory over PCIe (hipHostRegister / hipHostMalloc rows, 16-byte
+  // aligned). No slice buffers, no copy engines: the per-process setup is a stream and the kernel
+  // load. Falls back to the staged -s pipeline when a row is not mapped or not aligned.
+  bool zero_copy = false;
 };
 
 struct PipelineStats {
+  bool zero_copy = false;  // ran the zero-copy kernel (else the staged -s pipeline)
   double ms_setup = 0;    // stream/buffer/descriptor setup (alloc)
   double ms_stream = 0;   // H2D + kernel + D2H loop until the last stream drains
   double ms_teardown = 0;  // frees

@@ -10,12 +10,18 @@
 #include <stdexcept>
 
 #include "gfrs/format.h"
+#include "gfrs/host_desc.h"
 #include "gfrs/trace.h"
 
 namespace gfrs {
 namespace {
 
 using Clock = std::chrono::steady_clock;
+
+// Host row pitch of the codec's buffers: chunk rows start on 4 KiB boundaries (an odd C, e.g.
+// 2^30 / 10, would otherwise leave every row but the first unaligned), so the zero-copy pipeline
+// streams them with 16-byte vector loads and the staged one with 2-D copies.
+int64_t row_pitch(int64_t C) { return (C + 4095) / 4096 * 4096; }
 double ms_since(Clock::time_point t0) { return std::chrono::duration<double, std::milli>(Clock::now() - t0).count(); }
 
 struct Buf {
@@ -31,6 +37,51 @@ struct Buf {
   Buf& operator=(const Buf&) = delete;
 };
 
+// GF(2^16) coding blocks (gfrs/gf65536.h): the reference Vandermonde and Cauchy, and the
+// systematic Vandermonde V[k:] . inv(V[:k]) over the points 0..n-1.
+gf16w::Mat encoding_matrix16(MatrixKind kind, int k, int p) {
+  switch (kind) {
+    case MatrixKind::kVandermondeRef: return gf16w::vandermonde_ref(k, p);
+    case MatrixKind::kCauchy: return gf16w::cauchy(k, p);
+    case MatrixKind::kSysVandermonde: {
+      const int n = k + p;
+      gf16w::Mat v(size_t(n) * k);
+      for (int r = 0; r < n; ++r)
+        for (int j = 0; j < k; ++j) v[size_t(r) * k + j] = gf16w::pow(static_cast<uint16_t>(r), unsigned(j));
+      gf16w::Mat top(v.begin(), v.begin() + size_t(k) * k), top_inv;
+      if (!gf16w::invert(top, k, top_inv)) throw std::runtime_error("sys_vandermonde: singular top block");
+      return gf16w::matmul(gf16w::Mat(v.begin() + size_t(k) * k, v.end()), top_inv, p, k, k);
+    }
+  }
+  throw std::invalid_argument("bad matrix kind");
+}
+
+// Decode system of either field: rows of the inverse of G[rows], packed as GemmFn coefficients
+// (one byte per GF(2^8) entry, two per GF(2^16) entry). False when the pattern is singular.
+struct Solver {
+  const Metadata& md;
+  bool solve(const std::vector<int>& rows, const std::vector<int>* erased, Mat* coeff) const {
+    const int k = md.k;
+    if (md.w == 16) {
+      gf16w::Mat dm;
+      if (!gf16w::decode_matrix(md.g16, k, rows, dm)) return false;
+      if (erased && coeff) {
+        gf16w::Mat sel;
+        for (int e : *erased) sel.insert(sel.end(), dm.begin() + size_t(e) * k, dm.begin() + size_t(e + 1) * k);
+        *coeff = pack16(sel);
+      }
+      return true;
+    }
+    Mat dm;
+    if (!decode_matrix(md.g, k, rows, dm)) return false;
+    if (erased && coeff) {
+      coeff->clear();
+      for (int e : *erased) coeff->insert(coeff->end(), dm.begin() + size_t(e) * k, dm.begin() + size_t(e + 1) * k);
+    }
+    return true;
+  }
+};
+
 }  // namespace
 
 HostAlloc default_host_alloc() {
@@ -43,20 +94,25 @@ HostAlloc default_host_alloc() {
 }
 
 FileReport encode_file(const std::string& file, int k, int p, MatrixKind kind, const GemmFn& gemm,
-                       const HostAlloc& alloc, bool cpu_meta) {
-  if (k <= 0 || p < 0 || k + p > 256) throw std::invalid_argument("encode: need k >= 1, p >= 0, k + p <= 256");
+                       const HostAlloc& alloc, bool cpu_meta, int field_w) {
+  if (field_w != 8 && field_w != 16) throw std::invalid_argument("encode: field width must be 8 or 16");
+  if (k <= 0 || p < 0 || k + p > max_rows(field_w))
+    throw std::invalid_argument(field_w == 16 ? "encode: need k >= 1, p >= 0, k + p <= 65535 (GF(2^16))"
+                                              : "encode: need k >= 1, p >= 0, k + p <= 256");
+  if (field_w == 16 && cpu_meta) throw std::invalid_argument("encode: the 2-line CPU METADATA has no GF(2^16) form");
   FileReport r;
   r.k = k;
   r.p = p;
   auto t = Clock::now();
   r.total_size = file_size(file);
-  r.chunk_size = std::max<int64_t>(1, chunk_size(r.total_size, k));
+  r.chunk_size = std::max<int64_t>(field_w == 16 ? 2 : 1, chunk_size(r.total_size, k, field_w));
   const int64_t C = r.chunk_size;
+  const int64_t P = row_pitch(C);
   std::unique_ptr<Buf> data_b, parity_b;
   {
     TraceRange tr("encode/alloc");
-    data_b = std::make_unique<Buf>(alloc, size_t(k) * C);
-    parity_b = std::make_unique<Buf>(alloc, size_t(std::max(p, 1)) * C);
+    data_b = std::make_unique<Buf>(alloc, size_t(k) * P);
+    parity_b = std::make_unique<Buf>(alloc, size_t(std::max(p, 1)) * P);
   }
   Buf& data = *data_b;
   Buf& parity = *parity_b;
@@ -64,12 +120,19 @@ FileReport encode_file(const std::string& file, int k, int p, MatrixKind kind, c
   t = Clock::now();
   {
     TraceRange tr("encode/read");
-    read_into(file, 0, data.p, int64_t(k) * C);
-  }  // one contiguous read; tail zero-padded
+    for (int j = 0; j < k; ++j) read_into(file, int64_t(j) * C, data.p + size_t(j) * P, C);
+  }  // one read per chunk row; tail zero-padded
   r.ms_read = ms_since(t);
 
   t = Clock::now();
-  const Mat e = p ? encoding_matrix(kind, k, p) : Mat{};
+  gf16w::Mat e16;
+  Mat e;
+  if (p && field_w == 16) {
+    e16 = encoding_matrix16(kind, k, p);
+    e = pack16(e16);
+  } else if (p) {
+    e = encoding_matrix(kind, k, p);
+  }
   r.ms_matrix = ms_since(t);
 
   t = Clock::now();
@@ -77,9 +140,9 @@ FileReport encode_file(const std::string& file, int k, int p, MatrixKind kind, c
     TraceRange tr("encode/gemm");
     std::vector<const uint8_t*> in(k);
     std::vector<uint8_t*> out(p);
-    for (int j = 0; j < k; ++j) in[j] = data.p + size_t(j) * C;
-    for (int i = 0; i < p; ++i) out[i] = parity.p + size_t(i) * C;
-    gemm(in, out, e, C);
+    for (int j = 0; j < k; ++j) in[j] = data.p + size_t(j) * P;
+    for (int i = 0; i < p; ++i) out[i] = parity.p + size_t(i) * P;
+    gemm(in, out, e, C, field_w);
   }
   r.ms_compute = ms_since(t);
 
@@ -91,14 +154,17 @@ FileReport encode_file(const std::string& file, int k, int p, MatrixKind kind, c
     std::vector<std::thread> th;
     for (int i = 0; i < k + p; ++i)
       th.emplace_back([&, i] {
-        const uint8_t* row = i < k ? data.p + size_t(i) * C : parity.p + size_t(i - k) * C;
+        const uint8_t* row = i < k ? data.p + size_t(i) * P : parity.p + size_t(i - k) * P;
         crc[size_t(i)] = crc32(row, C);
       });
     for (auto& x : th) x.join();
   }
-  for (int i = 0; i < k; ++i) write_from(chunk_path(file, i), data.p + size_t(i) * C, C);
-  for (int i = 0; i < p; ++i) write_from(chunk_path(file, k + i), parity.p + size_t(i) * C, C);
-  write_metadata(metadata_path(file), r.total_size, p, k, e, !cpu_meta, crc);
+  for (int i = 0; i < k; ++i) write_from(chunk_path(file, i), data.p + size_t(i) * P, C);
+  for (int i = 0; i < p; ++i) write_from(chunk_path(file, k + i), parity.p + size_t(i) * P, C);
+  if (field_w == 16)
+    write_metadata16(metadata_path(file), r.total_size, p, k, e16, crc);
+  else
+    write_metadata(metadata_path(file), r.total_size, p, k, e, !cpu_meta, crc);
   r.ms_write = ms_since(t);
   return r;
 }
@@ -112,8 +178,10 @@ FileReport decode_file(const std::string& file, const std::string& conf, const s
   r.k = k;
   r.p = md.p;
   r.total_size = md.total_size;
-  r.chunk_size = std::max<int64_t>(1, chunk_size(md.total_size, k));
+  r.chunk_size = std::max<int64_t>(md.w == 16 ? 2 : 1, chunk_size(md.total_size, k, md.w));
   const int64_t C = r.chunk_size;
+  const int64_t P = row_pitch(C);
+  const Solver solver{md};
 
   // The reference uses exactly the first k names (src/decode.cu:302-318). Here the conf may list
   // more: chunks that are missing or fail their METADATA CRC-32 are skipped, and the first
@@ -138,7 +206,7 @@ FileReport decode_file(const std::string& file, const std::string& conf, const s
   std::unique_ptr<Buf> surv_b;
   {
     TraceRange tr("decode/alloc");
-    surv_b = std::make_unique<Buf>(alloc, size_t(k) * C);
+    surv_b = std::make_unique<Buf>(alloc, size_t(k) * P);
   }
   Buf& surv = *surv_b;
   r.ms_alloc = ms_since(t);
@@ -162,7 +230,7 @@ FileReport decode_file(const std::string& file, const std::string& conf, const s
   std::vector<int> verified;
   for (int ci = 0; ci < int(cand_idx.size()); ++ci) {
     if (int(verified.size()) < k) {
-      if (row_ok(ci, surv.p + size_t(verified.size()) * C)) verified.push_back(ci);
+      if (row_ok(ci, surv.p + size_t(verified.size()) * P)) verified.push_back(ci);
     } else {
       std::vector<uint8_t> tmp(static_cast<size_t>(C));
       if (row_ok(ci, tmp.data())) {
@@ -181,8 +249,7 @@ FileReport decode_file(const std::string& file, const std::string& conf, const s
     for (int i = 0; i < k; ++i) rr[i] = cand_idx[size_t(verified[size_t(pk[i])])];
     return rr;
   };
-  Mat probe;
-  bool found = decode_matrix(md.g, k, rows_of(pick), probe);
+  bool found = solver.solve(rows_of(pick), nullptr, nullptr);
   for (long tries = 0; !found && tries < 100000; ++tries) {  // next k-combination of the verified set
     int i = k - 1;
     const int V = int(verified.size());
@@ -190,7 +257,7 @@ FileReport decode_file(const std::string& file, const std::string& conf, const s
     if (i < 0) break;
     ++pick[i];
     for (int j = i + 1; j < k; ++j) pick[j] = pick[j - 1] + 1;
-    found = decode_matrix(md.g, k, rows_of(pick), probe);
+    found = solver.solve(rows_of(pick), nullptr, nullptr);
   }
   if (!found)
     throw std::runtime_error("unrecoverable erasure pattern: the selected rows of the generator are singular");
@@ -198,16 +265,13 @@ FileReport decode_file(const std::string& file, const std::string& conf, const s
   for (int i = 0; i < k; ++i) {
     const int pos = pick[i];
     if (pos == i) continue;
-    const uint8_t* src = pos < k ? surv.p + size_t(pos) * C : spare[size_t(pos - k)].data();
-    std::memcpy(surv.p + size_t(i) * C, src, size_t(C));  // pick is increasing: slot i <= pos, no clobber of later picks
+    const uint8_t* src = pos < k ? surv.p + size_t(pos) * P : spare[size_t(pos - k)].data();
+    std::memcpy(surv.p + size_t(i) * P, src, size_t(C));  // pick is increasing: slot i <= pos, no clobber of later picks
   }
   rows = rows_of(pick);
   r.ms_read = ms_meta + ms_since(t);
 
   t = Clock::now();
-  Mat dm;
-  if (!decode_matrix(md.g, k, rows, dm))
-    throw std::runtime_error("unrecoverable erasure pattern: the selected rows of the generator are singular");
   // survivors that are natives pass through; only erased natives are reconstructed
   std::vector<int> pos_of_native(k, -1);
   for (int i = 0; i < k; ++i)
@@ -215,25 +279,25 @@ FileReport decode_file(const std::string& file, const std::string& conf, const s
   std::vector<int> erased;
   for (int i = 0; i < k; ++i)
     if (pos_of_native[i] < 0) erased.push_back(i);
+  Mat coeff;  // the erased natives' rows of the inverse (packed for the field)
+  if (!solver.solve(rows, &erased, &coeff))
+    throw std::runtime_error("unrecoverable erasure pattern: the selected rows of the generator are singular");
   r.erased = int(erased.size());
   r.ms_matrix = ms_since(t);
   // (the output rows are allocated outside the timed GEMM region and outside the matrix time, like
   // encode's parity buffer: a pinned hipHostMalloc of ~GBs takes tens of ms)
   t = Clock::now();
-  Buf rec(alloc, size_t(std::max<size_t>(erased.size(), 1)) * C);
+  Buf rec(alloc, size_t(std::max<size_t>(erased.size(), 1)) * P);
   r.ms_alloc += ms_since(t);
 
   t = Clock::now();
   if (!erased.empty()) {
     TraceRange tr("decode/gemm");
-    Mat coeff(erased.size() * size_t(k));
-    for (size_t e = 0; e < erased.size(); ++e)
-      std::memcpy(&coeff[e * k], &dm[size_t(erased[e]) * k], size_t(k));
     std::vector<const uint8_t*> in(k);
     std::vector<uint8_t*> o(erased.size());
-    for (int j = 0; j < k; ++j) in[j] = surv.p + size_t(j) * C;
-    for (size_t e = 0; e < erased.size(); ++e) o[e] = rec.p + e * C;
-    gemm(in, o, coeff, C);
+    for (int j = 0; j < k; ++j) in[j] = surv.p + size_t(j) * P;
+    for (size_t e = 0; e < erased.size(); ++e) o[e] = rec.p + e * P;
+    gemm(in, o, coeff, C, md.w);
   }
   r.ms_compute = ms_since(t);
 
@@ -246,9 +310,9 @@ FileReport decode_file(const std::string& file, const std::string& conf, const s
   for (int i = 0; i < k && left > 0; ++i) {
     const uint8_t* row;
     if (pos_of_native[i] >= 0) {
-      row = surv.p + size_t(pos_of_native[i]) * C;
+      row = surv.p + size_t(pos_of_native[i]) * P;
     } else {
-      row = rec.p + e_idx * C;
+      row = rec.p + e_idx * P;
       ++e_idx;
     }
     const int64_t w = std::min(C, left);

@@ -248,7 +248,7 @@ StreamReport encode_file_stream(const std::string& file, int k, int p, MatrixKin
         std::vector<uint8_t*> op(p);
         for (int j = 0; j < k; ++j) ip[j] = row(set, j);
         for (int i = 0; i < p; ++i) op[i] = row(set, k + i);
-        gemm(ip, op, e, len);
+        gemm(ip, op, e, len, 8);
       },
       [&](int set, int64_t off, int64_t len) {
         for_rows(n, [&](int i) {
@@ -274,6 +274,8 @@ StreamReport decode_file_stream(const std::string& file, const std::string& conf
                                 const GemmFn& gemm, const HostAlloc& alloc, const StreamOptions& opt) {
   StreamReport rep;
   const Metadata md = read_metadata(metadata_path(file));
+  if (md.w != 8)
+    throw std::runtime_error("the windowed codec handles GF(2^8) stripes; decode a GF(2^16) stripe without --window");
   const int k = md.k, n = md.k + md.p;
   rep.k = k;
   rep.p = md.p;
@@ -402,7 +404,7 @@ StreamReport decode_file_stream(const std::string& file, const std::string& conf
         std::vector<uint8_t*> op(ne);
         for (int j = 0; j < k; ++j) ip[j] = row(set, j);
         for (int e = 0; e < ne; ++e) op[e] = row(set, k + e);
-        gemm(ip, op, coeff, len);
+        gemm(ip, op, coeff, len, 8);
       },
       [&](int set, int64_t off, int64_t len) {
         int e = 0;

@@ -2,6 +2,7 @@
 #include "bind_common.h"
 #include "gfrs/cpu_codec.h"
 #include "gfrs/format.h"
+#include "gfrs/host_desc.h"
 
 PYBIND11_MODULE(_cpu, m) {
   using namespace gfrs;
@@ -34,25 +35,55 @@ PYBIND11_MODULE(_cpu, m) {
       py::arg("in_ptrs"), py::arg("out_ptrs"), py::arg("coeff"), py::arg("ncols"), py::arg("strategy") = "simd",
       py::arg("threads") = 1);
 
+  m.def(
+      "gemm16",
+      [](const std::vector<uint64_t>& in, const std::vector<uint64_t>& out, const std::vector<int>& coeff,
+         int64_t ncols, int threads) {
+        const gf16w::Mat c(coeff.begin(), coeff.end());
+        auto ip = ptrs<const uint8_t*>(in);
+        auto op = ptrs<uint8_t*>(out);
+        py::gil_scoped_release nogil;
+        cpu_gemm16(ip, op, c, ncols, threads);
+      },
+      py::arg("in_ptrs"), py::arg("out_ptrs"), py::arg("coeff"), py::arg("ncols"), py::arg("threads") = 1);
+  // GF(2^16) host linear algebra (gfrs/gf65536.h): the decode system of a w = 16 code
+  m.def("gf16_mul", [](int a, int b) { return int(gf16w::mul(uint16_t(a), uint16_t(b))); });
+  m.def("gf16_invert", [](const std::vector<int>& a, int n) {
+    gf16w::Mat out;
+    if (!gf16w::invert(gf16w::Mat(a.begin(), a.end()), n, out)) throw py::value_error("singular matrix");
+    return std::vector<int>(out.begin(), out.end());
+  });
+  m.def("gf16_perm_quad", [](int c) {
+    const auto q = gf16w::perm_quad(uint16_t(c));
+    std::vector<uint32_t> w;
+    for (const auto& t : q) w.insert(w.end(), t.w, t.w + kPermStride);
+    return w;
+  });
+
   auto gemm_fn = [](const std::string& strategy, int threads) -> GemmFn {
     const CpuMul s = parse_cpu_mul(strategy);
     return [s, threads](const std::vector<const uint8_t*>& in, const std::vector<uint8_t*>& out, const Mat& coeff,
-                        int64_t ncols) { cpu_gemm(in, out, coeff, ncols, s, threads); };
+                        int64_t ncols, int field_w) {
+      if (field_w == 16)
+        cpu_gemm16(in, out, unpack16(coeff), ncols, threads);
+      else
+        cpu_gemm(in, out, coeff, ncols, s, threads);
+    };
   };
   m.def(
       "encode_file",
       [gemm_fn](const std::string& file, int k, int p, const std::string& matrix, bool cpu_meta,
-                const std::string& strategy, int threads) {
+                const std::string& strategy, int threads, int field_w) {
         const GemmFn g = gemm_fn(strategy, threads);
         FileReport r;
         {
           py::gil_scoped_release nogil;
-          r = encode_file(file, k, p, parse_matrix_kind(matrix), g, default_host_alloc(), cpu_meta);
+          r = encode_file(file, k, p, parse_matrix_kind(matrix), g, default_host_alloc(), cpu_meta, field_w);
         }
         return report(r);
       },
       py::arg("file"), py::arg("k"), py::arg("p"), py::arg("matrix") = "vandermonde", py::arg("cpu_meta") = false,
-      py::arg("strategy") = "simd", py::arg("threads") = 1);
+      py::arg("strategy") = "simd", py::arg("threads") = 1, py::arg("field_w") = 8);
   m.def(
       "decode_file",
       [gemm_fn](const std::string& file, const std::string& conf, const std::string& out, const std::string& strategy,
@@ -115,7 +146,8 @@ PYBIND11_MODULE(_cpu, m) {
     d["total_size"] = md.total_size;
     d["p"] = md.p;
     d["k"] = md.k;
-    d["g"] = from_mat(md.g);
+    d["w"] = md.w;
+    d["g"] = md.w == 16 ? py::object(py::cast(std::vector<int>(md.g16.begin(), md.g16.end()))) : py::object(from_mat(md.g));
     d["has_matrix"] = md.has_matrix;
     return d;
   });

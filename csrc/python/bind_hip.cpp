@@ -31,6 +31,7 @@ py::dict stats_dict(const gfrs::PipelineStats& s) {
   d["bytes_d2h"] = s.bytes_d2h;
   d["slices"] = s.slices;
   d["lanes"] = s.lanes;
+  d["zero_copy"] = s.zero_copy;
   return d;
 }
 
@@ -108,6 +109,15 @@ PYBIND11_MODULE(_hip, m) {
       },
       py::arg("a"), py::arg("a_inv"), py::arg("n"), py::arg("batch") = 1, py::arg("status") = 0, py::arg("desc") = 0,
       py::arg("sel_rows") = 0, py::arg("m") = 0, py::arg("m_pad") = 0, py::arg("stream") = 0);
+  m.def(
+      "gemm16",
+      [](uint64_t desc, int k, int m_pad, int64_t col0, int64_t ncols, bool symwise, int max_blocks, uint64_t stream) {
+        check(launch_gf_gemm16(reinterpret_cast<const void*>(desc), k, m_pad, col0, ncols, symwise, max_blocks,
+                               as_stream(stream)),
+              "gf_gemm16");
+      },
+      py::arg("desc"), py::arg("k"), py::arg("m_pad"), py::arg("col0"), py::arg("ncols"), py::arg("symwise") = false,
+      py::arg("max_blocks") = 0, py::arg("stream") = 0);
   m.def("gemm_lut", [](uint64_t desc, int k, int m_pad, int64_t col0, int64_t ncols, uint64_t stream) {
     check(launch_gf_gemm_lut(reinterpret_cast<const void*>(desc), k, m_pad, col0, ncols, as_stream(stream)),
           "gf_gemm_lut");
@@ -174,9 +184,10 @@ PYBIND11_MODULE(_hip, m) {
       "gemm_host",
       [](const std::vector<int>& devices, const std::vector<uint64_t>& in, const std::vector<uint64_t>& out,
          const py::bytes& coeff, int64_t ncols, int streams, int64_t slice, int max_blocks, bool bytewise,
-         int copy_streams, bool rect, int field_w) {
+         int copy_streams, bool rect, int field_w, bool zero_copy) {
         PipelineOptions opt;
         opt.field_w = field_w;
+        opt.zero_copy = zero_copy;
         opt.streams = streams;
         opt.slice_bytes = slice;
         opt.max_blocks = max_blocks;
@@ -203,21 +214,23 @@ PYBIND11_MODULE(_hip, m) {
       },
       py::arg("devices"), py::arg("in_ptrs"), py::arg("out_ptrs"), py::arg("coeff"), py::arg("ncols"),
       py::arg("streams") = 2, py::arg("slice") = 16 << 20, py::arg("max_blocks") = 0, py::arg("bytewise") = false,
-      py::arg("copy_streams") = 1, py::arg("rect") = true, py::arg("field_w") = 8);
+      py::arg("copy_streams") = 1, py::arg("rect") = true, py::arg("field_w") = 8, py::arg("zero_copy") = false);
 
   // `prep` (optional): setup started before the file reads; waited for on the first call
   m.def(
       "prepare_pipeline",
-      [](const std::vector<int>& devices, int k, int mm, int64_t ncols, int streams, int64_t slice) {
+      [](const std::vector<int>& devices, int k, int mm, int64_t ncols, int streams, int64_t slice, bool zero_copy) {
         hipError_t e;
+        PipelineOptions opt = pipeline_options(streams, slice, 0);
+        opt.zero_copy = zero_copy;
         {
           py::gil_scoped_release nogil;
-          e = prepare_pipeline_multi(devices, k, mm, ncols, pipeline_options(streams, slice, 0));
+          e = prepare_pipeline_multi(devices, k, mm, ncols, opt);
         }
         check(e, "prepare_pipeline");
       },
       py::arg("devices"), py::arg("k"), py::arg("m"), py::arg("ncols"), py::arg("streams") = 2,
-      py::arg("slice") = 16 << 20);
+      py::arg("slice") = 16 << 20, py::arg("zero_copy") = false);
   // pinned host memory with explicit hipHostMalloc flags (pipeline experiments: cold vs warm DMA)
   m.def("host_alloc", [](int64_t bytes, unsigned flags) {
     void* p = nullptr;
@@ -230,32 +243,34 @@ PYBIND11_MODULE(_hip, m) {
   auto gpu_gemm = [](const std::vector<int>& devices, int streams, int64_t slice, int max_blocks,
                      std::unique_ptr<AsyncPrepare>* prep = nullptr) -> GemmFn {
     return [=](const std::vector<const uint8_t*>& in, const std::vector<uint8_t*>& out, const Mat& coeff,
-               int64_t ncols) {
+               int64_t ncols, int field_w) {
       if (prep && *prep) {
         (*prep)->wait();
         prep->reset();
       }
-      check(gemm_host_multi(devices, in, out, coeff, ncols, pipeline_options(streams, slice, max_blocks), nullptr,
-                            nullptr),
-            "GPU pipeline");
+      PipelineOptions opt = pipeline_options(streams, slice, max_blocks);
+      opt.field_w = field_w;
+      check(gemm_host_multi(devices, in, out, coeff, ncols, opt, nullptr, nullptr), "GPU pipeline");
     };
   };
   m.def(
       "encode_file",
       [gpu_gemm](const std::string& file, int k, int p, const std::string& matrix, bool cpu_meta,
-                 const std::vector<int>& devices, int streams, int64_t slice, int max_blocks) {
+                 const std::vector<int>& devices, int streams, int64_t slice, int max_blocks, int field_w) {
         FileReport r;
         {
           py::gil_scoped_release nogil;
-          auto prep = prepare_for_encode(devices, pipeline_options(streams, slice, max_blocks), file, k, p);
+          PipelineOptions popt = pipeline_options(streams, slice, max_blocks);
+          popt.field_w = field_w;
+          auto prep = prepare_for_encode(devices, popt, file, k, p);
           r = encode_file(file, k, p, parse_matrix_kind(matrix), gpu_gemm(devices, streams, slice, max_blocks, &prep),
-                          pinned_alloc(), cpu_meta);
+                          pinned_alloc(), cpu_meta, field_w);
         }
         return report(r);
       },
       py::arg("file"), py::arg("k"), py::arg("p"), py::arg("matrix") = "vandermonde", py::arg("cpu_meta") = false,
       py::arg("devices") = std::vector<int>{0}, py::arg("streams") = 2, py::arg("slice") = 16 << 20,
-      py::arg("max_blocks") = 0);
+      py::arg("max_blocks") = 0, py::arg("field_w") = 8);
   m.def(
       "decode_file",
       [gpu_gemm](const std::string& file, const std::string& conf, const std::string& out,

@@ -57,6 +57,11 @@ struct Lane {
 struct Workspace {
   std::mutex mu;
   std::vector<Lane> lane;
+  // zero-copy path: one stream and one descriptor (pointing at mapped host rows)
+  hipStream_t zc_stream = nullptr;
+  void* zc_desc = nullptr;
+  size_t zc_cap = 0;
+  std::vector<uint8_t> zc_host;
 };
 
 std::mutex g_ws_mu;
@@ -229,6 +234,35 @@ hipError_t launch_slice(const void* desc, int k, int m, int64_t w, const Pipelin
   return launch_gf_gemm(desc, k, pad_m(m), 0, w, opt.bytewise, opt.max_blocks, s, /*copies=*/false);
 }
 
+// Device-visible address of a pinned host pointer (hipHostRegister'ed or hipHostMalloc'ed): 0 when
+// `p` is not host memory mapped for the current device.
+uint64_t mapped_addr(const void* p) {
+  hipPointerAttribute_t at{};
+  if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  if (at.type != hipMemoryTypeHost || !at.devicePointer) return 0;
+  return reinterpret_cast<uint64_t>(at.devicePointer);
+}
+
+// Device addresses of every row, or empty when one is unmapped or not 16-byte aligned (the
+// zero-copy kernel streams 16-byte groups; a byte-wise pass over PCIe would be slower than staging).
+template <class Ptr>
+std::vector<uint64_t> map_rows(const std::vector<Ptr>& rows) {
+  std::vector<uint64_t> a(rows.size());
+  for (size_t i = 0; i < rows.size(); ++i) {
+    a[i] = mapped_addr(rows[i]);
+    if (!a[i] || a[i] % 16) return {};
+  }
+  return a;
+}
+
+hipError_t zc_stream(Workspace& ws) {
+  if (!ws.zc_stream) GFRS_TRY(hipStreamCreateWithFlags(&ws.zc_stream, hipStreamNonBlocking));
+  return hipSuccess;
+}
+
 }  // namespace
 
 hipError_t release_workspaces() {
@@ -238,9 +272,57 @@ hipError_t release_workspaces() {
     GFRS_TRY(hipSetDevice(dev));
     for (auto& L : ws->lane) GFRS_TRY(free_lane(L));
     ws->lane.clear();
+    if (ws->zc_stream) GFRS_TRY(hipStreamSynchronize(ws->zc_stream));
+    if (ws->zc_desc) GFRS_TRY(hipFree(ws->zc_desc));
+    if (ws->zc_stream) GFRS_TRY(hipStreamDestroy(ws->zc_stream));
+    ws->zc_stream = nullptr;
+    ws->zc_desc = nullptr;
+    ws->zc_cap = 0;
+    ws->zc_host.clear();
   }
   return hipSuccess;
 }
+
+namespace {
+
+// The zero-copy GEMM over columns [c0, c1) of mapped host rows: one launch on the workspace's
+// stream, waited for. Returns hipErrorInvalidValue (nothing launched) when a row is not mapped.
+hipError_t gemm_zero_copy(Workspace& ws, const std::vector<const uint8_t*>& in_rows,
+                          const std::vector<uint8_t*>& out_rows, const Mat& coeff, int64_t c0, int64_t c1,
+                          const PipelineOptions& opt, PipelineStats& st) {
+  const int k = int(in_rows.size()), m = int(out_rows.size());
+  const auto t0 = Clock::now();
+  const std::vector<uint64_t> ip = map_rows(in_rows), op = map_rows(out_rows);
+  if (ip.empty() || op.empty()) return hipErrorInvalidValue;
+  std::vector<uint8_t> d = build_desc(k, m, ip, {}, op, coeff, opt.field_w);
+  GFRS_TRY(zc_stream(ws));
+  if (d != ws.zc_host) {
+    GFRS_TRY(ensure(&ws.zc_desc, ws.zc_cap, d.size()));
+    GFRS_TRY(hipMemcpy(ws.zc_desc, d.data(), d.size(), hipMemcpyHostToDevice));
+    ws.zc_host = std::move(d);
+  }
+  st.ms_setup = ms_since(t0);
+  const auto t1 = Clock::now();
+  {
+    TraceRange tr("pipeline/zero-copy");
+    const hipError_t e = opt.field_w == 16
+                             ? launch_gf_gemm16(ws.zc_desc, k, pad_m(m), c0, c1 - c0, false, opt.max_blocks, ws.zc_stream)
+                             : launch_gf_gemm(ws.zc_desc, k, pad_m(m), c0, c1 - c0, opt.bytewise, opt.max_blocks,
+                                              ws.zc_stream, /*copies=*/false);
+    const hipError_t e2 = hipStreamSynchronize(ws.zc_stream);
+    GFRS_TRY(e);
+    GFRS_TRY(e2);
+  }
+  st.ms_stream = ms_since(t1);
+  st.zero_copy = true;
+  st.bytes_h2d = int64_t(k) * (c1 - c0);
+  st.bytes_d2h = int64_t(m) * (c1 - c0);
+  st.slices = 1;
+  st.lanes = 0;
+  return hipSuccess;
+}
+
+}  // namespace
 
 hipError_t prepare_pipeline(int device, int k, int m, int64_t ncols, const PipelineOptions& opt,
                             PrepareStats* stats) {
@@ -259,6 +341,35 @@ hipError_t prepare_pipeline(int device, int k, int m, int64_t ncols, const Pipel
   Workspace& ws = workspace(device);
   std::lock_guard<std::mutex> guard(ws.mu);
   TraceRange tr("pipeline/prepare");
+  if (opt.zero_copy) {
+    // the zero-copy run needs only its stream and the kernel's code object: load it with one
+    // launch over a small device scratch row set (no slice buffers, no copy engines)
+    t = Clock::now();
+    GFRS_TRY(zc_stream(ws));
+    ps.ms_lanes = ms_since(t);
+    t = Clock::now();
+    constexpr int64_t kCols = 4096;
+    uint8_t* scratch = nullptr;
+    GFRS_TRY(hipMalloc(reinterpret_cast<void**>(&scratch), size_t(k + m) * kCols));
+    std::vector<uint64_t> ip(k), op(m);
+    for (int j = 0; j < k; ++j) ip[j] = reinterpret_cast<uint64_t>(scratch + size_t(j) * kCols);
+    for (int i = 0; i < m; ++i) op[i] = reinterpret_cast<uint64_t>(scratch + size_t(k + i) * kCols);
+    const std::vector<uint8_t> d = build_desc(k, m, ip, {}, op, Mat(coeff_bytes(m, k, opt.field_w), 0), opt.field_w);
+    void* dd = nullptr;
+    hipError_t err = hipMalloc(&dd, d.size());
+    if (err == hipSuccess) err = hipMemsetAsync(scratch, 0, size_t(k + m) * kCols, ws.zc_stream);
+    if (err == hipSuccess) err = hipMemcpyAsync(dd, d.data(), d.size(), hipMemcpyHostToDevice, ws.zc_stream);
+    if (err == hipSuccess)
+      err = opt.field_w == 16 ? launch_gf_gemm16(dd, k, pad_m(m), 0, kCols, false, 0, ws.zc_stream)
+                              : launch_gf_gemm(dd, k, pad_m(m), 0, kCols, false, 0, ws.zc_stream, /*copies=*/false);
+    const hipError_t e2 = hipStreamSynchronize(ws.zc_stream);
+    (void)hipFree(dd);
+    (void)hipFree(scratch);
+    ps.ms_kernel = ms_since(t);
+    ps.ms_total = ms_since(t_all);
+    if (stats) *stats = ps;
+    return err != hipSuccess ? err : e2;
+  }
   t = Clock::now();
   {
     TraceRange tl("pipeline/prepare/lanes");
@@ -349,6 +460,16 @@ hipError_t gemm_host(int device, const std::vector<const uint8_t*>& in_rows, con
 
   Workspace& ws = workspace(device);
   std::lock_guard<std::mutex> guard(ws.mu);
+  if (opt.zero_copy) {
+    const hipError_t e = gemm_zero_copy(ws, in_rows, out_rows, coeff, c0, c1, opt, st);
+    if (e == hipSuccess) {
+      st.ms_total = ms_since(t_all);
+      if (stats) *stats = st;
+      return hipSuccess;
+    }
+    if (e != hipErrorInvalidValue) return e;
+    st = PipelineStats{};  // a row is not mapped / aligned: the staged pipeline below
+  }
   {
     TraceRange tr("pipeline/setup");
     const hipError_t e = setup_lanes(ws, lanes, k, m, slice, coeff, opt.copy_streams > 0, opt.field_w);

@@ -228,3 +228,46 @@ def perm_apply(words: np.ndarray, x: np.ndarray) -> np.ndarray:
     t2 = np.frombuffer(b[16:20], dtype=np.uint8)
     x = np.asarray(x, dtype=np.uint8)
     return t0[x & 7] ^ t1[(x >> 3) & 7] ^ t2[x >> 6]
+
+
+# ---- GF(2^16) as four byte maps (what the gfx950 w = 16 kernel applies) --------------------------
+def perm_quads16(coeff: np.ndarray) -> np.ndarray:
+    """(m, k) GF(2^16) coefficients -> (m, k, 4, 8) uint32 v_perm records, the four byte maps of
+    each multiply in the order q = 2 * src_byte + dst_byte (``csrc/include/gfrs/gf65536.h``
+    perm_quad): c * (l | h << 8) = [L_ll(l) ^ L_hl(h)] | [L_lh(l) ^ L_hh(h)] << 8. Vectorised over
+    all coefficients."""
+    f = field(16)
+    c = np.asarray(coeff, dtype=np.int64)
+    m, k = c.shape
+    imgs = f.mul(c.reshape(-1, 1), (1 << np.arange(16)).reshape(1, -1))  # (m*k, 16) images of the bits
+    out = np.zeros((m * k, 4, 8), dtype=np.uint32)
+
+    def table(basis: np.ndarray, nbits: int) -> np.ndarray:  # (N, nbits) -> (N, 2**nbits) XOR combos
+        t = np.zeros((basis.shape[0], 1 << nbits), dtype=np.int64)
+        for v in range(1, 1 << nbits):
+            for b in range(nbits):
+                if v >> b & 1:
+                    t[:, v] ^= basis[:, b]
+        return t
+
+    def pack(t: np.ndarray) -> np.ndarray:  # (N, 4) bytes -> (N,) little-endian words
+        return (t[:, 0] | (t[:, 1] << 8) | (t[:, 2] << 16) | (t[:, 3] << 24)).astype(np.uint32)
+
+    for src in range(2):
+        for dst in range(2):
+            basis = (imgs[:, 8 * src: 8 * src + 8] >> (8 * dst)) & 0xFF  # (N, 8) byte images
+            t0, t1, t2 = table(basis[:, 0:3], 3), table(basis[:, 3:6], 3), table(basis[:, 6:8], 2)
+            q = 2 * src + dst
+            out[:, q, 0], out[:, q, 1] = pack(t0[:, 0:4]), pack(t0[:, 4:8])
+            out[:, q, 2], out[:, q, 3] = pack(t1[:, 0:4]), pack(t1[:, 4:8])
+            out[:, q, 4] = pack(t2)
+    return out.reshape(m, k, 4, 8)
+
+
+def quad_apply16(quad: np.ndarray, x: np.ndarray) -> np.ndarray:
+    """Host emulation of the device lookup of one GF(2^16) coefficient on uint16 symbols (tests)."""
+    x = np.asarray(x, dtype=np.uint16)
+    lo, hi = (x & 0xFF).astype(np.uint8), (x >> 8).astype(np.uint8)
+    ol = perm_apply(quad[0], lo) ^ perm_apply(quad[2], hi)
+    oh = perm_apply(quad[1], lo) ^ perm_apply(quad[3], hi)
+    return (ol.astype(np.uint16) | (oh.astype(np.uint16) << 8)).astype(np.uint16)

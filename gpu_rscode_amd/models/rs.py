@@ -20,7 +20,7 @@ import torch
 
 from .. import gf
 from .._native import cpu
-from ..ops.gemm import GemmPlan, _rows
+from ..ops.gemm import Gemm16Plan, GemmPlan, _rows
 from ..ops.inverse import decode_system_into_plan
 from ..ops.matrix import decode_matrix, encoding_matrix
 
@@ -74,8 +74,10 @@ class ReedSolomon:
         k: native (data) chunks. n: total chunks (k + parity).
         matrix: ``"vandermonde"`` (reference, not MDS — SURVEY §2.2), ``"cauchy"`` or
             ``"sys_vandermonde"`` (both MDS).
-        field: ``"gf256"`` (bytes are GF(2^8) symbols) or ``"gf16"`` (the design doc's GF(16)
-            method: each byte is two GF(2^4) symbols; needs n <= 16).
+        field: ``"gf256"`` (bytes are GF(2^8) symbols), ``"gf16"`` (the design doc's GF(16)
+            method: each byte is two GF(2^4) symbols; needs n <= 16) or ``"gf65536"`` (GF(2^16),
+            poly 0x1100B, ``src/galoisfield.cu:22-32``: rows hold little-endian 16-bit symbols, so
+            row lengths are even byte counts; n <= 65535).
         cpu_strategy / cpu_threads: multiply strategy and threads of the C++ CPU path.
     """
 
@@ -96,16 +98,51 @@ class ReedSolomon:
                 raise ValueError("GF(16) codes need n <= 16")
             self.gf = gf.field(4)
             self.E = self.gf.encoding_matrix(matrix, k, self.p).astype(np.uint8)
+        elif field == "gf65536":
+            if n > 65535:
+                raise ValueError("GF(2^16) codes need n <= 65535")
+            self.gf = gf.field(16)
+            self.E = self._e16(matrix, k, self.p)
         else:
             raise ValueError(f"unknown field {field!r}")
-        self.G = np.vstack([np.eye(k, dtype=np.uint8), self.E]).astype(np.uint8)
+        dt = np.uint16 if field == "gf65536" else np.uint8
+        self.G = np.vstack([np.eye(k, dtype=dt), self.E]).astype(dt)
         self._plans = _PlanCache()
         self._dm: dict = {}
         self._g_dev: dict = {}  # (device, id(G)) -> G on device, for the on-device decode system
 
     # ---- helpers -----------------------------------------------------------------------------
+    @property
+    def wide(self) -> bool:
+        """GF(2^16) symbols (two bytes each)."""
+        return self.field == "gf65536"
+
+    def _e16(self, matrix: str, k: int, p: int) -> np.ndarray:
+        f = self.gf
+        if matrix in ("vandermonde", "vand", "ref"):  # E[i][j] = (j+1)^i, as the C++ gf16w::vandermonde_ref
+            return np.array([[f.pow(j + 1, i) for j in range(k)] for i in range(p)], dtype=np.uint16).reshape(p, k)
+        if matrix == "cauchy":
+            x = np.arange(k, k + p)[:, None] ^ np.arange(k)[None, :]
+            return f.inv(x).astype(np.uint16)
+        if matrix in ("sys_vandermonde", "sysvand"):
+            n = k + p
+            v = np.array([[f.pow(r, j) for j in range(k)] for r in range(n)], dtype=np.int64)
+            top = self._invert16(v[:k])
+            return f.matmul(v[k:], top).astype(np.uint16)
+        raise ValueError(f"unknown matrix kind {matrix!r}")
+
+    @staticmethod
+    def _invert16(a: np.ndarray) -> np.ndarray:
+        """GF(2^16) inverse through the C++ host Gauss-Jordan (gfrs/gf65536.h)."""
+        n = a.shape[0]
+        try:
+            inv = cpu().gf16_invert([int(v) for v in np.asarray(a).reshape(-1)], n)
+        except ValueError as e:
+            raise UnrecoverableError(str(e)) from None
+        return np.asarray(inv, dtype=np.uint16).reshape(n, n)
+
     def _maps(self, coeff: np.ndarray) -> np.ndarray | None:
-        if self.field == "gf256":
+        if self.field in ("gf256", "gf65536"):
             return None
         m, k = coeff.shape
         return np.stack([np.stack([gf.byte_map_gf16_nibbles(int(coeff[i, j])) for j in range(k)]) for i in range(m)])
@@ -113,9 +150,12 @@ class ReedSolomon:
     def _plan(self, key, inputs, outputs, coeff, copies=None) -> GemmPlan:
         plan = self._plans.get(key)
         if plan is None:
-            maps = self._maps(coeff)
-            plan = GemmPlan(inputs, outputs, None if maps is not None else coeff, maps=maps, copies=copies,
-                            hold_buffers=False)
+            if self.wide:
+                plan = Gemm16Plan(inputs, outputs, coeff, copies=copies, hold_buffers=False)
+            else:
+                maps = self._maps(coeff)
+                plan = GemmPlan(inputs, outputs, None if maps is not None else coeff, maps=maps, copies=copies,
+                                hold_buffers=False)
             self._plans[key] = plan
         return plan
 
@@ -126,7 +166,12 @@ class ReedSolomon:
 
     def _cpu_gemm(self, coeff: np.ndarray, ins: list[torch.Tensor], outs: list[torch.Tensor]) -> None:
         ncols = min(r.numel() for r in ins + outs)
-        if self.field == "gf256":
+        if self.wide:
+            if ncols % 2:
+                raise ValueError("GF(2^16) rows hold 16-bit symbols: the column range must be an even byte count")
+            cpu().gemm16([int(r.data_ptr()) for r in ins], [int(r.data_ptr()) for r in outs],
+                         [int(v) for v in np.asarray(coeff).reshape(-1)], ncols, self.cpu_threads)
+        elif self.field == "gf256":
             cpu().gemm([int(r.data_ptr()) for r in ins], [int(r.data_ptr()) for r in outs],
                        np.ascontiguousarray(coeff, dtype=np.uint8).tobytes(), ncols, self.cpu_strategy,
                        self.cpu_threads)
@@ -177,6 +222,8 @@ class ReedSolomon:
         batched descriptor (grid.y = stripe) amortises it (serving path)."""
         if data.dim() != 3 or data.shape[1] != self.k:
             raise ValueError(f"expected [B, {self.k}, C]")
+        if self.wide:
+            raise ValueError("batched launches run GF(2^8) / GF(16) codes; encode GF(2^16) stripes one at a time")
         B, _, C = data.shape
         if parity is None:
             pitch = max(PITCH, (C + PITCH - 1) // PITCH * PITCH)
@@ -204,6 +251,8 @@ class ReedSolomon:
         surviving natives are copied in the same pass (batched fused copy) and the plan is cached
         per (buffers, pattern), so a repeated call is one kernel launch."""
         rows = [int(r) for r in rows]
+        if self.wide:
+            raise ValueError("batched launches run GF(2^8) / GF(16) codes; decode GF(2^16) stripes one at a time")
         B, k, C = survivors.shape
         if k != self.k:
             raise ValueError(f"expected [B, {self.k}, C]")
@@ -247,6 +296,8 @@ class ReedSolomon:
             try:
                 if self.field == "gf256":
                     dm = decode_matrix(self.G, rows)
+                elif self.wide:
+                    dm = self._invert16(self.G[list(rows)])
                 else:
                     dm = self.gf.decode_matrix(self.G, rows).astype(np.uint8)
             except gf.SingularMatrixError as e:
@@ -348,7 +399,7 @@ class ReedSolomon:
         if not erased:
             return stripe
         dm = self.decode_matrix(survivors)
-        coeff = self.gf.matmul(self.G[erased], dm).astype(np.uint8)
+        coeff = self.gf.matmul(self.G[erased], dm).astype(self.G.dtype)
         ins = [rows_all[s] for s in survivors]
         outs = [rows_all[e] for e in erased]
         if ins[0].device.type == "cuda":

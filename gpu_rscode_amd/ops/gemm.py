@@ -374,6 +374,100 @@ def _auto_engine(k: int, m: int, gf256: bool, bytewise: bool, batch: int) -> str
     return "valu"
 
 
+def _pack16(coeff) -> bytes:
+    """GF(2^16) coefficients as the native pipeline's packed form: little-endian byte pairs
+    (``gfrs::pack16``, ``csrc/include/gfrs/host_desc.h``)."""
+    return np.ascontiguousarray(np.asarray(coeff, dtype=np.int64).astype("<u2")).tobytes()
+
+
+def desc_layout16(k: int, m_pad: int) -> DescLayout:
+    """Mirror of ``gfrs::desc_layout16``: four 32-byte records per coefficient."""
+    lay = desc_layout(k, m_pad)
+    return DescLayout(lay.in_off, lay.copy_off, lay.out_off, lay.tab_off, lay.tab_off + 4 * 32 * k * m_pad)
+
+
+class Gemm16Plan:
+    """A reusable device GF(2^16) GEMM (``csrc/kernels/gf_gemm16.hip``): ``out[i] = XOR_j c[i][j] * in[j]``
+    over little-endian 16-bit symbols in uint8 byte rows.
+
+    The reference's field family names w = 16 (``src/galoisfield.cu:22-32``, poly 0x1100B) but only
+    GF(2^8) was ever built; here it runs on the same v_perm engine as four byte maps per coefficient.
+
+    Args:
+        inputs: k byte rows (2-D uint8 tensor or list of 1-D tensors) on one GPU, 2-byte aligned.
+        outputs: m byte rows on the same GPU.
+        coeff: (m, k) GF(2^16) coefficients (uint16-valued).
+        copies: optional k destination rows (or None entries): fused survivor copy of decode.
+        hold_buffers: as :class:`GemmPlan`.
+    Rows shorter than the others bound the column range, which must be a whole number of symbols.
+    """
+
+    def __init__(self, inputs, outputs, coeff, *, copies=None, hold_buffers: bool = True):
+        self.inputs, self.outputs = _rows(inputs), _rows(outputs)
+        self.copies = None if copies is None else list(copies)
+        dev = _check_rows(self.inputs, "input", None)
+        dev = _check_rows(self.outputs, "output", dev)
+        if self.copies is not None:
+            if len(self.copies) != len(self.inputs):
+                raise ValueError("copies must have one entry per input row")
+            dev = _check_rows([c for c in self.copies if c is not None], "copy", dev)
+        if dev.type != "cuda":
+            raise ValueError("Gemm16Plan runs on a GPU; use the CPU codec for host tensors")
+        self.device = dev
+        self.k, self.m = len(self.inputs), len(self.outputs)
+        if not (1 <= self.k <= 65535 and 1 <= self.m <= 65535):
+            raise ValueError("GF(2^16) GEMM supports 1 <= k, m <= 65535")
+        self.m_pad = pad_m(self.m)
+        rows = self.inputs + self.outputs + [c for c in (self.copies or []) if c is not None]
+        self.ncols = min(r.numel() for r in rows)
+        if self.ncols % 2:
+            raise ValueError("GF(2^16) rows hold 16-bit symbols: the column range must be an even byte count")
+        ptr = lambda t: int(t.data_ptr())  # noqa: E731
+        if any(ptr(r) % 2 for r in rows):
+            raise ValueError("GF(2^16) rows must be 2-byte aligned")
+        self.symwise = any(ptr(r) % 16 for r in rows)
+        coeff = np.asarray(coeff, dtype=np.int64).reshape(self.m, self.k)
+        if coeff.min() < 0 or coeff.max() > 65535:
+            raise ValueError("GF(2^16) coefficients must be in [0, 65535]")
+        self.layout = desc_layout16(self.k, self.m_pad)
+        lay = self.layout
+        host = np.zeros(lay.bytes, dtype=np.uint8)
+        host[0:16] = np.frombuffer(np.array([self.k, self.m, self.m_pad, 1], dtype="<i4").tobytes(), dtype=np.uint8)
+
+        def put(off, vals):
+            b = np.frombuffer(np.array(vals, dtype="<u8").tobytes(), dtype=np.uint8)
+            host[off: off + b.size] = b
+        put(lay.in_off, [ptr(r) for r in self.inputs])
+        if self.copies is not None:
+            put(lay.copy_off, [ptr(c) if c is not None else 0 for c in self.copies])
+        put(lay.out_off, [ptr(r) for r in self.outputs] + [0] * (self.m_pad - self.m))
+        t = np.zeros((self.k, self.m_pad, 4, 8), dtype="<u4")
+        t[:, : self.m] = np.transpose(gf.perm_quads16(coeff), (1, 0, 2, 3))
+        host[self.layout.tab_off:] = np.frombuffer(t.tobytes(), dtype=np.uint8)
+        self.desc = torch.from_numpy(host).to(self.device)
+        self.engine = "valu16"
+        if not hold_buffers:
+            self.inputs = self.outputs = self.copies = None
+        self._ready = torch.cuda.Event()
+        self._ready.record(torch.cuda.current_stream(self.device))
+
+    def run(self, stream: torch.cuda.Stream | None = None, col0: int = 0, ncols: int | None = None,
+            max_blocks: int = 0) -> None:
+        """Launch asynchronously on ``stream`` (default: the current stream); byte columns
+        ``[col0, col0 + ncols)``, both even."""
+        ncols = self.ncols - col0 if ncols is None else ncols
+        if col0 < 0 or ncols < 0 or col0 + ncols > self.ncols or (col0 | ncols) & 1:
+            raise ValueError(f"column range [{col0}, {col0 + ncols}) must be whole symbols inside {self.ncols} bytes")
+        st = stream or torch.cuda.current_stream(self.device)
+        if self._ready is not None:
+            st.wait_event(self._ready)
+            self._ready = None
+        if stream is not None:
+            self.desc.record_stream(stream)
+        hip().gemm16(int(self.desc.data_ptr()), self.k, self.m_pad, col0, ncols, self.symwise, max_blocks,
+                     st.cuda_stream)
+
+
 class _null:
     def __enter__(self):
         return None

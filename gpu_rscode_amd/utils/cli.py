@@ -36,6 +36,8 @@ def _parser() -> argparse.ArgumentParser:
     ap.add_argument("--backend", choices=["gpu", "cpu"], default=None)
     ap.add_argument("--matrix", default="vandermonde", choices=["vandermonde", "cauchy", "sys_vandermonde"])
     ap.add_argument("--cpu-meta", action="store_true", help="write the 2-line CPU-format METADATA")
+    ap.add_argument("-w", "-W", "--field-width", type=int, choices=[8, 16], default=8, dest="field_w",
+                    help="encode: symbol width, GF(2^8) or GF(2^16) (n <= 65535; decode reads it from METADATA)")
     ap.add_argument("--gpus", type=int, default=0, help="GPUs for the single-process pipeline (0 = all)")
     ap.add_argument("--slice", type=int, default=16 << 20)
     ap.add_argument("--threads", type=int, default=1, help="CPU backend threads")
@@ -62,6 +64,9 @@ def main(argv=None) -> int:
         _parser().print_help()
         return 2
     if a.dist:
+        if a.field_w != 8:
+            print("--dist runs GF(2^8) stripes; encode GF(2^16) in single-process mode", file=sys.stderr)
+            return 2
         return _main_dist(a)
     from .._native import cpu, gpu_available, hip
 
@@ -70,16 +75,20 @@ def main(argv=None) -> int:
         if not a.k or not a.n or a.n < a.k:
             print("encode needs -k K -n N -e FILE with 1 <= K <= N", file=sys.stderr)
             return 2
+        if a.field_w == 16 and (a.window is not None or a.cpu_meta):
+            print("-w 16 writes the versioned METADATA without --window / --cpu-meta", file=sys.stderr)
+            return 2
+        fw = {} if a.field_w == 8 else dict(field_w=a.field_w)
         t = time.perf_counter()
         st = {} if a.window is None else dict(window=a.window, resume=not a.no_resume, durable=not a.no_sync)
         if backend == "gpu":
             ndev = hip().device_count()
             devs = list(range(a.gpus or ndev))
             fn = hip().encode_file_stream if st else hip().encode_file
-            r = fn(a.encode_file, a.k, a.n - a.k, a.matrix, a.cpu_meta, devs, a.streams, a.slice, a.grid, **st)
+            r = fn(a.encode_file, a.k, a.n - a.k, a.matrix, a.cpu_meta, devs, a.streams, a.slice, a.grid, **st, **fw)
         else:
             fn = cpu().encode_file_stream if st else cpu().encode_file
-            r = fn(a.encode_file, a.k, a.n - a.k, a.matrix, a.cpu_meta, a.mul, a.threads, **st)
+            r = fn(a.encode_file, a.k, a.n - a.k, a.matrix, a.cpu_meta, a.mul, a.threads, **st, **fw)
         if st:
             _say(a, f"Streamed {r['windows']} window(s) of {r['window']} bytes per chunk "
                     f"(resumed at {r['resumed_from']})")
@@ -227,6 +236,8 @@ def _main_dist(a) -> int:
                 f"in {1e3 * (time.perf_counter() - t0):.1f}ms")
     else:
         md = ff.read_metadata(ff.metadata_path(a.in_file))
+        if md.w != 8:
+            raise SystemExit("--dist decodes GF(2^8) stripes; decode a GF(2^16) stripe in single-process mode")
         names = ff.read_conf(a.conf)[: md.k]
         rows = [ff.chunk_index(nm) for nm in names]
         k, C = md.k, ff.chunk_size(md.total_size, md.k)

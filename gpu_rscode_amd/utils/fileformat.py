@@ -6,7 +6,10 @@
   values (``src/encode.cu:61-101``); the CPU reference's 2-line form (``src/cpu-rs.c:465-476``) is
   accepted and G regenerated from the reference Vandermonde;
 * decode config: whitespace-separated chunk names, row index ``atoi(basename + 1)``
-  (``src/decode.cu:302-318``); ``worst_case_conf`` is ``src/unit-test.sh``.
+  (``src/decode.cu:302-318``); ``worst_case_conf`` is ``src/unit-test.sh``;
+* GF(2^16) stripes (extension; the reference's w = 16 field was never built): METADATA starts with
+  a version line ``GFRS-METADATA 2 16`` and carries 16-bit matrix values; chunk sizes are rounded up
+  to an even byte count (``csrc/include/gfrs/format.h``).
 
 The C++ implementation (``csrc/io/format.cpp``) is what the CLIs use; tests pin the two equal.
 """
@@ -38,8 +41,12 @@ def chunk_index(name: str) -> int:
     return int(m.group(1)) if m else -1
 
 
-def chunk_size(total: int, k: int) -> int:
-    return max(1, (total + k - 1) // k)
+METADATA_VERSION = 2  # the versioned (GF(2^16)) form; unversioned = the reference's
+
+
+def chunk_size(total: int, k: int, w: int = 8) -> int:
+    c = max(1, (total + k - 1) // k)
+    return (c + 1) // 2 * 2 if w == 16 else c
 
 
 @dataclass
@@ -50,6 +57,7 @@ class Metadata:
     g: np.ndarray  # (k+p) x k
     has_matrix: bool
     crc: list | None = None  # per-chunk CRC-32 (METADATA extension line "crc32 ...")
+    w: int = 8  # field width: 8 (reference format) or 16 (versioned format, uint16 g)
 
     @property
     def n(self) -> int:
@@ -61,8 +69,10 @@ class Metadata:
 
 
 def write_metadata(path: str, total_size: int, p: int, k: int, e: np.ndarray | None, with_matrix: bool = True,
-                   crc=None) -> None:
-    lines = [f"{total_size}\n", f"{p} {k}\n"]
+                   crc=None, w: int = 8) -> None:
+    if w == 16 and not with_matrix:
+        raise ValueError("the GF(2^16) METADATA always carries the matrix")
+    lines = ([f"GFRS-METADATA {METADATA_VERSION} 16\n"] if w == 16 else []) + [f"{total_size}\n", f"{p} {k}\n"]
     if with_matrix:
         for i in range(k):
             lines.append("".join("1 " if i == j else "0 " for j in range(k)) + "\n")
@@ -77,26 +87,32 @@ def write_metadata(path: str, total_size: int, p: int, k: int, e: np.ndarray | N
 def read_metadata(path: str) -> Metadata:
     with open(path) as f:
         toks = f.read().split()
+    w = 8
+    if toks and toks[0] == "GFRS-METADATA":
+        if len(toks) < 3 or toks[1] != str(METADATA_VERSION) or toks[2] != "16":
+            raise ValueError(f"unsupported metadata version/field in {path}")
+        w, toks = 16, toks[3:]
     if len(toks) < 3:
         raise ValueError(f"malformed metadata {path}")
     total, p, k = int(toks[0]), int(toks[1]), int(toks[2])
-    if k <= 0 or p < 0 or k + p > 256 or total < 0:
+    if k <= 0 or p < 0 or k + p > (65535 if w == 16 else 256) or total < 0:
         raise ValueError(f"metadata out of range in {path}")
     vals = toks[3:]
     need = (k + p) * k
-    if len(vals) == 0:
+    if len(vals) == 0 and w == 8:
         g = GF256.generator(GF256.vandermonde_ref(k, p))
         return Metadata(total, p, k, g, False)
     if len(vals) < need:
         raise ValueError(f"truncated metadata matrix in {path}")
     g = np.array([int(v) for v in vals[:need]], dtype=np.int64)
-    if g.min() < 0 or g.max() > 255:
+    if g.min() < 0 or g.max() > (1 << w) - 1:
         raise ValueError(f"metadata matrix entry out of range in {path}")
     crc = None
     rest = vals[need:]
     if rest and rest[0] == "crc32" and len(rest) >= 1 + k + p:
         crc = [int(h, 16) for h in rest[1 : 1 + k + p]]
-    return Metadata(total, p, k, g.astype(np.uint8).reshape(k + p, k), True, crc)
+    dt = np.uint16 if w == 16 else np.uint8
+    return Metadata(total, p, k, g.astype(dt).reshape(k + p, k), True, crc, w)
 
 
 def read_conf(path: str) -> list[str]:

@@ -486,3 +486,69 @@ def test_host_pipeline_gf16_nibble_method():
         for j in range(k):
             want[i] ^= maps[i, j][host[j].numpy()]
     assert np.array_equal(par.numpy(), want)
+
+
+def _pitched_pinned(rows, C, pitch=4096):
+    P = (C + pitch - 1) // pitch * pitch
+    base = torch.zeros(rows * P, dtype=torch.uint8).pin_memory()
+    return base.as_strided((rows, C), (P, 1))
+
+
+@pytest.mark.parametrize("field_w", [8, 16])
+def test_zero_copy_pipeline_matches_staged_and_oracle(field_w):
+    """zero_copy: the GEMM kernel reads the pinned host rows and writes the parity rows over PCIe
+    itself (no slice buffers, no copy engines). 4 KiB-pitched rows take it; a contiguous odd-C
+    buffer (unaligned rows) falls back to the staged pipeline, with the same bytes."""
+    from gpu_rscode_amd import gf
+    from gpu_rscode_amd.ops.gemm import _pack16
+
+    k, p = 10, 4
+    C = 3_000_018 if field_w == 16 else 3_000_017
+    rng = np.random.default_rng(field_w)
+    host = _pitched_pinned(k, C)
+    host.copy_(torch.from_numpy(rng.integers(0, 256, size=(k, C), dtype=np.uint8)))
+    h = hip()
+    if field_w == 16:
+        e = rng.integers(0, 65536, size=(p, k))
+        coeff = _pack16(e)
+        want = gf.field(16).gemm(e, host.numpy().copy().view("<u2")).view(np.uint8)
+    else:
+        e = GF256.vandermonde_ref(k, p)
+        coeff = e.tobytes()
+        want = GF256.gemm(e, host.numpy())
+    outs = {}
+    for zc in (True, False):
+        par = _pitched_pinned(p, C)
+        res = h.gemm_host([0], [host[j].data_ptr() for j in range(k)], [par[i].data_ptr() for i in range(p)],
+                          coeff, C, 2, 1 << 20, 0, False, field_w=field_w, zero_copy=zc)
+        assert res["devices"][0]["zero_copy"] is zc
+        outs[zc] = par.numpy().copy()
+    assert np.array_equal(outs[True], want) and np.array_equal(outs[False], want)
+    if field_w == 8:  # unaligned rows: staged fallback
+        flat = torch.from_numpy(rng.integers(0, 256, size=(k, C), dtype=np.uint8)).pin_memory()
+        par = torch.zeros((p, C), dtype=torch.uint8).pin_memory()
+        res = h.gemm_host([0], [flat[j].data_ptr() for j in range(k)], [par[i].data_ptr() for i in range(p)],
+                          coeff, C, 2, 1 << 20, 0, False, zero_copy=True)
+        assert res["devices"][0]["zero_copy"] is False
+        assert np.array_equal(par.numpy(), GF256.gemm(e, flat.numpy()))
+
+
+def test_rs_cli_zero_copy_roundtrip(tmp_path):
+    exe = str(binary("RS"))
+    payload = os.urandom(10_000_019)
+    (tmp_path / "f.bin").write_bytes(payload)
+    r = subprocess.run([exe, "-k", "10", "-n", "14", "-e", "f.bin", "--zero-copy"], cwd=tmp_path,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert "zero-copy kernel" in r.stdout
+    g = tmp_path / "g"
+    g.mkdir()
+    (g / "f.bin").write_bytes(payload)
+    cpu().encode_file(str(g / "f.bin"), 10, 4)
+    for i in range(14):
+        assert (tmp_path / f"_{i}_f.bin").read_bytes() == (g / f"_{i}_f.bin").read_bytes(), i
+    ff.write_conf(str(tmp_path / "conf"), ff.worst_case_conf("f.bin", 14, 10))
+    r = subprocess.run([exe, "-d", "-i", "f.bin", "-c", "conf", "-o", "o.bin", "--zero-copy"], cwd=tmp_path,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert (tmp_path / "o.bin").read_bytes() == payload
