@@ -135,7 +135,7 @@ def parse(argv=None):
     ap.add_argument("--no-compare", action="store_true", help="skip timing the other --comm / --scaling modes")
     ap.add_argument("--no-e2e", action="store_true", help="skip the pinned host->device->host timing")
     ap.add_argument("--e2e", action="store_true", help=argparse.SUPPRESS)  # (on by default)
-    # e2e -s 2 / 16 MiB: profiles/r02al (52.0 GB/s against 51.2 at -s 4 / 32 MiB)
+    # e2e -s 2 / 16 MiB: profiles/host_pipeline/r02al (52.0 GB/s against 51.2 at -s 4 / 32 MiB)
     ap.add_argument("--streams", type=int, default=2, help="e2e: HIP streams (-s) per GPU")
     ap.add_argument("--slice", type=int, default=16 << 20, help="e2e: column slice per stream step")
     ap.add_argument("--vec", type=int, default=None, help="kernel variant: 16-byte groups per lane (ablation)")
@@ -259,7 +259,7 @@ class GpuWorkload:
         # Look-ahead broadcast: step j's pattern is broadcast on its own stream while step j - ahead
         # is issued, into ring slot j % R; the solve of step j waits for that one broadcast only. An
         # RCCL kernel can sit queued behind a GEMM's workgroups for hundreds of microseconds (a small
-        # copy kernel on another queue waited 150-600 us in profiles/r03_rccl), and its peers hold
+        # copy kernel on another queue waited 150-600 us in profiles/multigpu/r03_rccl), and its peers hold
         # theirs until it starts, so in-line broadcasting would put that wait on the solve's path.
         self.ahead = max(0, a.bcast_ahead)
         self.ring = torch.empty((self.ahead + 2, k), dtype=torch.int32, device=dev)

@@ -1,6 +1,6 @@
 // Pinned host buffers for the file codecs without hipHostMalloc's cost.
 //
-// Measured on the MI355X box (scripts/pin_bench.cpp, profiles/r03_setup): pinning 1.4 GiB with
+// Measured on the MI355X box (scripts/pin_bench.cpp, profiles/host_pipeline/r03_setup): pinning 1.4 GiB with
 // hipHostMalloc takes ~360 ms (and hipHostFree ~230 ms) — 4 GB/s of page zeroing, pinning and IOMMU
 // mapping in 4 KiB pages, on the critical path of every bin/RS run before its first DMA. The same
 // bytes as anonymous memory backed by transparent huge pages (MADV_HUGEPAGE), first-touched by 8

@@ -38,7 +38,7 @@ using namespace permdev;  // Sel, mac_pair, DescView, map_block, ... (gfrs/perm_
 // next row's input as far as the compiler knows, so a plain load-use-store loop serialises every
 // load behind the previous store. One lane walking the whole tail that way cost ~20 us per launch
 // (k=10, 10-byte tail: 100 dependent HBM loads), the whole kernel time of a 1 MiB object
-// (scripts/tail_probe.py, profiles/r04_tail).
+// (scripts/tail_probe.py, profiles/headline/r04_tail).
 template <int MT>
 __device__ void tail_byte(const DescView& d, int k, int m_pad, int i0, bool do_copy, int64_t off) {
   constexpr int kB = 8;
@@ -212,7 +212,7 @@ __global__ __launch_bounds__(kBlock) void gf_gemm_vec_kernel(DescView d, int k, 
 // kernel's PF KiB, and each row is consumed as it lands (the compiler counts vmcnt exactly: the
 // loop is fully unrolled and every load unconditional). This is the access form that reaches the
 // pattern ceiling with no math at all (scripts/membench.hip: 252 us for 10 rows in and 4 out,
-// against 292 us for the PF = 2 vec kernel on the same box, profiles/r05_rows). Fused copies (tile
+// against 292 us for the PF = 2 vec kernel on the same box, profiles/headline/r05_rows). Fused copies (tile
 // 0 of a decode) are stored as their row lands.
 template <int MT, int K>
 __global__ __launch_bounds__(kBlock) void gf_gemm_rows_kernel(DescView d, int k_tail, int m_pad, int ntiles,
@@ -466,7 +466,7 @@ Cfg default_cfg(int mt) {
 }
 
 // Where the rows-in-flight kernel is the default (copy-free descriptors, uncapped grid): measured
-// on the encode shapes (scripts/kbench.py, profiles/r05_rows) it wins only at k = 10 with 4-row
+// on the encode shapes (scripts/kbench.py, profiles/headline/r05_rows) it wins only at k = 10 with 4-row
 // tiles (262.6 vs 278.5 us per GiB); at k = 4 and 16 and in the decode (fused copies) the vec kernel
 // is faster.
 bool rows_default(int k, int mt) { return k == 10 && mt == 4; }

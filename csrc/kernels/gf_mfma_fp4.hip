@@ -522,7 +522,7 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4_kernel(cptr<uint64_t> in, 
 // The kernel above idles its matrix pipe through every chunk epilogue: its 256 accumulators fill
 // the AGPRs, so a chunk cannot start before the 256 accumulator reads, 224 bit-field inserts and
 // 16 bias MFMAs of the previous one are done (65 % MFMA-pipe utilisation at k=128, p=32,
-// profiles/r02_pmc_fp4). Here the M-tiles run their K loops STAGGERED by one K-step each: at step
+// profiles/wide_stripe/r02_pmc_fp4). Here the M-tiles run their K loops STAGGERED by one K-step each: at step
 // j of a chunk, M-tile mt works on K-step (j - mt) mod NS (of the previous chunk while mt > j).
 // Tile j therefore finishes its chunk at step j-1 and is packed, stored and re-biased during step
 // j — one tile's epilogue per step over the first MG steps of every chunk, interleaved with the 14
@@ -1003,7 +1003,7 @@ hipError_t launch_copy_rows(cptr<uint64_t> in, cptr<uint64_t> copy, int k, int64
 
 // GFRS_FP4_COPY: fused (default) = copy inside the GEMM kernel; split = staggered GEMM, then the
 // side-stream copy; split_first = the copy launched first. Measured on k=128, 26 rebuilt rows +
-// 102 copies, 1 GiB (profiles/r02_split): fused 1019 us, split 1034, split_first 1081 (medians;
+// 102 copies, 1 GiB (profiles/wide_stripe/r02_split): fused 1019 us, split 1034, split_first 1081 (medians;
 // the plain GEMM alone 762, the copy alone 334) — the co-running copy costs the GEMM more than it
 // saves: re-reading the survivors adds 0.8 GB of HBM traffic, the chip holds a lower clock, and
 // the copy waves take issue slots on the GEMM's SIMDs. Kept as the measured alternative.
@@ -1141,7 +1141,7 @@ hipError_t launch_fp4_ring(const Fp4Geometry& geo, const Fp4Args& a, hipStream_t
 template <int MG, bool UNI, bool COPY>
 hipError_t launch_fp4_var(const Fp4Geometry& geo, const Fp4Args& a, hipStream_t stream) {
   // (fused-copy form: ring 4 only — the depth-8 form ran 0-6 % slower at m = 8..16,
-  // profiles/r02_exact_mg/session_k_*)
+  // profiles/wide_stripe/r02_exact_mg/session_k_*)
   if (geo.ksteps == 16)
     return COPY ? launch_fp4_ring<MG, UNI, COPY, 8, 4>(geo, a, stream) : launch_fp4_ring<MG, UNI, COPY, 8, 8, 4>(geo, a, stream);
   return launch_fp4_ring<MG, UNI, COPY, 0, 32, 16, 12, 8, 6, 4>(geo, a, stream);
@@ -1157,7 +1157,7 @@ hipError_t launch_fp4_any(const Fp4Geometry& geo, const Fp4Args& a, hipStream_t 
 
 // MG = 3, 5..7 exist for the static 8-slot chunk only (geometry() picks them there), ring depth 4:
 // the depth-8 forms fit the LDS but need ~90 more VGPRs (256 with spills into AGPRs) and ran
-// 0-19 % slower at every shape (profiles/r02_exact_mg: k=128, m=28 + 100 copies 885 vs 1050 us)
+// 0-19 % slower at every shape (profiles/wide_stripe/r02_exact_mg: k=128, m=28 + 100 copies 885 vs 1050 us)
 template <int MG>
 hipError_t launch_fp4_static_any(const Fp4Geometry& geo, const Fp4Args& a, hipStream_t stream) {
   if (geo.ksteps != 16) return hipErrorInvalidConfiguration;
@@ -1226,12 +1226,12 @@ bool use_sk(const Fp4Geometry& geo, bool copies) {
   const char* env = std::getenv("GFRS_FP4_KERNEL");
   if (env && std::strcmp(env, "v1") == 0) return false;
   if (env && std::strcmp(env, "sk") == 0) copies = false;  // (force it for the fused-copy form too)
-  // measured (profiles/r02_fp4): 6 % faster than v1 for plain GEMMs, 1 % slower with fused copies
+  // measured (profiles/wide_stripe/r02_fp4): 6 % faster than v1 for plain GEMMs, 1 % slower with fused copies
   return !copies && geo.ksteps == 16 && (geo.mg == 4 || geo.mg == 8);
 }
 
 // The A-resident kernel (gf_mfma_fp4ar.hip; k in (112, 128], all M-tiles in one group) where it
-// measured faster (profiles/r02_fp4_ablate, k=128, 1 GiB, medians of alternating runs): plain
+// measured faster (profiles/wide_stripe/r02_fp4_ablate, k=128, 1 GiB, medians of alternating runs): plain
 // GEMMs with 6 or 8 M-tiles (two row halves of 3 / 4, no padding tile: m=24 670 vs 714 us, m=32
 // 809 vs 842 — the p=32 encode) and 4 M-tiles with or without fused copies (one wave per column
 // group: m=16 490 vs 530 us plain, 659 vs 722 with 112 copies). It loses with padding tiles

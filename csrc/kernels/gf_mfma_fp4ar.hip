@@ -3,7 +3,7 @@
 // Same algebra, bit-matrix layout, B expansion and biased-float parity epilogue as
 // gf_mfma_fp4.hip (read its header first); what changes is where the operands live. The LDS
 // kernels there keep the whole coefficient bit-matrix (128 KiB at k=128, p=32) in LDS and their
-// 256 accumulators in AGPRs. Measured on the k=128, p=32 encode (profiles/r02_fp4_ablate), that
+// 256 accumulators in AGPRs. Measured on the k=128, p=32 encode (profiles/wide_stripe/r02_fp4_ablate), that
 // costs per MFMA: one v_accvgpr_read per accumulator in the epilogue, half an A-fragment
 // ds_read_b128, and a bias MFMA per accumulator tile per chunk — 4.05 VALU per MFMA, the issue
 // slots of the 32-cycle MFMA nearly full, and a power-capped clock (the kernel is clock-bound:

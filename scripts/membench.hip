@@ -159,7 +159,7 @@ int pattern_main(int argc, char** argv) {
 // Device-to-device bandwidth of hipMemcpyDeviceToDeviceNoCU (SDMA, no compute units) against the
 // blit-kernel copy, alone and beside a compute-bound kernel that holds every CU. Question it
 // answers: can the wide decode's survivor copy (102 rows x 8 MiB at k=128) run on the copy engines
-// under the MFMA-bound GEMM instead of inside it? (profiles/r05_sdma: no, ~0.12 TB/s per engine.)
+// under the MFMA-bound GEMM instead of inside it? (profiles/wide_stripe/r05_sdma: no, ~0.12 TB/s per engine.)
 // ALU-bound spin: every lane runs `iters` dependent FMAs; the result is stored so it is kept.
 __global__ void spin_kernel(float* out, int iters) {
   float a = threadIdx.x * 1e-3f, b = 1.0001f;

@@ -16,9 +16,9 @@ Measured per point:
                             GEMM + matrix generation / inversion
 Decode erases the first n-k natives (the reference's src/unit-test.sh worst case: conf = last k).
 
-  python scripts/sweep.py --part gpu --out profiles/r02_sweep/gpu.json     (on an MI355X)
-  python scripts/sweep.py --part cpu --out profiles/r02_sweep/cpu.json     (any host)
-  python scripts/sweep.py --table profiles/r02_sweep                       (README table)
+  python scripts/sweep.py --part gpu --out profiles/sweeps/r02_sweep/gpu.json     (on an MI355X)
+  python scripts/sweep.py --part cpu --out profiles/sweeps/r02_sweep/cpu.json     (any host)
+  python scripts/sweep.py --table profiles/sweeps/r02_sweep                       (README table)
 """
 from __future__ import annotations
 
