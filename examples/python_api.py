@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Python API tour: device-resident encode, erasure decode with the on-device inverse, in-place
-repair, batched small objects, the CPU fallback and the wide-stripe matrix-core engine.
+repair, batched small objects, the CPU fallback, the wide-stripe matrix-core engine and GF(2^16)
+codes past 256 chunks.
 
     python examples/python_api.py            # on an MI355X box (falls back to CPU tensors otherwise)
 """
@@ -13,7 +14,7 @@ import torch
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
 
 from gpu_rscode_amd import ReedSolomon, alloc_rows  # noqa: E402
-from gpu_rscode_amd.gf import GF256  # noqa: E402
+from gpu_rscode_amd.gf import GF256, field  # noqa: E402
 
 
 def main():
@@ -53,6 +54,17 @@ def main():
         wp = wide.encode(wd)
         torch.cuda.synchronize()
         assert np.array_equal(wp[:, :4096].cpu().numpy(), GF256.gemm(wide.E, wd[:, :4096].cpu().numpy()))
+    # GF(2^16) (the reference's w = 16 field): 16-bit symbols, so n may exceed 256
+    big = ReedSolomon(300, 340, field="gf65536", matrix="cauchy")
+    bd = alloc_rows(300, 2 * 4099, dev)  # even byte rows: little-endian 16-bit symbols
+    bd.copy_(torch.from_numpy(np.random.default_rng(3).integers(0, 256, size=(300, 2 * 4099), dtype=np.uint8)))
+    bp = big.encode(bd)
+    sym = bd.cpu().numpy().view("<u2")
+    assert np.array_equal(bp.cpu().numpy().view("<u2"), field(16).gemm(big.E, sym))
+    lost = set(range(0, 300, 8)) | {300, 333}  # 38 natives and 2 parity chunks
+    keep = [r for r in range(340) if r not in lost][:300]
+    bstripe = [bd[i] for i in range(300)] + [bp[i] for i in range(40)]
+    assert torch.equal(big.decode([bstripe[r] for r in keep], keep), bd)
     print(f"python API tour OK on {dev}")
 
 
