@@ -414,49 +414,63 @@ int gfrs_gemm_host(const int* devices, int ndev, int k, int m, const uint8_t* co
   });
 }
 
-int gfrs_encode_file(const char* file, int k, int p, int matrix_kind, const int* devices, int ndev, int streams,
-                     gfrs_file_report* report) {
+int gfrs_encode_file_ex(const char* file, int k, int p, int matrix_kind, int field_w, unsigned flags,
+                        const int* devices, int ndev, int streams, gfrs_file_report* report) {
   return guarded([&] {
     need(file && *file, "encode_file: no file");
     need(matrix_kind >= 0 && matrix_kind <= 2, "encode_file: bad matrix kind");
+    need(field_w == 8 || field_w == 16, "encode_file: field width must be 8 or 16");
     const std::vector<int> devs = device_list(devices, ndev);
-    const gfrs::PipelineOptions opt = pipe_opts(streams, 0);
+    gfrs::PipelineOptions opt = pipe_opts(streams, 0);
+    opt.field_w = field_w;
+    opt.zero_copy = (flags & GFRS_FLAG_ZERO_COPY) != 0;
     auto prep = gfrs::prepare_for_encode(devs, opt, file, k, p);  // device setup beside the reads
     const gfrs::GemmFn gemm = [&](const std::vector<const uint8_t*>& in, const std::vector<uint8_t*>& out,
-                                  const gfrs::Mat& coeff, int64_t ncols, int field_w) {
+                                  const gfrs::Mat& coeff, int64_t ncols, int fw) {
       if (prep) {
         prep->wait();
         prep.reset();
       }
       gfrs::PipelineOptions o = opt;
-      o.field_w = field_w;
+      o.field_w = fw;
       hip_check(gfrs::gemm_host_multi(devs, in, out, coeff, ncols, o, nullptr, nullptr), "GPU pipeline");
     };
     fill_report(gfrs::encode_file(file, k, p, static_cast<gfrs::MatrixKind>(matrix_kind), gemm,
-                                  gfrs::thp_pinned_host_alloc()),
+                                  gfrs::thp_pinned_host_alloc(), false, field_w),
                 report);
   });
 }
 
-int gfrs_decode_file(const char* file, const char* conf, const char* out, const int* devices, int ndev, int streams,
+int gfrs_encode_file(const char* file, int k, int p, int matrix_kind, const int* devices, int ndev, int streams,
                      gfrs_file_report* report) {
+  return gfrs_encode_file_ex(file, k, p, matrix_kind, 8, 0u, devices, ndev, streams, report);
+}
+
+int gfrs_decode_file_ex(const char* file, const char* conf, const char* out, unsigned flags, const int* devices,
+                        int ndev, int streams, gfrs_file_report* report) {
   return guarded([&] {
     need(file && *file && conf && *conf, "decode_file: file and conf are required");
     const std::vector<int> devs = device_list(devices, ndev);
-    const gfrs::PipelineOptions opt = pipe_opts(streams, 0);
+    gfrs::PipelineOptions opt = pipe_opts(streams, 0);
+    opt.zero_copy = (flags & GFRS_FLAG_ZERO_COPY) != 0;
     auto prep = gfrs::prepare_for_decode(devs, opt, file);
     const gfrs::GemmFn gemm = [&](const std::vector<const uint8_t*>& in, const std::vector<uint8_t*>& o,
-                                  const gfrs::Mat& coeff, int64_t ncols, int field_w) {
+                                  const gfrs::Mat& coeff, int64_t ncols, int fw) {
       if (prep) {
         prep->wait();
         prep.reset();
       }
       gfrs::PipelineOptions po = opt;
-      po.field_w = field_w;
+      po.field_w = fw;
       hip_check(gfrs::gemm_host_multi(devs, in, o, coeff, ncols, po, nullptr, nullptr), "GPU pipeline");
     };
     fill_report(gfrs::decode_file(file, conf, out ? out : "", gemm, gfrs::thp_pinned_host_alloc()), report);
   });
+}
+
+int gfrs_decode_file(const char* file, const char* conf, const char* out, const int* devices, int ndev, int streams,
+                     gfrs_file_report* report) {
+  return gfrs_decode_file_ex(file, conf, out, 0u, devices, ndev, streams, report);
 }
 
 int gfrs_release(void) {

@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define GFRS_API_VERSION 1
+#define GFRS_API_VERSION 2
 
 enum {
   GFRS_OK = 0,
@@ -99,6 +99,16 @@ int gfrs_encode_file(const char* file, int k, int p, int matrix_kind, const int*
 /* out NULL or "": overwrite `file`, as the reference does */
 int gfrs_decode_file(const char* file, const char* conf, const char* out, const int* devices, int ndev, int streams,
                      gfrs_file_report* report);
+
+/* Extended forms (API version 2). field_w: 8 (GF(2^8), the reference's field) or 16 (GF(2^16),
+ * poly 0x1100B: n <= 65535 chunks, even chunk size, versioned METADATA; decode reads the field from
+ * the METADATA). flags: GFRS_FLAG_ZERO_COPY — the GEMM kernel reads and writes the pinned host rows
+ * itself over PCIe (no device slice buffers, no copy engines). */
+enum { GFRS_FLAG_ZERO_COPY = 1 };
+int gfrs_encode_file_ex(const char* file, int k, int p, int matrix_kind, int field_w, unsigned flags,
+                        const int* devices, int ndev, int streams, gfrs_file_report* report);
+int gfrs_decode_file_ex(const char* file, const char* conf, const char* out, unsigned flags, const int* devices,
+                        int ndev, int streams, gfrs_file_report* report);
 
 /* frees the pipeline's persistent per-device workspaces */
 int gfrs_release(void);

@@ -118,3 +118,24 @@ def test_gpu_capi_file_codec_round_trip(lib, tmp_path):
                                 ctypes.byref(rep)) == 0, lib.gfrs_last_error()
     assert rep.erased == 4 and out.read_bytes() == data
     assert lib.gfrs_release() == 0
+
+
+@pytest.mark.gpu
+def test_gpu_capi_file_codec_ex_gf65536_zero_copy(lib, tmp_path):
+    """gfrs_encode_file_ex / gfrs_decode_file_ex (API version 2): a GF(2^16) stripe of 300 + 40
+    chunks (past GF(2^8)'s 256) encoded and decoded with the zero-copy kernel path."""
+    data = np.random.default_rng(5).integers(0, 256, size=2_000_011, dtype=np.uint8).tobytes()
+    f = tmp_path / "obj.bin"
+    f.write_bytes(data)
+    lib.gfrs_last_error.restype = ctypes.c_char_p
+    assert lib.gfrs_api_version() == 2
+    assert lib.gfrs_encode_file_ex(str(f).encode(), 300, 40, 1, 16, 1, None, 0, 2, None) == 0, lib.gfrs_last_error()
+    assert open(str(f) + ".METADATA").readline() == "GFRS-METADATA 2 16\n"
+    conf = tmp_path / "conf"
+    conf.write_text("".join(f"{tmp_path}/_{i}_obj.bin\n" for i in range(40, 340)))
+    out = tmp_path / "out.bin"
+    assert lib.gfrs_decode_file_ex(str(f).encode(), str(conf).encode(), str(out).encode(), 1, None, 0, 2,
+                                   None) == 0, lib.gfrs_last_error()
+    assert out.read_bytes() == data
+    assert lib.gfrs_encode_file_ex(str(f).encode(), 4, 2, 0, 12, 0, None, 0, 2, None) == -1  # bad field width
+    assert lib.gfrs_release() == 0
