@@ -142,6 +142,8 @@ def parse(argv=None):
     ap.add_argument("--pf", type=int, default=2, help="kernel variant: rows in flight (with --vec)")
     ap.add_argument("--nt", action="store_true", help="kernel variant: non-temporal (with --vec)")
     ap.add_argument("--no-overlap", action="store_true", help="solve on the main stream (no side stream)")
+    ap.add_argument("--side-priority", action="store_true",
+                    help="create the side stream (decode-system solve) with high priority")
     ap.add_argument("--bcast-ahead", type=int, default=2,
                     help="bcast: steps a pattern's broadcast runs ahead of the step that solves it (0: in line)")
     ap.add_argument("--lanes", type=int, default=None,
@@ -251,7 +253,8 @@ class GpuWorkload:
         self.streams = [torch.cuda.Stream(dev) for _ in range(self.lanes)]  # non-default (hipGraph capture)
         self.stream = self.streams[0]
         torch.cuda.set_stream(self.stream)
-        self.side = torch.cuda.Stream(dev)  # pattern + decode-system solve overlap the encode GEMM
+        # pattern + decode-system solve overlap the encode GEMM
+        self.side = torch.cuda.Stream(dev, priority=-1) if a.side_priority else torch.cuda.Stream(dev)
         self.inv_done = torch.cuda.Event()
         self.kv = dict(vec=a.vec, pf=a.pf, nt=a.nt)
         self.graph_mode = False

@@ -1091,8 +1091,7 @@ hipError_t launch_fp4(const Fp4Geometry& geo, int occ, const Fp4Args& a, hipStre
   // slot stays on one XCD
   const size_t lds = geo.fixed + ring_lds(R);
   (void)fp4_fn<MG, UNI, COPY, R, KS>();
-  int64_t slots = std::max<int64_t>(8, (int64_t(device_cu_count()) * occ / geo.groups) / 8 * 8);
-  slots = std::min<int64_t>(slots, (a.nchunks + 7) / 8 * 8);
+  const int64_t slots = persistent_slots(occ, geo.groups, a.nchunks);
   const unsigned blocks = unsigned(slots * geo.groups);
   gf_gemm_fp4_kernel<MG, UNI, COPY, R, KS><<<blocks, 256, lds, stream>>>(
       a.in, a.out, a.copy, static_cast<const i32x4*>(a.bitmat), a.k, a.m, geo.ksteps, geo.groups, a.col0, a.nchunks,
@@ -1183,8 +1182,7 @@ hipError_t launch_fp4sk(const Fp4Geometry& geo, const Fp4Args& a, hipStream_t st
     return o;
   });
   if (occ <= 0) return hipErrorInvalidConfiguration;
-  int64_t slots = std::max<int64_t>(8, (int64_t(device_cu_count()) * occ / geo.groups) / 8 * 8);
-  slots = std::min<int64_t>(slots, (a.nchunks + 7) / 8 * 8);
+  const int64_t slots = persistent_slots(occ, geo.groups, a.nchunks);
   const unsigned blocks = unsigned(slots * geo.groups);
   gf_gemm_fp4sk_kernel<MG, UNI, COPY, R, KS, ABL><<<blocks, 256, lds, stream>>>(
       a.in, a.out, a.copy, static_cast<const i32x4*>(a.bitmat), a.k, a.m, geo.groups, a.col0, a.nchunks, slots,

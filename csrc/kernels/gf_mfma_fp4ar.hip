@@ -439,8 +439,7 @@ hipError_t launch_ar(const Fp4ArLaunch& a, int64_t* done, hipStream_t stream) {
     const char* e = std::getenv("GFRS_FP4_SINK");
     return (e && std::atoi(e) == 1) ? 0 : 1;
   }();
-  int64_t slots = std::max<int64_t>(8, (int64_t(device_cu_count()) * occ) / 8 * 8);
-  slots = std::min<int64_t>(slots, (nchunks + 7) / 8 * 8);
+  const int64_t slots = persistent_slots(occ, 1, nchunks);
   gf_gemm_fp4ar_kernel<MGW, WPG, UNI, COPY, R><<<unsigned(slots), 256, lds, stream>>>(
       (cptr<uint64_t>)a.in, (cptr<uint64_t>)a.out, (cptr<uint64_t>)a.copy, static_cast<const i32x4*>(a.bitmat), a.k,
       a.m, a.mg, a.col0, nchunks, slots, a.in_stride, sink_spread);
