@@ -134,8 +134,8 @@ int main(int argc, char** argv) {
       if (!a.quiet) {
         for (size_t d = 0; d < st.size(); ++d)
           if (st[d].zero_copy)
-            std::printf("Device%zu: Total GPU %s time: %fms (zero-copy kernel %fms)\n", d, verb, st[d].ms_total,
-                        st[d].ms_stream);
+            std::printf("Device%zu: Total GPU %s time: %fms (zero-copy kernel %fms, row mapping + descriptor %fms)\n",
+                        d, verb, st[d].ms_total, st[d].ms_stream, st[d].ms_setup);
           else
             std::printf("Device%zu: Total GPU %s time: %fms (stream loop %fms, %d slices)\n", d, verb, st[d].ms_total,
                         st[d].ms_stream, st[d].slices);

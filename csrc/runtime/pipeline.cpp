@@ -258,8 +258,18 @@ std::vector<uint64_t> map_rows(const std::vector<Ptr>& rows) {
   return a;
 }
 
+// GFRS_ZC_NULL_STREAM=1: the zero-copy launches go to the null stream instead of a stream of
+// their own (measurement aid: a fresh process pays for its first stream creation)
+bool zc_null_stream() {
+  static const bool v = [] {
+    const char* e = std::getenv("GFRS_ZC_NULL_STREAM");
+    return e && std::atoi(e) == 1;
+  }();
+  return v;
+}
+
 hipError_t zc_stream(Workspace& ws) {
-  if (!ws.zc_stream) GFRS_TRY(hipStreamCreateWithFlags(&ws.zc_stream, hipStreamNonBlocking));
+  if (!ws.zc_stream && !zc_null_stream()) GFRS_TRY(hipStreamCreateWithFlags(&ws.zc_stream, hipStreamNonBlocking));
   return hipSuccess;
 }
 
