@@ -31,7 +31,9 @@ struct Args {
   bool resume = true;     // --no-resume: ignore a <target>.PROGRESS checkpoint
   bool sync = true;       // --no-sync: skip fdatasync before each checkpoint
   int field_w = 8;        // -w 8|16: symbol width (GF(2^8), or GF(2^16) for n up to 65535)
-  bool zero_copy = false;  // --zero-copy: kernels read/write the pinned host rows over PCIe (no staging)
+  // 1: the GEMM kernel reads / writes the pinned host rows over PCIe itself (no staging), 0: the
+  // staged -s stream pipeline; -1 (default): zero-copy unless -s or --slice asked for streams
+  int zero_copy = -1;
   bool streaming() const { return window >= 0; }
 };
 
@@ -65,8 +67,9 @@ inline void usage(const char* prog, bool gpu) {
     std::printf("  --gpus N                number of GPUs (default: all visible)\n");
     std::printf("  --devices I,J,...       explicit column-shard -> device list (a device may repeat)\n");
     std::printf("  --slice BYTES           column slice per stream step (default 16 MiB)\n");
-    std::printf("  --zero-copy             the GEMM kernel streams the pinned host rows itself over PCIe: no\n");
-    std::printf("                          device slice buffers or copy engines (-s/--slice then unused)\n");
+    std::printf("  --zero-copy             (default unless -s or --slice is given) the GEMM kernel streams the\n");
+    std::printf("                          pinned host rows itself over PCIe: no device slice buffers or copy engines\n");
+    std::printf("  --staged                the -s stream pipeline: H2D copies into device slices, kernel, D2H\n");
   } else {
     std::printf("  --mul logexp|logexp0|logexp1|logexp2|logexp3|loop|full|double|perm|row|simd\n");
     std::printf("  --threads T             worker threads (default 1, the reference's single thread)\n");
@@ -96,6 +99,7 @@ inline long long to_ll(const char* s, const char* what, long long lo) {
 
 inline Args parse(int argc, char** argv, bool gpu) {
   Args a;
+  bool streams_given = false;
   static const option longopts[] = {{"matrix", required_argument, nullptr, 1},
                                     {"cpu-meta", no_argument, nullptr, 2},
                                     {"gpus", required_argument, nullptr, 3},
@@ -109,6 +113,7 @@ inline Args parse(int argc, char** argv, bool gpu) {
                                     {"devices", required_argument, nullptr, 11},
                                     {"field-width", required_argument, nullptr, 'w'},
                                     {"zero-copy", no_argument, nullptr, 12},
+                                    {"staged", no_argument, nullptr, 13},
                                     {"help", no_argument, nullptr, 'h'},
                                     {nullptr, 0, nullptr, 0}};
   int c;
@@ -122,7 +127,7 @@ inline Args parse(int argc, char** argv, bool gpu) {
       case 'c': case 'C': a.conf = optarg; break;
       case 'o': case 'O': a.out = optarg; break;
       case 'p': case 'P': a.grid = to_int(optarg, "grid size", 0); break;
-      case 's': case 'S': a.streams = to_int(optarg, "stream number", 1); break;
+      case 's': case 'S': a.streams = to_int(optarg, "stream number", 1); streams_given = true; break;
       case 'q': a.quiet = true; break;
       case 'w': case 'W':
         a.field_w = to_int(optarg, "field width", 8);
@@ -134,14 +139,15 @@ inline Args parse(int argc, char** argv, bool gpu) {
       case 1: a.matrix = optarg; break;
       case 2: a.cpu_meta = true; break;
       case 3: a.gpus = to_int(optarg, "GPU count", 1); break;
-      case 4: a.slice = to_int(optarg, "slice bytes", 256); break;
+      case 4: a.slice = to_int(optarg, "slice bytes", 256); streams_given = true; break;
       case 5: a.mul = optarg; break;
       case 6: a.threads = to_int(optarg, "thread count", 0); break;
       case 7: a.op = Args::kMakeConf; break;
       case 8: a.window = to_ll(optarg, "window bytes", 0); break;
       case 9: a.resume = false; break;
       case 10: a.sync = false; break;
-      case 12: a.zero_copy = true; break;
+      case 12: a.zero_copy = 1; break;
+      case 13: a.zero_copy = 0; break;
       case 11: {
         std::string list = optarg ? optarg : "";
         size_t pos = 0;
@@ -157,6 +163,7 @@ inline Args parse(int argc, char** argv, bool gpu) {
       case 'h': default: usage(argv[0], gpu); std::exit(c == 'h' ? 0 : 2);
     }
   }
+  if (a.zero_copy < 0) a.zero_copy = streams_given ? 0 : 1;
   if (a.op == Args::kEncode) {
     const int cap = a.field_w == 16 ? 65535 : 256;
     if (a.k <= 0 || a.n <= a.k - 1 || a.in_file.empty() || a.n > cap) {

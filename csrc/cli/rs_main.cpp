@@ -72,7 +72,7 @@ int main(int argc, char** argv) {
     opt.streams = a.streams;
     opt.max_blocks = a.grid;
     opt.slice_bytes = a.slice;
-    opt.zero_copy = a.zero_copy;
+    opt.zero_copy = a.zero_copy == 1;
     const bool enc = a.op == gfrs_cli::Args::kEncode;
     const char* verb = enc ? "encoding" : "decoding";
     // device setup overlapped with the input reads (gfrs/async_prepare.h), sized for the whole
@@ -161,9 +161,9 @@ int main(int argc, char** argv) {
       std::printf("Host: HIP runtime init %fms, pinned buffers %fms, file read %fms\n", ms_init, r.ms_alloc,
                   r.ms_read);
       std::printf("GPU %s bandwidth: %.3f MB/s (%lld bytes in %.3f ms of GPU time: transfers + kernels, device "
-                  "setup excluded; k=%d, p=%d, %zu device shard(s), %d stream(s))\n",
+                  "setup excluded; k=%d, p=%d, %zu device shard(s), %s)\n",
                   verb, mb / (std::max(gpu_ms, 1e-9) / 1e3), static_cast<long long>(r.total_size), gpu_ms, r.k, r.p,
-                  devices.size(), a.streams);
+                  devices.size(), opt.zero_copy ? "zero-copy" : (std::to_string(a.streams) + " stream(s)").c_str());
       // the reference's "Total GPU ... time" window starts before its cudaMalloc/cudaStreamCreate
       // (src/encode.cu:117-119,168-232): setup on the critical path counts, overlapped setup does not
       std::printf("GPU %s bandwidth, reference window (setup on the critical path + transfers + kernels): %.3f MB/s "

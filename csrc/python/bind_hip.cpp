@@ -241,7 +241,7 @@ PYBIND11_MODULE(_hip, m) {
   m.def("device_shard", [](int64_t ncols, int devices, int d) { return device_shard(ncols, devices, d); });
 
   auto gpu_gemm = [](const std::vector<int>& devices, int streams, int64_t slice, int max_blocks,
-                     std::unique_ptr<AsyncPrepare>* prep = nullptr) -> GemmFn {
+                     std::unique_ptr<AsyncPrepare>* prep = nullptr, bool zero_copy = false) -> GemmFn {
     return [=](const std::vector<const uint8_t*>& in, const std::vector<uint8_t*>& out, const Mat& coeff,
                int64_t ncols, int field_w) {
       if (prep && *prep) {
@@ -250,41 +250,48 @@ PYBIND11_MODULE(_hip, m) {
       }
       PipelineOptions opt = pipeline_options(streams, slice, max_blocks);
       opt.field_w = field_w;
+      opt.zero_copy = zero_copy;
       check(gemm_host_multi(devices, in, out, coeff, ncols, opt, nullptr, nullptr), "GPU pipeline");
     };
   };
   m.def(
       "encode_file",
       [gpu_gemm](const std::string& file, int k, int p, const std::string& matrix, bool cpu_meta,
-                 const std::vector<int>& devices, int streams, int64_t slice, int max_blocks, int field_w) {
+                 const std::vector<int>& devices, int streams, int64_t slice, int max_blocks, int field_w,
+                 bool zero_copy) {
         FileReport r;
         {
           py::gil_scoped_release nogil;
           PipelineOptions popt = pipeline_options(streams, slice, max_blocks);
           popt.field_w = field_w;
+          popt.zero_copy = zero_copy;
           auto prep = prepare_for_encode(devices, popt, file, k, p);
-          r = encode_file(file, k, p, parse_matrix_kind(matrix), gpu_gemm(devices, streams, slice, max_blocks, &prep),
-                          pinned_alloc(), cpu_meta, field_w);
+          r = encode_file(file, k, p, parse_matrix_kind(matrix),
+                          gpu_gemm(devices, streams, slice, max_blocks, &prep, zero_copy), pinned_alloc(), cpu_meta,
+                          field_w);
         }
         return report(r);
       },
       py::arg("file"), py::arg("k"), py::arg("p"), py::arg("matrix") = "vandermonde", py::arg("cpu_meta") = false,
       py::arg("devices") = std::vector<int>{0}, py::arg("streams") = 2, py::arg("slice") = 16 << 20,
-      py::arg("max_blocks") = 0, py::arg("field_w") = 8);
+      py::arg("max_blocks") = 0, py::arg("field_w") = 8, py::arg("zero_copy") = false);
   m.def(
       "decode_file",
       [gpu_gemm](const std::string& file, const std::string& conf, const std::string& out,
-                 const std::vector<int>& devices, int streams, int64_t slice, int max_blocks) {
+                 const std::vector<int>& devices, int streams, int64_t slice, int max_blocks, bool zero_copy) {
         FileReport r;
         {
           py::gil_scoped_release nogil;
-          auto prep = prepare_for_decode(devices, pipeline_options(streams, slice, max_blocks), file);
-          r = decode_file(file, conf, out, gpu_gemm(devices, streams, slice, max_blocks, &prep), pinned_alloc());
+          PipelineOptions popt = pipeline_options(streams, slice, max_blocks);
+          popt.zero_copy = zero_copy;
+          auto prep = prepare_for_decode(devices, popt, file);
+          r = decode_file(file, conf, out, gpu_gemm(devices, streams, slice, max_blocks, &prep, zero_copy),
+                          pinned_alloc());
         }
         return report(r);
       },
       py::arg("file"), py::arg("conf"), py::arg("out") = "", py::arg("devices") = std::vector<int>{0},
-      py::arg("streams") = 2, py::arg("slice") = 16 << 20, py::arg("max_blocks") = 0);
+      py::arg("streams") = 2, py::arg("slice") = 16 << 20, py::arg("max_blocks") = 0, py::arg("zero_copy") = false);
   m.def("release_workspaces", [] { check(release_workspaces(), "release_workspaces"); });
   m.def(
       "encode_file_stream",

@@ -8,6 +8,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <string>
 #include <thread>
 
 #include "gfrs/host_desc.h"
@@ -258,12 +259,15 @@ std::vector<uint64_t> map_rows(const std::vector<Ptr>& rows) {
   return a;
 }
 
-// GFRS_ZC_NULL_STREAM=1: the zero-copy launches go to the null stream instead of a stream of
-// their own (measurement aid: a fresh process pays for its first stream creation)
+// The zero-copy launches go to the null stream: every hardware queue a process creates costs it
+// 8-25 ms on first use (the first stream even more), and the null stream is the one queue the
+// synchronous descriptor upload uses anyway (scripts/setup_probe.cpp, profiles/host_pipeline/r07_zc2:
+// a dedicated stream put 21-23 ms of stream creation plus 8 ms of null-stream bring-up into the
+// setup; the null stream alone costs ~26 ms once). GFRS_ZC_STREAM=own restores a stream of its own.
 bool zc_null_stream() {
   static const bool v = [] {
-    const char* e = std::getenv("GFRS_ZC_NULL_STREAM");
-    return e && std::atoi(e) == 1;
+    const char* e = std::getenv("GFRS_ZC_STREAM");
+    return !(e && std::string(e) == "own");
   }();
   return v;
 }

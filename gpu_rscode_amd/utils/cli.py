@@ -40,6 +40,8 @@ def _parser() -> argparse.ArgumentParser:
                     help="encode: symbol width, GF(2^8) or GF(2^16) (n <= 65535; decode reads it from METADATA)")
     ap.add_argument("--gpus", type=int, default=0, help="GPUs for the single-process pipeline (0 = all)")
     ap.add_argument("--slice", type=int, default=16 << 20)
+    ap.add_argument("--zero-copy", action="store_true",
+                    help="GPU backend: the GEMM kernel streams the pinned host rows over PCIe (no staging)")
     ap.add_argument("--threads", type=int, default=1, help="CPU backend threads")
     ap.add_argument("--mul", default="simd", help="CPU multiply strategy (row: the scalar product-row form)")
     ap.add_argument("--dist", action="store_true", help="torch.distributed multi-GPU mode (torchrun)")
@@ -79,6 +81,8 @@ def main(argv=None) -> int:
             print("-w 16 writes the versioned METADATA without --window / --cpu-meta", file=sys.stderr)
             return 2
         fw = {} if a.field_w == 8 else dict(field_w=a.field_w)
+        if a.zero_copy and backend == "gpu" and a.window is None:
+            fw["zero_copy"] = True
         t = time.perf_counter()
         st = {} if a.window is None else dict(window=a.window, resume=not a.no_resume, durable=not a.no_sync)
         if backend == "gpu":
@@ -103,7 +107,8 @@ def main(argv=None) -> int:
     if backend == "gpu":
         ndev = hip().device_count()
         fn = hip().decode_file_stream if st else hip().decode_file
-        r = fn(a.in_file, a.conf, a.out, list(range(a.gpus or ndev)), a.streams, a.slice, a.grid, **st)
+        zc = {"zero_copy": True} if (a.zero_copy and not st) else {}
+        r = fn(a.in_file, a.conf, a.out, list(range(a.gpus or ndev)), a.streams, a.slice, a.grid, **st, **zc)
     else:
         fn = cpu().decode_file_stream if st else cpu().decode_file
         r = fn(a.in_file, a.conf, a.out, a.mul, a.threads, **st)
