@@ -164,3 +164,80 @@ def test_gpu_encode_batch_matches_oracle(batch, case):
     torch.cuda.synchronize()
     for b in range(batch):
         assert np.array_equal(parity[b].cpu().numpy(), GF256.gemm(rs.E, host[b]))
+
+
+# ---- GF(2^16) (the reference's w = 16 field) -----------------------------------------------------
+F16 = None
+
+
+def _f16():
+    global F16
+    if F16 is None:
+        from gpu_rscode_amd.gf import field
+        F16 = field(16)
+    return F16
+
+
+@CPU_SETTINGS
+@given(st.integers(0, 65535), st.integers(0, 65535), st.integers(1, 65535))
+def test_gf65536_native_mul_and_byte_maps(a, b, c):
+    from gpu_rscode_amd.gf import perm_quads16, quad_apply16
+
+    f = _f16()
+    assert cpu().gf16_mul(a, b) == int(f.mul(a, b))
+    q = perm_quads16(np.array([[c]]))[0, 0]
+    x = np.array([a, b], dtype=np.uint16)
+    assert np.array_equal(quad_apply16(q, x), f.mul(c, x).astype(np.uint16))
+
+
+@st.composite
+def code16_case(draw, k_max=40, p_max=12, s_max=300):
+    k = draw(st.integers(1, k_max))
+    p = draw(st.integers(0, p_max))
+    C = 2 * draw(st.integers(1, s_max))  # whole 16-bit symbols
+    matrix = draw(st.sampled_from(["cauchy", "sys_vandermonde"]))
+    rows = sorted(draw(st.permutations(range(k + p)))[:k])
+    return k, p, C, matrix, rows, draw(st.integers(0, 2**31))
+
+
+@settings(max_examples=25, deadline=None, derandomize=True, suppress_health_check=[HealthCheck.too_slow])
+@given(code16_case())
+def test_cpu_gf65536_roundtrip_mds(case):
+    k, p, C, matrix, rows, seed = case
+    rs = ReedSolomon(k, k + p, matrix=matrix, field="gf65536")
+    host, data = _cpu_rows(k, C, seed)
+    parity = rs.encode(data)
+    assert np.array_equal(parity.numpy().view("<u2"), _f16().gemm(rs.E, host.view("<u2")))
+    stripe = [data[i] for i in range(k)] + [parity[i] for i in range(p)]
+    out = rs.decode(torch.stack([stripe[r] for r in rows]), rows)
+    assert np.array_equal(out.numpy(), host)
+
+
+@pytest.mark.gpu
+@GPU_SETTINGS
+@given(code16_case(k_max=300, p_max=40, s_max=20_000), st.booleans())
+@example(case=(300, 40, 2 * 4099, "cauchy", list(range(40, 340)), 11), aligned=False)
+def test_gpu_gf65536_roundtrip(case, aligned):
+    """Random GF(2^16) shapes on the device kernel (vector kernel on pitched rows, the symbol kernel
+    on rows 2 bytes off a 16-byte boundary), bit-exact against the numpy oracle."""
+    k, p, C, matrix, rows, seed = case
+    rs = ReedSolomon(k, k + p, matrix=matrix, field="gf65536")
+    host = np.random.default_rng(seed).integers(0, 256, size=(k, C), dtype=np.uint8)
+    if aligned:
+        data = alloc_rows(k, C, "cuda")
+        data.copy_(torch.from_numpy(host))
+        drows = [data[i] for i in range(k)]
+    else:
+        flat = torch.zeros(k * (C + 2) + 2, dtype=torch.uint8, device="cuda")
+        drows = [flat[2 + i * (C + 2): 2 + i * (C + 2) + C] for i in range(k)]
+        for i in range(k):
+            drows[i].copy_(torch.from_numpy(host[i]))
+    parity = alloc_rows(p, C, "cuda") if p else None
+    if p:
+        rs.encode(drows, parity)
+    stripe = drows + ([parity[i] for i in range(p)] if p else [])
+    out = rs.decode([stripe[r] for r in rows], rows)
+    torch.cuda.synchronize()
+    if p:
+        assert np.array_equal(parity.cpu().numpy().view("<u2"), _f16().gemm(rs.E, host.view("<u2"))), (k, p, C)
+    assert np.array_equal(out.cpu().numpy(), host), (k, p, C, rows)

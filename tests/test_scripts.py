@@ -14,7 +14,7 @@ def _run(*args, timeout=120):
 
 
 def test_sweep_table_renders_committed_points():
-    d = os.path.join(ROOT, "profiles", "r02_sweep")
+    d = os.path.join(ROOT, "profiles", "sweeps", "r02_sweep")
     if not os.path.exists(os.path.join(d, "gpu.json")):
         pytest.skip("sweep data not in this checkout")
     r = _run("scripts/sweep.py", "--table", d)
