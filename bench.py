@@ -896,7 +896,9 @@ def main(argv=None) -> int:
         rec["comparisons_complete"] = clean
     emitter.emit(rec)
     if has_pg and clean:
-        dist.destroy_process_group()
+        # (the record is out; a teardown that hangs must not hold the job: leave after 60 s)
+        with Watchdog(60.0, lambda: None, code=0 if ok else 1):
+            dist.destroy_process_group()
     if not clean:  # the group may be out of step: leave without another collective
         os._exit(0 if ok else 1)
     return 0 if ok else 1
