@@ -1224,6 +1224,13 @@ bool use_sk(const Fp4Geometry& geo, bool copies) {
   const char* env = std::getenv("GFRS_FP4_KERNEL");
   if (env && std::strcmp(env, "v1") == 0) return false;
   if (env && std::strcmp(env, "sk") == 0) copies = false;  // (force it for the fused-copy form too)
+  // GFRS_FP4_COPY_KERNEL=sk: the staggered form for fused-copy GEMMs only (the encode keeps its
+  // kernel); with GFRS_FP4_EXACT_MG=0 a 5..7-tile decode then runs as 8 staggered tiles (A/B)
+  static const bool copy_sk = [] {
+    const char* e = std::getenv("GFRS_FP4_COPY_KERNEL");
+    return e && std::strcmp(e, "sk") == 0;
+  }();
+  if (copies && copy_sk) copies = false;
   // measured (profiles/wide_stripe/r02_fp4): 6 % faster than v1 for plain GEMMs, 1 % slower with fused copies
   return !copies && geo.ksteps == 16 && (geo.mg == 4 || geo.mg == 8);
 }
