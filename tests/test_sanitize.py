@@ -59,3 +59,27 @@ def test_asan_streaming_codec(exe, tmp_path):
     assert _run(exe, ["-d", "-i", "s.bin", "-c", "c", "-o", "o", "--window", "1000", "--no-sync"],
                 tmp_path).returncode == 0
     assert (tmp_path / "o").read_bytes() == payload
+
+
+def test_asan_gf65536(exe, tmp_path):
+    """GF(2^16) (-w 16): odd file size (even chunks, padded tail), a 340-chunk stripe past GF(2^8)'s
+    n <= 256, the versioned METADATA, and a truncated version-2 matrix rejected."""
+    payload = os.urandom(77_777)
+    (tmp_path / "g.bin").write_bytes(payload)
+    assert _run(exe, ["-k", "10", "-n", "14", "-w", "16", "-e", "g.bin"], tmp_path).returncode == 0
+    assert (tmp_path / "g.bin.METADATA").read_text().startswith("GFRS-METADATA 2 16")
+    ff.write_conf(str(tmp_path / "c"), [f"_{r}_g.bin" for r in (1, 2, 4, 5, 6, 7, 9, 10, 12, 13)])
+    assert _run(exe, ["-d", "-i", "g.bin", "-c", "c", "-o", "o"], tmp_path).returncode == 0
+    assert (tmp_path / "o").read_bytes() == payload
+
+    wide = os.urandom(9_001)
+    (tmp_path / "w.bin").write_bytes(wide)
+    assert _run(exe, ["-k", "300", "-n", "340", "-w", "16", "-e", "w.bin", "--threads", "4"],
+                tmp_path).returncode == 0
+    ff.write_conf(str(tmp_path / "cw"), [f"_{r}_w.bin" for r in range(40, 340)])
+    assert _run(exe, ["-d", "-i", "w.bin", "-c", "cw", "-o", "ow"], tmp_path).returncode == 0
+    assert (tmp_path / "ow").read_bytes() == wide
+
+    md = (tmp_path / "g.bin.METADATA").read_text().splitlines()
+    (tmp_path / "g.bin.METADATA").write_text("\n".join(md[:4]) + "\n")  # header + part of the matrix
+    assert _run(exe, ["-d", "-i", "g.bin", "-c", "c", "-o", "o2"], tmp_path).returncode == 1
