@@ -28,12 +28,36 @@ PITCH = 256
 
 
 def alloc_rows(rows: int, ncols: int, device="cuda", fill: int | None = None) -> torch.Tensor:
-    """A [rows, ncols] uint8 view over storage whose row pitch is a multiple of 256 bytes."""
-    pitch = max(PITCH, (ncols + PITCH - 1) // PITCH * PITCH)
-    base = torch.empty(rows * pitch, dtype=torch.uint8, device=device)
+    """A [rows, ncols] uint8 view over storage whose row pitch is a multiple of 256 bytes
+    (:func:`row_pitch`; large device rows start on 2 MiB boundaries)."""
+    pitch = row_pitch(ncols, device)
+    align = (2 << 20) if pitch % (2 << 20) == 0 else 0
+    base = torch.empty(rows * pitch + align, dtype=torch.uint8, device=device)
+    off = (-base.data_ptr()) % align if align else 0
     if fill is not None:
         base.fill_(fill)
-    return base.as_strided((rows, ncols), (pitch, 1))
+    return base.as_strided((rows, ncols), (pitch, 1), off)
+
+
+def _row_align() -> int:
+    import os
+    return int(os.environ.get("GFRS_ROW_ALIGN", str(2 << 20)))
+
+
+def row_pitch(ncols: int, device="cuda") -> int:
+    """Row pitch of :func:`alloc_rows`: ``ncols`` rounded up to 256 bytes (every row 16-byte
+    aligned for odd C), and for device rows of at least 8 MiB up to 2 MiB, with the first row on a
+    2 MiB boundary. Measured on MI355X (``scripts/membench.hip pitch``,
+    ``profiles/headline/r07_pitch``): the k=10 encode pattern (10 rows in, 4 out) streams at
+    6.26 TB/s with 2 MiB-aligned rows against 5.93 at 256-byte pitch, the decode pattern (10 in,
+    10 out) at 5.77 against 5.33 — the rows' placement in HBM's channel interleave, not the kernel.
+    ``GFRS_ROW_ALIGN`` (bytes, power of two, 256 = the old layout) overrides the large-row
+    alignment."""
+    p = max(PITCH, (ncols + PITCH - 1) // PITCH * PITCH)
+    if torch.device(device).type == "cuda" and ncols >= (8 << 20):
+        a = max(PITCH, _row_align())
+        p = (ncols + a - 1) // a * a
+    return p
 
 
 class UnrecoverableError(gf.SingularMatrixError):
@@ -226,7 +250,7 @@ class ReedSolomon:
             raise ValueError("batched launches run GF(2^8) / GF(16) codes; encode GF(2^16) stripes one at a time")
         B, _, C = data.shape
         if parity is None:
-            pitch = max(PITCH, (C + PITCH - 1) // PITCH * PITCH)
+            pitch = row_pitch(C, data.device)
             base = torch.empty(B * self.p * pitch, dtype=torch.uint8, device=data.device)
             parity = base.as_strided((B, self.p, C), (self.p * pitch, pitch, 1))
         if self.p == 0:
@@ -257,7 +281,7 @@ class ReedSolomon:
         if k != self.k:
             raise ValueError(f"expected [B, {self.k}, C]")
         if out is None:
-            pitch = max(PITCH, (C + PITCH - 1) // PITCH * PITCH)
+            pitch = row_pitch(C, survivors.device)
             base = torch.empty(B * self.k * pitch, dtype=torch.uint8, device=survivors.device)
             out = base.as_strided((B, self.k, C), (self.k * pitch, pitch, 1))
         pos = {r: j for j, r in enumerate(rows)}

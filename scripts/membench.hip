@@ -5,6 +5,7 @@
 // Build: hipcc -O3 --offload-arch=gfx950 -o build/membench scripts/membench.hip
 // Run:   build/membench [REPS]     (prints one JSON object)
 //        build/membench sdma [ROWS WIDTH]   (copy engines vs blit copies, one JSON line per case)
+//        build/membench pitch [REPS]        (enc / dec patterns at different row pitches)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -285,7 +286,68 @@ int sdma_main(int argc, char** argv) {
   return 0;
 }
 
+// `membench pitch`: the enc (10 in / 4 out) and dec (10 in / 10 out) patterns at different row
+// pitches and output-buffer offsets — does the placement of the rows in HBM's channel interleave
+// move the ceiling? Pitch = C rounded up to `align`, plus `extra` bytes; the output rows start
+// `ooff` bytes after a 2 MiB-aligned base. One JSON line per case.
+int pitch_main(int argc, char** argv) {
+  const int64_t C = 107374183;
+  const int reps = argc > 1 ? atoi(argv[1]) : 20;
+  struct P {
+    int64_t align, extra, ooff;
+  };
+  const std::vector<P> ps = {
+      {256, 0, 0},          {4096, 2048, 0},        {2 << 20, 0, 0},        {2 << 20, 256, 0},
+      {2 << 20, 512, 0},    {2 << 20, 1024, 0},     {2 << 20, 2048, 0},     {2 << 20, 65536, 0},
+      {2 << 20, 1 << 20, 0}, {1 << 20, 0, 0},       {512 << 10, 0, 0},      {4 << 20, 0, 0},
+      {8 << 20, 0, 0},      {2 << 20, 0, 1 << 20},  {2 << 20, 0, 256 << 10}, {2 << 20, 0, 4096},
+      {2 << 20, 0, 256}};
+  const Case cs[2] = {mk<10, 4, 1, true, false, 256>("enc"), mk<10, 10, 1, true, false, 256>("dec")};
+  const int64_t maxpitch = C + (8 << 20) + (1 << 20);
+  uint8_t *in, *out;
+  CHECK(hipMalloc(&in, 10 * maxpitch + (4 << 20)));
+  CHECK(hipMalloc(&out, 10 * maxpitch + (4 << 20)));
+  CHECK(hipMemset(in, 0x5a, 10 * maxpitch));
+  uint8_t* in0 = reinterpret_cast<uint8_t*>((reinterpret_cast<uintptr_t>(in) + (2 << 20) - 1) & ~uintptr_t((2 << 20) - 1));
+  uint8_t* out0 = reinterpret_cast<uint8_t*>((reinterpret_cast<uintptr_t>(out) + (2 << 20) - 1) & ~uintptr_t((2 << 20) - 1));
+  hipEvent_t e0, e1;
+  CHECK(hipEventCreate(&e0));
+  CHECK(hipEventCreate(&e1));
+  std::vector<std::vector<float>> t(ps.size() * 2);
+  for (int round = 0; round < 5; ++round)
+    for (size_t i = 0; i < ps.size(); ++i)
+      for (int c = 0; c < 2; ++c) {
+        const int64_t pitch = (C + ps[i].align - 1) / ps[i].align * ps[i].align + ps[i].extra;
+        const int64_t nspans = (C / 16) / 64;
+        const int64_t blocks = (nspans + 3) / 4;
+        uint8_t* o = out0 + ps[i].ooff;
+        hipLaunchKernelGGL(cs[c].fn, dim3(unsigned(blocks)), dim3(256), 0, 0, in0, o, pitch, nspans);
+        CHECK(hipEventRecord(e0));
+        for (int r = 0; r < reps; ++r)
+          hipLaunchKernelGGL(cs[c].fn, dim3(unsigned(blocks)), dim3(256), 0, 0, in0, o, pitch, nspans);
+        CHECK(hipEventRecord(e1));
+        CHECK(hipEventSynchronize(e1));
+        CHECK(hipGetLastError());
+        float ms = 0;
+        CHECK(hipEventElapsedTime(&ms, e0, e1));
+        t[2 * i + c].push_back(ms / reps * 1e3f);
+      }
+  for (size_t i = 0; i < ps.size(); ++i)
+    for (int c = 0; c < 2; ++c) {
+      std::vector<float> v = t[2 * i + c];
+      std::sort(v.begin(), v.end());
+      const int64_t pitch = (C + ps[i].align - 1) / ps[i].align * ps[i].align + ps[i].extra;
+      const double bytes = double(cs[c].R + cs[c].W) * ((C / 16) / 64) * 64 * 16;
+      printf("{\"case\": \"%s\", \"align\": %lld, \"extra\": %lld, \"out_offset\": %lld, \"pitch_mod_64k\": %lld, "
+             "\"us_median\": %.2f, \"us_min\": %.2f, \"TBps\": %.3f}\n",
+             c ? "dec" : "enc", (long long)ps[i].align, (long long)ps[i].extra, (long long)ps[i].ooff,
+             (long long)(pitch % 65536), v[v.size() / 2], v[0], bytes / (v[v.size() / 2] * 1e-6) / 1e12);
+    }
+  return 0;
+}
+
 int main(int argc, char** argv) {
   if (argc > 1 && std::string(argv[1]) == "sdma") return sdma_main(argc - 1, argv + 1);
+  if (argc > 1 && std::string(argv[1]) == "pitch") return pitch_main(argc - 1, argv + 1);
   return pattern_main(argc, argv);
 }
