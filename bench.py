@@ -120,6 +120,10 @@ def parse(argv=None):
     ap.add_argument("--gpus", type=int, default=None, help="ranks / GPUs (default: WORLD_SIZE, else 1)")
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--min-warmup-ms", type=float, default=None,
+                    help="before the --warmup steps, run local steps (no collectives) until this many ms have "
+                         "passed, so the timed steps start at sustained clocks (default 250 on cuda, 0 on cpu; "
+                         "GFRS_MIN_WARMUP_MS; 0: off)")
     ap.add_argument("--k", type=int, default=None)
     ap.add_argument("--n", type=int, default=None)
     ap.add_argument("--bytes", type=int, default=None, help="input bytes per GPU (weak) / in total (strong)")
@@ -175,6 +179,8 @@ def parse(argv=None):
             setattr(a, key, val)
     if a.device == "cpu" and "--bytes" not in " ".join(argv if argv is not None else sys.argv):
         a.bytes = 1 << 20  # plumbing runs: 1 MiB per rank
+    if a.min_warmup_ms is None:
+        a.min_warmup_ms = float(os.environ.get("GFRS_MIN_WARMUP_MS", 250 if a.device == "cuda" else 0))
     a.force_pg = a.force_pg or os.environ.get("GFRS_FORCE_PG") == "1"
     if a.pg_backend is None:
         a.pg_backend = "nccl" if a.device == "cuda" else "gloo"
@@ -495,10 +501,27 @@ def max_over_ranks(x: float, dev, world: int) -> float:
     return max(gather_over_ranks(x, dev, world))
 
 
-def warm(work, xchg, steps: int) -> None:
+def warm(work, xchg, steps: int, min_ms: float = 0.0) -> dict:
+    """Untimed: first a pre-warm of local steps until `min_ms` has passed (no collectives: every
+    rank draws its step's pattern from its own copy of the broadcast pool, so ranks need not agree on
+    a count), then the `steps` warmup steps of the mode itself (with its traffic). The pre-warm is
+    there because the GPU's clocks leave their idle state over the first ~100 ms of load: after 5
+    warmup steps (~3 ms) the next 20 steps ran 4 % slower than after 300 (profiles/headline/r07_warm)."""
+    info = {"steps": 0, "ms": 0.0}
+    if min_ms > 0:
+        bcast, work.bcast = work.bcast, False
+        work.reset()
+        t0 = time.perf_counter()
+        while (time.perf_counter() - t0) * 1e3 < min_ms:
+            _run_steps(work, _NoExchange(), 4)
+            work.sync()
+            info["steps"] += 4
+        info["ms"] = round((time.perf_counter() - t0) * 1e3, 1)
+        work.bcast = bcast
     work.reset()
     _run_steps(work, xchg, steps)
     work.sync()
+    return info
 
 
 class _NoExchange:
@@ -594,7 +617,7 @@ def run_weak_mode(a, work, mode, world, dev, has_pg, steps, warmup, graph=False)
     slots = len(work.parity)
     xchg = ParityExchange([work.flat_parity(s) for s in range(slots)], mode if mode in ("owners", "root") else "none")
     work.bcast = has_pg and mode != "none"
-    warm(work, xchg, warmup)
+    pre = warm(work, xchg, warmup, a.min_warmup_ms)
     if graph:
         work.graph_mode = True
         graphs = []
@@ -615,7 +638,7 @@ def run_weak_mode(a, work, mode, world, dev, has_pg, steps, warmup, graph=False)
         per_rank = timed_loop(work, xchg, steps, world, dev, f"timed/weak/{mode}")
     ok = all(xchg.verify(s) for s in range(slots))
     return dict(elapsed=max(per_rank), per_rank=per_rank, steps=steps, ok=ok, sent=xchg.bytes_sent,
-                recv=xchg.bytes_received, link=xchg.bytes_per_link, bytes=2 * k * C * world)
+                recv=xchg.bytes_received, link=xchg.bytes_per_link, bytes=2 * k * C * world, prewarm=pre)
 
 
 def run_strong(a, k, n, e_mat, g, pool_dev, rank, world, dev, has_pg, steps, warmup):
@@ -645,10 +668,11 @@ def run_strong(a, k, n, e_mat, g, pool_dev, rank, world, dev, has_pg, steps, war
         gather = StripeGather([work.piece_rows(s) for s in range(slots)], fulls, widths)
     xchg = gather if (gather is not None and a.gather == "step") else _NoExchange()
     work.bcast = has_pg
-    warm(work, xchg, warmup)
+    pre = warm(work, xchg, warmup, a.min_warmup_ms)
     per_rank = timed_loop(work, xchg, steps, world, dev, f"timed/strong/{a.gather}")
     ok = all(xchg.verify(s) for s in range(slots))
     out = dict(elapsed=max(per_rank), per_rank=per_rank, steps=steps, ok=ok, bytes=2 * k * Ct, total_cols=Ct,
+               prewarm=pre,
                widths=widths, gather=a.gather, link=gather.bytes_per_link if gather else 0,
                recv=gather.bytes_received if (gather and rank == 0) else 0)
     if a.gather == "end":
@@ -946,6 +970,9 @@ def headline_record(a, k, n, C, world, rank, dev, has_pg, work, head, head_stron
         "n_gpus": world,
         "steps": a.steps,
         "warmup": a.warmup,
+        "prewarm": {**head.get("prewarm", {}), "min_ms": a.min_warmup_ms,
+                    "what": "untimed local steps (no collectives) run before the warmup steps until min_ms "
+                            "passed: clocks leave idle over the first ~100 ms of load"},
         "ms_per_step": round(ms, 4),
         "higher_is_better": True,
         "scaling": "strong" if head_strong else "weak",

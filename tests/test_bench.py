@@ -122,6 +122,20 @@ def test_single_rank_record_and_comm_choice():
         assert key in rec
 
 
+def test_prewarm_runs_local_steps_before_the_warmup():
+    """--min-warmup-ms: untimed local steps until the floor has passed, recorded; the timed loop is
+    still exactly --steps steps after --warmup steps (3 ranks: the pre-warm issues no collective,
+    so ranks that run different counts of it must not hang)."""
+    r = _run(["--device", "cpu", "--gpus", "3", "--steps", "2", "--warmup", "1", "--bytes", str(60_000),
+              "--min-warmup-ms", "30", "--no-compare"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = _record(r.stdout)
+    assert rec["verified"] is True and rec["steps"] == 2 and rec["warmup"] == 1
+    assert rec["prewarm"]["steps"] > 0 and rec["prewarm"]["ms"] >= 30 and rec["prewarm"]["min_ms"] == 30
+    r = _run(["--device", "cpu", "--steps", "2", "--warmup", "1"])
+    assert _record(r.stdout)["prewarm"]["steps"] == 0  # off by default on the CPU
+
+
 def test_every_preset_parses():
     import importlib.util
 
@@ -132,6 +146,7 @@ def test_every_preset_parses():
         a = bench.parse(["--preset", name])
         assert (a.k, a.n, a.bytes, a.erasures) == (pr["k"], pr["n"], pr["bytes"], pr["erasures"])
         assert a.scaling == pr.get("scaling", "weak") and a.lanes == pr.get("lanes", 2)
+        assert a.min_warmup_ms == float(os.environ.get("GFRS_MIN_WARMUP_MS", 250))  # cuda default
     a = bench.parse(["--preset", "k16n20_64g", "--scaling", "weak", "--lanes", "2"])
     assert a.scaling == "weak" and a.lanes == 2  # explicit flags win over the preset
 
