@@ -296,14 +296,26 @@ int pitch_main(int argc, char** argv) {
   struct P {
     int64_t align, extra, ooff;
   };
-  const std::vector<P> ps = {
+  std::vector<P> ps = {
       {256, 0, 0},          {4096, 2048, 0},        {2 << 20, 0, 0},        {2 << 20, 256, 0},
       {2 << 20, 512, 0},    {2 << 20, 1024, 0},     {2 << 20, 2048, 0},     {2 << 20, 65536, 0},
       {2 << 20, 1 << 20, 0}, {1 << 20, 0, 0},       {512 << 10, 0, 0},      {4 << 20, 0, 0},
       {8 << 20, 0, 0},      {2 << 20, 0, 1 << 20},  {2 << 20, 0, 256 << 10}, {2 << 20, 0, 4096},
       {2 << 20, 0, 256}};
+  // `membench pitch REPS MiB...`: explicit pitches in MiB instead (align 1 MiB, extra = the rest)
+  if (argc > 2) {
+    ps.clear();
+    for (int i = 2; i < argc; ++i) {
+      const int64_t p = int64_t(atoi(argv[i])) << 20;
+      if (p < C || p > (int64_t(160) << 20)) {
+        fprintf(stderr, "pitch %s MiB: need C <= pitch <= 160 MiB\n", argv[i]);
+        return 2;
+      }
+      ps.push_back({1 << 20, p - (C + (1 << 20) - 1) / (1 << 20) * (1 << 20), 0});
+    }
+  }
   const Case cs[2] = {mk<10, 4, 1, true, false, 256>("enc"), mk<10, 10, 1, true, false, 256>("dec")};
-  const int64_t maxpitch = C + (8 << 20) + (1 << 20);
+  const int64_t maxpitch = int64_t(161) << 20;
   uint8_t *in, *out;
   CHECK(hipMalloc(&in, 10 * maxpitch + (4 << 20)));
   CHECK(hipMalloc(&out, 10 * maxpitch + (4 << 20)));
