@@ -82,6 +82,20 @@ __device__ __forceinline__ gptr<u32x4> row_vec_w(uint64_t base, int64_t off) {
   return (gptr<u32x4>)(base + uint64_t(off));
 }
 
+// A wave-uniform int that the compiler computed on the VALU (e.g. the output tile, which comes out
+// of a runtime division: AMDGPU divides in float on the VALU) moved into an SGPR once. Left in a
+// VGPR, every table address formed from it is built with 64-bit VALU adds and read back with
+// v_readfirstlane before each s_load (32 + 16 VALU per 16-byte group in the k=10 rows kernel).
+// The empty asm hides the value's uniformity so the compiler keeps the readfirstlane builtin (it
+// drops it for a value it knows is uniform) and inserts the wait states the VALU-write ->
+// v_readfirstlane hazard needs itself. (A v_readfirstlane written as inline asm got none: it read
+// a stale VGPR and the table s_loads fed by it faulted, gf_gemm_vec_kernel<2,1,2>, round 4.)
+// Called at the top of a kernel, before any divergent branch.
+__device__ __forceinline__ int sgpr_int(int v) {
+  asm volatile("" : "+v"(v));
+  return __builtin_amdgcn_readfirstlane(v);
+}
+
 // Block -> (column block, output tile) mapping. Blocks b and b+8 share an XCD under the observed
 // round-robin dispatch; consecutive `local` ids of one XCD sweep the tiles of one column block.
 // Placement only affects speed, never correctness.

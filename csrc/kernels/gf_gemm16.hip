@@ -90,8 +90,8 @@ __global__ __launch_bounds__(kBlock) void gf_gemm16_vec_kernel(DescView d, int k
                                                                int64_t ngroups, int64_t nblk, int64_t ncb,
                                                                int tail_syms) {
   const TileMap tm = map_block(ntiles);
+  const int i0 = sgpr_int(tm.tile * MT);  // (first, with every lane active)
   if (tm.cb0 >= ncb) return;
-  const int i0 = tm.tile * MT;
   const bool do_copy = (tm.tile == 0);
 
   for (int64_t cb = tm.cb0; cb < nblk; cb += ncb) {
@@ -154,8 +154,8 @@ template <int MT>
 __global__ __launch_bounds__(kBlock) void gf_gemm16_sym_kernel(DescView d, int k, int m_pad, int ntiles, int64_t col0,
                                                                int64_t nsyms, int64_t nblk, int64_t ncb) {
   const TileMap tm = map_block(ntiles);
+  const int i0 = sgpr_int(tm.tile * MT);  // (first, with every lane active)
   if (tm.cb0 >= ncb) return;
-  const int i0 = tm.tile * MT;
   const bool do_copy = (tm.tile == 0);
   for (int64_t cb = tm.cb0; cb < nblk; cb += ncb) {
     const int64_t s = cb * kBlock + threadIdx.x;
