@@ -22,6 +22,9 @@
 //     its destination row in the same pass (saves a full re-read of the survivors).
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+#include <cstring>
+
 #include <cstdint>
 
 #include "gfrs/desc.h"
@@ -457,11 +460,31 @@ hipError_t launch_vec(const DescView& d, int k, int m_pad, int batch, int64_t co
 // (profiles/r01_kbench/kbench.json): non-temporal streaming with two rows in flight wins on every
 // HBM-bound shape (k=10 encode 5.6 TB/s, 4-erasure decode 5.8 TB/s); the VALU-bound wide tile
 // (MT = 16) prefers two 16-byte groups per lane to amortise the per-row table moves.
+// GFRS_VEC_CFG="V,PF,NT" (e.g. "1,4,1") replaces the default for every vector-kernel launch
+// without an explicit variant (in the k=10 step: the decode; A/B measurements)
 Cfg default_cfg(int mt) {
+  static const int env[3] = {[] {
+    const char* e = std::getenv("GFRS_VEC_CFG");
+    return e ? std::atoi(e) : 0;
+  }(), [] {
+    const char* e = std::getenv("GFRS_VEC_CFG");
+    const char* c = e ? std::strchr(e, ',') : nullptr;
+    return c ? std::atoi(c + 1) : 0;
+  }(), [] {
+    const char* e = std::getenv("GFRS_VEC_CFG");
+    const char* c = e ? std::strchr(e, ',') : nullptr;
+    c = c ? std::strchr(c + 1, ',') : nullptr;
+    return c ? std::atoi(c + 1) : 1;
+  }()};
   Cfg c;
   c.vec = mt >= 16 ? 2 : 1;
   c.pf = 2;
   c.nt = true;
+  if (env[0] > 0 && env[1] > 0) {
+    c.vec = env[0];
+    c.pf = env[1];
+    c.nt = env[2] != 0;
+  }
   return c;
 }
 
