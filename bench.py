@@ -94,7 +94,7 @@ import torch.distributed as dist  # noqa: E402
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 from gpu_rscode_amd import gf  # noqa: E402
-from gpu_rscode_amd.models import ReedSolomon, alloc_rows  # noqa: E402
+from gpu_rscode_amd.models import ReedSolomon, alloc_rows, flat_rows  # noqa: E402
 from gpu_rscode_amd.parallel.dist import shard_range  # noqa: E402
 from gpu_rscode_amd.parallel.placement import ParityExchange, StripeGather  # noqa: E402
 from gpu_rscode_amd.utils.timing import trace_range  # noqa: E402
@@ -240,7 +240,7 @@ class GpuWorkload:
         self.lanes = 1 if a.graph else max(1, a.lanes)
         slots = max(slots, self.lanes)
         self.data = alloc_rows(k, C, dev)
-        fill_random_(self.data.as_strided((self.data.untyped_storage().nbytes(),), (1,)),
+        fill_random_(flat_rows(self.data),
                      seed=rank + 1 if seed is None else seed)
         self.parity = parity_bufs or [alloc_rows(self.p, C, dev) for _ in range(slots)]
         self.outs = out_bufs or [alloc_rows(k, C, dev) for _ in range(self.lanes)]
@@ -279,7 +279,7 @@ class GpuWorkload:
 
     def flat_parity(self, slot: int) -> torch.Tensor:
         par = self.parity[slot]
-        return par.as_strided((par.untyped_storage().nbytes(),), (1,))
+        return flat_rows(par)
 
     def piece_rows(self, slot: int) -> list[torch.Tensor]:
         """The rows a strong-scaling gather moves for `slot`: parity, then the decoded natives."""

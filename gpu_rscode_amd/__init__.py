@@ -16,8 +16,8 @@ import torch  # noqa: F401  — load torch's HIP runtime before the native exten
 
 from . import gf  # noqa: E402
 from .gf import GF, SingularMatrixError
-from .models import ReedSolomon, UnrecoverableError, alloc_rows
+from .models import ReedSolomon, UnrecoverableError, alloc_rows, flat_rows
 
 __version__ = "0.2.0"
 
-__all__ = ["gf", "GF", "SingularMatrixError", "ReedSolomon", "UnrecoverableError", "alloc_rows", "__version__"]
+__all__ = ["gf", "GF", "SingularMatrixError", "ReedSolomon", "UnrecoverableError", "alloc_rows", "flat_rows", "__version__"]

@@ -39,6 +39,12 @@ def alloc_rows(rows: int, ncols: int, device="cuda", fill: int | None = None) ->
     return base.as_strided((rows, ncols), (pitch, 1), off)
 
 
+def flat_rows(t: torch.Tensor) -> torch.Tensor:
+    """The bytes of an :func:`alloc_rows` tensor's rows, pitch padding included, as one 1-D view
+    (from the tensor's own storage offset: the rows may start past the allocation's first byte)."""
+    return t.as_strided((t.shape[0] * t.stride(0),), (1,))
+
+
 def _row_align() -> int:
     import os
     return int(os.environ.get("GFRS_ROW_ALIGN", str(2 << 20)))

@@ -14,7 +14,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from gpu_rscode_amd import gf  # noqa: E402
-from gpu_rscode_amd.models import alloc_rows  # noqa: E402
+from gpu_rscode_amd.models import alloc_rows, flat_rows  # noqa: E402
 from gpu_rscode_amd.ops import GemmPlan, fill_random_  # noqa: E402
 
 
@@ -22,7 +22,7 @@ def main():
     k, m, iters = 128, 32, 20
     C = (1 << 30) // k
     data = alloc_rows(k, C, "cuda")
-    fill_random_(data.as_strided((data.untyped_storage().nbytes(),), (1,)), seed=3)
+    fill_random_(flat_rows(data), seed=3)
     coeff = np.random.default_rng(5).integers(1, 256, size=(m, k), dtype=np.uint8)
     out = alloc_rows(m, C, "cuda")
     plan = GemmPlan(data, out, coeff, engine="mfma")

@@ -13,14 +13,14 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from gpu_rscode_amd import gf  # noqa: E402
-from gpu_rscode_amd.models import alloc_rows  # noqa: E402
+from gpu_rscode_amd.models import alloc_rows, flat_rows  # noqa: E402
 from gpu_rscode_amd.ops import GemmPlan, fill_random_  # noqa: E402
 
 
 def main():
     k, C, iters = 128, (1 << 30) // 128, 15
     data = alloc_rows(k, C, "cuda")
-    fill_random_(data.as_strided((data.untyped_storage().nbytes(),), (1,)), seed=3)
+    fill_random_(flat_rows(data), seed=3)
     dst = alloc_rows(k, C, "cuda")
     res = {"env": {x: os.environ.get(x) for x in ("GFRS_FP4_EXACT_MG", "GFRS_FP4_KERNEL", "GFRS_FP4_COPY", "GFRS_FP4_SINK")}}
     rng = np.random.default_rng(5)

@@ -21,7 +21,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-from gpu_rscode_amd import ReedSolomon, alloc_rows  # noqa: E402
+from gpu_rscode_amd import ReedSolomon, alloc_rows, flat_rows  # noqa: E402
 from gpu_rscode_amd.ops import fill_random_  # noqa: E402
 
 
@@ -46,7 +46,7 @@ def case(k: int, n: int, nbytes: int, field: str, reps: int) -> dict:
         C += C % 2
     rs = ReedSolomon(k, n, field=field, matrix="cauchy" if n > 256 else "vandermonde")
     data = alloc_rows(k, C, "cuda")
-    fill_random_(data.as_strided((data.untyped_storage().nbytes(),), (1,)), seed=k)
+    fill_random_(flat_rows(data), seed=k)
     par = alloc_rows(p, C, "cuda")
     enc_ms = _time(lambda: rs.encode(data, par), reps)
     e = min(k, p)

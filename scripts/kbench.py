@@ -18,7 +18,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from gpu_rscode_amd import gf  # noqa: E402
-from gpu_rscode_amd.models import alloc_rows  # noqa: E402
+from gpu_rscode_amd.models import alloc_rows, flat_rows  # noqa: E402
 from gpu_rscode_amd.ops import GemmPlan, fill_random_, gf_invert  # noqa: E402
 
 VARIANTS = [None, (1, 1, False), (1, 2, False), (1, 4, False), (1, 2, True), (1, 4, True), (2, 1, False),
@@ -38,7 +38,7 @@ def timed(fn, reps):
 def make_case(name, k, m, ncopy, total_bytes):
     C = (total_bytes + k - 1) // k
     data = alloc_rows(k, C, "cuda")
-    fill_random_(data.as_strided((data.untyped_storage().nbytes(),), (1,)), seed=k)
+    fill_random_(flat_rows(data), seed=k)
     out = alloc_rows(m, C, "cuda")
     copies = None
     if ncopy:

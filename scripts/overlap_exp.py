@@ -17,7 +17,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-from gpu_rscode_amd.models import alloc_rows  # noqa: E402
+from gpu_rscode_amd.models import alloc_rows, flat_rows  # noqa: E402
 from gpu_rscode_amd.ops import GemmPlan, fill_random_  # noqa: E402
 
 
@@ -45,7 +45,7 @@ def main():
     a = ap.parse_args()
     C = (a.bytes + a.k - 1) // a.k
     data = alloc_rows(a.k, C, "cuda")
-    fill_random_(data.as_strided((data.untyped_storage().nbytes(),), (1,)), seed=1)
+    fill_random_(flat_rows(data), seed=1)
     out = alloc_rows(a.m, C, "cuda")
     dst = alloc_rows(a.copies, C, "cuda")
     coeff = np.random.default_rng(0).integers(1, 256, size=(a.m, a.k), dtype=np.uint8)

@@ -51,7 +51,7 @@ PUBLISHED = {  # (p, what) -> ms per k in KS
 def gpu_point(k: int, p: int, reps: int = 5) -> dict:
     import torch
 
-    from gpu_rscode_amd import ReedSolomon, alloc_rows
+    from gpu_rscode_amd import ReedSolomon, alloc_rows, flat_rows
     from gpu_rscode_amd._native import hip
     from gpu_rscode_amd.ops import GemmPlan, decode_system_into_plan, fill_random_
 
@@ -60,7 +60,7 @@ def gpu_point(k: int, p: int, reps: int = 5) -> dict:
     dev = torch.device("cuda", 0)
     rs = ReedSolomon(k, n)
     data = alloc_rows(k, C, dev)
-    fill_random_(data.as_strided((data.untyped_storage().nbytes(),), (1,)), seed=k * 7 + p)
+    fill_random_(flat_rows(data), seed=k * 7 + p)
     parity = alloc_rows(p, C, dev)
     out = alloc_rows(k, C, dev)
     enc = GemmPlan(data, parity, rs.E)
@@ -128,7 +128,7 @@ def gf16_point(reps: int = 5) -> dict:
     GF(2^8) k=4 point; the reference's GF(16) ran 17x faster than its log/exp GF(256) kernel."""
     import torch
 
-    from gpu_rscode_amd import ReedSolomon, alloc_rows
+    from gpu_rscode_amd import ReedSolomon, alloc_rows, flat_rows
     from gpu_rscode_amd._native import hip
     from gpu_rscode_amd.ops import GemmPlan, fill_random_
 
@@ -137,7 +137,7 @@ def gf16_point(reps: int = 5) -> dict:
     dev = torch.device("cuda", 0)
     rs = ReedSolomon(k, n, field="gf16")
     data = alloc_rows(k, C, dev)
-    fill_random_(data.as_strided((data.untyped_storage().nbytes(),), (1,)), seed=16)
+    fill_random_(flat_rows(data), seed=16)
     parity = alloc_rows(p, C, dev)
     out = alloc_rows(k, C, dev)
     enc = GemmPlan(data, parity, maps=rs._maps(rs.E))

@@ -14,7 +14,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-from gpu_rscode_amd import ReedSolomon, alloc_rows  # noqa: E402
+from gpu_rscode_amd import ReedSolomon, alloc_rows, flat_rows  # noqa: E402
 from gpu_rscode_amd.ops import GemmPlan, fill_random_  # noqa: E402
 
 
@@ -38,7 +38,7 @@ def main():
     args = [a for a in sys.argv[1:] if not a.startswith("--")]
     for C in [int(x) for x in (args[0] if args else "107374183,107374176,104858,104848").split(",")]:
         data = alloc_rows(10, C, "cuda")
-        fill_random_(data.as_strided((data.untyped_storage().nbytes(),), (1,)), seed=1)
+        fill_random_(flat_rows(data), seed=1)
         par = alloc_rows(4, C, "cuda")
         out = alloc_rows(10, C, "cuda")
         enc = GemmPlan(data, par, rs.E)

@@ -326,3 +326,13 @@ def test_row_pitch_layout(monkeypatch):
     assert row_pitch(C, "cuda") == 107374336
     t = alloc_rows(3, 1001, "cpu", fill=7)
     assert t.shape == (3, 1001) and t.stride() == (1024, 1) and int(t.sum()) == 7 * 3 * 1001
+
+
+def test_flat_rows_view_starts_at_the_rows():
+    """flat_rows covers exactly the rows (pitch included) from the tensor's own storage offset."""
+    from gpu_rscode_amd import flat_rows
+    base = torch.arange(5000, dtype=torch.int64).to(torch.uint8)
+    t = base.as_strided((3, 1000), (1024, 1), 700)
+    f = flat_rows(t)
+    assert f.shape == (3072,) and f.data_ptr() == t.data_ptr()
+    assert torch.equal(f[1024:2024], t[1])
