@@ -62,14 +62,20 @@ struct Solver {
   const Metadata& md;
   bool solve(const std::vector<int>& rows, const std::vector<int>* erased, Mat* coeff) const {
     const int k = md.k;
-    if (md.w == 16) {
-      gf16w::Mat dm;
-      if (!gf16w::decode_matrix(md.g16, k, rows, dm)) return false;
-      if (erased && coeff) {
-        gf16w::Mat sel;
-        for (int e : *erased) sel.insert(sel.end(), dm.begin() + size_t(e) * k, dm.begin() + size_t(e + 1) * k);
-        *coeff = pack16(sel);
+    if (md.w == 16) {  // the e x e systematic solve of the erased rows only (gf16w::decode_rows)
+      std::vector<int> want;
+      if (erased) {
+        want = *erased;
+      } else {
+        std::vector<char> seen(size_t(k), 0);
+        for (int r : rows)
+          if (r >= 0 && r < k) seen[size_t(r)] = 1;
+        for (int i = 0; i < k; ++i)
+          if (!seen[size_t(i)]) want.push_back(i);
       }
+      gf16w::Mat sel;
+      if (!gf16w::decode_rows(md.g16, k, rows, want, sel)) return false;
+      if (erased && coeff) *coeff = pack16(sel);
       return true;
     }
     Mat dm;

@@ -1,4 +1,6 @@
 // _cpu extension: CPU reference codec, GF(2^8) scalar ops, formats, file-level codec.
+#include <cstring>
+
 #include "bind_common.h"
 #include "gfrs/cpu_codec.h"
 #include "gfrs/format.h"
@@ -52,6 +54,25 @@ PYBIND11_MODULE(_cpu, m) {
     gf16w::Mat out;
     if (!gf16w::invert(gf16w::Mat(a.begin(), a.end()), n, out)) throw py::value_error("singular matrix");
     return std::vector<int>(out.begin(), out.end());
+  });
+  // rows `want` of inv(G[rows]) (gfrs/gf65536.h decode_rows: the e x e systematic solve); G and
+  // the result as little-endian uint16 bytes (no per-element Python objects: k = 300 is 90 k entries)
+  m.def("gf16_decode_rows", [](const py::bytes& g, int k, const std::vector<int>& rows, const std::vector<int>& want) {
+    const std::string gs = g;
+    if (k <= 0 || gs.size() % (2 * size_t(k)) != 0) throw py::value_error("G must be n x k uint16");
+    const size_t n = gs.size() / (2 * size_t(k));
+    for (int r : rows)
+      if (r < 0 || size_t(r) >= n) throw py::value_error("chunk id out of range");
+    gf16w::Mat gm(n * size_t(k));
+    std::memcpy(gm.data(), gs.data(), gs.size());
+    gf16w::Mat out;
+    bool ok;
+    {
+      py::gil_scoped_release nogil;
+      ok = gf16w::decode_rows(gm, k, rows, want, out);
+    }
+    if (!ok) throw py::value_error("singular matrix");
+    return py::bytes(reinterpret_cast<const char*>(out.data()), out.size() * 2);
   });
   m.def("gf16_perm_quad", [](int c) {
     const auto q = gf16w::perm_quad(uint16_t(c));

@@ -136,10 +136,23 @@ class ReedSolomon:
         else:
             raise ValueError(f"unknown field {field!r}")
         dt = np.uint16 if field == "gf65536" else np.uint8
+        self._dm: dict = {}
+        self._g16_bytes: tuple | None = None  # (the G it was made from, its uint16 bytes)
         self.G = np.vstack([np.eye(k, dtype=dt), self.E]).astype(dt)
         self._plans = _PlanCache()
-        self._dm: dict = {}
         self._g_dev: dict = {}  # (device, id(G)) -> G on device, for the on-device decode system
+
+    @property
+    def G(self) -> np.ndarray:
+        """The n x k generator [I_k; E]. Assigning a new one drops the decode matrices derived
+        from the old one (per-pattern caches)."""
+        return self._G
+
+    @G.setter
+    def G(self, g: np.ndarray) -> None:
+        self._G = g
+        self._dm.clear()
+        self._g16_bytes = None
 
     # ---- helpers -----------------------------------------------------------------------------
     @property
@@ -335,6 +348,28 @@ class ReedSolomon:
             self._dm[rows] = dm
         return dm
 
+    def _erased_rows(self, rows: Sequence[int], erased: Sequence[int]) -> np.ndarray:
+        """Rows ``erased`` of the decode matrix (what a decode GEMM applies). GF(2^16): the C++
+        e x e systematic solve (``gf16_decode_rows``) instead of the full k x k inverse — 0.6 ms
+        against 38 ms at k=300, e=40 — cached per pattern; other fields: rows of decode_matrix."""
+        if not self.wide:
+            return self.decode_matrix(rows)[list(erased)]
+        rows = tuple(int(r) for r in rows)
+        key = ("rows", rows, tuple(int(e) for e in erased))
+        dm = self._dm.get(key)
+        if dm is None:
+            if len(rows) != self.k or len(set(rows)) != self.k or min(rows) < 0 or max(rows) >= self.n:
+                raise ValueError(f"need {self.k} distinct chunk ids in [0, {self.n})")
+            if self._g16_bytes is None or self._g16_bytes[0] is not self.G:
+                self._g16_bytes = (self.G, np.ascontiguousarray(self.G, dtype="<u2").tobytes())
+            try:
+                raw = cpu().gf16_decode_rows(self._g16_bytes[1], self.k, list(rows), [int(e) for e in key[2]])
+            except ValueError as e:
+                raise UnrecoverableError(str(e)) from None
+            dm = np.frombuffer(raw, dtype="<u2").astype(np.uint16).reshape(len(key[2]), self.k)
+            self._dm[key] = dm
+        return dm
+
     def is_recoverable(self, rows: Sequence[int]) -> bool:
         try:
             self.decode_matrix(rows)
@@ -382,8 +417,7 @@ class ReedSolomon:
                 if r < self.k:
                     outs[r][:ncols].copy_(ins[j][:ncols])
             if erased:
-                dm = self.decode_matrix(rows)
-                self._cpu_gemm(dm[erased], ins, [outs[i] for i in erased])
+                self._cpu_gemm(self._erased_rows(rows, erased), ins, [outs[i] for i in erased])
             return out
         if not erased:  # pure copy: one fused pass with a single dummy output row would waste work
             for j, r in enumerate(rows):
@@ -406,8 +440,7 @@ class ReedSolomon:
             decode_system_into_plan(g_dev, plan.rows_dev, plan.erased_dev, plan, status=plan.status, stream=stream)
             self.last_status = plan.status
         else:
-            dm = self.decode_matrix(rows)
-            plan = self._plan(key, ins, [outs[i] for i in erased], dm[erased], copies=copies)
+            plan = self._plan(key, ins, [outs[i] for i in erased], self._erased_rows(rows, erased), copies=copies)
             if fast is not None:
                 self._plans[fast] = plan
         plan.run(stream)

@@ -81,6 +81,39 @@ def test_mds_matrices_and_singular_patterns():
         rs.decode_matrix([2, 3])
 
 
+@pytest.mark.parametrize("matrix", ["vandermonde", "cauchy"])
+def test_erased_rows_solve_matches_the_full_inverse(matrix):
+    """The e x e systematic solve (gf16_decode_rows) gives exactly the erased rows of the full
+    inverse, for random patterns, survivors in any order, and wanted rows that survived."""
+    k, n = 24, 34
+    rs = ReedSolomon(k, n, matrix=matrix, field="gf65536")
+    g = np.random.default_rng(5)
+    for _ in range(25):
+        rows = [int(r) for r in g.permutation(n)[:k]]
+        if not rs.is_recoverable(rows):
+            with pytest.raises(UnrecoverableError):
+                rs._erased_rows(rows, [i for i in range(k) if i not in rows])
+            continue
+        full = rs.decode_matrix(rows)
+        erased = [i for i in range(k) if i not in rows]
+        assert np.array_equal(rs._erased_rows(rows, erased), full[erased])
+        some = [0, k - 1, erased[0]] if erased else [0]
+        raw = cpu().gf16_decode_rows(np.ascontiguousarray(rs.G, dtype="<u2").tobytes(), k, rows, some)
+        assert np.array_equal(np.frombuffer(raw, dtype="<u2").reshape(len(some), k), full[some])
+    g2 = np.array(rs.G)  # a non-systematic G takes the full-inverse fallback
+    g2[0, 1] ^= 1
+    rs.G = g2  # (assigning G drops the patterns cached for the old one)
+    rows = list(range(n - k, n))
+    a = rs.G[rows]
+    inv = np.asarray(cpu().gf16_invert([int(v) for v in a.reshape(-1)], k), dtype=np.uint16).reshape(k, k)
+    erased = list(range(n - k))
+    assert np.array_equal(rs._erased_rows(rows, erased), inv[erased])
+    rs2 = ReedSolomon(2, 4, field="gf65536")
+    rs2.G = np.array([[1, 0], [0, 1], [1, 1], [1, 1]], dtype=np.uint16)  # rows 2 and 3 equal: singular
+    with pytest.raises(UnrecoverableError):
+        rs2._erased_rows([2, 3], [0, 1])
+
+
 def test_odd_byte_rows_are_rejected():
     rs = ReedSolomon(4, 6, field="gf65536")
     with pytest.raises(ValueError, match="even byte count"):
