@@ -26,8 +26,9 @@ hipError_t launch_gf_gemm16(const void* desc, int k, int m_pad, int64_t col0, in
 
 // Batched form: `batch` stripes of identical shape share the coefficient tables (small-object
 // serving: one launch for many objects). desc built with desc_layout(k, m_pad, batch).
+// copies = false promises no fused-copy rows (a batched encode: the rows-in-flight kernel may run).
 hipError_t launch_gf_gemm_batched(const void* desc, int k, int m_pad, int batch, int64_t col0, int64_t ncols,
-                                  bool force_bytewise, hipStream_t stream);
+                                  bool force_bytewise, hipStream_t stream, bool copies = true);
 
 // Variant selector for benchmarks/ablation: vec = 16-byte groups per lane (0 = byte kernel, -1 = the
 // byte kernel's serial round-3 form),

@@ -22,6 +22,7 @@
 //     its destination row in the same pass (saves a full re-read of the survivors).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 
@@ -282,6 +283,71 @@ __global__ __launch_bounds__(kBlock) void gf_gemm_rows_kernel(DescView d, int k_
   }
 }
 
+// The rows kernel's latency form, for copy-free launches up to rows_lat_groups() (serving batches,
+// single objects). In the kernel above the compiler issues every row pair's table loads up front,
+// each behind its own lgkmcnt(0), and spills them to VGPR lanes (102 SGPRs, 140-151 VGPRs at
+// K = 10, MT = 4): a serial chain of scalar-load latencies that a lone wave cannot hide. Here the
+// table pointer is re-issued by an empty asm after each pair's math (its input), so each pair's
+// loads wait only for the previous pair, and the tile index sits in an SGPR: no spills, 74 VGPRs.
+// Alone it is also faster on big launches (245.7 vs 250.7 us per GiB), but in the two-lane
+// bench step it competes with the other lane's decode instead of trickling beside it and the step
+// runs 6 % slower (profiles/headline/r07_rows), so big launches keep the kernel above.
+template <int MT, int K>
+__global__ __launch_bounds__(kBlock) void gf_gemm_rows_lat_kernel(DescView d, int k_tail, int m_pad, int ntiles,
+                                                                  int64_t col0, int64_t ngroups, int tail) {
+  d = stripe(d, K, m_pad);
+  const TileMap tm = map_block(ntiles);
+  const int i0 = sgpr_int(tm.tile * MT);
+  const int64_t g = tm.cb0 * kBlock + threadIdx.x;
+  if (g >= ngroups) {
+    if (g - ngroups < tail) tail_byte<MT>(d, k_tail, m_pad, i0, false, col0 + ngroups * 16 + (g - ngroups));
+    return;
+  }
+  const int64_t off = col0 + g * 16;
+  u32x4 x[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) x[j] = ld16<true>(row_vec(d.in[j], off));
+  u32x4 acc[MT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i) acc[i] = u32x4{0u, 0u, 0u, 0u};
+  uint64_t tb = (uint64_t)d.tab;
+#pragma unroll
+  for (int j = 0; j < K; j += 2) {
+    if (j > 0) {
+#pragma unroll
+      for (int i = 0; i < MT; ++i) asm volatile("" ::"v"(acc[i]));
+    }
+    asm volatile("" : "+s"(tb));
+    asm volatile("" : "+v"(x[j]));
+    if (j + 1 < K) asm volatile("" : "+v"(x[j + 1]));
+    const auto t0 = (cptr<uint32_t>)tb + (size_t(j) * m_pad + i0) * kPermStride;
+    if (j + 1 < K) {
+      const auto t1 = t0 + size_t(m_pad) * kPermStride;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        const Sel s0 = make_sel(x[j][w]);
+        const Sel s1 = make_sel(x[j + 1][w]);
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+          acc[i][w] = mac_pair(acc[i][w], t0 + i * kPermStride, s0, t1 + i * kPermStride, s1);
+      }
+    } else {
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        const Sel s = make_sel(x[j][w]);
+#pragma unroll
+        for (int i = 0; i < MT; ++i) acc[i][w] = mac_map(acc[i][w], t0 + i * kPermStride, s);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+#pragma unroll
+  for (int i = 0; i < MT; ++i) {
+    const uint64_t op = d.out[i0 + i];
+    if (op) st16<true>(row_vec_w(op, off), acc[i]);
+  }
+}
+
 // Byte kernel: one lane per byte column; any alignment (unaligned rows, column starts off a 16-byte
 // boundary). Each lane runs tail_byte: its k row bytes are loaded 8 at a time before use. SERIAL =
 // the round-3 form (load, copy-store, use, one row at a time: every load waits for the previous
@@ -391,14 +457,31 @@ struct Cfg {
   bool nt = false;
 };
 
+// Launches of at most this many 16-byte groups (all stripes of a batch) take the latency form of
+// the rows kernel: 2^22 groups = 64 MiB of every row. Measured (profiles/serving/r07_serve):
+// every serving batch up to 256 x 1 MiB objects encodes 15-30 % faster with it (256 x 64 KiB
+// 20.6 vs 28.0 us, 256 x 1 MiB 67 vs 96 us); the 1 GiB headline stripe (6.7 M groups) keeps the
+// throughput form for its two-lane overlap. GFRS_ROWS_LAT_GROUPS overrides (0 = never).
+int64_t rows_lat_groups() {
+  static const int64_t v = [] {
+    const char* e = std::getenv("GFRS_ROWS_LAT_GROUPS");
+    return e ? std::max<int64_t>(0, std::atoll(e)) : int64_t(1) << 22;
+  }();
+  return v;
+}
+
 template <int MT, int K>
 hipError_t launch_rows_k(const DescView& d, int m_pad, int batch, int64_t col0, int64_t ngroups, int tail,
-                         hipStream_t stream) {
+                         bool copies, hipStream_t stream) {
   const int ntiles = m_pad / MT;
   const Grid g = make_grid(ngroups + tail, ntiles, 0);  // one group per lane: the whole grid
   if (g.nblk == 0) return hipSuccess;
   if (g.ncb < g.nblk) return hipErrorInvalidValue;  // beyond one launch's work-items
-  gf_gemm_rows_kernel<MT, K><<<dim3(g.blocks, batch), kBlock, 0, stream>>>(d, K, m_pad, ntiles, col0, ngroups, tail);
+  if (!copies && (ngroups + tail) * batch <= rows_lat_groups())
+    gf_gemm_rows_lat_kernel<MT, K>
+        <<<dim3(g.blocks, batch), kBlock, 0, stream>>>(d, K, m_pad, ntiles, col0, ngroups, tail);
+  else
+    gf_gemm_rows_kernel<MT, K><<<dim3(g.blocks, batch), kBlock, 0, stream>>>(d, K, m_pad, ntiles, col0, ngroups, tail);
   return hipGetLastError();
 }
 
@@ -408,13 +491,13 @@ bool rows_supported(int k, int mt) { return mt <= 4 && (k == 4 || k == 8 || k ==
 
 template <int MT>
 hipError_t launch_rows(const DescView& d, int k, int m_pad, int batch, int64_t col0, int64_t ngroups, int tail,
-                       hipStream_t stream) {
+                       bool copies, hipStream_t stream) {
   if constexpr (MT <= 4) {
     switch (k) {
-      case 4: return launch_rows_k<MT, 4>(d, m_pad, batch, col0, ngroups, tail, stream);
-      case 8: return launch_rows_k<MT, 8>(d, m_pad, batch, col0, ngroups, tail, stream);
-      case 10: return launch_rows_k<MT, 10>(d, m_pad, batch, col0, ngroups, tail, stream);
-      case 16: return launch_rows_k<MT, 16>(d, m_pad, batch, col0, ngroups, tail, stream);
+      case 4: return launch_rows_k<MT, 4>(d, m_pad, batch, col0, ngroups, tail, copies, stream);
+      case 8: return launch_rows_k<MT, 8>(d, m_pad, batch, col0, ngroups, tail, copies, stream);
+      case 10: return launch_rows_k<MT, 10>(d, m_pad, batch, col0, ngroups, tail, copies, stream);
+      case 16: return launch_rows_k<MT, 16>(d, m_pad, batch, col0, ngroups, tail, copies, stream);
       default: break;
     }
   }
@@ -431,9 +514,9 @@ hipError_t launch_vec(const DescView& d, int k, int m_pad, int batch, int64_t co
     const int mt = c.pf == 0 ? MT : -c.pf;
     if (c.vec != 1 || max_blocks > 0 || m_pad % mt != 0 || !rows_supported(k, mt)) return hipErrorInvalidValue;
     switch (mt) {
-      case 1: return launch_rows<1>(d, k, m_pad, batch, col0, ngroups, tail, stream);
-      case 2: return launch_rows<2>(d, k, m_pad, batch, col0, ngroups, tail, stream);
-      case 4: return launch_rows<4>(d, k, m_pad, batch, col0, ngroups, tail, stream);
+      case 1: return launch_rows<1>(d, k, m_pad, batch, col0, ngroups, tail, true, stream);
+      case 2: return launch_rows<2>(d, k, m_pad, batch, col0, ngroups, tail, true, stream);
+      case 4: return launch_rows<4>(d, k, m_pad, batch, col0, ngroups, tail, true, stream);
       default: return hipErrorInvalidValue;
     }
   }
@@ -505,7 +588,7 @@ hipError_t run(const void* desc, int k, int m_pad, int batch, int64_t col0, int6
       return launch_byte<MT>(d, k, m_pad, batch, col0, ncols, max_blocks, stream, cfg && cfg->vec < 0);
     if (!cfg && !copies && max_blocks == 0 && rows_default(k, MT) &&
         (ncols / 16 + kBlock) / kBlock <= grid_cap(m_pad / MT))
-      return launch_rows<MT>(d, k, m_pad, batch, col0, ncols / 16, int(ncols % 16), stream);
+      return launch_rows<MT>(d, k, m_pad, batch, col0, ncols / 16, int(ncols % 16), false, stream);
     return launch_vec<MT>(d, k, m_pad, batch, col0, ncols, cfg ? *cfg : default_cfg(MT), max_blocks, stream);
   });
 }
@@ -518,8 +601,8 @@ hipError_t launch_gf_gemm(const void* desc, int k, int m_pad, int64_t col0, int6
 }
 
 hipError_t launch_gf_gemm_batched(const void* desc, int k, int m_pad, int batch, int64_t col0, int64_t ncols,
-                                  bool force_bytewise, hipStream_t stream) {
-  return run(desc, k, m_pad, batch, col0, ncols, force_bytewise, nullptr, 0, stream);
+                                  bool force_bytewise, hipStream_t stream, bool copies) {
+  return run(desc, k, m_pad, batch, col0, ncols, force_bytewise, nullptr, 0, stream, copies);
 }
 
 hipError_t launch_gf_gemm_variant(const void* desc, int k, int m_pad, int64_t col0, int64_t ncols, int vec, int pf,

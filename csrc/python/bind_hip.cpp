@@ -81,13 +81,14 @@ PYBIND11_MODULE(_hip, m) {
       py::arg("max_blocks") = 0, py::arg("stream") = 0, py::arg("copies") = true);
   m.def(
       "gemm_batched",
-      [](uint64_t desc, int k, int m_pad, int batch, int64_t col0, int64_t ncols, bool bytewise, uint64_t stream) {
+      [](uint64_t desc, int k, int m_pad, int batch, int64_t col0, int64_t ncols, bool bytewise, uint64_t stream,
+         bool copies) {
         check(launch_gf_gemm_batched(reinterpret_cast<const void*>(desc), k, m_pad, batch, col0, ncols, bytewise,
-                                     as_stream(stream)),
+                                     as_stream(stream), copies),
               "gf_gemm_batched");
       },
       py::arg("desc"), py::arg("k"), py::arg("m_pad"), py::arg("batch"), py::arg("col0"), py::arg("ncols"),
-      py::arg("bytewise") = false, py::arg("stream") = 0);
+      py::arg("bytewise") = false, py::arg("stream") = 0, py::arg("copies") = true);
   m.def(
       "gemm_variant",
       [](uint64_t desc, int k, int m_pad, int64_t col0, int64_t ncols, int vec, int pf, bool nt, int max_blocks,

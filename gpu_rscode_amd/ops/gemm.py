@@ -346,7 +346,8 @@ class GemmPlan:
         if self.batch > 1:
             if vec is not None:
                 raise ValueError("kernel variants are not selectable on batched plans")
-            h.gemm_batched(int(self.desc.data_ptr()), self.k, self.m_pad, self.batch, col0, ncols, self.bytewise, s)
+            h.gemm_batched(int(self.desc.data_ptr()), self.k, self.m_pad, self.batch, col0, ncols, self.bytewise, s,
+                           self.has_copies)
         elif self.engine == "mfma" and vec is None and col0 % 2 == 0:
             h.gemm_fp4(int(self.bitmat.data_ptr()), int(self.desc.data_ptr()), self.k, self.m, col0, ncols,
                        self.mfma_mg, self.in_stride, self.has_copies, s)
