@@ -292,15 +292,17 @@ __global__ __launch_bounds__(kBlock) void gf_gemm_rows_kernel(DescView d, int k_
 // Alone it is also faster on big launches (245.7 vs 250.7 us per GiB), but in the two-lane
 // bench step it competes with the other lane's decode instead of trickling beside it and the step
 // runs 6 % slower (profiles/headline/r07_rows), so big launches keep the kernel above.
-template <int MT, int K>
+// COPY: fused survivor copies (tile 0 of a decode), stored as each row pair is consumed.
+template <int MT, int K, bool COPY>
 __global__ __launch_bounds__(kBlock) void gf_gemm_rows_lat_kernel(DescView d, int k_tail, int m_pad, int ntiles,
                                                                   int64_t col0, int64_t ngroups, int tail) {
   d = stripe(d, K, m_pad);
   const TileMap tm = map_block(ntiles);
   const int i0 = sgpr_int(tm.tile * MT);
+  const bool do_copy = COPY && (tm.tile == 0);
   const int64_t g = tm.cb0 * kBlock + threadIdx.x;
   if (g >= ngroups) {
-    if (g - ngroups < tail) tail_byte<MT>(d, k_tail, m_pad, i0, false, col0 + ngroups * 16 + (g - ngroups));
+    if (g - ngroups < tail) tail_byte<MT>(d, k_tail, m_pad, i0, do_copy, col0 + ngroups * 16 + (g - ngroups));
     return;
   }
   const int64_t off = col0 + g * 16;
@@ -320,6 +322,14 @@ __global__ __launch_bounds__(kBlock) void gf_gemm_rows_lat_kernel(DescView d, in
     asm volatile("" : "+s"(tb));
     asm volatile("" : "+v"(x[j]));
     if (j + 1 < K) asm volatile("" : "+v"(x[j + 1]));
+    if (COPY && do_copy) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+        if (j + u < K) {
+          const uint64_t cp = d.copy[j + u];
+          if (cp) st16<true>(row_vec_w(cp, off), x[j + u]);
+        }
+    }
     const auto t0 = (cptr<uint32_t>)tb + (size_t(j) * m_pad + i0) * kPermStride;
     if (j + 1 < K) {
       const auto t1 = t0 + size_t(m_pad) * kPermStride;
@@ -477,10 +487,14 @@ hipError_t launch_rows_k(const DescView& d, int m_pad, int batch, int64_t col0, 
   const Grid g = make_grid(ngroups + tail, ntiles, 0);  // one group per lane: the whole grid
   if (g.nblk == 0) return hipSuccess;
   if (g.ncb < g.nblk) return hipErrorInvalidValue;  // beyond one launch's work-items
-  if (!copies && (ngroups + tail) * batch <= rows_lat_groups())
-    gf_gemm_rows_lat_kernel<MT, K>
-        <<<dim3(g.blocks, batch), kBlock, 0, stream>>>(d, K, m_pad, ntiles, col0, ngroups, tail);
-  else
+  if ((ngroups + tail) * batch <= rows_lat_groups()) {
+    if (copies)
+      gf_gemm_rows_lat_kernel<MT, K, true>
+          <<<dim3(g.blocks, batch), kBlock, 0, stream>>>(d, K, m_pad, ntiles, col0, ngroups, tail);
+    else
+      gf_gemm_rows_lat_kernel<MT, K, false>
+          <<<dim3(g.blocks, batch), kBlock, 0, stream>>>(d, K, m_pad, ntiles, col0, ngroups, tail);
+  } else
     gf_gemm_rows_kernel<MT, K><<<dim3(g.blocks, batch), kBlock, 0, stream>>>(d, K, m_pad, ntiles, col0, ngroups, tail);
   return hipGetLastError();
 }
@@ -586,8 +600,13 @@ hipError_t run(const void* desc, int k, int m_pad, int batch, int64_t col0, int6
     constexpr int MT = decltype(mt)::value;
     if (bytewise || (col0 & 15) || (cfg && cfg->vec < 0))
       return launch_byte<MT>(d, k, m_pad, batch, col0, ncols, max_blocks, stream, cfg && cfg->vec < 0);
-    if (!cfg && !copies && max_blocks == 0 && rows_default(k, MT) &&
-        (ncols / 16 + kBlock) / kBlock <= grid_cap(m_pad / MT))
+    const bool fits = (ncols / 16 + kBlock) / kBlock <= grid_cap(m_pad / MT);
+    // small launches (serving): the latency form of the rows kernel for every shape it has, with
+    // or without fused copies (launch_rows_k picks it by size)
+    if (!cfg && max_blocks == 0 && fits && rows_supported(k, MT) &&
+        (ncols / 16 + ncols % 16) * batch <= rows_lat_groups())
+      return launch_rows<MT>(d, k, m_pad, batch, col0, ncols / 16, int(ncols % 16), copies, stream);
+    if (!cfg && !copies && max_blocks == 0 && rows_default(k, MT) && fits)
       return launch_rows<MT>(d, k, m_pad, batch, col0, ncols / 16, int(ncols % 16), false, stream);
     return launch_vec<MT>(d, k, m_pad, batch, col0, ncols, cfg ? *cfg : default_cfg(MT), max_blocks, stream);
   });
