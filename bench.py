@@ -764,7 +764,7 @@ def mode_entry(r, rank) -> dict:
             "steps": r["steps"], "bytes_sent_per_rank_step": r["sent"],
             "bytes_recv_rank0_step": r["recv"] if rank == 0 else None,
             "busiest_link_bytes_per_step": r["link"],
-            "busiest_link_GBps_implied": round(r["link"] / (r["elapsed"] / r["steps"]) / 1e9, 2),
+            "busiest_link_GBps_implied": round(r["link"] / (r["elapsed"] / r["steps"]) / 1e9, 4),
             "step_ms_by_rank": [round(x / r["steps"] * 1e3, 4) for x in r["per_rank"]],
             "verified": r["ok"]}
 
