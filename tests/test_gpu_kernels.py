@@ -473,3 +473,42 @@ def test_lds_lut_kernel_gf16_maps():
         for j in range(k):
             want[i] ^= maps[i, j][host[j]]
     assert np.array_equal(out.cpu().numpy(), want)
+
+
+_FORMS_SNIPPET = r"""
+import sys
+import numpy as np, torch
+sys.path.insert(0, %r)
+from gpu_rscode_amd.gf import GF256
+from gpu_rscode_amd.models import alloc_rows
+from gpu_rscode_amd.ops import GemmPlan
+for k, m, C, copies in ((10, 4, 1000003, False), (10, 4, 1000003, True), (4, 2, 65536 + 5, True), (16, 3, 77777, False)):
+    g = np.random.default_rng(k * 7 + m)
+    host = g.integers(0, 256, size=(k, C), dtype=np.uint8)
+    coeff = g.integers(0, 256, size=(m, k), dtype=np.uint8)
+    dev = alloc_rows(k, C, "cuda"); dev.copy_(torch.from_numpy(host))
+    out = alloc_rows(m, C, "cuda", fill=0xAB)
+    cp = alloc_rows(k, C, "cuda", fill=0) if copies else None
+    GemmPlan(dev, out, coeff, copies=[cp[j] for j in range(k)] if copies else None).run()
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), GF256.gemm(coeff, host)), (k, m, C, copies)
+    if copies:
+        assert np.array_equal(cp.cpu().numpy(), host), (k, m, C)
+print("FORMS-OK")
+"""
+
+
+@pytest.mark.parametrize("lat_groups", ["0", "1000000000"])
+def test_rows_kernel_forms_match_oracle(lat_groups):
+    """Both forms of the rows-in-flight kernel on the same shapes: GFRS_ROWS_LAT_GROUPS=0 forces the
+    throughput form (the 1 GiB headline's; small test launches otherwise take the latency form),
+    10^9 the latency form (also for fused-copy decodes). Subprocess: the threshold is read once."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, GFRS_ROWS_LAT_GROUPS=lat_groups)
+    r = subprocess.run([sys.executable, "-c", _FORMS_SNIPPET % root], capture_output=True, text=True, timeout=300,
+                       env=env)
+    assert r.returncode == 0 and "FORMS-OK" in r.stdout, (r.stdout[-2000:], r.stderr[-3000:])
