@@ -222,7 +222,7 @@ class GemmPlan:
         self.desc = torch.from_numpy(host).to(self.device)
         self.layout = desc_layout(self.k, self.m_pad, self.batch)
         if engine == "auto":
-            engine = _auto_engine(self.k, self.m, maps is None, self.bytewise, self.batch)
+            engine = _auto_engine(self.k, self.m, maps is None, self.bytewise, self.batch, self.ncols)
         self.engine = engine
         self.bitmat = None
         if engine in ("mfma", "mfma_i8"):
@@ -367,10 +367,22 @@ class GemmPlan:
 # from k*m ~ 2k coefficients (k=128, p=32: 1.10 ms vs 1.45 ms per GiB); narrow codes stay on the
 # v_perm kernel, which is at the HBM roofline there (k=10, p=4: 0.27 ms vs 0.87 ms).
 _MFMA_MIN_K, _MFMA_MIN_M = 64, 16
+# Short rows move the crossover down: the v_perm kernel parallelises over columns (and output
+# tiles) only, so a few-KiB stripe leaves most of the chip idle while each lane walks all k rows,
+# whereas the FP4 kernel reduces over k in the matrix cores. scripts/engine_cross.py on MI355X
+# (profiles/sweeps/r07_engine_cross): up to 512 KiB per row the FP4 kernel wins from k = 16, m = 4
+# (k=16 m=4: 7.4 vs 8.8 us; k=32 m=8: 7.5 vs 25.5; k=128 m=32: 17.6 vs 261), up to 4 MiB from
+# k = 32, m = 8 (k=32 m=8: 49 vs 62 us); past that only the wide codes above.
+_SHORT_ROW, _MID_ROW = 512 << 10, 4 << 20
 
 
-def _auto_engine(k: int, m: int, gf256: bool, bytewise: bool, batch: int) -> str:
-    if gf256 and not bytewise and batch == 1 and k >= _MFMA_MIN_K and m >= _MFMA_MIN_M:
+def _auto_engine(k: int, m: int, gf256: bool, bytewise: bool, batch: int, ncols: int | None = None) -> str:
+    if not gf256 or bytewise or batch != 1:
+        return "valu"
+    if k >= _MFMA_MIN_K and m >= _MFMA_MIN_M:
+        return "mfma"
+    if ncols is not None and ((ncols <= _SHORT_ROW and k >= 16 and m >= 4) or
+                              (ncols <= _MID_ROW and k >= 32 and m >= 8)):
         return "mfma"
     return "valu"
 
