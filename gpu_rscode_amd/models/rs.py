@@ -396,12 +396,19 @@ class ReedSolomon:
                 exception (checked lazily, no host sync on the hot path).
         """
         fast = None
-        if (not device_invert and isinstance(survivors, torch.Tensor) and isinstance(out, torch.Tensor)
-                and survivors.is_cuda):
-            # repeat calls on the same 2-D buffers and pattern: one dict lookup (see encode)
-            fast = ("dec2d", tuple(int(r) for r in rows), survivors.data_ptr(), survivors.shape, survivors.stride(),
-                    out.data_ptr(), out.shape, out.stride())
-            plan = self._plans.get(fast)
+        if not device_invert and isinstance(out, torch.Tensor) and out.dim() == 2 and out.is_cuda:
+            # repeat calls on the same buffers and pattern: one dict lookup (see encode). Survivors as
+            # a 2-D tensor key on its pointer / shape / strides; as a list of rows (the usual decode:
+            # surviving chunks live in different buffers) on each row's pointer and length — 64
+            # per-row views of `out` and a per-row key of both sides cost ~180 us a call at k = 64
+            if isinstance(survivors, torch.Tensor):
+                if survivors.is_cuda:
+                    fast = ("dec2d", tuple(int(r) for r in rows), survivors.data_ptr(), survivors.shape,
+                            survivors.stride(), out.data_ptr(), out.shape, out.stride())
+            else:
+                fast = ("decL", tuple(int(r) for r in rows), tuple((s.data_ptr(), s.numel()) for s in survivors),
+                        out.data_ptr(), out.shape, out.stride())
+            plan = self._plans.get(fast) if fast is not None else None
             if plan is not None:
                 plan.run(stream)
                 return out
