@@ -235,11 +235,16 @@ class ReedSolomon:
     def encode(self, data, parity=None, stream: torch.cuda.Stream | None = None):
         """parity = E . data. ``data``: [k, C] tensor or k rows. Returns the parity rows."""
         fast = None
-        if isinstance(data, torch.Tensor) and isinstance(parity, torch.Tensor) and data.is_cuda:
-            # repeat calls on the same 2-D buffers: one dict lookup, no per-row views (a small-object
-            # encode is launch-bound; building 14 row views and their key took longer than the kernel)
-            fast = ("enc2d", data.data_ptr(), data.shape, data.stride(), parity.data_ptr(), parity.shape,
-                    parity.stride())
+        if isinstance(parity, torch.Tensor) and parity.dim() == 2 and parity.is_cuda:
+            # repeat calls on the same buffers: one dict lookup, no per-row views (a small-object
+            # encode is launch-bound; building 14 row views and their key took longer than the kernel);
+            # data as a list of rows keys on each row's pointer and length
+            if isinstance(data, torch.Tensor):
+                fast = ("enc2d", data.data_ptr(), data.shape, data.stride(), parity.data_ptr(), parity.shape,
+                        parity.stride())
+            else:
+                fast = ("encL", tuple((d.data_ptr(), d.numel()) for d in data), parity.data_ptr(), parity.shape,
+                        parity.stride())
             plan = self._plans.get(fast)
             if plan is not None:
                 plan.run(stream)
