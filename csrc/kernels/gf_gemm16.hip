@@ -22,6 +22,7 @@
 // aligned. Rows must be 2-byte aligned and column ranges whole symbols (even byte offsets/counts).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 
 #include "gfrs/desc.h"
@@ -184,8 +185,8 @@ inline Grid make_grid(int64_t items, int ntiles, int max_blocks) {
 // Output tile of the w = 16 kernel: the GF(2^8) tile (gfrs/desc.h tile_for) capped at 8, since
 // each output holds four accumulator dwords per 16-byte group here (two planes x two dwords).
 template <typename F>
-hipError_t dispatch16(int m_pad, F&& f) {
-  switch (tile_for(m_pad)) {
+hipError_t dispatch16(int m_pad, int mt_cap, F&& f) {
+  switch (std::min(tile_for(m_pad), mt_cap)) {
     case 1: return f(std::integral_constant<int, 1>{});
     case 2: return f(std::integral_constant<int, 2>{});
     case 4: return f(std::integral_constant<int, 4>{});
@@ -201,7 +202,19 @@ hipError_t launch_gf_gemm16(const void* desc, int k, int m_pad, int64_t col0, in
   if ((col0 | ncols) & 1) return hipErrorInvalidValue;  // whole 16-bit symbols only
   if (m_pad % tile_for(m_pad) != 0) return hipErrorInvalidValue;
   const DescView d = view16(desc, k, m_pad);
-  return dispatch16(m_pad, [&](auto mt) -> hipError_t {
+  // Short rows: one output per tile. The kernel parallelises over columns and output tiles only,
+  // so a row of a few KiB is a handful of blocks each walking all k rows for 8 outputs (k = 300,
+  // m = 40, 3.4 KiB: 5 blocks). One output per tile puts m times as many blocks on the chip; the
+  // inputs they re-read are small enough to stay in L2. GFRS_GF16_SHORT_GROUPS sets the cut
+  // (16-byte groups per row, default 32768 = 512 KiB; 0 = never). Measured (profiles/gf65536/
+  // r07_short): k = 300 m = 40, 3.4 KiB rows 1.05 -> 0.24 ms, 218 KiB rows 1.11 -> 0.64 ms;
+  // k = 64 m = 16, 256 KiB rows 0.145 -> 0.055 ms; at 1 MiB rows one output per tile loses.
+  static const int64_t short_groups = [] {
+    const char* e = std::getenv("GFRS_GF16_SHORT_GROUPS");
+    return e ? std::max<int64_t>(0, std::atoll(e)) : int64_t(32768);
+  }();
+  const int mt_cap = ncols / 16 < short_groups ? 1 : 8;
+  return dispatch16(m_pad, mt_cap, [&](auto mt) -> hipError_t {
     constexpr int MT = decltype(mt)::value;
     const int ntiles = m_pad / MT;
     if (symwise || (col0 & 15)) {
