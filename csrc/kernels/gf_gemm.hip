@@ -358,6 +358,87 @@ __global__ __launch_bounds__(kBlock) void gf_gemm_rows_lat_kernel(DescView d, in
   }
 }
 
+// K-split kernel (short rows of wide codes, e.g. batched RS(128,160) serving objects): the vec
+// kernel parallelises over 16-byte column groups and output tiles only, so a 512-byte row gives
+// 32 lanes per tile and each of them walks all k rows with PF in flight — at k = 128 a 64-deep
+// chain of load latencies per launch (~70 us whatever the batch, profiles/serving/r07_wide).
+// Here the k rows are split over the KS waves of a block (wave s owns rows [s R, s R + R), R =
+// ceil(k / KS), 8 in flight per lane), each wave covers the same 64 column groups, and the KS
+// partial products are XOR-reduced through LDS; every thread of the block then stores part of
+// the MT x 64 result groups. Fused copies: tile 0 stores each row it loads. Column tails
+// (ncols % 16) go to the byte kernel.
+template <int MT, int KS>
+__global__ __launch_bounds__(64 * KS) void gf_gemm_ksplit_kernel(DescView d, int k, int m_pad, int ntiles,
+                                                                 int64_t col0, int64_t ngroups, int copies) {
+  constexpr int kRB = 8;
+  __shared__ u32x4 red[KS][MT][64];
+  d = stripe(d, k, m_pad);
+  const int tile = int(blockIdx.x % unsigned(ntiles));
+  const int64_t cb = int64_t(blockIdx.x / unsigned(ntiles));
+  const int i0 = tile * MT;
+  const int lane = int(threadIdx.x & 63u);
+  const int s = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
+  const int64_t g = cb * 64 + lane;
+  const bool live = g < ngroups;
+  const int64_t off = col0 + (live ? g : cb * 64) * 16;  // dead lanes re-read the block's first group
+  const bool do_copy = copies && tile == 0;
+  const int R = (k + KS - 1) / KS;
+  const int jb = s * R, je = min(k, jb + R);
+
+  u32x4 acc[MT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i) acc[i] = u32x4{0u, 0u, 0u, 0u};
+  for (int j0 = jb; j0 < je; j0 += kRB) {
+    u32x4 x[kRB];
+#pragma unroll
+    for (int u = 0; u < kRB; ++u) x[u] = j0 + u < je ? ld16<false>(row_vec(d.in[j0 + u], off)) : u32x4{0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int u = 0; u < kRB; u += 2) {
+      const int j = j0 + u;
+      if (j >= je) break;
+      if (do_copy && live) {
+        const uint64_t cp0 = d.copy[j];
+        if (cp0) st16<false>(row_vec_w(cp0, off), x[u]);
+        if (j + 1 < je) {
+          const uint64_t cp1 = d.copy[j + 1];
+          if (cp1) st16<false>(row_vec_w(cp1, off), x[u + 1]);
+        }
+      }
+      const auto t0 = d.tab + (size_t(j) * m_pad + i0) * kPermStride;
+      if (j + 1 < je) {
+        const auto t1 = t0 + size_t(m_pad) * kPermStride;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+          const Sel s0 = make_sel(x[u][w]);
+          const Sel s1 = make_sel(x[u + 1][w]);
+#pragma unroll
+          for (int i = 0; i < MT; ++i)
+            acc[i][w] = mac_pair(acc[i][w], t0 + i * kPermStride, s0, t1 + i * kPermStride, s1);
+        }
+      } else {
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+          const Sel s0 = make_sel(x[u][w]);
+#pragma unroll
+          for (int i = 0; i < MT; ++i) acc[i][w] = mac_map(acc[i][w], t0 + i * kPermStride, s0);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < MT; ++i) red[s][i][lane] = acc[i];
+  __syncthreads();
+  for (int r = int(threadIdx.x); r < MT * 64; r += 64 * KS) {
+    const int i = r >> 6, l = r & 63;
+    u32x4 v = red[0][i][l];
+#pragma unroll
+    for (int q = 1; q < KS; ++q) v ^= red[q][i][l];
+    const int64_t gg = cb * 64 + l;
+    const uint64_t op = d.out[i0 + i];
+    if (gg < ngroups && op) st16<false>(row_vec_w(op, col0 + gg * 16), v);
+  }
+}
+
 // Byte kernel: one lane per byte column; any alignment (unaligned rows, column starts off a 16-byte
 // boundary). Each lane runs tail_byte: its k row bytes are loaded 8 at a time before use. SERIAL =
 // the round-3 form (load, copy-store, use, one row at a time: every load waits for the previous
@@ -450,8 +531,7 @@ hipError_t launch_byte(const DescView& d, int k, int m_pad, int batch, int64_t c
 }
 
 template <typename F>
-hipError_t dispatch_tile(int m_pad, F&& f) {
-  const int t = tile_for(m_pad);
+hipError_t dispatch_tile(int t, F&& f) {
   switch (t) {
     case 1: return f(std::integral_constant<int, 1>{});
     case 2: return f(std::integral_constant<int, 2>{});
@@ -478,6 +558,52 @@ int64_t rows_lat_groups() {
     return e ? std::max<int64_t>(0, std::atoll(e)) : int64_t(1) << 22;
   }();
   return v;
+}
+
+// Lane target of a wide-code launch (output tile of 8+ rows) that the k-split kernel does not
+// take, before its tile is narrowed; GFRS_SHORT_LANES sets it (default 0 = never narrow: the
+// k-split kernel beat every narrowed tile on the short-row points, profiles/serving/r07_wide).
+int64_t short_lanes() {
+  static const int64_t v = [] {
+    const char* e = std::getenv("GFRS_SHORT_LANES");
+    return e ? std::max<int64_t>(0, std::atoll(e)) : int64_t(0);
+  }();
+  return v;
+}
+
+// Launches whose lanes (16-byte groups x stripes x output tiles at the widest tile) number fewer
+// than this take the k-split kernel when k >= 32; GFRS_KSPLIT_LANES overrides (0 = never).
+// Measured with scripts/serve_bench.py --code (profiles/serving/r07_wide): RS(128,160) encode
+// 16 x 64 KiB 272 -> 20 us, 256 x 1 MiB (262 K lanes) 2826 -> 721 us, decode 72 -> 23 us;
+// RS(64,80) 256 x 1 MiB 749 -> 314 us; RS(32,40) 256 x 1 MiB (524 K lanes) is the one point
+// where the vec kernel stays ahead (109 vs 176 us), so the bound sits between the two.
+int64_t ksplit_lanes() {
+  static const int64_t v = [] {
+    const char* e = std::getenv("GFRS_KSPLIT_LANES");
+    return e ? std::max<int64_t>(0, std::atoll(e)) : int64_t(1) << 19;
+  }();
+  return v;
+}
+
+constexpr int kSplit = 8;  // waves per k-split block
+
+template <int MT>
+hipError_t launch_ksplit(const DescView& d, int k, int m_pad, int batch, int64_t col0, int64_t ncols, bool copies,
+                         hipStream_t stream) {
+  if constexpr (MT > 8) {
+    return hipErrorInvalidValue;  // LDS: KS x MT x 1 KiB
+  } else {
+    const int ntiles = m_pad / MT;
+    const int64_t ngroups = ncols / 16;
+    const int64_t ncb = (ngroups + 63) / 64;
+    if (ncb * ntiles > int64_t(UINT32_MAX)) return hipErrorInvalidValue;
+    if (ncb > 0)
+      gf_gemm_ksplit_kernel<MT, kSplit><<<dim3(unsigned(ncb * ntiles), batch), 64 * kSplit, 0, stream>>>(
+          d, k, m_pad, ntiles, col0, ngroups, copies ? 1 : 0);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess || ncols % 16 == 0) return e;
+    return launch_byte<MT>(d, k, m_pad, batch, col0 + ngroups * 16, ncols % 16, 0, stream);
+  }
 }
 
 template <int MT, int K>
@@ -596,8 +722,22 @@ hipError_t run(const void* desc, int k, int m_pad, int batch, int64_t col0, int6
   if (k <= 0 || m_pad <= 0 || ncols <= 0 || batch <= 0) return batch < 0 ? hipErrorInvalidValue : hipSuccess;
   if (m_pad % tile_for(m_pad) != 0 || batch > 65535) return hipErrorInvalidValue;
   const DescView d = view(desc, k, m_pad, batch);
-  return dispatch_tile(m_pad, [&](auto mt) -> hipError_t {
+  int tile = tile_for(m_pad);
+  const bool auto_cfg = !cfg && max_blocks == 0 && !bytewise && !(col0 & 15);
+  const bool ksplit = auto_cfg && k >= 32 && (ncols / 16 + ncols % 16) * batch * (m_pad / tile) < ksplit_lanes();
+  if (ksplit) tile = std::min(tile, 8);
+  if (auto_cfg && !ksplit && tile >= 8) {
+    // short rows of a wide code: the column groups alone leave lanes idle, so trade output-tile
+    // width for more tiles until the launch has short_lanes() lanes
+    int64_t lanes = (ncols / 16 + ncols % 16) * batch * (m_pad / tile);
+    while (tile > 1 && lanes < short_lanes()) {
+      tile /= 2;
+      lanes *= 2;
+    }
+  }
+  return dispatch_tile(tile, [&](auto mt) -> hipError_t {
     constexpr int MT = decltype(mt)::value;
+    if (ksplit) return launch_ksplit<MT>(d, k, m_pad, batch, col0, ncols, copies, stream);
     if (bytewise || (col0 & 15) || (cfg && cfg->vec < 0))
       return launch_byte<MT>(d, k, m_pad, batch, col0, ncols, max_blocks, stream, cfg && cfg->vec < 0);
     const bool fits = (ncols / 16 + kBlock) / kBlock <= grid_cap(m_pad / MT);

@@ -48,8 +48,7 @@ def timed(fn, reps: int) -> float:
     return float(np.median(ts))
 
 
-def point(S: int, B: int, reps: int) -> dict:
-    k, n = 10, 14
+def point(S: int, B: int, reps: int, k: int = 10, n: int = 14) -> dict:
     p = n - k
     C = (S + k - 1) // k
     dev = torch.device("cuda", 0)
@@ -57,7 +56,11 @@ def point(S: int, B: int, reps: int) -> dict:
     data, dbase = batch_rows(B, k, C, dev)
     fill_random_(dbase, seed=S + B)
     parity, _ = batch_rows(B, p, C, dev)
-    rows = [0, 2, 3, 4, 6, 7, 9, 10, 11, 13]  # natives 1, 5, 8 and parity 12 lost on every object
+    if (k, n) == (10, 14):
+        rows = [0, 2, 3, 4, 6, 7, 9, 10, 11, 13]  # natives 1, 5, 8 and parity 12 lost on every object
+    else:  # up to three natives and the first parity lost
+        lost = sorted({1, k // 2, k - 2})[:max(1, min(3, p - 1))] + ([k] if p > 1 else [])
+        rows = [r for r in range(n) if r not in lost][:k]
     surv, _ = batch_rows(B, k, C, dev)
     out, _ = batch_rows(B, k, C, dev)
 
@@ -119,12 +122,13 @@ def main() -> int:
     ap.add_argument("--sizes", default="65536,262144,1048576,4194304")
     ap.add_argument("--batches", default="1,16,256")
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--code", default="10:14", help="k:n of the code (default the headline's RS(10,14))")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     pts = []
     for S in map(int, a.sizes.split(",")):
         for B in map(int, a.batches.split(",")):
-            r = point(S, B, a.reps)
+            r = point(S, B, a.reps, *(int(v) for v in a.code.split(":")))
             print(json.dumps(r), flush=True)
             pts.append(r)
             torch.cuda.empty_cache()

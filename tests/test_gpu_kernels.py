@@ -512,3 +512,50 @@ def test_rows_kernel_forms_match_oracle(lat_groups):
     r = subprocess.run([sys.executable, "-c", _FORMS_SNIPPET % root], capture_output=True, text=True, timeout=300,
                        env=env)
     assert r.returncode == 0 and "FORMS-OK" in r.stdout, (r.stdout[-2000:], r.stderr[-3000:])
+
+
+_WIDE_BATCH_SNIPPET = r"""
+import sys
+import numpy as np, torch
+sys.path.insert(0, %r)
+from gpu_rscode_amd.gf import GF256
+from gpu_rscode_amd.models import alloc_rows
+from gpu_rscode_amd.ops import GemmPlan
+for k, m, C, B, copies in ((128, 32, 512, 3, False), (128, 3, 8192, 2, True), (33, 5, 1000, 4, True),
+                           (64, 16, 4099, 2, False), (40, 9, 70000, 2, True)):
+    g = np.random.default_rng(k * 7 + m + C)
+    host = g.integers(0, 256, size=(B, k, C), dtype=np.uint8)
+    coeff = g.integers(0, 256, size=(m, k), dtype=np.uint8)
+    ins = [alloc_rows(k, C, "cuda") for _ in range(B)]
+    for b in range(B):
+        ins[b].copy_(torch.from_numpy(host[b]))
+    outs = [alloc_rows(m, C, "cuda", fill=0xAB) for _ in range(B)]
+    cps = [alloc_rows(k, C, "cuda", fill=0) for _ in range(B)] if copies else None
+    plan = GemmPlan([[r for r in x] for x in ins], [[r for r in o] for o in outs], coeff,
+                    copies=[[c[j] if j %% 3 else None for j in range(k)] for c in cps] if copies else None)
+    plan.run()
+    torch.cuda.synchronize()
+    for b in range(B):
+        assert np.array_equal(outs[b].cpu().numpy(), GF256.gemm(coeff, host[b])), (k, m, C, B, b)
+        if copies:
+            want = host[b].copy(); want[::3] = 0
+            assert np.array_equal(cps[b].cpu().numpy(), want), (k, m, C, B, b)
+print("WIDE-OK")
+"""
+
+
+@pytest.mark.parametrize("knobs", [("0", "0"), ("0", "1000000000000"), ("1000000000000", "0")])
+def test_batched_wide_kernels_match_oracle(knobs):
+    """Batched wide-code launches on every kernel that can take them: the vec kernel at its widest
+    tile (both knobs 0), with the tile narrowed for short rows (GFRS_SHORT_LANES), and the k-split
+    kernel (GFRS_KSPLIT_LANES, LDS reduction over row slices; ragged columns and fused copies
+    included). Subprocess: the thresholds are read once."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, GFRS_KSPLIT_LANES=knobs[0], GFRS_SHORT_LANES=knobs[1])
+    r = subprocess.run([sys.executable, "-c", _WIDE_BATCH_SNIPPET % root], capture_output=True, text=True,
+                       timeout=300, env=env)
+    assert r.returncode == 0 and "WIDE-OK" in r.stdout, (r.stdout[-2000:], r.stderr[-3000:])
