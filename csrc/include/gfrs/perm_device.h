@@ -98,13 +98,16 @@ __device__ __forceinline__ int sgpr_int(int v) {
 
 // Block -> (column block, output tile) mapping. Blocks b and b+8 share an XCD under the observed
 // round-robin dispatch; consecutive `local` ids of one XCD sweep the tiles of one column block.
-// Placement only affects speed, never correctness.
+// Placement only affects speed, never correctness. Grids of fewer than 8 column blocks are not
+// padded to 8 (make_grid) and map plainly: padded, their live blocks sat on the first ncb XCDs
+// only — for every stripe of a batch, since a row of 8 x ntiles blocks keeps x & 7 = XCD.
 struct TileMap {
   int tile;
   int64_t cb0;
 };
 __device__ __forceinline__ TileMap map_block(int ntiles) {
   const int bid = blockIdx.x;
+  if (gridDim.x % (8u * unsigned(ntiles)) != 0) return {bid % ntiles, int64_t(bid / ntiles)};
   const int xcd = bid & 7;
   const int local = bid >> 3;
   return {local % ntiles, int64_t(local / ntiles) * 8 + xcd};

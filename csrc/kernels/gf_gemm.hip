@@ -498,7 +498,7 @@ inline Grid make_grid(int64_t items, int ntiles, int max_blocks) {
   g.ncb = g.nblk;
   if (max_blocks > 0 && g.ncb > max_blocks) g.ncb = max_blocks;
   if (g.ncb > grid_cap(ntiles)) g.ncb = grid_cap(ntiles);
-  const int64_t ncb8 = (g.ncb + 7) / 8 * 8;
+  const int64_t ncb8 = g.ncb < 8 ? g.ncb : (g.ncb + 7) / 8 * 8;  // short: unpadded (map_block)
   g.blocks = static_cast<unsigned>(ncb8 * ntiles);
   return g;
 }
@@ -573,14 +573,15 @@ int64_t short_lanes() {
 
 // Launches whose lanes (16-byte groups x stripes x output tiles at the widest tile) number fewer
 // than this take the k-split kernel when k >= 32; GFRS_KSPLIT_LANES overrides (0 = never).
-// Measured with scripts/serve_bench.py --code (profiles/serving/r07_wide): RS(128,160) encode
-// 16 x 64 KiB 272 -> 20 us, 256 x 1 MiB (262 K lanes) 2826 -> 721 us, decode 72 -> 23 us;
-// RS(64,80) 256 x 1 MiB 749 -> 314 us; RS(32,40) 256 x 1 MiB (524 K lanes) is the one point
-// where the vec kernel stays ahead (109 vs 176 us), so the bound sits between the two.
+// Measured with scripts/serve_bench.py --code (profiles/serving/r07_wide/xcd): the k-split kernel
+// wins every point up to 65 K lanes (RS(128,160) 16 x 64 KiB encode 294 -> 23 us, 16 x 1 MiB
+// 263 -> 51 us; RS(64,80) 16 x 4 MiB 141 -> 88 us; RS(32,40) 16 x 1 MiB 33 -> 18 us) and the vec
+// kernel every point from 131 K (RS(128,160) 256 x 1 MiB 432 vs 738 us; RS(32,40) 256 x 256 KiB
+// 41 vs 51 us).
 int64_t ksplit_lanes() {
   static const int64_t v = [] {
     const char* e = std::getenv("GFRS_KSPLIT_LANES");
-    return e ? std::max<int64_t>(0, std::atoll(e)) : int64_t(1) << 19;
+    return e ? std::max<int64_t>(0, std::atoll(e)) : int64_t(1) << 17;
   }();
   return v;
 }

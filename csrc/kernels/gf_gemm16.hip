@@ -178,7 +178,7 @@ inline Grid make_grid(int64_t items, int ntiles, int max_blocks) {
   if (max_blocks > 0 && g.ncb > max_blocks) g.ncb = max_blocks;
   const int64_t cap = kMaxGridBlocks / ntiles / 8 * 8;
   if (g.ncb > cap) g.ncb = cap;
-  g.blocks = static_cast<unsigned>((g.ncb + 7) / 8 * 8 * ntiles);
+  g.blocks = static_cast<unsigned>((g.ncb < 8 ? g.ncb : (g.ncb + 7) / 8 * 8) * ntiles);  // see map_block
   return g;
 }
 
