@@ -1,6 +1,7 @@
 """Host sanitizer run: the CPU codec, METADATA/conf parsing and the file codec under
 ASan + UBSan (bin/CPU-RS-asan, built by `make -C csrc sanitize`). Exercises odd sizes, every
 erasure subset at (4,6), wide stripes, CRC rejection and malformed inputs."""
+import fcntl
 import itertools
 import os
 import subprocess
@@ -13,7 +14,11 @@ from gpu_rscode_amd.utils import fileformat as ff
 
 @pytest.fixture(scope="module")
 def exe():
-    r = subprocess.run(["make", "-C", str(CSRC), "-j8", "sanitize"], capture_output=True, text=True, timeout=600)
+    # one build at a time: parallel test workers (pytest -n) would otherwise relink the binary
+    # while another worker runs it
+    with open(os.path.join(str(CSRC), ".sanitize.lock"), "w") as lock:
+        fcntl.flock(lock, fcntl.LOCK_EX)
+        r = subprocess.run(["make", "-C", str(CSRC), "-j8", "sanitize"], capture_output=True, text=True, timeout=600)
     if r.returncode != 0:
         pytest.skip(f"sanitizer build unavailable: {r.stderr[-500:]}")
     return str(binary("CPU-RS-asan"))
