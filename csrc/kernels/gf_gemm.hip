@@ -371,7 +371,9 @@ template <int MT, int KS>
 __global__ __launch_bounds__(64 * KS) void gf_gemm_ksplit_kernel(DescView d, int k, int m_pad, int ntiles,
                                                                  int64_t col0, int64_t ngroups, int copies) {
   constexpr int kRB = 8;
-  __shared__ u32x4 red[KS][MT][64];
+  // one LDS area, used twice: first the tile's perm records of all k rows (k x MT x 32 bytes, at
+  // most 256 x MT x 32 = KS x MT KiB), then the KS partial products for the reduction
+  __shared__ u32x4 smem[KS * MT * 64];
   d = stripe(d, k, m_pad);
   const int tile = int(blockIdx.x % unsigned(ntiles));
   const int64_t cb = int64_t(blockIdx.x / unsigned(ntiles));
@@ -384,6 +386,15 @@ __global__ __launch_bounds__(64 * KS) void gf_gemm_ksplit_kernel(DescView d, int
   const bool do_copy = copies && tile == 0;
   const int R = (k + KS - 1) / KS;
   const int jb = s * R, je = min(k, jb + R);
+
+  // stage the tables: one L2 round trip per block instead of a chain of scalar loads per row (the
+  // scalar cache cannot hold a wide code's tables, 32 KiB per tile at k = 128)
+  for (int c = int(threadIdx.x); c < k * MT * 2; c += 64 * KS) {
+    const int row = c / (MT * 2), part = c % (MT * 2);
+    smem[c] = ((gptr<const u32x4>)(uint64_t)(d.tab + (size_t(row) * m_pad + i0) * kPermStride))[part];
+  }
+  __syncthreads();
+  const uint32_t* tl = reinterpret_cast<const uint32_t*>(smem);
 
   u32x4 acc[MT];
 #pragma unroll
@@ -404,9 +415,9 @@ __global__ __launch_bounds__(64 * KS) void gf_gemm_ksplit_kernel(DescView d, int
           if (cp1) st16<false>(row_vec_w(cp1, off), x[u + 1]);
         }
       }
-      const auto t0 = d.tab + (size_t(j) * m_pad + i0) * kPermStride;
+      const uint32_t* t0 = tl + size_t(j) * MT * kPermStride;
       if (j + 1 < je) {
-        const auto t1 = t0 + size_t(m_pad) * kPermStride;
+        const uint32_t* t1 = t0 + MT * kPermStride;
 #pragma unroll
         for (int w = 0; w < 4; ++w) {
           const Sel s0 = make_sel(x[u][w]);
@@ -425,14 +436,15 @@ __global__ __launch_bounds__(64 * KS) void gf_gemm_ksplit_kernel(DescView d, int
       }
     }
   }
+  __syncthreads();  // every wave is done with the tables
 #pragma unroll
-  for (int i = 0; i < MT; ++i) red[s][i][lane] = acc[i];
+  for (int i = 0; i < MT; ++i) smem[(s * MT + i) * 64 + lane] = acc[i];
   __syncthreads();
   for (int r = int(threadIdx.x); r < MT * 64; r += 64 * KS) {
     const int i = r >> 6, l = r & 63;
-    u32x4 v = red[0][i][l];
+    u32x4 v = smem[i * 64 + l];
 #pragma unroll
-    for (int q = 1; q < KS; ++q) v ^= red[q][i][l];
+    for (int q = 1; q < KS; ++q) v ^= smem[(q * MT + i) * 64 + l];
     const int64_t gg = cb * 64 + l;
     const uint64_t op = d.out[i0 + i];
     if (gg < ngroups && op) st16<false>(row_vec_w(op, col0 + gg * 16), v);
@@ -572,7 +584,8 @@ int64_t short_lanes() {
 }
 
 // Launches whose lanes (16-byte groups x stripes x output tiles at the widest tile) number fewer
-// than this take the k-split kernel when k >= 32; GFRS_KSPLIT_LANES overrides (0 = never).
+// than this take the k-split kernel when 32 <= k <= 256 (its LDS holds 256 rows of tables);
+// GFRS_KSPLIT_LANES overrides (0 = never).
 // Measured with scripts/serve_bench.py --code (profiles/serving/r07_wide/xcd): the k-split kernel
 // wins every point up to 65 K lanes (RS(128,160) 16 x 64 KiB encode 294 -> 23 us, 16 x 1 MiB
 // 263 -> 51 us; RS(64,80) 16 x 4 MiB 141 -> 88 us; RS(32,40) 16 x 1 MiB 33 -> 18 us) and the vec
@@ -725,7 +738,7 @@ hipError_t run(const void* desc, int k, int m_pad, int batch, int64_t col0, int6
   const DescView d = view(desc, k, m_pad, batch);
   int tile = tile_for(m_pad);
   const bool auto_cfg = !cfg && max_blocks == 0 && !bytewise && !(col0 & 15);
-  const bool ksplit = auto_cfg && k >= 32 && (ncols / 16 + ncols % 16) * batch * (m_pad / tile) < ksplit_lanes();
+  const bool ksplit = auto_cfg && k >= 32 && k <= 256 && (ncols / 16 + ncols % 16) * batch * (m_pad / tile) < ksplit_lanes();
   if (ksplit) tile = std::min(tile, 8);
   if (auto_cfg && !ksplit && tile >= 8) {
     // short rows of a wide code: the column groups alone leave lanes idle, so trade output-tile
