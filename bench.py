@@ -102,6 +102,9 @@ from gpu_rscode_amd.utils.timing import trace_range  # noqa: E402
 BASELINE_GBPS = 2 * 1_096_310_784 / 1.72168 / 1e9  # 1.2736 GB/s
 METRIC = "encode+decode throughput (GB/s) at k=10,n=14 on 1 GiB; 1/2/4/8-GPU scaling"
 COMM_MODES = ("bcast", "owners", "root", "none")
+# BASELINE.json's other configs (#4, #5, #1's shape at GPU scale) and the w = 16 field, timed by the
+# headline run itself (N = 1) so the driver's record carries them
+CONFIG_PRESETS = ("k128n160", "k16n20_8g", "k4n6", "k10n14_w16")
 
 # BASELINE.json configs. Weak presets are per GPU; strong presets are the whole job's bytes.
 PRESETS = {
@@ -112,6 +115,8 @@ PRESETS = {
     "k16n20_64g": dict(k=16, n=20, bytes=64 << 30, erasures=4, scaling="strong", gather="end", lanes=1),
     "k128n160": dict(k=128, n=160, bytes=1 << 30, erasures=32),
     "k4n6": dict(k=4, n=6, bytes=1_096_310_784, erasures=2),
+    # the reference's w = 16 field (src/galoisfield.cu:22-32), same stripe shape as the headline
+    "k10n14_w16": dict(k=10, n=14, bytes=1 << 30, erasures=4, field="gf65536"),
 }
 
 
@@ -128,6 +133,8 @@ def parse(argv=None):
     ap.add_argument("--n", type=int, default=None)
     ap.add_argument("--bytes", type=int, default=None, help="input bytes per GPU (weak) / in total (strong)")
     ap.add_argument("--erasures", type=int, default=None)
+    ap.add_argument("--field", default=None, choices=["gf256", "gf65536"],
+                    help="symbol field: GF(2^8) (default) or GF(2^16) (16-bit symbols, poly 0x1100B)")
     ap.add_argument("--comm", default="bcast", choices=COMM_MODES, help="per-step RCCL traffic (headline mode)")
     ap.add_argument("--scaling", default=None, choices=["weak", "strong"],
                     help="weak: a stripe per GPU (default); strong: one stripe column-sharded over all GPUs")
@@ -172,13 +179,28 @@ def parse(argv=None):
                     help="process-group timeout (init_process_group(timeout=)); longer than both budgets")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu: the C++ CPU codec over gloo (launcher / communication plumbing on a host)")
+    ap.add_argument("--configs", default=None,
+                    help="N = 1: after the headline, time these presets (comma list) each in a fresh child "
+                         "process and embed their records under configs (default on cuda with the k10n14 "
+                         f"headline: {','.join(CONFIG_PRESETS)}; 'none': off)")
+    ap.add_argument("--config-steps", type=int, default=20, help="timed steps of each --configs child")
+    ap.add_argument("--config-warmup", type=int, default=5, help="warmup steps of each --configs child")
+    ap.add_argument("--configs-budget", type=float, default=float(os.environ.get("GFRS_CONFIGS_BUDGET_S", 150)),
+                    help="seconds for all --configs children together (each gets what is left, at most 75)")
     a = ap.parse_args(argv)
-    pr = {"scaling": "weak", "gather": "step", "lanes": 2, **PRESETS[a.preset]}
+    pr = {"scaling": "weak", "gather": "step", "lanes": 2, "field": "gf256", **PRESETS[a.preset]}
     for key, val in pr.items():
         if getattr(a, key) is None:
             setattr(a, key, val)
     if a.device == "cpu" and "--bytes" not in " ".join(argv if argv is not None else sys.argv):
         a.bytes = 1 << 20  # plumbing runs: 1 MiB per rank
+    if a.configs is None:
+        headline = a.preset == "k10n14" and a.bytes == PRESETS["k10n14"]["bytes"] and a.field == "gf256"
+        a.configs = ",".join(CONFIG_PRESETS) if (a.device == "cuda" and headline and not a.graph) else "none"
+    a.configs = [] if a.configs in ("", "none") else [c for c in a.configs.split(",") if c]
+    bad = [c for c in a.configs if c not in PRESETS]
+    if bad:
+        ap.error(f"--configs: unknown preset(s) {bad}")
     if a.min_warmup_ms is None:
         a.min_warmup_ms = float(os.environ.get("GFRS_MIN_WARMUP_MS", 250 if a.device == "cuda" else 0))
     a.force_pg = a.force_pg or os.environ.get("GFRS_FORCE_PG") == "1"
@@ -222,10 +244,22 @@ def erasure_pool(k: int, n: int, erasures: int, rs: ReedSolomon, size: int = 16)
     return pool
 
 
-def _check_windows(C: int, width: int = 1 << 16) -> list[tuple[int, int]]:
-    """Head, middle and ragged-tail column windows used to check full parity rows."""
-    wins = {(0, min(C, width)), (max(0, C // 2 - width // 2), min(C, C // 2 + width // 2)), (max(0, C - width), C)}
+def _check_windows(C: int, width: int = 1 << 16, even: bool = False) -> list[tuple[int, int]]:
+    """Head, middle and ragged-tail column windows used to check full parity rows (``even``: whole
+    16-bit symbols, C even)."""
+    mid = C // 2 - width // 2
+    if even:
+        mid -= mid % 2
+    wins = {(0, min(C, width)), (max(0, mid), min(C, mid + width)), (max(0, C - width), C)}
     return sorted(wins)
+
+
+def _oracle_gemm(e_mat: np.ndarray, x: np.ndarray, wide: bool) -> np.ndarray:
+    """numpy GF oracle of parity = E . x over byte rows (GF(2^16): little-endian 16-bit symbols)."""
+    if not wide:
+        return gf.GF256.gemm(e_mat, x)
+    out = gf.field(16).gemm(e_mat, np.ascontiguousarray(x).view("<u2"))
+    return np.ascontiguousarray(out.astype("<u2")).view(np.uint8)
 
 
 class GpuWorkload:
@@ -237,6 +271,7 @@ class GpuWorkload:
 
         hip()  # fail loudly if the native extension is missing
         self.a, self.k, self.p, self.C, self.rank = a, k, n - k, C, rank
+        self.wide = a.field == "gf65536"
         self.lanes = 1 if a.graph else max(1, a.lanes)
         slots = max(slots, self.lanes)
         self.data = alloc_rows(k, C, dev)
@@ -244,13 +279,18 @@ class GpuWorkload:
                      seed=rank + 1 if seed is None else seed)
         self.parity = parity_bufs or [alloc_rows(self.p, C, dev) for _ in range(slots)]
         self.outs = out_bufs or [alloc_rows(k, C, dev) for _ in range(self.lanes)]
-        self.g_dev = torch.from_numpy(np.ascontiguousarray(g)).to(dev)
+        if self.wide:  # GF(2^16): the generator as 16-bit words, the v_perm w = 16 engine
+            from gpu_rscode_amd.ops import Gemm16Plan
+            self.g_dev = torch.from_numpy(np.ascontiguousarray(g, dtype="<u2").view(np.int16)).to(dev)
+        else:
+            self.g_dev = torch.from_numpy(np.ascontiguousarray(g)).to(dev)
         self.e_mat = e_mat
         self.pool_dev = pool_dev
         # erased natives per pool pattern (known on the host: it picks the plan shape, the pattern
         # itself only ever travels on the device)
         self.e_of = [k - sum(1 for r in rows if r < k) for rows in pool_dev.tolist()]
-        self.enc = [GemmPlan(self.data, par, e_mat, engine=a.engine) for par in self.parity]
+        self.enc = [Gemm16Plan(self.data, par, e_mat) if self.wide else GemmPlan(self.data, par, e_mat, engine=a.engine)
+                    for par in self.parity]
         # one device-built decode plan per (slot, number of erased natives)
         self.dec = [{e: PatternDecoder(self.g_dev, [self.data[i] for i in range(k)] + [par[i] for i in range(self.p)],
                                        [self.outs[s % self.lanes][i] for i in range(k)], e)
@@ -262,7 +302,7 @@ class GpuWorkload:
         # pattern + decode-system solve overlap the encode GEMM
         self.side = torch.cuda.Stream(dev, priority=-1) if a.side_priority else torch.cuda.Stream(dev)
         self.inv_done = torch.cuda.Event()
-        self.kv = dict(vec=a.vec, pf=a.pf, nt=a.nt)
+        self.kv = {} if self.wide else dict(vec=a.vec, pf=a.pf, nt=a.nt)
         self.graph_mode = False
         self.bcast = False  # rank 0 RCCL-broadcasts each step's pattern (set per timed mode)
         # Look-ahead broadcast: step j's pattern is broadcast on its own stream while step j - ahead
@@ -398,8 +438,8 @@ class GpuWorkload:
                     want = sorted(set(range(self.k)) - set(pool[d.last_i % len(pool)]))
                     ok = ok and sorted(d.erased.tolist()) == want
         ok = ok and all(torch.equal(out, self.data) for out in self.outs)
-        for a, b in _check_windows(self.C):
-            want = gf.GF256.gemm(self.e_mat, self.data[:, a:b].cpu().numpy())
+        for a, b in _check_windows(self.C, even=self.wide):
+            want = _oracle_gemm(self.e_mat, self.data[:, a:b].cpu().numpy(), self.wide)
             ok = ok and all(np.array_equal(par[:, a:b].cpu().numpy(), want) for par in self.parity)
         return bool(ok)
 
@@ -409,7 +449,8 @@ class CpuWorkload:
 
     def __init__(self, a, k, n, C, e_mat, g, pool_dev, rank, slots, parity_bufs=None, out_bufs=None, seed=None):
         self.k, self.p, self.C, self.rank = k, n - k, C, rank
-        self.rs = ReedSolomon(k, n)
+        self.wide = a.field == "gf65536"
+        self.rs = ReedSolomon(k, n, field=a.field)
         self.rs.E, self.rs.G = e_mat, g
         gen = torch.Generator().manual_seed(rank + 1 if seed is None else seed)
         self.data = torch.randint(0, 256, (k, C), dtype=torch.uint8, generator=gen)
@@ -446,7 +487,7 @@ class CpuWorkload:
         pass
 
     def verify(self) -> bool:
-        want = gf.GF256.gemm(self.rs.E, self.data.numpy())
+        want = _oracle_gemm(self.rs.E, self.data.numpy(), self.wide)
         return all(torch.equal(o, self.data) for o in self.outs) and all(
             np.array_equal(par.numpy(), want) for par in self.parity)
 
@@ -564,7 +605,8 @@ def e2e(a, k, n, C, rs: ReedSolomon, rows: list[int], work: GpuWorkload, dev, wo
     h.prepare_pipeline([dev.index], k, max(p, k), C, a.streams, a.slice)
 
     def run(ins, outs, mat):
-        return h.gemm_host([dev.index], ins, outs, mat, C, a.streams, a.slice, 0, False)["devices"][0]
+        return h.gemm_host([dev.index], ins, outs, mat, C, a.streams, a.slice, 0, False,
+                           field_w=16 if work.wide else 8)["devices"][0]
 
     res = {}
     for name, ins, outs, mat in (("encode", enc_in, enc_out, emat), ("decode", dec_in, dec_out, dmat),
@@ -580,7 +622,7 @@ def e2e(a, k, n, C, rs: ReedSolomon, rows: list[int], work: GpuWorkload, dev, wo
                 best = (t, st)
         res[name] = best
     ok = True
-    for a0, b0 in _check_windows(C):
+    for a0, b0 in _check_windows(C, even=work.wide):
         ok = ok and np.array_equal(par[:, a0:b0].numpy(), work.parity[0][:, a0:b0].cpu().numpy())
     ok = ok and torch.equal(rec, host[erased]) and torch.equal(image, host)
     stripe_bytes = k * C * world
@@ -607,6 +649,8 @@ def e2e(a, k, n, C, rs: ReedSolomon, rows: list[int], work: GpuWorkload, dev, wo
 def weak_work(a, k, n, e_mat, g, pool_dev, rank, dev, has_pg):
     """The weak-scaling workload: every rank encodes and decodes its own a.bytes stripe."""
     C = (a.bytes + k - 1) // k
+    if a.field == "gf65536":
+        C += C % 2  # whole 16-bit symbols
     slots = 2 if has_pg else 1  # parity double-buffered while its exchange is in flight
     return make_work(a, k, n, C, e_mat, g, pool_dev, rank, dev, slots), C
 
@@ -688,6 +732,86 @@ def run_strong(a, k, n, e_mat, g, pool_dev, rank, world, dev, has_pg, steps, war
                    gather_GBps=round(gather.bytes_per_link * max(1, world - 1) / gt / 1e9, 3) if world > 1 else None)
         out["ok"] = out["ok"] and out["gather_ok"]
     return work, out
+
+
+# ---- other BASELINE configs, each in a fresh child process (N = 1) ----------------------------
+def _last_json(text: str) -> dict | None:
+    for line in reversed(text.splitlines()):
+        line = line.strip()
+        if line.startswith("{"):
+            try:
+                return json.loads(line)
+            except ValueError:
+                return None
+    return None
+
+
+def run_config_child(a, preset: str, timeout_s: float) -> dict:
+    """``bench.py --preset <preset>`` as a CHILD process (never an exec of this one) with its own
+    timeout and process group; its one JSON line, condensed. A crash, a hang or a bad record gives
+    ``{"error": ..., "rc": ...}`` — the caller's headline record is never touched."""
+    cmd = [sys.executable, os.path.abspath(__file__), "--preset", preset, "--steps", str(a.config_steps),
+           "--warmup", str(a.config_warmup), "--no-e2e", "--configs", "none", "--device", a.device,
+           "--headline-budget", str(max(10.0, timeout_s - 5))]
+    env = dict(os.environ, GFRS_CONFIG_CHILD=preset)
+    t0 = time.perf_counter()
+    try:
+        proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env,
+                                start_new_session=True)
+    except OSError as ex:
+        return {"error": f"could not start: {ex}", "rc": None}
+    try:
+        out, err = proc.communicate(timeout=timeout_s)
+    except subprocess.TimeoutExpired:
+        try:
+            os.killpg(proc.pid, 9)  # the child's own session: its group is exactly what we started
+        except OSError:
+            pass
+        proc.communicate()
+        return {"error": f"timed out after {timeout_s:.0f} s", "rc": None,
+                "wall_s": round(time.perf_counter() - t0, 2)}
+    wall = round(time.perf_counter() - t0, 2)
+    rec = _last_json(out)
+    if proc.returncode != 0 or rec is None or rec.get("value") is None:
+        tail = (err or out or "").strip().splitlines()[-3:]
+        return {"error": " | ".join(tail)[-400:] or "no record", "rc": proc.returncode, "wall_s": wall,
+                **({"verified": rec.get("verified")} if rec else {})}
+    cfg = rec.get("config", {})
+    return {"metric": rec.get("metric"), "value": rec.get("value"), "unit": rec.get("unit"),
+            "ms_per_step": rec.get("ms_per_step"), "verified": rec.get("verified"), "steps": rec.get("steps"),
+            "warmup": rec.get("warmup"), "dtype": rec.get("dtype"), "model": cfg.get("model"),
+            "global_batch": cfg.get("global_batch"), "engine": cfg.get("engine"), "rc": proc.returncode,
+            "wall_s": wall}
+
+
+def run_configs(a, rec: dict) -> None:
+    """Time each of ``a.configs`` in its own child process (after the headline is verified and held
+    in ``rec``) and embed the condensed records under ``rec["configs"]``."""
+    if not a.configs:
+        return
+    deadline = time.perf_counter() + a.configs_budget
+    rec["configs"] = {}
+    for preset in a.configs:
+        left = deadline - time.perf_counter()
+        if left < 10:
+            rec["configs"][preset] = {"skipped": f"--configs-budget ({a.configs_budget:g} s) spent"}
+            continue
+        rec["configs"][preset] = run_config_child(a, preset, min(75.0, left))
+    rec["configs_what"] = ("other BASELINE configs, each timed by bench.py --preset P in a fresh child process "
+                           "after the headline (steps / warmup as listed; verified like the headline)")
+
+
+def _maybe_child_fault(preset: str) -> None:
+    """Test hook: GFRS_CONFIG_FAULT=<preset>:crash|hang makes that --configs child fail."""
+    spec = os.environ.get("GFRS_CONFIG_FAULT", "")
+    if os.environ.get("GFRS_CONFIG_CHILD") != preset or ":" not in spec:
+        return
+    which, kind = spec.split(":", 1)
+    if which != preset:
+        return
+    if kind == "hang":
+        time.sleep(3600)
+    os._exit(7)
 
 
 # ---- failure isolation (N > 1) ---------------------------------------------------------------
@@ -785,6 +909,7 @@ def main(argv=None) -> int:
     if env_world is None and (a.gpus or 1) > 1:
         return launch(a.gpus, argv)  # parent: no GPU call before (or after) this
     world = int(env_world or "1")
+    _maybe_child_fault(a.preset)
     if a.gpus is not None and a.gpus != world:
         print(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world}", file=sys.stderr)
         return 2
@@ -823,15 +948,21 @@ def main(argv=None) -> int:
             raise SystemExit("--graph is single-GPU only, without a process group (per-step RCCL traffic)")
 
         # ---- setup: E and the erasure-pattern pool come from rank 0 (RCCL broadcast) ---------
-        rs = ReedSolomon(k, n)
+        rs = ReedSolomon(k, n, field=a.field)
+        wide = rs.wide
         pool = erasure_pool(k, n, a.erasures, rs)
-        e_t = torch.from_numpy(rs.E.copy()).to(dev)
+        # (GF(2^16): E travels as int16 words — the collectives have no uint16)
+        e_t = torch.from_numpy(rs.E.astype("<u2").view(np.int16) if wide else rs.E.copy()).to(dev)
         pool_t = torch.tensor(pool, dtype=torch.int32, device=dev)
         if has_pg:
             dist.broadcast(e_t, 0)
             dist.broadcast(pool_t, 0)
         e_mat = e_t.cpu().numpy()
-        rs.E, rs.G = e_mat, gf.GF256.generator(e_mat)
+        if wide:
+            e_mat = e_mat.view("<u2").astype(np.uint16)
+            rs.E, rs.G = e_mat, np.vstack([np.eye(k, dtype=np.uint16), e_mat])
+        else:
+            rs.E, rs.G = e_mat, gf.GF256.generator(e_mat)
 
         # ---- the headline: timed, verified and reduced before anything else runs --------------
         head_strong = a.scaling == "strong"
@@ -883,7 +1014,7 @@ def main(argv=None) -> int:
         emitter.emit(rec)
 
     clean = True
-    with Watchdog(a.compare_budget, compare_expired, code=0):
+    with Watchdog(a.compare_budget, compare_expired, code=0 if ok else 1):
         for i, (kind, m) in enumerate(todo):
             done["n"] = i
             try:
@@ -918,6 +1049,8 @@ def main(argv=None) -> int:
             done["n"] = len(todo)
     if compare:
         rec["comparisons_complete"] = clean
+    if world == 1 and clean:
+        run_configs(a, rec)
     emitter.emit(rec)
     if has_pg and clean:
         # (the record is out; a teardown that hangs must not hold the job: leave after 60 s)
@@ -945,9 +1078,10 @@ def headline_record(a, k, n, C, world, rank, dev, has_pg, work, head, head_stron
     ms = head["elapsed"] / head["steps"] * 1e3
     value = gbps_of(head)
     metric = METRIC
-    if a.preset != "k10n14" or a.bytes != PRESETS["k10n14"]["bytes"] or head_strong:
+    if a.preset != "k10n14" or a.bytes != PRESETS["k10n14"]["bytes"] or head_strong or a.field != "gf256":
         per = "in total, one stripe sharded over the GPUs" if head_strong else "per GPU"
-        metric = f"encode+decode throughput (GB/s) at k={k},n={n} on {a.bytes / 2**30:.3g} GiB {per}"
+        fld = ", GF(2^16)" if a.field == "gf65536" else ""
+        metric = f"encode+decode throughput (GB/s) at k={k},n={n}{fld} on {a.bytes / 2**30:.3g} GiB {per}"
     comm_desc = {"bcast": "rank 0 RCCL-broadcasts the step's erasure pattern; parity and decoded rows stay in "
                           "each GPU's HBM (as at N = 1)",
                  "owners": "pattern broadcast + parity all_to_all to chunk owners over RCCL/xGMI",
@@ -977,9 +1111,10 @@ def headline_record(a, k, n, C, world, rank, dev, has_pg, work, head, head_stron
         "higher_is_better": True,
         "scaling": "strong" if head_strong else "weak",
         "vs_baseline": round(value / BASELINE_GBPS, 1),
-        "dtype": "uint8 (GF(2^8) symbols)",
+        "dtype": "uint16 (GF(2^16) symbols)" if a.field == "gf65536" else "uint8 (GF(2^8) symbols)",
         "data": "synthetic (device-generated random bytes)" if dev.type == "cuda" else "synthetic (host random bytes)",
-        "config": {"model": f"RS(k={k},n={n}) reference Vandermonde, GF(2^8) poly 0x11D",
+        "config": {"model": (f"RS(k={k},n={n}) reference Vandermonde, GF(2^16) poly 0x1100B" if a.field == "gf65536"
+                             else f"RS(k={k},n={n}) reference Vandermonde, GF(2^8) poly 0x11D"),
                    "global_batch": (f"{a.bytes} B in total ({k} x {C} B columns per rank shard)" if head_strong
                                     else f"{a.bytes} B per GPU ({k} x {C} B chunks)"),
                    "seq_len": C, "parallelism": parallelism,

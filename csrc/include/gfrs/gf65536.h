@@ -164,6 +164,12 @@ inline bool decode_matrix(const Mat& g, int k, const std::vector<int>& rows, Mat
 // Returns false when G[rows] is singular.
 inline bool decode_rows(const Mat& g, int k, const std::vector<int>& rows, const std::vector<int>& want, Mat& out) {
   if (int(rows.size()) != k) throw std::invalid_argument("gf2^16 decode_rows: need exactly k rows");
+  if (k <= 0 || g.size() % size_t(k)) throw std::invalid_argument("gf2^16 decode_rows: G is not n x k");
+  const int n = int(g.size() / size_t(k));
+  for (int r : rows)
+    if (r < 0 || r >= n) throw std::invalid_argument("gf2^16 decode_rows: bad chunk id");
+  for (int i : want)  // checked before either path (the full-inverse fallback indexes with it)
+    if (i < 0 || i >= k) throw std::invalid_argument("gf2^16 decode_rows: wanted row is not a native");
   bool systematic = true;
   for (int i = 0; i < k && systematic; ++i)
     for (int j = 0; j < k; ++j)

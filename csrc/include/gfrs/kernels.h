@@ -60,6 +60,18 @@ hipError_t launch_gf_decode_system(const uint8_t* g, int k, const int* rows, int
 hipError_t launch_gf_invert(const uint8_t* a, uint8_t* a_inv, int n, int batch, int* status,
                             void* desc, const int* sel_rows, int m, int m_pad, hipStream_t stream);
 
+// GF(2^16) form (csrc/kernels/gf_decode16.hip): g = G (n x k little-endian uint16, [I; E]), rows =
+// the k survivor ids (device int32). `erased` (device int32 [e]) is always an OUTPUT: the erased
+// natives, ascending, derived from rows. Writes X (e x k uint16) to dm (optional), status (0 ok,
+// 1 singular, 2 invalid survivor list) and, into a desc_layout16 descriptor (k inputs, m_pad >= e
+// outputs), the four v_perm records per coefficient; with ptrs = {chunk row 0..n-1, output row
+// 0..k-1} also the descriptor's row pointers. One workgroup, the system in LDS:
+// decode_system16_supported says whether (n, k, e) fits (e <= 256, ~ 8 e (e + k) + 4 n + 4 k bytes).
+bool decode_system16_supported(int n, int k, int e);
+hipError_t launch_gf_decode_system16(const uint16_t* g, int n, int k, const int* rows, int* erased, int e,
+                                     uint16_t* dm, int* status, void* desc, int m_pad, hipStream_t stream,
+                                     const uint64_t* ptrs = nullptr);
+
 // ---- matrix utilities (csrc/kernels/gf_matrix.hip) -------------------------------------------
 // kind: 0 = reference Vandermonde, 1 = Cauchy. Writes the p x k block.
 hipError_t launch_gen_matrix(uint8_t* e, int k, int p, int kind, hipStream_t stream);

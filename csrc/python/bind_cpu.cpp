@@ -51,6 +51,9 @@ PYBIND11_MODULE(_cpu, m) {
   // GF(2^16) host linear algebra (gfrs/gf65536.h): the decode system of a w = 16 code
   m.def("gf16_mul", [](int a, int b) { return int(gf16w::mul(uint16_t(a), uint16_t(b))); });
   m.def("gf16_invert", [](const std::vector<int>& a, int n) {
+    if (n <= 0 || a.size() != size_t(n) * size_t(n)) throw py::value_error("gf16_invert: need n * n entries");
+    for (int v : a)
+      if (v < 0 || v > 0xFFFF) throw py::value_error("gf16_invert: entries are 16-bit symbols");
     gf16w::Mat out;
     if (!gf16w::invert(gf16w::Mat(a.begin(), a.end()), n, out)) throw py::value_error("singular matrix");
     return std::vector<int>(out.begin(), out.end());

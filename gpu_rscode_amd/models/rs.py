@@ -19,9 +19,9 @@ import numpy as np
 import torch
 
 from .. import gf
-from .._native import cpu
+from .._native import cpu, hip
 from ..ops.gemm import Gemm16Plan, GemmPlan, _rows
-from ..ops.inverse import decode_system_into_plan
+from ..ops.inverse import decode_system16_into_plan, decode_system_into_plan
 from ..ops.matrix import decode_matrix, encoding_matrix
 
 PITCH = 256
@@ -149,8 +149,10 @@ class ReedSolomon:
 
     @property
     def G(self) -> np.ndarray:
-        """The n x k generator [I_k; E]. Assigning a new one drops the decode matrices derived
-        from the old one (per-pattern caches); replace it rather than editing it in place."""
+        """The n x k generator [I_k; E]. Assigning a new one drops everything derived from the old
+        one: the decode matrices, the cached GEMM plans (their tables hold the old inverse's
+        coefficients, keyed on buffers and pattern only) and the device copy of G. Replace it
+        rather than editing it in place."""
         return self._G
 
     @G.setter
@@ -158,6 +160,21 @@ class ReedSolomon:
         self._G = g
         self._dm.clear()
         self._g16_bytes = None
+        if hasattr(self, "_plans"):  # (absent during __init__)
+            self._plans.clear()
+            self._g_dev.clear()
+
+    @property
+    def E(self) -> np.ndarray:
+        """The p x k encoding matrix. Assigning a new one drops the cached GEMM plans (the encode
+        plans' tables hold the old coefficients); assign G as well for decode."""
+        return self._E
+
+    @E.setter
+    def E(self, e: np.ndarray) -> None:
+        self._E = e
+        if hasattr(self, "_plans"):
+            self._plans.clear()
 
     # ---- helpers -----------------------------------------------------------------------------
     @property
@@ -396,9 +413,11 @@ class ReedSolomon:
                 order, ``src/decode.cu:302-318``).
             rows: the chunk ids (0..n-1) of the survivors.
             out: optional [k, C] destination for the natives.
-            device_invert: invert on the GPU (``gf_invert`` kernel writing the GEMM tables directly);
-                a singular pattern then yields zeros and a nonzero ``self.last_status`` instead of an
-                exception (checked lazily, no host sync on the hot path).
+            device_invert: solve the decode system on the GPU (``gf_invert.hip`` / for GF(2^16)
+                ``gf_decode16.hip``, writing the GEMM tables directly); a singular pattern then yields
+                zeros and a nonzero ``self.last_status`` instead of an exception (checked lazily, no
+                host sync on the hot path). GF(2^16) systems too large for one workgroup's LDS are
+                solved on the host.
         """
         fast = None
         if not device_invert and isinstance(out, torch.Tensor) and out.dim() == 2 and out.is_cuda:
@@ -455,6 +474,23 @@ class ReedSolomon:
                 g_dev = self._g_dev[(dev, id(self.G))] = torch.from_numpy(np.ascontiguousarray(self.G)).to(dev)
             # systematic decode solved on device: e x (e+k) Gauss-Jordan, tables written in place
             decode_system_into_plan(g_dev, plan.rows_dev, plan.erased_dev, plan, status=plan.status, stream=stream)
+            self.last_status = plan.status
+        elif device_invert and self.wide and hip().decode_system16_supported(self.n, self.k, len(erased)):
+            plan = self._plans.get(key)
+            if plan is None:
+                plan = Gemm16Plan(ins, [outs[i] for i in erased], copies=copies, device_tables=True,
+                                  hold_buffers=False)
+                self._plans[key] = plan
+                plan.rows_dev = torch.tensor(rows, dtype=torch.int32, device=dev)
+                plan.erased_dev = torch.zeros(len(erased), dtype=torch.int32, device=dev)
+                plan.status = torch.zeros(1, dtype=torch.int32, device=dev)
+            g_dev = self._g_dev.get((dev, id(self.G)))
+            if g_dev is None:
+                self._g_dev.clear()
+                g16 = np.ascontiguousarray(self.G, dtype="<u2").view(np.int16)
+                g_dev = self._g_dev[(dev, id(self.G))] = torch.from_numpy(g16).to(dev)
+            # the GF(2^16) e x (e+k) solve on device (gf_decode16.hip), tables written in place
+            decode_system16_into_plan(g_dev, plan.rows_dev, plan.erased_dev, plan, status=plan.status, stream=stream)
             self.last_status = plan.status
         else:
             plan = self._plan(key, ins, [outs[i] for i in erased], self._erased_rows(rows, erased), copies=copies)

@@ -409,13 +409,17 @@ class Gemm16Plan:
     Args:
         inputs: k byte rows (2-D uint8 tensor or list of 1-D tensors) on one GPU, 2-byte aligned.
         outputs: m byte rows on the same GPU.
-        coeff: (m, k) GF(2^16) coefficients (uint16-valued).
+        coeff: (m, k) GF(2^16) coefficients (uint16-valued); or None with ``device_tables=True``
+            (the tables are written later on the device, :func:`~gpu_rscode_amd.ops.inverse.PatternDecoder`).
         copies: optional k destination rows (or None entries): fused survivor copy of decode.
         hold_buffers: as :class:`GemmPlan`.
     Rows shorter than the others bound the column range, which must be a whole number of symbols.
     """
 
-    def __init__(self, inputs, outputs, coeff, *, copies=None, hold_buffers: bool = True):
+    def __init__(self, inputs, outputs, coeff=None, *, copies=None, device_tables: bool = False,
+                 hold_buffers: bool = True):
+        if coeff is None and not device_tables:
+            raise ValueError("need coeff or device_tables=True")
         self.inputs, self.outputs = _rows(inputs), _rows(outputs)
         self.copies = None if copies is None else list(copies)
         dev = _check_rows(self.inputs, "input", None)
@@ -439,9 +443,10 @@ class Gemm16Plan:
         if any(ptr(r) % 2 for r in rows):
             raise ValueError("GF(2^16) rows must be 2-byte aligned")
         self.symwise = any(ptr(r) % 16 for r in rows)
-        coeff = np.asarray(coeff, dtype=np.int64).reshape(self.m, self.k)
-        if coeff.min() < 0 or coeff.max() > 65535:
-            raise ValueError("GF(2^16) coefficients must be in [0, 65535]")
+        if coeff is not None:
+            coeff = np.asarray(coeff, dtype=np.int64).reshape(self.m, self.k)
+            if coeff.min() < 0 or coeff.max() > 65535:
+                raise ValueError("GF(2^16) coefficients must be in [0, 65535]")
         self.layout = desc_layout16(self.k, self.m_pad)
         lay = self.layout
         host = np.zeros(lay.bytes, dtype=np.uint8)
@@ -454,9 +459,10 @@ class Gemm16Plan:
         if self.copies is not None:
             put(lay.copy_off, [ptr(c) if c is not None else 0 for c in self.copies])
         put(lay.out_off, [ptr(r) for r in self.outputs] + [0] * (self.m_pad - self.m))
-        t = np.zeros((self.k, self.m_pad, 4, 8), dtype="<u4")
-        t[:, : self.m] = np.transpose(gf.perm_quads16(coeff), (1, 0, 2, 3))
-        host[self.layout.tab_off:] = np.frombuffer(t.tobytes(), dtype=np.uint8)
+        if coeff is not None:  # else written on the device (decode_system16_into_plan)
+            t = np.zeros((self.k, self.m_pad, 4, 8), dtype="<u4")
+            t[:, : self.m] = np.transpose(gf.perm_quads16(coeff), (1, 0, 2, 3))
+            host[self.layout.tab_off:] = np.frombuffer(t.tobytes(), dtype=np.uint8)
         self.desc = torch.from_numpy(host).to(self.device)
         self.engine = "valu16"
         if not hold_buffers:

@@ -12,7 +12,7 @@ import torch
 
 from ..gf import SingularMatrixError
 from .._native import hip
-from .gemm import GemmPlan
+from .gemm import Gemm16Plan, GemmPlan
 
 
 def gf_invert(a: torch.Tensor, *, check: bool = True, stream: torch.cuda.Stream | None = None):
@@ -114,6 +114,41 @@ def decode_system_into_plan(g: torch.Tensor, rows: torch.Tensor, erased: torch.T
     return status
 
 
+def _is_w16(g: torch.Tensor) -> bool:
+    return g.dtype in (torch.int16, torch.uint16)
+
+
+def decode_system16_into_plan(g: torch.Tensor, rows: torch.Tensor, erased: torch.Tensor, plan: Gemm16Plan, *,
+                              status: torch.Tensor | None = None, stream: torch.cuda.Stream | None = None,
+                              ptrs: torch.Tensor | None = None, dm: torch.Tensor | None = None) -> torch.Tensor:
+    """GF(2^16) form of :func:`decode_system_into_plan` (``csrc/kernels/gf_decode16.hip``): ``g`` is
+    the (n, k) generator as a 16-bit device tensor; ``erased`` (device int32 [e]) is always written
+    by the kernel (derived from ``rows``); ``dm`` (optional, int16 [e, k]) receives the decode rows.
+    Writes the plan's four-record tables (and with ``ptrs`` its row pointers). Graph-capturable.
+    Returns the device status word (0 ok, 1 singular, 2 invalid survivor list)."""
+    n, k = g.shape
+    e = erased.numel()
+    if plan.k != k or plan.m != e or rows.numel() != k:
+        raise ValueError("plan shape does not match (k survivors in, e erased natives out)")
+    for t in (rows, erased):
+        if t.dtype != torch.int32 or t.device != g.device:
+            raise ValueError("rows / erased must be int32 tensors on the generator's device")
+    if not hip().decode_system16_supported(n, k, e):
+        raise ValueError(f"GF(2^16) device decode system (n={n}, k={k}, e={e}) does not fit one workgroup's LDS")
+    if status is None:
+        status = torch.zeros(1, dtype=torch.int32, device=g.device)
+    if ptrs is not None and (ptrs.dtype != torch.int64 or ptrs.device != g.device or ptrs.numel() != n + k):
+        raise ValueError("ptrs must be a device int64 tensor of n chunk + k output row addresses")
+    if dm is not None and (dm.device != g.device or dm.numel() != e * k or not dm.is_contiguous()):
+        raise ValueError("dm must be a contiguous [e, k] 16-bit device tensor")
+    st = stream or torch.cuda.current_stream(g.device)
+    g = g.contiguous()
+    hip().decode_system16(g.data_ptr(), n, k, rows.data_ptr(), erased.data_ptr(), e,
+                          0 if dm is None else dm.data_ptr(), status.data_ptr(), plan.desc.data_ptr(), plan.m_pad,
+                          st.cuda_stream, 0 if ptrs is None else ptrs.data_ptr())
+    return status
+
+
 class PatternDecoder:
     """A decode whose erasure pattern lives in DEVICE memory: one plan serves every pattern with
     ``e`` erased natives, and nothing about the pattern passes through the host.
@@ -124,6 +159,9 @@ class PatternDecoder:
     step). :meth:`solve` checks the pattern, solves the systematic decode system and writes the
     descriptor (row pointers and tables) on the device; :meth:`run` rebuilds the erased natives
     into ``out`` and copies the surviving natives in the same pass. Both are graph-capturable.
+
+    GF(2^16) codes (``g`` a 16-bit tensor: int16 / uint16 holding the field's symbols) run the same
+    way on :class:`~gpu_rscode_amd.ops.gemm.Gemm16Plan` with the w = 16 solve (gf_decode16.hip).
 
     Args:
         g: (n, k) generator [I; E] on the device.
@@ -144,9 +182,16 @@ class PatternDecoder:
         if any(r.dtype != torch.uint8 or r.dim() != 1 or r.device != g.device or r.data_ptr() % 16 for r in rows_all):
             raise ValueError("chunk / output rows must be 16-byte aligned uint8 rows on the generator's device")
         self.g, self.k, self.n, self.e = g, k, n, e
+        self.wide = _is_w16(g)
         # placeholders until the first solve: inputs = the natives, outputs = the first e output rows
-        self.plan = GemmPlan(chunks[:k], out[:e], copies=out, device_tables=True, engine=engine)
-        self.plan.ncols = min(r.numel() for r in rows_all)
+        if self.wide:
+            if not hip().decode_system16_supported(n, k, e):
+                raise ValueError(f"GF(2^16) device decode system (n={n}, k={k}, e={e}) does not fit one workgroup")
+            self.plan = Gemm16Plan(chunks[:k], out[:e], copies=out, device_tables=True)
+        else:
+            self.plan = GemmPlan(chunks[:k], out[:e], copies=out, device_tables=True, engine=engine)
+        ncols = min(r.numel() for r in rows_all)
+        self.plan.ncols = ncols - (ncols % 2 if self.wide else 0)
         if self.plan.engine == "mfma":
             self.plan.in_stride = 0  # survivors are not equally spaced: DMA row pointers come from the descriptor
         dev = g.device
@@ -166,8 +211,13 @@ class PatternDecoder:
         rows = self.rows if rows is None else rows
         if rows.dtype != torch.int32 or rows.device != self.g.device or rows.numel() != self.k or not rows.is_contiguous():
             raise ValueError("rows must be a contiguous int32 [k] tensor on the decoder's device")
+        if self.wide:
+            return decode_system16_into_plan(self.g, rows, self.erased, self.plan, status=self.status, stream=stream,
+                                             ptrs=self.ptrs)
         return decode_system_into_plan(self.g, rows, self.erased, self.plan, status=self.status, stream=stream,
                                        ptrs=self.ptrs)
 
     def run(self, stream: torch.cuda.Stream | None = None, **kw) -> None:
+        if self.wide:  # (the v_perm variant knobs are GF(2^8) ablations)
+            kw = {key: v for key, v in kw.items() if key in ("col0", "ncols", "max_blocks")}
         self.plan.run(stream, **kw)

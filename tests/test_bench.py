@@ -245,3 +245,47 @@ def test_gpu_bench_graph_replay_verifies():
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
     rec = _record(r.stdout)
     assert rec["verified"] is True and rec["config"]["graph"] is True
+
+
+def test_configs_children_embed_records_and_survive_a_crash_and_a_hang():
+    """N = 1: each --configs preset runs in a fresh child process after the headline; the records
+    are embedded under configs. A child that crashes (rc 7) or hangs (killed at its timeout) is
+    recorded as an error and the headline record is unchanged and verified."""
+    r = _run(["--device", "cpu", "--steps", "2", "--warmup", "1", "--configs", "k4n6,k10n14_w16",
+              "--config-steps", "3", "--config-warmup", "1"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = _record(r.stdout)
+    cf = rec["configs"]
+    assert set(cf) == {"k4n6", "k10n14_w16"} and rec["verified"] is True
+    assert all(c["verified"] is True and c["steps"] == 3 and c["warmup"] == 1 and c["value"] > 0 for c in cf.values())
+    assert "GF(2^16)" in cf["k10n14_w16"]["metric"] and cf["k10n14_w16"]["dtype"].startswith("uint16")
+    r = _run(["--device", "cpu", "--steps", "2", "--warmup", "1", "--configs", "k4n6,k10n14_w16",
+              "--config-steps", "2", "--configs-budget", "40"],
+             env={"GFRS_CONFIG_FAULT": "k4n6:crash"})
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = _record(r.stdout)
+    assert rec["verified"] is True and rec["value"] > 0
+    assert rec["configs"]["k4n6"]["rc"] == 7 and "error" in rec["configs"]["k4n6"]
+    assert rec["configs"]["k10n14_w16"]["verified"] is True
+    r = _run(["--device", "cpu", "--steps", "2", "--warmup", "1", "--configs", "k10n14_w16,k4n6",
+              "--config-steps", "2", "--configs-budget", "25"],
+             env={"GFRS_CONFIG_FAULT": "k10n14_w16:hang"}, timeout=120)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = _record(r.stdout)
+    assert rec["verified"] is True
+    assert "timed out" in rec["configs"]["k10n14_w16"]["error"]
+    assert "skipped" in rec["configs"]["k4n6"] or rec["configs"]["k4n6"].get("verified") is True
+
+
+def test_configs_default_only_for_the_headline():
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("bench_mod2", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    assert bench.parse([]).configs == list(bench.CONFIG_PRESETS)
+    assert bench.parse(["--bytes", str(64 << 20)]).configs == []
+    assert bench.parse(["--preset", "k128n160"]).configs == []
+    assert bench.parse(["--device", "cpu"]).configs == []
+    assert bench.parse(["--configs", "none"]).configs == []
+    assert bench.parse(["--configs", "k4n6"]).configs == ["k4n6"]

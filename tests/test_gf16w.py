@@ -114,6 +114,29 @@ def test_erased_rows_solve_matches_the_full_inverse(matrix):
         rs2._erased_rows([2, 3], [0, 1])
 
 
+def test_bad_inputs_are_rejected():
+    """Wanted rows are range-checked on both paths (the full-inverse fallback included), chunk ids
+    against n, and gf16_invert's entry count against n * n."""
+    k, n = 6, 9
+    rs = ReedSolomon(k, n, field="gf65536")
+    gb = np.ascontiguousarray(rs.G, dtype="<u2").tobytes()
+    rows = list(range(n - k, n))
+    g2 = np.array(rs.G)
+    g2[0, 1] ^= 1  # non-systematic: the fallback path
+    for gbytes in (gb, np.ascontiguousarray(g2, dtype="<u2").tobytes()):
+        for bad in ([-1], [k], [0, 10_000]):
+            with pytest.raises(ValueError):
+                cpu().gf16_decode_rows(gbytes, k, rows, bad)
+    with pytest.raises(ValueError):
+        cpu().gf16_decode_rows(gb, k, [0, 1, 2, 3, 4, n], [0])
+    with pytest.raises(ValueError):
+        cpu().gf16_invert([1, 0, 0], 2)
+    with pytest.raises(ValueError):
+        cpu().gf16_invert([1, 0, 0, 1], 3)
+    with pytest.raises(ValueError):
+        cpu().gf16_invert([1, 0, 0, 70000], 2)
+
+
 def test_odd_byte_rows_are_rejected():
     rs = ReedSolomon(4, 6, field="gf65536")
     with pytest.raises(ValueError, match="even byte count"):

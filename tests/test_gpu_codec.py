@@ -69,6 +69,27 @@ def test_device_invert_flags_singular_pattern():
     assert int(rs.last_status.item()) == 1
 
 
+def test_reassigning_g_drops_cached_decode_plans():
+    """Decode a pattern, replace E and G by another code's, re-encode and decode the SAME pattern on
+    the SAME buffers: the cached plan (keyed on buffers + pattern) must not replay the old inverse."""
+    k, n = 8, 11
+    rs = ReedSolomon(k, n)
+    other = ReedSolomon(k, n, matrix="cauchy")
+    host, data = _data(k, 20_011, 6)
+    parity = alloc_rows(n - k, 20_011, "cuda")
+    out = alloc_rows(k, 20_011, "cuda")
+    rows = [2, 3, 4, 5, 6, 7, 8, 9]  # natives 0, 1 lost
+    for code in (rs, other):
+        if code is other:
+            rs.E, rs.G = other.E, other.G
+        rs.encode(data, parity)
+        stripe = [data[i] for i in range(k)] + [parity[i] for i in range(n - k)]
+        rs.decode([stripe[r] for r in rows], rows, out=out)
+        torch.cuda.synchronize()
+        assert np.array_equal(parity.cpu().numpy(), GF256.gemm(other.E if code is other else rs.E, host))
+        assert np.array_equal(out.cpu().numpy(), host)
+
+
 def test_reconstruct_natives_and_parity_in_place():
     k, n = 12, 16
     rs = ReedSolomon(k, n, matrix="cauchy")

@@ -112,3 +112,70 @@ def test_gpu_cli_w16_roundtrip(tmp_path):
                        capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr
     assert (tmp_path / "o.bin").read_bytes() == payload
+
+
+@pytest.mark.parametrize("k,n,e,matrix", [(10, 14, 4, "vandermonde"), (300, 340, 40, "cauchy"), (6, 9, 1, "cauchy")])
+def test_device_built_w16_decode_plans(k, n, e, matrix):
+    """GF(2^16) PatternDecoder: the survivor list lives on the device, the kernel (gf_decode16.hip)
+    checks it, derives the erased natives, solves the e x (e + k) system and writes the plan's
+    tables and row pointers; the decode rebuilds the natives bit-exactly, survivors copied in the
+    same pass, for several patterns through one decoder."""
+    from gpu_rscode_amd.ops import PatternDecoder
+
+    C = 2 * 9_001
+    rs = ReedSolomon(k, n, field="gf65536", matrix=matrix)
+    data = alloc_rows(k, C, "cuda")
+    data.copy_(_rand(k, C, k + e))
+    par = rs.encode(data)
+    g = torch.from_numpy(np.ascontiguousarray(rs.G, dtype="<u2").view(np.int16)).cuda()
+    out = alloc_rows(k, C, "cuda")
+    dec = PatternDecoder(g, [data[i] for i in range(k)] + [par[i] for i in range(n - k)], [out[i] for i in range(k)], e)
+    rng = np.random.default_rng(e)
+    done = 0
+    while done < 3:
+        erased = sorted(rng.choice(k, size=e, replace=False).tolist())
+        lost_par = sorted(rng.choice(n - k, size=n - k - e, replace=False).tolist())
+        rows = [r for r in range(n) if r not in erased and (r < k or (r - k) not in lost_par)]
+        rng.shuffle(rows)
+        if not rs.is_recoverable(rows):
+            continue
+        out.fill_(0)
+        dec.rows.copy_(torch.tensor(rows, dtype=torch.int32))
+        dec.solve()
+        dec.run()
+        torch.cuda.synchronize()
+        assert int(dec.status.item()) == 0
+        assert dec.erased.tolist() == erased
+        assert torch.equal(out, data), (rows, erased)
+        done += 1
+    # a chunk listed twice: status 2, nothing written (no output pointers)
+    bad = list(range(k - 1)) + [0]
+    dec.rows.copy_(torch.tensor(bad, dtype=torch.int32))
+    out.fill_(7)
+    dec.solve()
+    dec.run()
+    torch.cuda.synchronize()
+    assert int(dec.status.item()) == 2 and bool((out == 7).all())
+
+
+def test_rs_decode_device_invert_w16_matches_host_plan():
+    """ReedSolomon.decode(device_invert=True) for GF(2^16): the device-solved plan equals the host
+    one; a singular pattern reports status 1."""
+    k, n, C = 12, 16, 2 * 5_003
+    rs = ReedSolomon(k, n, field="gf65536")
+    data = alloc_rows(k, C, "cuda")
+    data.copy_(_rand(k, C, 77))
+    par = rs.encode(data)
+    stripe = [data[i] for i in range(k)] + [par[i] for i in range(n - k)]
+    rows = [1, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 15]
+    for dev_inv in (False, True):
+        out = rs.decode([stripe[r] for r in rows], rows, device_invert=dev_inv)
+        torch.cuda.synchronize()
+        assert torch.equal(out, data), dev_inv
+    assert int(rs.last_status.item()) == 0
+    rs.G = np.array(rs.G)
+    rs.G[14] = rs.G[12]  # two equal parity rows: any pattern using both is singular
+    rows = [2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 14]
+    rs.decode([stripe[r] for r in rows], rows, device_invert=True)
+    torch.cuda.synchronize()
+    assert int(rs.last_status.item()) == 1
