@@ -170,8 +170,8 @@ inline Args parse(int argc, char** argv, bool gpu) {
       std::fprintf(stderr, "encode needs -k K -n N -e FILE with 1 <= K <= N <= %d\n", cap);
       std::exit(2);
     }
-    if (a.field_w == 16 && (a.streaming() || a.cpu_meta)) {
-      std::fprintf(stderr, "-w 16 writes the versioned METADATA without --window / --cpu-meta\n");
+    if (a.field_w == 16 && a.cpu_meta) {
+      std::fprintf(stderr, "-w 16 writes the versioned METADATA (no --cpu-meta form)\n");
       std::exit(2);
     }
   } else if (a.op == Args::kDecode) {

@@ -31,6 +31,7 @@ int main(int argc, char** argv) {
       so.window = a.window;
       so.resume = a.resume;
       so.durable = a.sync;
+      so.field_w = a.field_w;
       const FileReport r = a.streaming() ? encode_file_stream(a.in_file, a.k, a.n - a.k, parse_matrix_kind(a.matrix),
                                                               gemm, default_host_alloc(), so, a.cpu_meta)
                                          : encode_file(a.in_file, a.k, a.n - a.k, parse_matrix_kind(a.matrix), gemm,

@@ -81,6 +81,7 @@ int main(int argc, char** argv) {
     so.window = a.window;
     so.resume = a.resume;
     so.durable = a.sync;
+    so.field_w = enc ? a.field_w : 8;
     const StreamOptions* sop = a.streaming() ? &so : nullptr;
     double gpu_ms = 0;  // stream-loop time: transfers + kernels + frees, all devices (setup excluded)
     double setup_ms = 0, setup_past_ms = 0;  // helper-thread device setup, and the part the GEMM waited for

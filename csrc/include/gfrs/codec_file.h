@@ -11,6 +11,7 @@
 #include <string>
 #include <vector>
 
+#include "gfrs/format.h"
 #include "gfrs/matrix.h"
 
 namespace gfrs {
@@ -44,6 +45,14 @@ FileReport encode_file(const std::string& file, int k, int p, MatrixKind kind, c
 // unrecoverable (singular) erasure pattern. The field comes from the METADATA.
 FileReport decode_file(const std::string& file, const std::string& conf, const std::string& out,
                        const GemmFn& gemm, const HostAlloc& alloc);
+
+// GF(2^16) coding block of `kind` (reference Vandermonde, Cauchy, systematic Vandermonde).
+gf16w::Mat encoding_matrix16(MatrixKind kind, int k, int p);
+
+// Decode coefficients in the METADATA's field: rows `erased` of inv(G[rows]) packed as GemmFn
+// coefficients (GF(2^16): the e x e systematic solve). With erased == nullptr only checks that the
+// pattern is recoverable. False when G[rows] is singular.
+bool decode_coefficients(const Metadata& md, const std::vector<int>& rows, const std::vector<int>* erased, Mat* coeff);
 
 // The reference's src/unit-test.sh: conf keeping the LAST k chunks (erases natives 0..n-k-1).
 std::vector<std::string> worst_case_conf(const std::string& file, int n, int k);

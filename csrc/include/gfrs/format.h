@@ -41,6 +41,10 @@ struct Metadata {
 // carry a line "crc32 <c_0> ... <c_{n-1}>" (hex). The reference's reader stops after the matrix
 // (src/decode.cu:272-281) and ignores it, so files stay readable by the reference.
 uint32_t crc32(const uint8_t* data, int64_t len, uint32_t crc = 0);
+// CRC-32 of A || B from crc32(A), crc32(B) and len(B): advances crc(A) over len(B) zero bytes (a
+// 32 x 32 GF(2) operator raised to 8 len(B) by repeated squaring). Column shards of a chunk, each
+// CRC'd by its own rank, combine into the chunk's METADATA CRC this way (multi-GPU file codec).
+uint32_t crc32_combine(uint32_t crc_a, uint32_t crc_b, int64_t len_b);
 
 std::string chunk_path(const std::string& file, int index);
 std::string metadata_path(const std::string& file);

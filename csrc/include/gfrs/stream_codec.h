@@ -16,6 +16,7 @@
 #include <cstdint>
 #include <functional>
 #include <string>
+#include <vector>
 
 #include "gfrs/codec_file.h"
 
@@ -26,14 +27,34 @@ struct StreamOptions {
   bool resume = true;   // continue from a matching <target>.PROGRESS
   bool durable = true;  // fdatasync the outputs before each checkpoint
   int stop_after = -1;  // testing: return after this many windows of this call (simulated crash)
+  int field_w = 8;      // encode: GF(2^8) or GF(2^16) symbols (decode reads it from METADATA)
+  // Column shard (the multi-GPU file codec, one rank per GPU: the reference's per-device column
+  // split, src/encode.cu:368-381): process chunk columns [col_lo, col_hi) only (col_hi < 0: to C;
+  // GF(2^16): even offsets). With `shard`, the outputs must already exist at their full size (one
+  // coordinator creates them): they are neither truncated nor resized, no METADATA is written, the
+  // checkpoint is "<target>.PROGRESS.<lo>-<hi>", and StreamReport::crc holds the shard's per-chunk
+  // CRC-32s (crc32_combine them in column order for the METADATA).
+  int64_t col_lo = 0, col_hi = -1;
+  bool shard = false;
+  // decode: decode from exactly these survivor chunk ids, in this order (chosen and CRC-verified by
+  // a coordinator, choose_survivors), instead of searching the conf; their names come from the conf.
+  std::vector<int> rows;
 };
 
 struct StreamReport : FileReport {
   int64_t window = 0;
   int windows = 0;           // windows processed by this call
-  int64_t resumed_from = 0;  // chunk offset this call started at (0 = fresh)
+  int64_t resumed_from = 0;  // chunk offset this call started at (col_lo = fresh)
   bool complete = false;
+  int64_t col_lo = 0, col_hi = 0;  // the column range processed
+  std::vector<uint32_t> crc;       // encode: per-chunk CRC-32 of columns [col_lo, col_hi)
+  std::vector<int> rows;           // decode: the survivor chunk ids used, in system order
 };
+
+// Decode survivors for `file` + `conf`: the first recoverable k-subset, in conf order, of the chunks
+// that exist and match their METADATA CRC-32 (the aggressive read of decode_file). Streams every
+// candidate through its CRC in bounded windows. `rejected` counts CRC mismatches.
+std::vector<int> choose_survivors(const std::string& file, const std::string& conf, int* rejected = nullptr);
 
 StreamReport encode_file_stream(const std::string& file, int k, int p, MatrixKind kind, const GemmFn& gemm,
                                 const HostAlloc& alloc, const StreamOptions& opt, bool cpu_meta = false);

@@ -37,6 +37,8 @@ struct Buf {
   Buf& operator=(const Buf&) = delete;
 };
 
+}  // namespace
+
 // GF(2^16) coding blocks (gfrs/gf65536.h): the reference Vandermonde and Cauchy, and the
 // systematic Vandermonde V[k:] . inv(V[:k]) over the points 0..n-1.
 gf16w::Mat encoding_matrix16(MatrixKind kind, int k, int p) {
@@ -55,6 +57,8 @@ gf16w::Mat encoding_matrix16(MatrixKind kind, int k, int p) {
   }
   throw std::invalid_argument("bad matrix kind");
 }
+
+namespace {
 
 // Decode system of either field: rows of the inverse of G[rows], packed as GemmFn coefficients
 // (one byte per GF(2^8) entry, two per GF(2^16) entry). False when the pattern is singular.
@@ -89,6 +93,10 @@ struct Solver {
 };
 
 }  // namespace
+
+bool decode_coefficients(const Metadata& md, const std::vector<int>& rows, const std::vector<int>* erased, Mat* coeff) {
+  return Solver{md}.solve(rows, erased, coeff);
+}
 
 HostAlloc default_host_alloc() {
   return {[](size_t n) -> uint8_t* {

@@ -78,6 +78,41 @@ uint32_t crc32(const uint8_t* data, int64_t len, uint32_t crc) {
   return ~crc;
 }
 
+namespace {
+// 32 x 32 GF(2) matrices as 32 column words: op[i] = image of register bit i
+uint32_t gf2_apply(const uint32_t op[32], uint32_t v) {
+  uint32_t r = 0;
+  for (int i = 0; v; ++i, v >>= 1)
+    if (v & 1u) r ^= op[i];
+  return r;
+}
+void gf2_compose(uint32_t out[32], const uint32_t a[32], const uint32_t b[32]) {  // out = a . b
+  for (int i = 0; i < 32; ++i) out[i] = gf2_apply(a, b[i]);
+}
+}  // namespace
+
+uint32_t crc32_combine(uint32_t crc_a, uint32_t crc_b, int64_t len_b) {
+  if (len_b <= 0) return crc_a ^ crc_b;  // (crc of nothing is 0)
+  // one zero bit through the reflected register: bit 0 falls out through the polynomial, every
+  // other bit moves down by one
+  uint32_t step[32], tmp[32];
+  step[0] = 0xEDB88320u;
+  for (int i = 1; i < 32; ++i) step[i] = 1u << (i - 1);
+  for (int s = 0; s < 3; ++s) {  // one zero byte: the bit operator squared three times (2^3 bits)
+    gf2_compose(tmp, step, step);
+    std::memcpy(step, tmp, sizeof(step));
+  }
+  uint32_t reg = crc_a;
+  for (int64_t n = len_b; n; n >>= 1) {  // step = byte operator ^ (2^j) at bit j of len_b
+    if (n & 1) reg = gf2_apply(step, reg);
+    if (n > 1) {
+      gf2_compose(tmp, step, step);
+      std::memcpy(step, tmp, sizeof(step));
+    }
+  }
+  return reg ^ crc_b;
+}
+
 void write_metadata(const std::string& path, int64_t total_size, int p, int k, const Mat& e, bool with_matrix,
                     const std::vector<uint32_t>& crc) {
   FILE* fp = std::fopen(path.c_str(), "wb");

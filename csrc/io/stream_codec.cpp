@@ -18,6 +18,7 @@
 #include <thread>
 
 #include "gfrs/format.h"
+#include "gfrs/host_desc.h"
 #include "gfrs/trace.h"
 
 namespace gfrs {
@@ -190,41 +191,89 @@ int64_t stream_window(const StreamOptions& opt, int rows, int64_t C) { return pi
 
 std::string progress_path(const std::string& target) { return target + ".PROGRESS"; }
 
+namespace {
+
+// The column range [lo, hi) of a call (validated), the checkpoint path and the window.
+struct Range {
+  int64_t lo = 0, hi = 0, W = 0;
+  std::string prog;
+};
+
+Range column_range(const StreamOptions& opt, const std::string& target, int rows, int64_t C, int field_w) {
+  Range r;
+  r.lo = opt.col_lo;
+  r.hi = opt.col_hi < 0 ? C : std::min<int64_t>(opt.col_hi, C);
+  if (r.lo < 0 || r.lo > r.hi) throw std::invalid_argument("stream codec: bad column range");
+  if (field_w == 16 && (r.lo % 2 || r.hi % 2)) throw std::invalid_argument("stream codec: GF(2^16) columns are whole symbols");
+  r.W = pick_window(opt, rows, std::max<int64_t>(1, r.hi - r.lo));
+  if (field_w == 16) r.W += r.W % 2;  // whole 16-bit symbols per window
+  r.prog = progress_path(target);
+  if (opt.shard) r.prog += "." + std::to_string(r.lo) + "-" + std::to_string(r.hi);
+  return r;
+}
+
+// Checkpoint "<key> <offset> [crc ...]": the offset reached (in [lo, hi]) when the key matches.
+bool resume_point(const std::string& prog, const std::string& key, size_t extra, int64_t lo, int64_t hi,
+                  int64_t& off, std::vector<std::string>& rest) {
+  const auto tok = read_progress(prog);
+  std::istringstream ks(key);
+  std::vector<std::string> kt;
+  for (std::string x; ks >> x;) kt.push_back(x);
+  if (tok.size() != kt.size() + 1 + extra || !std::equal(kt.begin(), kt.end(), tok.begin())) return false;
+  off = std::stoll(tok[kt.size()]);
+  if (off < lo || off > hi) return false;
+  rest.assign(tok.begin() + long(kt.size()) + 1, tok.end());
+  return true;
+}
+
+}  // namespace
+
 StreamReport encode_file_stream(const std::string& file, int k, int p, MatrixKind kind, const GemmFn& gemm,
                                 const HostAlloc& alloc, const StreamOptions& opt, bool cpu_meta) {
-  if (k <= 0 || p < 0 || k + p > 256) throw std::invalid_argument("encode: need k >= 1, p >= 0, k + p <= 256");
+  const int fw = opt.field_w;
+  if (fw != 8 && fw != 16) throw std::invalid_argument("encode: field width must be 8 or 16");
+  if (k <= 0 || p < 0 || k + p > max_rows(fw))
+    throw std::invalid_argument(fw == 16 ? "encode: need k >= 1, p >= 0, k + p <= 65535 (GF(2^16))"
+                                         : "encode: need k >= 1, p >= 0, k + p <= 256");
+  if (fw == 16 && cpu_meta) throw std::invalid_argument("encode: the 2-line CPU METADATA has no GF(2^16) form");
   StreamReport rep;
   rep.k = k;
   rep.p = p;
   rep.total_size = file_size(file);
-  const int64_t C = std::max<int64_t>(1, chunk_size(rep.total_size, k));
+  const int64_t C = std::max<int64_t>(fw == 16 ? 2 : 1, chunk_size(rep.total_size, k, fw));
   rep.chunk_size = C;
   const int n = k + p;
-  const int64_t W = pick_window(opt, n, C);
+  const Range rg = column_range(opt, file, n, C, fw);
+  const int64_t W = rg.W;
   rep.window = W;
+  rep.col_lo = rg.lo;
+  rep.col_hi = rg.hi;
   auto t = Clock::now();
-  const Mat e = p ? encoding_matrix(kind, k, p) : Mat{};
+  gf16w::Mat e16;
+  Mat e;
+  if (p && fw == 16) {
+    e16 = encoding_matrix16(kind, k, p);
+    e = pack16(e16);
+  } else if (p) {
+    e = encoding_matrix(kind, k, p);
+  }
   rep.ms_matrix = ms_since(t);
 
-  // resume point
-  const std::string prog = progress_path(file);
+  // resume point (the key names everything the bytes depend on, the column range included)
   std::ostringstream key;
-  key << "gfrs-progress 1 encode " << rep.total_size << ' ' << k << ' ' << p << ' ' << int(kind) << ' '
-      << int(cpu_meta) << ' ' << C;
-  int64_t start = 0;
+  key << "gfrs-progress 2 encode " << rep.total_size << ' ' << k << ' ' << p << ' ' << int(kind) << ' '
+      << int(cpu_meta) << ' ' << C << ' ' << fw << ' ' << rg.lo << ' ' << rg.hi;
+  int64_t start = rg.lo;
   std::vector<uint32_t> crc(size_t(n), 0);
   if (opt.resume) {
-    const auto tok = read_progress(prog);
-    std::istringstream ks(key.str());
-    std::vector<std::string> kt;
-    for (std::string x; ks >> x;) kt.push_back(x);
-    if (tok.size() == kt.size() + 1 + size_t(n) && std::equal(kt.begin(), kt.end(), tok.begin())) {
-      const int64_t off = std::stoll(tok[kt.size()]);
-      bool ok = off >= 0 && off <= C;
-      for (int i = 0; ok && i < n; ++i) ok = file_at_least(chunk_path(file, i), off);
+    int64_t off;
+    std::vector<std::string> rest;
+    if (resume_point(rg.prog, key.str(), size_t(n), rg.lo, rg.hi, off, rest)) {
+      bool ok = true;
+      for (int i = 0; ok && i < n; ++i) ok = file_at_least(chunk_path(file, i), opt.shard ? C : off);
       if (ok) {
         start = off;
-        for (int i = 0; i < n; ++i) crc[size_t(i)] = uint32_t(std::stoul(tok[kt.size() + 1 + size_t(i)]));
+        for (int i = 0; i < n; ++i) crc[size_t(i)] = uint32_t(std::stoul(rest[size_t(i)]));
       }
     }
   }
@@ -232,13 +281,13 @@ StreamReport encode_file_stream(const std::string& file, int k, int p, MatrixKin
 
   Fd in = open_or_throw(file, O_RDONLY);
   std::vector<Fd> outs;
-  for (int i = 0; i < n; ++i)
-    outs.push_back(open_or_throw(chunk_path(file, i), O_WRONLY | O_CREAT | (start ? 0 : O_TRUNC)));
+  const int oflags = opt.shard ? O_WRONLY : (O_WRONLY | O_CREAT | (start > rg.lo || rg.lo > 0 ? 0 : O_TRUNC));
+  for (int i = 0; i < n; ++i) outs.push_back(open_or_throw(chunk_path(file, i), oflags));
   Block buf(alloc, size_t(3) * n * size_t(W));
   auto row = [&](int set, int i) { return buf.p + (size_t(set) * n + size_t(i)) * size_t(W); };
 
   run_windows(
-      start, C, W, opt.stop_after,
+      start, rg.hi, W, opt.stop_after,
       [&](int set, int64_t off, int64_t len) {
         for_rows(k, [&](int j) { pread_full(in.fd, row(set, j), len, int64_t(j) * C + off); });
       },
@@ -248,7 +297,7 @@ StreamReport encode_file_stream(const std::string& file, int k, int p, MatrixKin
         std::vector<uint8_t*> op(p);
         for (int j = 0; j < k; ++j) ip[j] = row(set, j);
         for (int i = 0; i < p; ++i) op[i] = row(set, k + i);
-        gemm(ip, op, e, len, 8);
+        gemm(ip, op, e, len, fw);
       },
       [&](int set, int64_t off, int64_t len) {
         for_rows(n, [&](int i) {
@@ -256,55 +305,67 @@ StreamReport encode_file_stream(const std::string& file, int k, int p, MatrixKin
           pwrite_full(outs[size_t(i)].fd, row(set, i), len, off);
           if (opt.durable) ::fdatasync(outs[size_t(i)].fd);
         });
-        write_progress(prog, key.str() + ' ' + std::to_string(off + len) + join_u32(crc) + '\n', opt.durable);
+        write_progress(rg.prog, key.str() + ' ' + std::to_string(off + len) + join_u32(crc) + '\n', opt.durable);
       },
       rep);
 
   const int64_t done = start + int64_t(rep.windows) * W;
-  if (done < C) return rep;  // stopped early (stop_after): the checkpoint says where to resume
+  if (done < rg.hi) return rep;  // stopped early (stop_after): the checkpoint says where to resume
+  if (opt.shard) {  // the coordinator combines the shards' CRCs and writes the METADATA
+    rep.crc = crc;
+    std::remove(rg.prog.c_str());
+    rep.complete = true;
+    return rep;
+  }
+  if (rg.lo != 0 || rg.hi != C) throw std::invalid_argument("encode: a partial column range needs shard mode");
   for (int i = 0; i < n; ++i)
     if (::ftruncate(outs[size_t(i)].fd, C) != 0) throw std::runtime_error("cannot size chunk file");
-  write_metadata(metadata_path(file), rep.total_size, p, k, e, !cpu_meta, cpu_meta ? std::vector<uint32_t>{} : crc);
-  std::remove(prog.c_str());
+  if (fw == 16)
+    write_metadata16(metadata_path(file), rep.total_size, p, k, e16, crc);
+  else
+    write_metadata(metadata_path(file), rep.total_size, p, k, e, !cpu_meta, cpu_meta ? std::vector<uint32_t>{} : crc);
+  rep.crc = crc;
+  std::remove(rg.prog.c_str());
   rep.complete = true;
   return rep;
 }
 
-StreamReport decode_file_stream(const std::string& file, const std::string& conf, const std::string& out,
-                                const GemmFn& gemm, const HostAlloc& alloc, const StreamOptions& opt) {
-  StreamReport rep;
-  const Metadata md = read_metadata(metadata_path(file));
-  if (md.w != 8)
-    throw std::runtime_error("the windowed codec handles GF(2^8) stripes; decode a GF(2^16) stripe without --window");
-  const int k = md.k, n = md.k + md.p;
-  rep.k = k;
-  rep.p = md.p;
-  rep.total_size = md.total_size;
-  const int64_t C = std::max<int64_t>(1, chunk_size(md.total_size, k));
-  rep.chunk_size = C;
-  const int64_t W = pick_window(opt, 2 * k, C);
-  rep.window = W;
+namespace {
 
-  // candidate chunks in conf order (see decode_file: aggressive read); verification streams each
-  // chunk through its CRC-32 in windows, so no chunk is ever held whole in memory
-  auto t = Clock::now();
+struct Candidates {
+  std::vector<int> idx;
+  std::vector<std::string> path;
+};
+
+Candidates conf_candidates(const std::string& file, const std::string& conf, const Metadata& md) {
+  const int k = md.k, n = md.k + md.p;
   const std::vector<std::string> names = read_conf(conf);
   if (int(names.size()) < k)
     throw std::runtime_error("configuration lists " + std::to_string(names.size()) + " chunks, need k = " +
                              std::to_string(k));
-  std::vector<int> cand_idx;
-  std::vector<std::string> cand_path;
+  Candidates c;
   std::set<int> seen;
   for (const auto& nm : names) {
     const int idx = chunk_index(nm);
     if (idx < 0 || idx >= n) throw std::runtime_error("bad chunk name in configuration: " + nm);
     if (!seen.insert(idx).second) throw std::runtime_error("duplicate chunk in configuration: " + nm);
-    cand_idx.push_back(idx);
-    cand_path.push_back(resolve_chunk(nm, file));
+    c.idx.push_back(idx);
+    c.path.push_back(resolve_chunk(nm, file));
   }
-  std::vector<uint8_t> scratch(static_cast<size_t>(std::min<int64_t>(W, int64_t(16) << 20)));
+  return c;
+}
+
+int64_t stripe_chunk(const Metadata& md) {
+  return std::max<int64_t>(md.w == 16 ? 2 : 1, chunk_size(md.total_size, md.k, md.w));
+}
+
+// First recoverable k-subset (conf order) of the candidates that exist and pass their CRC; returns
+// positions into the candidate list.
+std::vector<int> pick_survivors(const Metadata& md, const Candidates& cand, int64_t C, int* rejected) {
+  const int k = md.k;
+  std::vector<uint8_t> scratch(size_t(std::min<int64_t>(std::max<int64_t>(C, 1), int64_t(16) << 20)));
   auto verified_ok = [&](int ci) -> bool {
-    const std::string& path = cand_path[size_t(ci)];
+    const std::string& path = cand.path[size_t(ci)];
     if (!file_at_least(path, md.total_size > 0 ? C : 0)) return false;
     if (md.crc.empty()) return true;
     Fd f(::open(path.c_str(), O_RDONLY | O_CLOEXEC));
@@ -315,16 +376,14 @@ StreamReport decode_file_stream(const std::string& file, const std::string& conf
       pread_full(f.fd, scratch.data(), len, off);
       c = crc32(scratch.data(), len, c);
     }
-    if (c != md.crc[size_t(cand_idx[size_t(ci)])]) {
-      ++rep.rejected;
+    if (c != md.crc[size_t(cand.idx[size_t(ci)])]) {
+      if (rejected) ++*rejected;
       return false;
     }
     return true;
   };
-  std::vector<int> verified, rows;
-  Mat dm;
-  bool found = false;
-  for (int ci = 0; ci < int(cand_idx.size()) && !found; ++ci) {
+  std::vector<int> verified;
+  for (int ci = 0; ci < int(cand.idx.size()); ++ci) {
     if (!verified_ok(ci)) continue;
     verified.push_back(ci);
     if (int(verified.size()) < k) continue;
@@ -334,14 +393,11 @@ StreamReport decode_file_stream(const std::string& file, const std::string& conf
     const int V = int(verified.size());
     for (long tries = 0; tries < 100000; ++tries) {
       std::vector<int> rr(k);
-      for (int i = 0; i < k; ++i) rr[i] = cand_idx[size_t(verified[size_t(pick[i])])];
-      if (decode_matrix(md.g, k, rr, dm)) {
-        rows = rr;
+      for (int i = 0; i < k; ++i) rr[i] = cand.idx[size_t(verified[size_t(pick[i])])];
+      if (decode_coefficients(md, rr, nullptr, nullptr)) {
         std::vector<int> chosen(k);
         for (int i = 0; i < k; ++i) chosen[i] = verified[size_t(pick[i])];
-        verified = chosen;
-        found = true;
-        break;
+        return chosen;
       }
       int i = k - 1;
       while (i >= 0 && pick[i] == V - k + i) --i;
@@ -350,11 +406,61 @@ StreamReport decode_file_stream(const std::string& file, const std::string& conf
       for (int j = i + 1; j < k; ++j) pick[j] = pick[j - 1] + 1;
     }
   }
-  if (!found) {
-    if (int(verified.size()) < k)
-      throw std::runtime_error("only " + std::to_string(verified.size()) + " intact chunks available, need k = " +
-                               std::to_string(k));
-    throw std::runtime_error("unrecoverable erasure pattern: the selected rows of the generator are singular");
+  if (int(verified.size()) < k)
+    throw std::runtime_error("only " + std::to_string(verified.size()) + " intact chunks available, need k = " +
+                             std::to_string(k));
+  throw std::runtime_error("unrecoverable erasure pattern: the selected rows of the generator are singular");
+}
+
+}  // namespace
+
+std::vector<int> choose_survivors(const std::string& file, const std::string& conf, int* rejected) {
+  const Metadata md = read_metadata(metadata_path(file));
+  const Candidates cand = conf_candidates(file, conf, md);
+  const std::vector<int> pos = pick_survivors(md, cand, stripe_chunk(md), rejected);
+  std::vector<int> rows;
+  for (int ci : pos) rows.push_back(cand.idx[size_t(ci)]);
+  return rows;
+}
+
+StreamReport decode_file_stream(const std::string& file, const std::string& conf, const std::string& out,
+                                const GemmFn& gemm, const HostAlloc& alloc, const StreamOptions& opt) {
+  StreamReport rep;
+  const Metadata md = read_metadata(metadata_path(file));
+  const int k = md.k;
+  rep.k = k;
+  rep.p = md.p;
+  rep.total_size = md.total_size;
+  const int64_t C = stripe_chunk(md);
+  rep.chunk_size = C;
+  const std::string dst = out.empty() ? file : out;
+  const Range rg = column_range(opt, dst, 2 * k, C, md.w);
+  const int64_t W = rg.W;
+  rep.window = W;
+  rep.col_lo = rg.lo;
+  rep.col_hi = rg.hi;
+
+  // survivors: the coordinator's choice (opt.rows), else the aggressive read over the conf (every
+  // candidate streamed through its CRC-32 in windows, so no chunk is ever held whole in memory)
+  auto t = Clock::now();
+  const Candidates cand = conf_candidates(file, conf, md);
+  std::vector<int> rows;
+  std::vector<std::string> paths;
+  if (!opt.rows.empty()) {
+    if (int(opt.rows.size()) != k) throw std::runtime_error("decode: the given survivor list needs k entries");
+    for (int r : opt.rows) {
+      const auto it = std::find(cand.idx.begin(), cand.idx.end(), r);
+      if (it == cand.idx.end()) throw std::runtime_error("decode: survivor chunk " + std::to_string(r) + " is not in the configuration");
+      const std::string& path = cand.path[size_t(it - cand.idx.begin())];
+      if (!file_at_least(path, md.total_size > 0 ? C : 0)) throw std::runtime_error("decode: chunk missing or short: " + path);
+      rows.push_back(r);
+      paths.push_back(path);
+    }
+  } else {
+    for (int ci : pick_survivors(md, cand, C, &rep.rejected)) {
+      rows.push_back(cand.idx[size_t(ci)]);
+      paths.push_back(cand.path[size_t(ci)]);
+    }
   }
   std::vector<int> pos_of_native(k, -1);
   for (int i = 0; i < k; ++i)
@@ -363,38 +469,35 @@ StreamReport decode_file_stream(const std::string& file, const std::string& conf
   for (int i = 0; i < k; ++i)
     if (pos_of_native[i] < 0) erased.push_back(i);
   rep.erased = int(erased.size());
+  rep.rows = rows;
   const int ne = int(erased.size());
-  Mat coeff(size_t(ne) * k);
-  for (int e = 0; e < ne; ++e) std::memcpy(&coeff[size_t(e) * k], &dm[size_t(erased[e]) * k], size_t(k));
+  Mat coeff;
+  if (!decode_coefficients(md, rows, &erased, &coeff))
+    throw std::runtime_error("unrecoverable erasure pattern: the selected rows of the generator are singular");
   rep.ms_matrix = ms_since(t);
 
-  const std::string dst = out.empty() ? file : out;
-  const std::string prog = progress_path(dst);
   std::ostringstream key;
-  key << "gfrs-progress 1 decode " << md.total_size << ' ' << k << ' ' << md.p << ' ' << C;
+  key << "gfrs-progress 2 decode " << md.total_size << ' ' << k << ' ' << md.p << ' ' << C << ' ' << md.w << ' '
+      << rg.lo << ' ' << rg.hi;
   for (int r : rows) key << ' ' << r;
-  int64_t start = 0;
+  int64_t start = rg.lo;
   if (opt.resume) {
-    const auto tok = read_progress(prog);
-    std::istringstream ks(key.str());
-    std::vector<std::string> kt;
-    for (std::string x; ks >> x;) kt.push_back(x);
-    if (tok.size() == kt.size() + 1 && std::equal(kt.begin(), kt.end(), tok.begin())) {
-      const int64_t off = std::stoll(tok.back());
-      if (off >= 0 && off <= C && ::access(dst.c_str(), F_OK) == 0) start = off;
-    }
+    int64_t off;
+    std::vector<std::string> rest;
+    if (resume_point(rg.prog, key.str(), 0, rg.lo, rg.hi, off, rest) && ::access(dst.c_str(), F_OK) == 0) start = off;
   }
   rep.resumed_from = start;
 
   std::vector<Fd> ins;
-  for (int i = 0; i < k; ++i) ins.push_back(open_or_throw(cand_path[size_t(verified[size_t(i)])], O_RDONLY));
-  Fd of = open_or_throw(dst, O_WRONLY | O_CREAT | (start ? 0 : O_TRUNC));
+  for (int i = 0; i < k; ++i) ins.push_back(open_or_throw(paths[size_t(i)], O_RDONLY));
+  const int oflags = opt.shard ? O_WRONLY : (O_WRONLY | O_CREAT | (start > rg.lo || rg.lo > 0 ? 0 : O_TRUNC));
+  Fd of = open_or_throw(dst, oflags);
   const int R = k + std::max(ne, 1);
   Block buf(alloc, size_t(3) * R * size_t(W));
   auto row = [&](int set, int i) { return buf.p + (size_t(set) * R + size_t(i)) * size_t(W); };
 
   run_windows(
-      start, C, W, opt.stop_after,
+      start, rg.hi, W, opt.stop_after,
       [&](int set, int64_t off, int64_t len) {
         for_rows(k, [&](int j) { pread_full(ins[size_t(j)].fd, row(set, j), len, off); });
       },
@@ -404,7 +507,7 @@ StreamReport decode_file_stream(const std::string& file, const std::string& conf
         std::vector<uint8_t*> op(ne);
         for (int j = 0; j < k; ++j) ip[j] = row(set, j);
         for (int e = 0; e < ne; ++e) op[e] = row(set, k + e);
-        gemm(ip, op, coeff, len, 8);
+        gemm(ip, op, coeff, len, md.w);
       },
       [&](int set, int64_t off, int64_t len) {
         int e = 0;
@@ -415,14 +518,17 @@ StreamReport decode_file_stream(const std::string& file, const std::string& conf
           if (w > 0) pwrite_full(of.fd, src, w, foff);
         }
         if (opt.durable) ::fdatasync(of.fd);
-        write_progress(prog, key.str() + ' ' + std::to_string(off + len) + '\n', opt.durable);
+        write_progress(rg.prog, key.str() + ' ' + std::to_string(off + len) + '\n', opt.durable);
       },
       rep);
 
   const int64_t done = start + int64_t(rep.windows) * W;
-  if (done < C) return rep;
-  if (::ftruncate(of.fd, md.total_size) != 0) throw std::runtime_error("cannot size output file " + dst);
-  std::remove(prog.c_str());
+  if (done < rg.hi) return rep;
+  if (!opt.shard) {
+    if (rg.lo != 0 || rg.hi != C) throw std::invalid_argument("decode: a partial column range needs shard mode");
+    if (::ftruncate(of.fd, md.total_size) != 0) throw std::runtime_error("cannot size output file " + dst);
+  }
+  std::remove(rg.prog.c_str());
   rep.complete = true;
   return rep;
 }

@@ -55,15 +55,26 @@ inline py::dict stream_report(const gfrs::StreamReport& r) {
   d["windows"] = r.windows;
   d["resumed_from"] = r.resumed_from;
   d["complete"] = r.complete;
+  d["col_lo"] = r.col_lo;
+  d["col_hi"] = r.col_hi;
+  d["crc"] = r.crc;
+  d["rows"] = r.rows;
   return d;
 }
 
-inline gfrs::StreamOptions stream_options(int64_t window, bool resume, bool durable, int stop_after) {
+inline gfrs::StreamOptions stream_options(int64_t window, bool resume, bool durable, int stop_after, int field_w = 8,
+                                          int64_t col_lo = 0, int64_t col_hi = -1, bool shard = false,
+                                          const std::vector<int>& rows = {}) {
   gfrs::StreamOptions o;
   o.window = window;
   o.resume = resume;
   o.durable = durable;
   o.stop_after = stop_after;
+  o.field_w = field_w;
+  o.col_lo = col_lo;
+  o.col_hi = col_hi;
+  o.shard = shard;
+  o.rows = rows;
   return o;
 }
 

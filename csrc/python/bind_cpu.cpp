@@ -125,35 +125,54 @@ PYBIND11_MODULE(_cpu, m) {
   m.def(
       "encode_file_stream",
       [gemm_fn](const std::string& file, int k, int p, const std::string& matrix, bool cpu_meta,
-                const std::string& strategy, int threads, int64_t window, bool resume, bool durable, int stop_after) {
+                const std::string& strategy, int threads, int64_t window, bool resume, bool durable, int stop_after,
+                int field_w, int64_t col_lo, int64_t col_hi, bool shard) {
         const GemmFn g = gemm_fn(strategy, threads);
         StreamReport r;
         {
           py::gil_scoped_release nogil;
           r = encode_file_stream(file, k, p, parse_matrix_kind(matrix), g, default_host_alloc(),
-                                 stream_options(window, resume, durable, stop_after), cpu_meta);
+                                 stream_options(window, resume, durable, stop_after, field_w, col_lo, col_hi, shard),
+                                 cpu_meta);
         }
         return stream_report(r);
       },
       py::arg("file"), py::arg("k"), py::arg("p"), py::arg("matrix") = "vandermonde", py::arg("cpu_meta") = false,
       py::arg("strategy") = "simd", py::arg("threads") = 1, py::arg("window") = 0, py::arg("resume") = true,
-      py::arg("durable") = true, py::arg("stop_after") = -1);
+      py::arg("durable") = true, py::arg("stop_after") = -1, py::arg("field_w") = 8, py::arg("col_lo") = 0,
+      py::arg("col_hi") = -1, py::arg("shard") = false);
   m.def(
       "decode_file_stream",
       [gemm_fn](const std::string& file, const std::string& conf, const std::string& out, const std::string& strategy,
-                int threads, int64_t window, bool resume, bool durable, int stop_after) {
+                int threads, int64_t window, bool resume, bool durable, int stop_after, int64_t col_lo, int64_t col_hi,
+                bool shard, const std::vector<int>& rows) {
         const GemmFn g = gemm_fn(strategy, threads);
         StreamReport r;
         {
           py::gil_scoped_release nogil;
           r = decode_file_stream(file, conf, out, g, default_host_alloc(),
-                                 stream_options(window, resume, durable, stop_after));
+                                 stream_options(window, resume, durable, stop_after, 8, col_lo, col_hi, shard, rows));
         }
         return stream_report(r);
       },
       py::arg("file"), py::arg("conf"), py::arg("out") = "", py::arg("strategy") = "simd", py::arg("threads") = 1,
-      py::arg("window") = 0, py::arg("resume") = true, py::arg("durable") = true, py::arg("stop_after") = -1);
+      py::arg("window") = 0, py::arg("resume") = true, py::arg("durable") = true, py::arg("stop_after") = -1,
+      py::arg("col_lo") = 0, py::arg("col_hi") = -1, py::arg("shard") = false, py::arg("rows") = std::vector<int>{});
   m.def("progress_path", &progress_path);
+  m.def("choose_survivors", [](const std::string& file, const std::string& conf) {
+    int rejected = 0;
+    std::vector<int> rows;
+    {
+      py::gil_scoped_release nogil;
+      rows = choose_survivors(file, conf, &rejected);
+    }
+    return py::make_tuple(rows, rejected);
+  });
+  m.def("crc32", [](const py::bytes& b, uint32_t crc) {
+    const std::string s = b;
+    return crc32(reinterpret_cast<const uint8_t*>(s.data()), int64_t(s.size()), crc);
+  }, py::arg("data"), py::arg("crc") = 0);
+  m.def("crc32_combine", &crc32_combine);
 
   m.def("chunk_path", &chunk_path);
   m.def("chunk_index", &chunk_index);

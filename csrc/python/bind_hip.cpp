@@ -311,34 +311,39 @@ PYBIND11_MODULE(_hip, m) {
       "encode_file_stream",
       [gpu_gemm](const std::string& file, int k, int p, const std::string& matrix, bool cpu_meta,
                  const std::vector<int>& devices, int streams, int64_t slice, int max_blocks, int64_t window,
-                 bool resume, bool durable, int stop_after) {
+                 bool resume, bool durable, int stop_after, int field_w, int64_t col_lo, int64_t col_hi, bool shard) {
         const GemmFn g = gpu_gemm(devices, streams, slice, max_blocks);
         StreamReport r;
         {
           py::gil_scoped_release nogil;
           r = encode_file_stream(file, k, p, parse_matrix_kind(matrix), g, pinned_alloc(),
-                                 stream_options(window, resume, durable, stop_after), cpu_meta);
+                                 stream_options(window, resume, durable, stop_after, field_w, col_lo, col_hi, shard),
+                                 cpu_meta);
         }
         return stream_report(r);
       },
       py::arg("file"), py::arg("k"), py::arg("p"), py::arg("matrix") = "vandermonde", py::arg("cpu_meta") = false,
       py::arg("devices") = std::vector<int>{0}, py::arg("streams") = 2, py::arg("slice") = 16 << 20,
       py::arg("max_blocks") = 0, py::arg("window") = 0, py::arg("resume") = true, py::arg("durable") = true,
-      py::arg("stop_after") = -1);
+      py::arg("stop_after") = -1, py::arg("field_w") = 8, py::arg("col_lo") = 0, py::arg("col_hi") = -1,
+      py::arg("shard") = false);
   m.def(
       "decode_file_stream",
       [gpu_gemm](const std::string& file, const std::string& conf, const std::string& out,
                  const std::vector<int>& devices, int streams, int64_t slice, int max_blocks, int64_t window,
-                 bool resume, bool durable, int stop_after) {
+                 bool resume, bool durable, int stop_after, int64_t col_lo, int64_t col_hi, bool shard,
+                 const std::vector<int>& rows) {
         const GemmFn g = gpu_gemm(devices, streams, slice, max_blocks);
         StreamReport r;
         {
           py::gil_scoped_release nogil;
-          r = decode_file_stream(file, conf, out, g, pinned_alloc(), stream_options(window, resume, durable, stop_after));
+          r = decode_file_stream(file, conf, out, g, pinned_alloc(),
+                                 stream_options(window, resume, durable, stop_after, 8, col_lo, col_hi, shard, rows));
         }
         return stream_report(r);
       },
       py::arg("file"), py::arg("conf"), py::arg("out") = "", py::arg("devices") = std::vector<int>{0},
       py::arg("streams") = 2, py::arg("slice") = 16 << 20, py::arg("max_blocks") = 0, py::arg("window") = 0,
-      py::arg("resume") = true, py::arg("durable") = true, py::arg("stop_after") = -1);
+      py::arg("resume") = true, py::arg("durable") = true, py::arg("stop_after") = -1, py::arg("col_lo") = 0,
+      py::arg("col_hi") = -1, py::arg("shard") = false, py::arg("rows") = std::vector<int>{});
 }

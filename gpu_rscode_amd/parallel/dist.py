@@ -23,6 +23,7 @@ link-bound. Shards are 4 KiB-aligned column ranges so every rank's rows stay 16-
 """
 from __future__ import annotations
 
+import datetime
 import os
 import socket
 from dataclasses import dataclass
@@ -49,8 +50,13 @@ class DistContext:
         return self.rank == 0
 
 
-def init_distributed(backend: str | None = None, force_pg: bool | None = None) -> DistContext:
+def init_distributed(backend: str | None = None, force_pg: bool | None = None,
+                     timeout_s: float | None = None) -> DistContext:
     """Initialise from torchrun's environment (RANK, WORLD_SIZE, LOCAL_RANK, MASTER_*).
+
+    The process group gets a bounded timeout (``timeout_s``, default ``GFRS_PG_TIMEOUT_S`` or 600 s):
+    a collective whose peer is gone raises (gloo) or is aborted by the RCCL watchdog after at most
+    that long, instead of hanging the job.
 
     Backend defaults to ``nccl`` (RCCL) when a GPU is visible, else ``gloo``. Safe to call when a
     process group already exists. At world 1 no process group is created unless ``force_pg`` (or
@@ -78,7 +84,9 @@ def init_distributed(backend: str | None = None, force_pg: bool | None = None) -
         kw = {"device_id": device} if device.type == "cuda" else {}
         if world == 1 and "MASTER_PORT" not in os.environ:
             kw.update(init_method=f"tcp://127.0.0.1:{free_port()}", rank=0, world_size=1)
-        dist.init_process_group(backend, **kw)
+        if timeout_s is None:
+            timeout_s = float(os.environ.get("GFRS_PG_TIMEOUT_S", 600))
+        dist.init_process_group(backend, timeout=datetime.timedelta(seconds=timeout_s), **kw)
     return DistContext(rank, world, local, device, backend)
 
 

@@ -5,11 +5,11 @@
     torchrun --nproc-per-node 8 -m gpu_rscode_amd.utils.cli --dist -k 16 -n 20 -e FILE
 
 Single-process modes call the native file codec (``csrc/io/codec_file.cpp``) with either the gfx950
-streaming pipeline or the C++ CPU codec. ``--dist`` is the multi-GPU mode: every rank reads its own
-4 KiB-aligned column range of every chunk straight from the file (no scatter) in bounded column
-windows (``--window``, default 64 MiB per chunk row), encodes/decodes it on its GPU, and the results
-are either gathered into rank 0 over RCCL point-to-point (default) or written in place by each rank
-(``--gather none``, parallel pwrite).
+streaming pipeline or the C++ CPU codec. ``--dist`` is the multi-GPU mode (one rank per GPU): every
+rank streams its own 4 KiB-aligned column range of every chunk through the native windowed codec
+(``csrc/io/stream_codec.cpp``, shard mode: read / GEMM / write overlapped, pinned buffers,
+checkpointed per shard), reading its columns straight from the file and writing them straight into
+the outputs; only the survivor choice and the per-chunk CRC-32s cross the process group.
 """
 from __future__ import annotations
 
@@ -45,7 +45,8 @@ def _parser() -> argparse.ArgumentParser:
     ap.add_argument("--threads", type=int, default=1, help="CPU backend threads")
     ap.add_argument("--mul", default="simd", help="CPU multiply strategy (row: the scalar product-row form)")
     ap.add_argument("--dist", action="store_true", help="torch.distributed multi-GPU mode (torchrun)")
-    ap.add_argument("--gather", choices=["rccl", "none"], default="rccl")
+    ap.add_argument("--pg-timeout", type=float, default=float(os.environ.get("GFRS_PG_TIMEOUT_S", 300)),
+                    help="--dist: process-group timeout in seconds (a lost peer ends the job after at most this)")
     ap.add_argument("--window", type=int, default=None,
                     help="bounded-memory streaming codec: column windows of this many bytes per chunk "
                          "(0 = auto), checkpointed to <target>.PROGRESS and resumable")
@@ -66,9 +67,6 @@ def main(argv=None) -> int:
         _parser().print_help()
         return 2
     if a.dist:
-        if a.field_w != 8:
-            print("--dist runs GF(2^8) stripes; encode GF(2^16) in single-process mode", file=sys.stderr)
-            return 2
         return _main_dist(a)
     from .._native import cpu, gpu_available, hip
 
@@ -77,8 +75,8 @@ def main(argv=None) -> int:
         if not a.k or not a.n or a.n < a.k:
             print("encode needs -k K -n N -e FILE with 1 <= K <= N", file=sys.stderr)
             return 2
-        if a.field_w == 16 and (a.window is not None or a.cpu_meta):
-            print("-w 16 writes the versioned METADATA without --window / --cpu-meta", file=sys.stderr)
+        if a.field_w == 16 and a.cpu_meta:
+            print("-w 16 writes the versioned METADATA (no --cpu-meta form)", file=sys.stderr)
             return 2
         fw = {} if a.field_w == 8 else dict(field_w=a.field_w)
         if a.zero_copy and backend == "gpu" and a.window is None:
@@ -89,6 +87,8 @@ def main(argv=None) -> int:
             ndev = hip().device_count()
             devs = list(range(a.gpus or ndev))
             fn = hip().encode_file_stream if st else hip().encode_file
+            if st:
+                fw.pop("zero_copy", None)
             r = fn(a.encode_file, a.k, a.n - a.k, a.matrix, a.cpu_meta, devs, a.streams, a.slice, a.grid, **st, **fw)
         else:
             fn = cpu().encode_file_stream if st else cpu().encode_file
@@ -117,181 +117,145 @@ def main(argv=None) -> int:
 
 
 # ---- distributed mode -------------------------------------------------------------------------
-DIST_WINDOW = 64 << 20  # default column window per chunk row and rank (host RAM ~ (k + p) x window)
-
-
-def _read_cols(path: str, offset: int, nbytes: int, out: np.ndarray) -> None:
-    """pread ``nbytes`` at ``offset`` into ``out``; zero-fill the rest (past EOF / past nbytes)."""
-    got = 0
-    if nbytes > 0:
-        fd = os.open(path, os.O_RDONLY)
-        try:
-            view = memoryview(out)[:nbytes]
-            while got < nbytes:
-                n = os.preadv(fd, [view[got:]], offset + got)
-                if n <= 0:
-                    break
-                got += n
-        finally:
-            os.close(fd)
-    out[got:] = 0
-
-
-def _pwrite(fd: int, offset: int, data: np.ndarray) -> None:
-    view = memoryview(np.ascontiguousarray(data)).cast("B")
-    done = 0
-    while done < len(view):
-        done += os.pwrite(fd, view[done:], offset + done)
-
-
-def _windows(world: int, C: int, window: int):
-    """Per window index t: every rank's (column offset, width) — identical on all ranks, so the
-    collective per window lines up even where a rank's shard is exhausted (width 0)."""
-    from ..parallel.dist import shard_range
-
-    spans = [shard_range(C, world, r) for r in range(world)]
-    nwin = max(((b - a) + window - 1) // window for a, b in spans) if C else 0
-    for t in range(nwin):
-        yield [(a + t * window, max(0, min(window, b - a - t * window))) for a, b in spans]
+def _create(path: str, size: int) -> None:
+    """Create (or truncate) ``path`` and size it: shards then write their columns in place, so no
+    stale bytes of an older, longer file survive."""
+    fd = os.open(path, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644)
+    try:
+        os.ftruncate(fd, size)
+    finally:
+        os.close(fd)
 
 
 def _main_dist(a) -> int:
-    """Windowed, column-sharded encode/decode over torch.distributed.
+    """Multi-GPU file codec: one rank per GPU (torchrun), each running its column shard through the
+    native streaming codec.
 
-    Every rank owns a 4 KiB-aligned column range of every chunk (the reference's per-device split,
-    src/encode.cu:368-381) and walks it in windows of ``--window`` bytes per chunk row, so host
-    memory stays bounded at ~(k + p) x window per rank whatever the file size. Per window: pread
-    of the rank's columns, H2D, GF-GEMM on the rank's GPU, then either every rank pwrites its own
-    columns (``--gather none``) or the window's results travel to rank 0 over RCCL point-to-point
-    (received in place, one xGMI link per peer) and rank 0 writes them (``--gather rccl``, the
-    reference's gather-to-one-writer, src/encode.cu:410-429). Rank 0 creates every output at its
-    final size first, so no stale bytes of an older, longer file survive."""
+    The reference splits every chunk's columns over its GPUs (src/encode.cu:368-381,
+    src/decode.cu:335-408), stages the slices through pinned host buffers and gathers the results
+    into one writer (src/encode.cu:389-398, 410-429). Here every rank owns a 4 KiB-aligned column
+    range of every chunk (``shard_range``) and streams it through ``encode_file_stream`` /
+    ``decode_file_stream`` in shard mode — the three-stage read / GEMM / write window pipeline of
+    ``csrc/io/stream_codec.cpp`` with pinned buffers on its own GPU, checkpointed per shard — reading
+    its columns straight from the input file and pwriting them straight into the outputs. What
+    crosses the process group is tiny: rank 0 creates the outputs at their final size, picks and
+    CRC-verifies the decode survivors (broadcast), and combines every rank's per-chunk CRC-32s
+    (``crc32_combine`` in column order) into the METADATA.
+
+    A rank that fails exits non-zero at once, issuing no further collective: its peers' next one
+    fails (gloo) or is aborted by the process group's bounded timeout (``--pg-timeout``), and torchrun
+    ends the job."""
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # (before the first HIP call: RCCL peers)
+    from ..parallel.dist import init_distributed
+
+    ctx = init_distributed(timeout_s=a.pg_timeout)
+    try:
+        rc = _dist_run(a, ctx)
+    except Exception as ex:  # noqa: BLE001 — this rank stops here, without another collective
+        print(f"[rank {ctx.rank}] --dist failed: {type(ex).__name__}: {ex}", file=sys.stderr, flush=True)
+        sys.stdout.flush()
+        os._exit(1)
+    import torch.distributed as dist
+
+    if dist.is_initialized():
+        dist.destroy_process_group()
+    return rc
+
+
+def _dist_run(a, ctx) -> int:
     import torch
     import torch.distributed as dist
 
+    from .._native import cpu, hip
     from ..models import ReedSolomon
-    from ..parallel.dist import broadcast_matrix, gather_pieces, init_distributed
+    from ..parallel.dist import shard_range
     from . import fileformat as ff
 
-    ctx = init_distributed()
     world, rank = ctx.world, ctx.rank
-    window = max(4096, ((a.window or DIST_WINDOW) + 4095) // 4096 * 4096)
-    t0 = time.perf_counter()
+    on_gpu = ctx.device.type == "cuda"
 
     def barrier():
         if world > 1:
             dist.barrier()
 
-    def create(path: str, size: int) -> None:
-        fd = os.open(path, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644)
-        try:
-            os.ftruncate(fd, size)
-        finally:
-            os.close(fd)
-
+    fault = os.environ.get("GFRS_DIST_FAULT_RANK")
+    t0 = time.perf_counter()
+    st = dict(window=a.window or 0, resume=not a.no_resume, durable=not a.no_sync)
     if a.encode_file:
         path = a.encode_file
+        if not a.k or not a.n or a.n < a.k:
+            raise ValueError("encode needs -k K -n N -e FILE with 1 <= K <= N")
+        if a.field_w == 16 and a.cpu_meta:
+            raise ValueError("-w 16 writes the versioned METADATA (no --cpu-meta form)")
         total = os.path.getsize(path)
-        k, p = a.k, a.n - a.k
-        C = ff.chunk_size(total, k)
-        e = ReedSolomon(k, a.n, matrix=a.matrix).E if ctx.is_root else None
-        e = broadcast_matrix(e, ctx.device)
-        rs = ReedSolomon(k, a.n)
-        rs.E, rs.G = e, np.vstack([np.eye(k, dtype=np.uint8), e])
+        k, p, n = a.k, a.n - a.k, a.n
+        C = max(2 if a.field_w == 16 else 1, ff.chunk_size(total, k, a.field_w))
         if ctx.is_root:
-            for i in range(a.n):
-                create(ff.chunk_path(path, i), C)
+            for i in range(n):
+                _create(ff.chunk_path(path, i), C)
         barrier()
-        fds = [os.open(ff.chunk_path(path, i), os.O_WRONLY) for i in range(a.n)]
-        host = np.zeros((k, window), dtype=np.uint8)
+        if fault is not None and int(fault) == rank:
+            raise RuntimeError("injected fault (GFRS_DIST_FAULT_RANK)")
+        lo, hi = shard_range(C, world, rank)
+        kw = dict(st, field_w=a.field_w, col_lo=lo, col_hi=hi, shard=True)
+        if on_gpu:
+            r = hip().encode_file_stream(path, k, p, a.matrix, a.cpu_meta, [ctx.local_rank], a.streams, a.slice,
+                                         a.grid, **kw)
+        else:
+            r = cpu().encode_file_stream(path, k, p, a.matrix, a.cpu_meta, a.mul, a.threads, **kw)
+        # every rank's shard CRCs (and width) to rank 0, combined in column order
+        mine = torch.tensor([hi - lo] + list(r["crc"]), dtype=torch.int64, device=ctx.device)
+        parts = [torch.zeros_like(mine) for _ in range(world)] if world > 1 else [mine]
+        if world > 1:
+            dist.all_gather(parts, mine)
+        if ctx.is_root:
+            crc = [0] * n
+            for part in parts:
+                vals = part.tolist()
+                crc = [cpu().crc32_combine(c, int(x), vals[0]) for c, x in zip(crc, vals[1:])]
+            e = ReedSolomon(k, n, matrix=a.matrix, field="gf65536" if a.field_w == 16 else "gf256").E
+            ff.write_metadata(ff.metadata_path(path), total, p, k, e, with_matrix=not a.cpu_meta,
+                              crc=None if a.cpu_meta else crc, w=a.field_w)
+        barrier()
+        _say(a, f"[rank {rank}] encoded columns [{lo}, {hi}) of {C} in {r['windows']} window(s) of {r['window']} B "
+                f"in {1e3 * (time.perf_counter() - t0):.1f}ms (read {r['ms_read']:.1f}, GEMM {r['ms_compute']:.1f}, "
+                f"write {r['ms_write']:.1f} ms, overlapped)")
+        return 0
+    if not a.in_file or not a.conf:
+        raise ValueError("decode needs -d -i FILE -c CONF")
+    md = ff.read_metadata(ff.metadata_path(a.in_file))
+    C = max(2 if md.w == 16 else 1, ff.chunk_size(md.total_size, md.k, md.w))
+    dst = a.out or a.in_file
+    # rank 0 picks (and CRC-verifies) the survivors; status first: a failure there stops every rank
+    pick = torch.zeros(md.k + 1, dtype=torch.int64, device=ctx.device)
+    if ctx.is_root:
         try:
-            for spans in _windows(world, C, window):
-                o, w = spans[rank]
-                if w:
-                    for j in range(k):  # natives: this rank's columns of chunk j, zero past EOF
-                        start = j * C + o
-                        _read_cols(path, start, max(0, min(w, total - start)), host[j, :w])
-                        _pwrite(fds[j], o, host[j, :w])
-                    parity = rs.encode(torch.from_numpy(host[:, :w]).to(ctx.device))
-                else:
-                    parity = torch.empty((p, 0), dtype=torch.uint8, device=ctx.device)
-                if a.gather == "rccl" and world > 1:
-                    if ctx.device.type == "cuda":
-                        torch.cuda.synchronize()
-                    full = gather_pieces(parity, [ww for _, ww in spans])
-                    if ctx.is_root:
-                        ph = full.cpu().numpy()
-                        col = 0
-                        for ro, rw in spans:
-                            for i in range(p):
-                                _pwrite(fds[k + i], ro, ph[i, col:col + rw])
-                            col += rw
-                elif w:
-                    ph = parity.cpu().numpy()
-                    for i in range(p):
-                        _pwrite(fds[k + i], o, ph[i, :w])
-        finally:
-            for fd in fds:
-                os.close(fd)
-        if ctx.is_root:
-            ff.write_metadata(ff.metadata_path(path), total, p, k, e, with_matrix=not a.cpu_meta)
-        barrier()
-        lo, hi = spans_of(world, C, rank)
-        _say(a, f"[rank {rank}] encoded columns [{lo}, {hi}) in windows of {window} B "
-                f"in {1e3 * (time.perf_counter() - t0):.1f}ms")
-    else:
-        md = ff.read_metadata(ff.metadata_path(a.in_file))
-        if md.w != 8:
-            raise SystemExit("--dist decodes GF(2^8) stripes; decode a GF(2^16) stripe in single-process mode")
-        names = ff.read_conf(a.conf)[: md.k]
-        rows = [ff.chunk_index(nm) for nm in names]
-        k, C = md.k, ff.chunk_size(md.total_size, md.k)
-        rs = ReedSolomon(k, md.n)
-        rs.E, rs.G = md.e, md.g
-        dst = a.out or a.in_file
-        if ctx.is_root:
-            create(dst, md.total_size)
-        barrier()
-        paths = [ff.resolve_chunk(nm, a.in_file) for nm in names]
-        fd_out = os.open(dst, os.O_WRONLY)
-        host = np.zeros((k, window), dtype=np.uint8)
-
-        def write_natives(nat: np.ndarray, o: int, w: int) -> None:
-            for j in range(k):
-                start = j * C + o
-                n = max(0, min(w, md.total_size - start))
-                if n:
-                    _pwrite(fd_out, start, nat[j, :n])
-
-        try:
-            for spans in _windows(world, C, window):
-                o, w = spans[rank]
-                if w:
-                    for j, pth in enumerate(paths):
-                        _read_cols(pth, o, w, host[j, :w])
-                    out = rs.decode(torch.from_numpy(host[:, :w]).to(ctx.device), rows)
-                else:
-                    out = torch.empty((k, 0), dtype=torch.uint8, device=ctx.device)
-                if a.gather == "rccl" and world > 1:
-                    if ctx.device.type == "cuda":
-                        torch.cuda.synchronize()
-                    full = gather_pieces(out, [ww for _, ww in spans])
-                    if ctx.is_root:
-                        fh = full.cpu().numpy()
-                        col = 0
-                        for ro, rw in spans:
-                            write_natives(fh[:, col:col + rw], ro, rw)
-                            col += rw
-                elif w:
-                    write_natives(out.cpu().numpy(), o, w)
-        finally:
-            os.close(fd_out)
-        barrier()
-        lo, hi = spans_of(world, C, rank)
-        _say(a, f"[rank {rank}] decoded columns [{lo}, {hi}) in windows of {window} B "
-                f"in {1e3 * (time.perf_counter() - t0):.1f}ms")
+            rows, _ = cpu().choose_survivors(a.in_file, a.conf)
+            pick[1:] = torch.tensor(rows, dtype=torch.int64)
+        except Exception as ex:  # noqa: BLE001 — told to every rank through the broadcast
+            pick[0] = 1
+            err = ex
+        if not int(pick[0].item()):
+            _create(dst, md.total_size)
     if world > 1:
-        dist.destroy_process_group()
+        dist.broadcast(pick, 0)
+    if int(pick[0].item()):
+        if ctx.is_root:
+            raise err
+        raise RuntimeError("rank 0 could not choose the decode survivors")
+    rows = [int(x) for x in pick[1:].tolist()]
+    barrier()
+    if fault is not None and int(fault) == rank:
+        raise RuntimeError("injected fault (GFRS_DIST_FAULT_RANK)")
+    lo, hi = shard_range(C, world, rank)
+    kw = dict(st, col_lo=lo, col_hi=hi, shard=True, rows=rows)
+    if on_gpu:
+        r = hip().decode_file_stream(a.in_file, a.conf, dst, [ctx.local_rank], a.streams, a.slice, a.grid, **kw)
+    else:
+        r = cpu().decode_file_stream(a.in_file, a.conf, dst, a.mul, a.threads, **kw)
+    barrier()
+    _say(a, f"[rank {rank}] decoded columns [{lo}, {hi}) of {C} ({r['erased']} erased native(s)) in "
+            f"{r['windows']} window(s) of {r['window']} B in {1e3 * (time.perf_counter() - t0):.1f}ms")
     return 0
 
 

@@ -34,8 +34,8 @@ def test_python_cli_cpu_roundtrip(tmp_path):
     assert (tmp_path / "o.bin").read_bytes() == payload
 
 
-@pytest.mark.parametrize("gather", ["rccl", "none"])
-def test_torchrun_dist_cli_matches_single_process(tmp_path, gather):
+@pytest.mark.parametrize("w", [8, 16])
+def test_torchrun_dist_cli_matches_single_process(tmp_path, w):
     payload = os.urandom(3 * 4096 * 10 + 999)
     d1, d2 = tmp_path / "dist", tmp_path / "single"
     d1.mkdir()
@@ -44,14 +44,16 @@ def test_torchrun_dist_cli_matches_single_process(tmp_path, gather):
     (d2 / "f.bin").write_bytes(payload)
     env = dict(os.environ, PYTHONPATH=ROOT, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
     base = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-            "--master-addr=127.0.0.1", f"--master-port={_port()}", "-m", "gpu_rscode_amd", "--dist", "--gather", gather]
-    r = subprocess.run(base + ["-k", "10", "-n", "14", "-e", "f.bin"], cwd=d1, capture_output=True, text=True,
-                       timeout=300, env=env)
+            "--master-addr=127.0.0.1", f"--master-port={_port()}", "-m", "gpu_rscode_amd", "--dist"]
+    r = subprocess.run(base + ["-k", "10", "-n", "14", "-w", str(w), "-e", "f.bin"], cwd=d1, capture_output=True,
+                       text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
-    r = _py(["-k", "10", "-n", "14", "-e", "f.bin", "--backend", "cpu"], d2)
+    r = _py(["-k", "10", "-n", "14", "-w", str(w), "-e", "f.bin", "--backend", "cpu"], d2)
     assert r.returncode == 0, r.stderr
     for i in range(14):
         assert (d1 / f"_{i}_f.bin").read_bytes() == (d2 / f"_{i}_f.bin").read_bytes(), i
+    # the METADATA (matrix and the CRCs combined from both ranks' shards) is the single process's
+    assert (d1 / "f.bin.METADATA").read_bytes() == (d2 / "f.bin.METADATA").read_bytes()
     ff.write_conf(str(d1 / "conf"), [f"_{i}_f.bin" for i in (1, 2, 3, 5, 6, 8, 10, 11, 12, 13)])
     base[6] = f"--master-port={_port()}"
     r = subprocess.run(base + ["-d", "-i", "f.bin", "-c", "conf", "-o", "o.bin"], cwd=d1, capture_output=True,
@@ -60,8 +62,7 @@ def test_torchrun_dist_cli_matches_single_process(tmp_path, gather):
     assert (d1 / "o.bin").read_bytes() == payload
 
 
-@pytest.mark.parametrize("gather", ["rccl", "none"])
-def test_torchrun_dist_cli_windows_world3_and_stale_outputs(tmp_path, gather):
+def test_torchrun_dist_cli_windows_world3_and_stale_outputs(tmp_path):
     """3 ranks walking their shards in 4 KiB windows (uneven shard sizes, so some ranks run out of
     columns while the window collective continues), over stale, longer chunk / output files."""
     payload = os.urandom(7 * 4096 * 12 + 4321)
@@ -75,8 +76,8 @@ def test_torchrun_dist_cli_windows_world3_and_stale_outputs(tmp_path, gather):
     (d1 / "o.bin").write_bytes(b"\xee" * (2 * len(payload)))
     env = dict(os.environ, PYTHONPATH=ROOT, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
     base = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=3",
-            "--master-addr=127.0.0.1", f"--master-port={_port()}", "-m", "gpu_rscode_amd", "--dist", "--gather", gather,
-            "--window", "4096"]
+            "--master-addr=127.0.0.1", f"--master-port={_port()}", "-m", "gpu_rscode_amd", "--dist",
+            "--window", "4096", "--no-sync"]
     r = subprocess.run(base + ["-k", "12", "-n", "16", "-e", "f.bin"], cwd=d1, capture_output=True, text=True,
                        timeout=300, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
@@ -109,8 +110,8 @@ def test_torchrun_dist_cli_bounded_host_memory(tmp_path):
     assert r.returncode == 0, r.stderr
     base_kib = resource.getrusage(resource.RUSAGE_CHILDREN).ru_maxrss
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-           "--master-addr=127.0.0.1", f"--master-port={_port()}", "-m", "gpu_rscode_amd", "--dist", "--gather", "rccl",
-           "--window", str(4 << 20)]
+           "--master-addr=127.0.0.1", f"--master-port={_port()}", "-m", "gpu_rscode_amd", "--dist",
+           "--window", str(4 << 20), "--no-sync"]
     r = subprocess.run(cmd + ["-k", "4", "-n", "6", "-e", "f.bin"], cwd=tmp_path, capture_output=True, text=True,
                        timeout=600, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
@@ -127,3 +128,36 @@ def test_torchrun_dist_cli_bounded_host_memory(tmp_path):
             if not x:
                 break
     assert peak_kib - base_kib < 160 * 1024, (base_kib, peak_kib)
+
+
+def test_torchrun_dist_cli_rank_failure_exits_in_bounded_time(tmp_path):
+    """World 3, rank 1 fails inside its shard (GFRS_DIST_FAULT_RANK): it exits non-zero without
+    another collective, the job ends non-zero well inside the process-group timeout, and rank 0's
+    METADATA is never written (no half-encoded stripe looks complete)."""
+    import time
+
+    payload = os.urandom(5 * 4096 * 9 + 77)
+    (tmp_path / "f.bin").write_bytes(payload)
+    env = dict(os.environ, PYTHONPATH=ROOT, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="",
+               GFRS_DIST_FAULT_RANK="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=3",
+           "--master-addr=127.0.0.1", f"--master-port={_port()}", "-m", "gpu_rscode_amd", "--dist",
+           "--pg-timeout", "60", "-k", "8", "-n", "11", "-e", "f.bin"]
+    t0 = time.monotonic()
+    r = subprocess.run(cmd, cwd=tmp_path, capture_output=True, text=True, timeout=240, env=env)
+    took = time.monotonic() - t0
+    assert r.returncode != 0 and "injected fault" in r.stderr, r.stderr[-3000:]
+    assert took < 120, took
+    assert not (tmp_path / "f.bin.METADATA").exists()
+    # and a decode whose rank fails after the survivor broadcast
+    env.pop("GFRS_DIST_FAULT_RANK")
+    cmd[6] = f"--master-port={_port()}"
+    r = subprocess.run(cmd, cwd=tmp_path, capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    ff.write_conf(str(tmp_path / "conf"), [f"_{i}_f.bin" for i in range(3, 11)])
+    env["GFRS_DIST_FAULT_RANK"] = "2"
+    dcmd = cmd[:10] + ["--pg-timeout", "60", "-d", "-i", "f.bin", "-c", "conf", "-o", "o.bin"]
+    dcmd[6] = f"--master-port={_port()}"
+    t0 = time.monotonic()
+    r = subprocess.run(dcmd, cwd=tmp_path, capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode != 0 and "injected fault" in r.stderr and time.monotonic() - t0 < 120, r.stderr[-3000:]

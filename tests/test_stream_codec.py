@@ -137,3 +137,98 @@ def test_python_cli_streaming_cpu_backend(tmp_path):
     assert main(["-d", "-i", str(f), "-c", str(conf), "-o", str(tmp_path / "o"), "--backend", "cpu",
                  "--window", "0", "-q"]) == 0
     assert (tmp_path / "o").read_bytes() == payload
+
+
+def test_crc32_combine_matches_zlib():
+    import zlib
+
+    rng = os.urandom
+    for la, lb in [(0, 0), (1, 0), (0, 5), (1, 1), (17, 4095), (100_003, 65_537), (3, 1 << 20)]:
+        a, b = rng(la), rng(lb)
+        assert cpu().crc32(a) == zlib.crc32(a)
+        assert cpu().crc32_combine(cpu().crc32(a), cpu().crc32(b), lb) == zlib.crc32(a + b)
+
+
+@pytest.mark.parametrize("size,k,p,w,cuts", [(3_000_017, 10, 4, 8, (0, 100_000, 222_224, None)),
+                                             (1_000_001, 10, 4, 16, (0, 4096, 50_002, None)),
+                                             (99_999, 6, 3, 8, (0, 0, 16_667, None))])
+def test_column_shards_equal_the_whole_encode(tmp_path, size, k, p, w, cuts):
+    """The multi-GPU file codec's building block: every shard [lo, hi) of the columns encoded on its
+    own into pre-sized chunk files (shard=True: no truncation, no METADATA, per-shard checkpoint),
+    shard CRCs combined in column order == the one-call encode's files and METADATA CRCs (an empty
+    shard included)."""
+    payload = os.urandom(size)
+    ref, sh = tmp_path / "ref", tmp_path / "sh"
+    ref.mkdir()
+    sh.mkdir()
+    (ref / "f.bin").write_bytes(payload)
+    (sh / "f.bin").write_bytes(payload)
+    cpu().encode_file_stream(str(ref / "f.bin"), k, p, window=8192, durable=False, field_w=w)
+    C = ff.chunk_size(size, k, w)
+    for i in range(k + p):
+        with open(ff.chunk_path(str(sh / "f.bin"), i), "wb") as fh:
+            fh.truncate(C)
+    bounds = [c if c is not None else C for c in cuts]
+    crc = [0] * (k + p)
+    for lo, hi in zip(bounds, bounds[1:]):
+        r = cpu().encode_file_stream(str(sh / "f.bin"), k, p, window=6000, durable=False, field_w=w, col_lo=lo,
+                                     col_hi=hi, shard=True)
+        assert r["complete"] and (r["col_lo"], r["col_hi"]) == (lo, hi) and len(r["crc"]) == k + p
+        crc = [cpu().crc32_combine(a, b, hi - lo) for a, b in zip(crc, r["crc"])]
+        assert not os.path.exists(str(sh / "f.bin.METADATA"))
+    md = ff.read_metadata(str(ref / "f.bin.METADATA"))
+    assert crc == md.crc
+    for i in range(k + p):
+        assert (sh / f"_{i}_f.bin").read_bytes() == (ref / f"_{i}_f.bin").read_bytes(), i
+    # shard decode with a coordinator-chosen survivor list, each shard into the pre-sized output
+    rows, rejected = cpu().choose_survivors(str(ref / "f.bin"), _conf(ref, "f.bin", list(range(p, k + p))))
+    assert rejected == 0 and rows == list(range(p, k + p))
+    out = tmp_path / "out"
+    with open(out, "wb") as fh:
+        fh.truncate(size)
+    for lo, hi in zip(bounds, bounds[1:]):
+        r = cpu().decode_file_stream(str(ref / "f.bin"), str(ref / "conf"), str(out), window=5000, durable=False,
+                                     col_lo=lo, col_hi=hi, shard=True, rows=rows)
+        assert r["complete"] and r["rows"] == rows
+    assert out.read_bytes() == payload
+
+
+def test_stream_w16_roundtrip_with_resume(tmp_path):
+    """GF(2^16) through the windowed codec: a crash after 3 windows, resume, files identical to the
+    in-memory GF(2^16) encode; the streamed decode (another crash + resume) restores the payload."""
+    payload = os.urandom(1_234_567)
+    a, b = tmp_path / "mem", tmp_path / "str"
+    a.mkdir()
+    b.mkdir()
+    (a / "f.bin").write_bytes(payload)
+    (b / "f.bin").write_bytes(payload)
+    cpu().encode_file(str(a / "f.bin"), 10, 4, field_w=16)
+    f = str(b / "f.bin")
+    r1 = cpu().encode_file_stream(f, 10, 4, window=8191, stop_after=3, durable=False, field_w=16)
+    assert not r1["complete"] and r1["window"] % 2 == 0
+    r2 = cpu().encode_file_stream(f, 10, 4, window=8191, durable=False, field_w=16)
+    assert r2["complete"] and r2["resumed_from"] == 3 * r1["window"]
+    assert _files(a, "f.bin", 14) == _files(b, "f.bin", 14)
+    conf = _conf(b, "f.bin", (4, 5, 6, 7, 8, 9, 10, 11, 12, 13))
+    out = str(b / "out")
+    r3 = cpu().decode_file_stream(f, conf, out, window=4097, stop_after=2, durable=False)
+    assert not r3["complete"]
+    r4 = cpu().decode_file_stream(f, conf, out, window=4097, durable=False)
+    assert r4["complete"] and r4["resumed_from"] > 0 and r4["erased"] == 4
+    assert (b / "out").read_bytes() == payload
+
+
+def test_cpu_rs_cli_w16_window(tmp_path):
+    exe = str(binary("CPU-RS"))
+    payload = os.urandom(300_001)
+    (tmp_path / "f.bin").write_bytes(payload)
+    r = subprocess.run([exe, "-k", "300", "-n", "340", "-w", "16", "-e", "f.bin", "--window", "512", "--no-sync", "-q"],
+                       cwd=tmp_path, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    md = ff.read_metadata(str(tmp_path / "f.bin.METADATA"))
+    assert md.w == 16 and md.k == 300
+    ff.write_conf(str(tmp_path / "conf"), ff.worst_case_conf("f.bin", 340, 300))
+    r = subprocess.run([exe, "-d", "-i", "f.bin", "-c", "conf", "-o", "o.bin", "--window", "0", "-q"],
+                       cwd=tmp_path, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert (tmp_path / "o.bin").read_bytes() == payload
