@@ -52,12 +52,14 @@ inline uint8_t* thp_pinned_alloc(size_t n, int touch_threads = 8) {
       for (size_t o = a; o < b; o += 4096) p[o] = 0;  // one store per 4 KiB page faults it in
     });
   for (auto& t : th) t.join();
-  if (hipHostRegister(p, len, hipHostRegisterDefault) != hipSuccess) {
+  // portable + mapped: every device of the process sees the rows (the multi-device zero-copy
+  // pipeline maps them per device, gemm_host_multi)
+  if (hipHostRegister(p, len, hipHostRegisterPortable | hipHostRegisterMapped) != hipSuccess) {
     // registration refused (e.g. a locked-memory limit): fall back to the runtime's own pinned
     // allocator rather than failing the codec
     munmap(p, len);
     void* q = nullptr;
-    if (hipHostMalloc(&q, n ? n : 1, hipHostMallocDefault) != hipSuccess) return nullptr;
+    if (hipHostMalloc(&q, n ? n : 1, hipHostMallocPortable | hipHostMallocMapped) != hipSuccess) return nullptr;
     std::lock_guard<std::mutex> g(host_alloc_detail::mu());
     host_alloc_detail::sizes()[static_cast<uint8_t*>(q)] = 0;  // 0: hipHostFree on release
     return static_cast<uint8_t*>(q);

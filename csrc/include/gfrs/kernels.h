@@ -21,8 +21,10 @@ hipError_t launch_gf_gemm(const void* desc, int k, int m_pad, int64_t col0, int6
 // GF(2^16) form (csrc/kernels/gf_gemm16.hip): desc built with desc_layout16 (build_desc field_w =
 // 16); rows hold little-endian 16-bit symbols, col0 and ncols are even byte counts. `symwise`
 // routes every column through the one-symbol-per-lane kernel (rows not 16-byte aligned).
+// one_tile: keep every output in one tile whatever the row length (the zero-copy pipeline, whose
+// inputs cross PCIe once per tile; short rows otherwise run one output per tile).
 hipError_t launch_gf_gemm16(const void* desc, int k, int m_pad, int64_t col0, int64_t ncols, bool symwise,
-                            int max_blocks, hipStream_t stream);
+                            int max_blocks, hipStream_t stream, bool one_tile = false);
 
 // Batched form: `batch` stripes of identical shape share the coefficient tables (small-object
 // serving: one launch for many objects). desc built with desc_layout(k, m_pad, batch).

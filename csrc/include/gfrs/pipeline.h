@@ -43,8 +43,18 @@ struct PipelineOptions {
   bool zero_copy = false;
 };
 
+// Why a device asked for the zero-copy kernel ran the staged pipeline instead (PipelineStats).
+enum ZcFallback : int {
+  kZcNone = 0,        // not asked for, or ran zero-copy
+  kZcUnmapped = 1,    // a host row is not pinned / not mapped into THIS device's address space
+  kZcUnaligned = 2,   // a host row is not 16-byte aligned (the kernel streams 16-byte groups)
+  kZcWideCode = 3,    // more outputs than one tile: every tile would re-read the host rows over PCIe
+};
+const char* zc_fallback_name(int reason);
+
 struct PipelineStats {
   bool zero_copy = false;  // ran the zero-copy kernel (else the staged -s pipeline)
+  int zc_fallback = kZcNone;  // zero-copy asked for but refused on this device: why (ZcFallback)
   double ms_setup = 0;    // stream/buffer/descriptor setup (alloc)
   double ms_stream = 0;   // H2D + kernel + D2H loop until the last stream drains
   double ms_teardown = 0;  // frees

@@ -197,7 +197,7 @@ hipError_t dispatch16(int m_pad, int mt_cap, F&& f) {
 }  // namespace
 
 hipError_t launch_gf_gemm16(const void* desc, int k, int m_pad, int64_t col0, int64_t ncols, bool symwise,
-                            int max_blocks, hipStream_t stream) {
+                            int max_blocks, hipStream_t stream, bool one_tile) {
   if (k <= 0 || m_pad <= 0 || ncols <= 0) return ncols < 0 ? hipErrorInvalidValue : hipSuccess;
   if ((col0 | ncols) & 1) return hipErrorInvalidValue;  // whole 16-bit symbols only
   if (m_pad % tile_for(m_pad) != 0) return hipErrorInvalidValue;
@@ -213,7 +213,7 @@ hipError_t launch_gf_gemm16(const void* desc, int k, int m_pad, int64_t col0, in
     const char* e = std::getenv("GFRS_GF16_SHORT_GROUPS");
     return e ? std::max<int64_t>(0, std::atoll(e)) : int64_t(32768);
   }();
-  const int mt_cap = ncols / 16 < short_groups ? 1 : 8;
+  const int mt_cap = (ncols / 16 < short_groups && !one_tile) ? 1 : 8;
   return dispatch16(m_pad, mt_cap, [&](auto mt) -> hipError_t {
     constexpr int MT = decltype(mt)::value;
     const int ntiles = m_pad / MT;

@@ -32,6 +32,7 @@ py::dict stats_dict(const gfrs::PipelineStats& s) {
   d["slices"] = s.slices;
   d["lanes"] = s.lanes;
   d["zero_copy"] = s.zero_copy;
+  d["zero_copy_refused"] = std::string(gfrs::zc_fallback_name(s.zc_fallback));
   return d;
 }
 
@@ -311,8 +312,9 @@ PYBIND11_MODULE(_hip, m) {
       "encode_file_stream",
       [gpu_gemm](const std::string& file, int k, int p, const std::string& matrix, bool cpu_meta,
                  const std::vector<int>& devices, int streams, int64_t slice, int max_blocks, int64_t window,
-                 bool resume, bool durable, int stop_after, int field_w, int64_t col_lo, int64_t col_hi, bool shard) {
-        const GemmFn g = gpu_gemm(devices, streams, slice, max_blocks);
+                 bool resume, bool durable, int stop_after, int field_w, int64_t col_lo, int64_t col_hi, bool shard,
+                 bool zero_copy) {
+        const GemmFn g = gpu_gemm(devices, streams, slice, max_blocks, nullptr, zero_copy);
         StreamReport r;
         {
           py::gil_scoped_release nogil;
@@ -326,14 +328,14 @@ PYBIND11_MODULE(_hip, m) {
       py::arg("devices") = std::vector<int>{0}, py::arg("streams") = 2, py::arg("slice") = 16 << 20,
       py::arg("max_blocks") = 0, py::arg("window") = 0, py::arg("resume") = true, py::arg("durable") = true,
       py::arg("stop_after") = -1, py::arg("field_w") = 8, py::arg("col_lo") = 0, py::arg("col_hi") = -1,
-      py::arg("shard") = false);
+      py::arg("shard") = false, py::arg("zero_copy") = false);
   m.def(
       "decode_file_stream",
       [gpu_gemm](const std::string& file, const std::string& conf, const std::string& out,
                  const std::vector<int>& devices, int streams, int64_t slice, int max_blocks, int64_t window,
                  bool resume, bool durable, int stop_after, int64_t col_lo, int64_t col_hi, bool shard,
-                 const std::vector<int>& rows) {
-        const GemmFn g = gpu_gemm(devices, streams, slice, max_blocks);
+                 const std::vector<int>& rows, bool zero_copy) {
+        const GemmFn g = gpu_gemm(devices, streams, slice, max_blocks, nullptr, zero_copy);
         StreamReport r;
         {
           py::gil_scoped_release nogil;
@@ -345,5 +347,6 @@ PYBIND11_MODULE(_hip, m) {
       py::arg("file"), py::arg("conf"), py::arg("out") = "", py::arg("devices") = std::vector<int>{0},
       py::arg("streams") = 2, py::arg("slice") = 16 << 20, py::arg("max_blocks") = 0, py::arg("window") = 0,
       py::arg("resume") = true, py::arg("durable") = true, py::arg("stop_after") = -1, py::arg("col_lo") = 0,
-      py::arg("col_hi") = -1, py::arg("shard") = false, py::arg("rows") = std::vector<int>{});
+      py::arg("col_hi") = -1, py::arg("shard") = false, py::arg("rows") = std::vector<int>{},
+      py::arg("zero_copy") = false);
 }

@@ -247,17 +247,26 @@ uint64_t mapped_addr(const void* p) {
   return reinterpret_cast<uint64_t>(at.devicePointer);
 }
 
-// Device addresses of every row, or empty when one is unmapped or not 16-byte aligned (the
-// zero-copy kernel streams 16-byte groups; a byte-wise pass over PCIe would be slower than staging).
+// Device addresses of every row on the CURRENT device (each gemm_host thread has set its own), or
+// empty when one is unmapped there or not 16-byte aligned (the zero-copy kernel streams 16-byte
+// groups; a byte-wise pass over PCIe would be slower than staging); `why` says which.
 template <class Ptr>
-std::vector<uint64_t> map_rows(const std::vector<Ptr>& rows) {
+std::vector<uint64_t> map_rows(const std::vector<Ptr>& rows, int& why) {
   std::vector<uint64_t> a(rows.size());
   for (size_t i = 0; i < rows.size(); ++i) {
     a[i] = mapped_addr(rows[i]);
-    if (!a[i] || a[i] % 16) return {};
+    if (!a[i] || a[i] % 16) {
+      why = !a[i] ? kZcUnmapped : kZcUnaligned;
+      return {};
+    }
   }
   return a;
 }
+
+// Zero-copy needs the whole output set in ONE tile: each tile's lanes read all k host rows, so a
+// second tile would pull every input byte over PCIe again (GF(2^8): 16 outputs per tile; GF(2^16):
+// 8, gf_gemm16.hip).
+bool zc_one_tile(int m, int field_w) { return pad_m(m) <= (field_w == 16 ? 8 : kMaxTile); }
 
 // The zero-copy launches go to the null stream: every hardware queue a process creates costs it
 // 8-25 ms on first use (the first stream even more), and the null stream is the one queue the
@@ -278,6 +287,16 @@ hipError_t zc_stream(Workspace& ws) {
 }
 
 }  // namespace
+
+const char* zc_fallback_name(int reason) {
+  switch (reason) {
+    case kZcNone: return "";
+    case kZcUnmapped: return "a host row is not mapped into this device";
+    case kZcUnaligned: return "a host row is not 16-byte aligned";
+    case kZcWideCode: return "more outputs than one kernel tile (host rows would cross PCIe once per tile)";
+  }
+  return "unknown";
+}
 
 hipError_t release_workspaces() {
   std::lock_guard<std::mutex> g(g_ws_mu);
@@ -306,8 +325,17 @@ hipError_t gemm_zero_copy(Workspace& ws, const std::vector<const uint8_t*>& in_r
                           const PipelineOptions& opt, PipelineStats& st) {
   const int k = int(in_rows.size()), m = int(out_rows.size());
   const auto t0 = Clock::now();
-  const std::vector<uint64_t> ip = map_rows(in_rows), op = map_rows(out_rows);
-  if (ip.empty() || op.empty()) return hipErrorInvalidValue;
+  if (!zc_one_tile(m, opt.field_w)) {
+    st.zc_fallback = kZcWideCode;
+    return hipErrorInvalidValue;
+  }
+  int why = kZcNone;
+  const std::vector<uint64_t> ip = map_rows(in_rows, why);
+  const std::vector<uint64_t> op = ip.empty() ? std::vector<uint64_t>{} : map_rows(out_rows, why);
+  if (ip.empty() || op.empty()) {
+    st.zc_fallback = why;
+    return hipErrorInvalidValue;
+  }
   std::vector<uint8_t> d = build_desc(k, m, ip, {}, op, coeff, opt.field_w);
   GFRS_TRY(zc_stream(ws));
   if (d != ws.zc_host) {
@@ -320,7 +348,8 @@ hipError_t gemm_zero_copy(Workspace& ws, const std::vector<const uint8_t*>& in_r
   {
     TraceRange tr("pipeline/zero-copy");
     const hipError_t e = opt.field_w == 16
-                             ? launch_gf_gemm16(ws.zc_desc, k, pad_m(m), c0, c1 - c0, false, opt.max_blocks, ws.zc_stream)
+                             ? launch_gf_gemm16(ws.zc_desc, k, pad_m(m), c0, c1 - c0, false, opt.max_blocks, ws.zc_stream,
+                                                /*one_tile=*/true)
                              : launch_gf_gemm(ws.zc_desc, k, pad_m(m), c0, c1 - c0, opt.bytewise, opt.max_blocks,
                                               ws.zc_stream, /*copies=*/false);
     const hipError_t e2 = hipStreamSynchronize(ws.zc_stream);
@@ -482,7 +511,9 @@ hipError_t gemm_host(int device, const std::vector<const uint8_t*>& in_rows, con
       return hipSuccess;
     }
     if (e != hipErrorInvalidValue) return e;
-    st = PipelineStats{};  // a row is not mapped / aligned: the staged pipeline below
+    const int why = st.zc_fallback;  // refused (reason recorded): the staged pipeline below
+    st = PipelineStats{};
+    st.zc_fallback = why;
   }
   {
     TraceRange tr("pipeline/setup");

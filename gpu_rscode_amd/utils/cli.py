@@ -53,6 +53,7 @@ def _parser() -> argparse.ArgumentParser:
     ap.add_argument("--no-resume", action="store_true", help="with --window: ignore a matching checkpoint")
     ap.add_argument("--no-sync", action="store_true", help="with --window: no fdatasync before checkpoints")
     ap.add_argument("-q", action="store_true", dest="quiet")
+    ap.add_argument("--json", action="store_true", help="--dist: rank 0 prints a JSON line of the job's codec time")
     return ap
 
 
@@ -79,7 +80,7 @@ def main(argv=None) -> int:
             print("-w 16 writes the versioned METADATA (no --cpu-meta form)", file=sys.stderr)
             return 2
         fw = {} if a.field_w == 8 else dict(field_w=a.field_w)
-        if a.zero_copy and backend == "gpu" and a.window is None:
+        if a.zero_copy and backend == "gpu":
             fw["zero_copy"] = True
         t = time.perf_counter()
         st = {} if a.window is None else dict(window=a.window, resume=not a.no_resume, durable=not a.no_sync)
@@ -87,8 +88,6 @@ def main(argv=None) -> int:
             ndev = hip().device_count()
             devs = list(range(a.gpus or ndev))
             fn = hip().encode_file_stream if st else hip().encode_file
-            if st:
-                fw.pop("zero_copy", None)
             r = fn(a.encode_file, a.k, a.n - a.k, a.matrix, a.cpu_meta, devs, a.streams, a.slice, a.grid, **st, **fw)
         else:
             fn = cpu().encode_file_stream if st else cpu().encode_file
@@ -107,7 +106,7 @@ def main(argv=None) -> int:
     if backend == "gpu":
         ndev = hip().device_count()
         fn = hip().decode_file_stream if st else hip().decode_file
-        zc = {"zero_copy": True} if (a.zero_copy and not st) else {}
+        zc = {"zero_copy": True} if a.zero_copy else {}
         r = fn(a.in_file, a.conf, a.out, list(range(a.gpus or ndev)), a.streams, a.slice, a.grid, **st, **zc)
     else:
         fn = cpu().decode_file_stream if st else cpu().decode_file
@@ -198,9 +197,10 @@ def _dist_run(a, ctx) -> int:
             raise RuntimeError("injected fault (GFRS_DIST_FAULT_RANK)")
         lo, hi = shard_range(C, world, rank)
         kw = dict(st, field_w=a.field_w, col_lo=lo, col_hi=hi, shard=True)
+        t_codec = time.perf_counter()
         if on_gpu:
             r = hip().encode_file_stream(path, k, p, a.matrix, a.cpu_meta, [ctx.local_rank], a.streams, a.slice,
-                                         a.grid, **kw)
+                                         a.grid, zero_copy=a.zero_copy, **kw)
         else:
             r = cpu().encode_file_stream(path, k, p, a.matrix, a.cpu_meta, a.mul, a.threads, **kw)
         # every rank's shard CRCs (and width) to rank 0, combined in column order
@@ -220,6 +220,7 @@ def _dist_run(a, ctx) -> int:
         _say(a, f"[rank {rank}] encoded columns [{lo}, {hi}) of {C} in {r['windows']} window(s) of {r['window']} B "
                 f"in {1e3 * (time.perf_counter() - t0):.1f}ms (read {r['ms_read']:.1f}, GEMM {r['ms_compute']:.1f}, "
                 f"write {r['ms_write']:.1f} ms, overlapped)")
+        _dist_summary(a, ctx, "encode", total, t0, t_codec)
         return 0
     if not a.in_file or not a.conf:
         raise ValueError("decode needs -d -i FILE -c CONF")
@@ -249,14 +250,38 @@ def _dist_run(a, ctx) -> int:
         raise RuntimeError("injected fault (GFRS_DIST_FAULT_RANK)")
     lo, hi = shard_range(C, world, rank)
     kw = dict(st, col_lo=lo, col_hi=hi, shard=True, rows=rows)
+    t_codec = time.perf_counter()
     if on_gpu:
-        r = hip().decode_file_stream(a.in_file, a.conf, dst, [ctx.local_rank], a.streams, a.slice, a.grid, **kw)
+        r = hip().decode_file_stream(a.in_file, a.conf, dst, [ctx.local_rank], a.streams, a.slice, a.grid,
+                                     zero_copy=a.zero_copy, **kw)
     else:
         r = cpu().decode_file_stream(a.in_file, a.conf, dst, a.mul, a.threads, **kw)
     barrier()
     _say(a, f"[rank {rank}] decoded columns [{lo}, {hi}) of {C} ({r['erased']} erased native(s)) in "
             f"{r['windows']} window(s) of {r['window']} B in {1e3 * (time.perf_counter() - t0):.1f}ms")
+    _dist_summary(a, ctx, "decode", md.total_size, t0, t_codec)
     return 0
+
+
+def _dist_summary(a, ctx, op: str, size: int, t0: float, t_codec: float) -> None:
+    """``--json``: rank 0 prints one line with the job's codec time (max over ranks, from the shard
+    codec call to the final barrier) and its time since the process group existed."""
+    if not a.json:
+        return
+    import json
+
+    import torch
+    import torch.distributed as dist
+
+    now = time.perf_counter()
+    t = torch.tensor([now - t_codec, now - t0], dtype=torch.float64, device=ctx.device)
+    if ctx.world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    if ctx.is_root:
+        codec_s, total_s = (float(x) for x in t.tolist())
+        print(json.dumps({"op": op, "ranks": ctx.world, "bytes": size, "codec_ms": round(codec_s * 1e3, 3),
+                          "codec_GBps": round(size / codec_s / 1e9, 3), "since_pg_ms": round(total_s * 1e3, 3)}),
+              flush=True)
 
 
 def spans_of(world: int, C: int, rank: int) -> tuple[int, int]:

@@ -573,3 +573,38 @@ def test_rs_cli_zero_copy_roundtrip(tmp_path):
                        capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     assert (tmp_path / "o.bin").read_bytes() == payload
+
+
+def test_zero_copy_path_is_reported_per_device():
+    """gemm_host over devices [0, 0] (two shards, one thread each): with every row pinned both shards
+    run the zero-copy kernel; with one pageable (unregistered) input row each device reports the
+    staged pipeline and why; a wide code (more outputs than one tile) is refused the same way. The
+    bytes stay bit-exact on every path."""
+    k, p, C = 8, 3, 2 * 4096 * 33 + 4096
+    rng = np.random.default_rng(11)
+    host = _pitched_pinned(k, C)
+    host.copy_(torch.from_numpy(rng.integers(0, 256, size=(k, C), dtype=np.uint8)))
+    e = GF256.vandermonde_ref(k, p)
+    h = hip()
+
+    def run(rows, m, coeff):
+        par = _pitched_pinned(m, C)
+        res = h.gemm_host([0, 0], [r.data_ptr() for r in rows], [par[i].data_ptr() for i in range(m)],
+                          coeff.tobytes(), C, 2, 1 << 20, 0, False, zero_copy=True)
+        return res["devices"], par.numpy().copy()
+
+    devs, par = run([host[j] for j in range(k)], p, e)
+    assert [d["zero_copy"] for d in devs] == [True, True] and all(d["zero_copy_refused"] == "" for d in devs)
+    assert np.array_equal(par, GF256.gemm(e, host.numpy()))
+    pageable = torch.empty(C + 64, dtype=torch.uint8)  # not registered with HIP: not device-mapped
+    off = (-pageable.data_ptr()) % 16
+    row3 = pageable[off:off + C]
+    row3.copy_(host[3])
+    devs, par = run([host[j] if j != 3 else row3 for j in range(k)], p, e)
+    assert [d["zero_copy"] for d in devs] == [False, False]
+    assert all("not mapped" in d["zero_copy_refused"] for d in devs)
+    assert np.array_equal(par, GF256.gemm(e, host.numpy()))
+    wide = rng.integers(0, 256, size=(20, k)).astype(np.uint8)  # m_pad 32 > one 16-row tile
+    devs, par = run([host[j] for j in range(k)], 20, wide)
+    assert [d["zero_copy"] for d in devs] == [False, False] and all("tile" in d["zero_copy_refused"] for d in devs)
+    assert np.array_equal(par, GF256.gemm(wide, host.numpy()))
