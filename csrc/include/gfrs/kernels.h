@@ -102,6 +102,16 @@ size_t mfma_bitmat_bytes(int k, int m);
 hipError_t launch_gf_gemm_fp4(const void* bitmat, const void* desc, int k, int m, int64_t col0,
                               int64_t ncols, int mg_cap, int64_t in_stride, bool copies, hipStream_t stream);
 size_t fp4_bitmat_bytes(int k, int m, int mg_cap);
+// Batched form (small-object serving): `batch` stripes of identical shape whose rows sit at fixed
+// strides — stripe b's input rows are stripe 0's + b * in_bstride, its output and copy rows stripe
+// 0's + b * out_bstride (desc built with desc_layout(k, m_pad, batch); the kernel reads stripe 0's
+// tables). ncols per stripe; whole chunks of every stripe run in ONE persistent matrix-core launch
+// (A loaded once per wave for the whole batch), the ragged remainders on the batched v_perm kernel.
+// hipErrorNotSupported when the shape has no batched matrix-core form (currently the A-resident
+// kernel: k in (112, 128], one M-tile group), so the caller keeps the v_perm path.
+hipError_t launch_gf_gemm_fp4_batched(const void* bitmat, const void* desc, int k, int m, int batch, int64_t col0,
+                                      int64_t ncols, int mg_cap, int64_t in_stride, int64_t in_bstride,
+                                      int64_t out_bstride, bool copies, hipStream_t stream);
 hipError_t launch_fp4_bitmat(const uint8_t* coeff, int m, int k, void* bitmat, int mg_cap, hipStream_t stream);
 // row o of the coefficient matrix = coeff + sel[o] * ld (device pointers; e.g. erased rows of a
 // device-computed inverse, so a decode needs no host round trip)
@@ -127,6 +137,10 @@ struct Fp4ArLaunch {
   const void* bitmat;
   int k, m, mg;
   int64_t col0, ncols, in_stride;
+  // batched launch: `batch` stripes whose rows are stripe 0's (the tables above) plus b * in_bstride
+  // (inputs) / b * out_bstride (outputs and copies); ncols is per stripe, *done per stripe
+  int batch = 1;
+  int64_t in_bstride = 0, out_bstride = 0;
 };
 bool fp4ar_supported(int k, int mg);
 hipError_t launch_gf_gemm_fp4ar(const Fp4ArLaunch& a, int64_t* done, hipStream_t stream);

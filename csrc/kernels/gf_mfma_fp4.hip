@@ -1351,4 +1351,36 @@ hipError_t launch_gf_gemm_fp4(const void* bitmat, const void* desc, int k, int m
   return hipSuccess;
 }
 
+hipError_t launch_gf_gemm_fp4_batched(const void* bitmat, const void* desc, int k, int m, int batch, int64_t col0,
+                                      int64_t ncols, int mg_cap, int64_t in_stride, int64_t in_bstride,
+                                      int64_t out_bstride, bool copies, hipStream_t stream) {
+  if (k <= 0 || m <= 0 || ncols < 0 || (col0 & 1) || mg_cap < 1 || batch < 1 || batch > 65535)
+    return hipErrorInvalidValue;
+  const int m_pad = pad_m(m);
+  const Fp4Geometry geo = geometry(k, m, mg_cap, copies);
+  if (geo.groups != 1 || !fp4ar_supported(k, geo.mg)) return hipErrorNotSupported;
+  const DescLayout l = desc_layout(k, m_pad, batch);
+  const char* b = static_cast<const char*>(desc);
+  Fp4ArLaunch a{};
+  a.in = reinterpret_cast<const uint64_t*>(b + l.in_off);  // stripe 0's tables (the first k / m_pad entries)
+  a.out = reinterpret_cast<const uint64_t*>(b + l.out_off);
+  a.copy = copies ? reinterpret_cast<const uint64_t*>(b + l.copy_off) : nullptr;
+  a.bitmat = bitmat;
+  a.k = k;
+  a.m = m;
+  a.mg = geo.mg;
+  a.col0 = col0;
+  a.ncols = ncols;
+  a.in_stride = copies ? 0 : in_stride;
+  a.batch = batch;
+  a.in_bstride = in_bstride;
+  a.out_bstride = out_bstride;
+  int64_t done = 0;
+  const hipError_t e = launch_gf_gemm_fp4ar(a, &done, stream);
+  if (e != hipSuccess) return e;
+  // every stripe's ragged remainder (under one chunk) on the batched v_perm kernel
+  if (done < ncols) return launch_gf_gemm_batched(desc, k, m_pad, batch, col0 + done, ncols - done, false, stream, copies);
+  return hipSuccess;
+}
+
 }  // namespace gfrs

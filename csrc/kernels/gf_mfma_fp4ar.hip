@@ -29,6 +29,7 @@
 // constant; a phantom chunk drains the last real one.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 #include <type_traits>
@@ -99,12 +100,17 @@ __host__ __device__ constexpr int ar_wait_count(int sp, int mgw, int r, bool cop
 // wave storing everything while its partner parked its stores on the shared sink lines (every CU
 // serialised on them, 1100 vs 880 us at m = 24), or both storing everything (non-temporal: both
 // reach HBM, 1320 us)); R: ring slots per wave (divides the 8-slot chunk).
-template <int MGW, int WPG, bool UNI, bool COPY, int R>
+// BATCH: nchunks counts the chunks of `batch` stripes laid out at fixed strides (cps chunks each):
+// global chunk g is chunk g % cps of stripe g / cps, whose rows are stripe 0's (the pointer tables)
+// plus (g / cps) * in_bstride (inputs) / out_bstride (outputs and copies) — one persistent grid,
+// one A load per wave, for a whole batch of small objects (serving).
+template <int MGW, int WPG, bool UNI, bool COPY, int R, bool BATCH = false>
 __global__ __launch_bounds__(256, 1) void gf_gemm_fp4ar_kernel(cptr<uint64_t> in, cptr<uint64_t> out,
                                                                cptr<uint64_t> copy, const i32x4* __restrict__ bitmat,
                                                                int k, int m, int mg, int64_t col0, int64_t nchunks,
                                                                int64_t chunk_slots, int64_t in_stride,
-                                                               int sink_spread) {
+                                                               int sink_spread, int64_t cps, int64_t in_bstride,
+                                                               int64_t out_bstride) {
   constexpr int CG = 4 / WPG;               // column groups per block
   constexpr int kBC = CG * kCW;             // block columns per chunk
   constexpr int WN = MGW == 3 ? 4 : MGW;    // B window (a power of two dividing kNS, >= MGW)
@@ -171,12 +177,33 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4ar_kernel(cptr<uint64_t> in
   for (int v = 0; v < 16; ++v) bias[v] = float(1u << (23 - (v & 7)));
 
   uint64_t pn = UNI ? 0 : rowptr[dma_row(R % kKS)];
+  // Byte offsets of this block's chunk ci from column col0 of stripe 0's rows, inputs and outputs
+  // (plain: the global chunk's columns; BATCH: its stripe's offset plus its columns there). Rolled
+  // once per chunk (prev / cur / next), so a batched launch divides once per chunk.
+  struct Off {
+    int64_t in, out;
+  };
+  auto chunk_off = [&](int ci) __attribute__((always_inline)) {
+    const int64_t gc = slot0 + int64_t(ci) * chunk_slots;
+    if constexpr (BATCH) {
+      const int64_t b = int64_t(uint32_t(gc) / uint32_t(cps));  // (gc, cps < 2^31: host-checked)
+      const int64_t lc = (gc - b * cps) * kBC;
+      return Off{b * in_bstride + lc, b * out_bstride + lc};
+    } else {
+      return Off{gc * kBC, gc * kBC};
+    }
+  };
+  const Off off_first = chunk_off(0);
+  Off off_prev = off_first, off_cur = off_first, off_nxt = chunk_off(1);
+  // DMA of slot T of chunk ci + T / kKS (T / kKS: 0 = cur, 1 = next; past my_chunks: chunk 0 into
+  // the spare slot)
   auto dma_issue = [&](int ci, auto t_tag, uint64_t rowp) __attribute__((always_inline)) {
     constexpr int T = decltype(t_tag)::value;
     constexpr int p = T % kKS, ring_slot = T % R;
+    static_assert(T / kKS <= 1, "a DMA runs at most one chunk ahead");
     const int chunk = ci + T / kKS;
     const bool live = chunk < my_chunks;
-    const int64_t col = col0 + (slot0 + int64_t(live ? chunk : 0) * chunk_slots) * kBC + dcol;
+    const int64_t col = col0 + (live ? (T / kKS ? off_nxt.in : off_cur.in) : off_first.in) + dcol;
     uint64_t sa;
     if constexpr (UNI)
       sa = in0 + uint64_t(int64_t(dma_row(p)) * in_stride + col);
@@ -266,9 +293,9 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4ar_kernel(cptr<uint64_t> in
 
   auto chunk_body = [&](int ci) __attribute__((always_inline)) {
     const bool live = ci < my_chunks;
-    const int64_t cbase = col0 + (slot0 + int64_t(ci) * chunk_slots) * kBC;
+    const int64_t cbase = col0 + off_cur.out;  // this chunk's output columns (copies)
     const bool plive = ci > 0;  // packs of "chunk -1" go to the sink
-    const int64_t pcolw = cbase - chunk_slots * kBC + cg * kCW + 2 * c;
+    const int64_t pcolw = col0 + off_prev.out + cg * kCW + 2 * c;
     using cvec = std::conditional_t<WPG == 1, u32x4, unsigned __attribute__((ext_vector_type(2)))>;
     [[maybe_unused]] cvec cdat;
     [[maybe_unused]] uint64_t cp = 0;
@@ -412,16 +439,21 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4ar_kernel(cptr<uint64_t> in
     });
   };
 
-  for (int ci = 0; ci <= my_chunks; ++ci) chunk_body(ci);
+  for (int ci = 0; ci <= my_chunks; ++ci) {
+    chunk_body(ci);
+    off_prev = off_cur;
+    off_cur = off_nxt;
+    off_nxt = chunk_off(ci + 2);
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA (dummy or not) outlives the wave
 }
 
 constexpr size_t ar_lds(int r) { return size_t(kPtrBytes) + (4 * size_t(r) + 1) * kSlotBytes; }
 
-template <int MGW, int WPG, bool UNI, bool COPY, int R>
+template <int MGW, int WPG, bool UNI, bool COPY, int R, bool BATCH>
 hipError_t launch_ar(const Fp4ArLaunch& a, int64_t* done, hipStream_t stream) {
   constexpr int kBC = (4 / WPG) * kCW;
-  const void* f = reinterpret_cast<const void*>(&gf_gemm_fp4ar_kernel<MGW, WPG, UNI, COPY, R>);
+  const void* f = reinterpret_cast<const void*>(&gf_gemm_fp4ar_kernel<MGW, WPG, UNI, COPY, R, BATCH>);
   const size_t lds = ar_lds(R);
   hipError_t e = ensure_lds_optin(f, int(lds));
   if (e != hipSuccess) return e;
@@ -432,26 +464,33 @@ hipError_t launch_ar(const Fp4ArLaunch& a, int64_t* done, hipStream_t stream) {
     return o;
   });
   if (occ <= 0) return hipErrorInvalidConfiguration;
-  const int64_t nchunks = a.ncols / kBC;
-  *done = nchunks * kBC;
+  const int64_t cps = a.ncols / kBC;  // chunks per stripe
+  const int64_t nchunks = cps * std::max(1, a.batch);
+  *done = cps * kBC;
   if (nchunks == 0) return hipSuccess;
+  if (BATCH && nchunks >= (int64_t(1) << 31)) return hipErrorInvalidValue;
   static const int sink_spread = [] {  // GFRS_FP4_SINK=1: one shared sink slot (A/B only)
     const char* e = std::getenv("GFRS_FP4_SINK");
     return (e && std::atoi(e) == 1) ? 0 : 1;
   }();
   const int64_t slots = persistent_slots(occ, 1, nchunks);
-  gf_gemm_fp4ar_kernel<MGW, WPG, UNI, COPY, R><<<unsigned(slots), 256, lds, stream>>>(
+  gf_gemm_fp4ar_kernel<MGW, WPG, UNI, COPY, R, BATCH><<<unsigned(slots), 256, lds, stream>>>(
       (cptr<uint64_t>)a.in, (cptr<uint64_t>)a.out, (cptr<uint64_t>)a.copy, static_cast<const i32x4*>(a.bitmat), a.k,
-      a.m, a.mg, a.col0, nchunks, slots, a.in_stride, sink_spread);
+      a.m, a.mg, a.col0, nchunks, slots, a.in_stride, sink_spread, cps, a.in_bstride, a.out_bstride);
   return hipGetLastError();
 }
 
-template <int MGW, int WPG>
+template <int MGW, int WPG, bool BATCH>
 hipError_t launch_ar_var(const Fp4ArLaunch& a, int64_t* done, hipStream_t stream) {
   constexpr int R = 8;
-  if (a.copy) return launch_ar<MGW, WPG, false, true, R>(a, done, stream);
-  return a.in_stride ? launch_ar<MGW, WPG, true, false, R>(a, done, stream)
-                     : launch_ar<MGW, WPG, false, false, R>(a, done, stream);
+  if (a.copy) return launch_ar<MGW, WPG, false, true, R, BATCH>(a, done, stream);
+  return a.in_stride ? launch_ar<MGW, WPG, true, false, R, BATCH>(a, done, stream)
+                     : launch_ar<MGW, WPG, false, false, R, BATCH>(a, done, stream);
+}
+
+template <int MGW, int WPG>
+hipError_t launch_ar_b(const Fp4ArLaunch& a, int64_t* done, hipStream_t stream) {
+  return a.batch > 1 ? launch_ar_var<MGW, WPG, true>(a, done, stream) : launch_ar_var<MGW, WPG, false>(a, done, stream);
 }
 
 }  // namespace
@@ -464,13 +503,13 @@ hipError_t launch_gf_gemm_fp4ar(const Fp4ArLaunch& a, int64_t* done, hipStream_t
   // rows split in two halves of at most 4 tiles when more than 4 tiles (padding tiles read zero A
   // and store to the sink), else one wave covers every tile and the block 4 column groups
   switch (a.mg) {
-    case 1: return launch_ar_var<1, 1>(a, done, stream);
-    case 2: return launch_ar_var<2, 1>(a, done, stream);
-    case 3: return launch_ar_var<3, 1>(a, done, stream);
-    case 4: return launch_ar_var<4, 1>(a, done, stream);
+    case 1: return launch_ar_b<1, 1>(a, done, stream);
+    case 2: return launch_ar_b<2, 1>(a, done, stream);
+    case 3: return launch_ar_b<3, 1>(a, done, stream);
+    case 4: return launch_ar_b<4, 1>(a, done, stream);
     case 5:
-    case 6: return launch_ar_var<3, 2>(a, done, stream);
-    default: return launch_ar_var<4, 2>(a, done, stream);
+    case 6: return launch_ar_b<3, 2>(a, done, stream);
+    default: return launch_ar_b<4, 2>(a, done, stream);
   }
 }
 

@@ -178,6 +178,21 @@ PYBIND11_MODULE(_hip, m) {
                              ncols, mg_cap, in_stride, copies, as_stream(stream)),
           "gf_gemm_fp4");
   });
+  m.def("gemm_fp4_batched", [](uint64_t bitmat, uint64_t desc, int k, int mm, int batch, int64_t col0, int64_t ncols,
+                               int mg_cap, int64_t in_stride, int64_t in_bstride, int64_t out_bstride, bool copies,
+                               uint64_t stream) {
+    check(launch_gf_gemm_fp4_batched(reinterpret_cast<const void*>(bitmat), reinterpret_cast<const void*>(desc), k, mm,
+                                     batch, col0, ncols, mg_cap, in_stride, in_bstride, out_bstride, copies,
+                                     as_stream(stream)),
+          "gf_gemm_fp4_batched");
+  });
+  m.def("fp4_batched_supported", [](int k, int mm, int mg_cap) {
+    // (the A-resident kernel: k in (112, 128] and every M-tile in one group)
+    const int mtiles = (mm + 3) / 4;
+    int mg = 1;
+    while (mg < mtiles && mg < mg_cap) mg <<= 1;
+    return k > 112 && k <= 128 && mtiles <= mg && fp4ar_supported(k, mg);
+  });
   m.def("gen_matrix", [](uint64_t e, int k, int p, int kind, uint64_t stream) {
     check(launch_gen_matrix(reinterpret_cast<uint8_t*>(e), k, p, kind, as_stream(stream)), "gen_matrix");
   });

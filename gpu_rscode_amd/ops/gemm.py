@@ -168,8 +168,8 @@ class GemmPlan:
             # batched: B stripes of identical shape, one launch (grid.y = stripe)
             if len(bi) != len(bo) or len(bi) < 1 or len(bi) > 65535:
                 raise ValueError("batched plan needs 1..65535 stripes in inputs and outputs")
-            if engine not in ("valu", "auto"):
-                raise ValueError("batched plans run on the v_perm kernel (engine='valu')")
+            if engine not in ("valu", "auto", "mfma"):
+                raise ValueError("batched plans run on the v_perm kernel or, for wide codes, the FP4 matrix cores")
             self.batch = len(bi)
             self._stripes_in, self._stripes_out = bi, bo
             inputs, outputs = bi[0], bo[0]
@@ -221,17 +221,29 @@ class GemmPlan:
                           tables, self.batch)
         self.desc = torch.from_numpy(host).to(self.device)
         self.layout = desc_layout(self.k, self.m_pad, self.batch)
+        # batched matrix-core launches address stripe b's rows as stripe 0's plus b fixed strides
+        self.in_bstride = self.out_bstride = None
+        if self.batch > 1:
+            strides = _batch_strides(self._stripes_in, self._stripes_out,
+                                     self._stripes_copy if self.copies is not None else None)
+            if strides is not None:
+                self.in_bstride, self.out_bstride = strides
         if engine == "auto":
-            engine = _auto_engine(self.k, self.m, maps is None, self.bytewise, self.batch, self.ncols)
+            engine = _auto_engine(self.k, self.m, maps is None, self.bytewise, self.batch, self.ncols,
+                                  batch_fp4=self.batch > 1 and self.in_bstride is not None
+                                  and hip().fp4_batched_supported(self.k, self.m, mfma_mg))
         self.engine = engine
         self.bitmat = None
+        if engine == "mfma" and self.batch > 1 and (
+                self.in_bstride is None or not hip().fp4_batched_supported(self.k, self.m, mfma_mg)):
+            raise ValueError("batched engine='mfma' needs k in (112, 128], m <= 32 and stripes at fixed strides")
         if engine in ("mfma", "mfma_i8"):
             # matrix-core GF(2) bit-matrix paths: "mfma" = FP4 block-scaled MFMA
             # (csrc/kernels/gf_mfma_fp4.hip), "mfma_i8" = int8 MFMA (csrc/kernels/gf_mfma.hip).
             # GF(2^8) coefficients (host coeff=, or device_tables=True and set_device_coeff /
             # invert_into_plan later), aligned rows; fused copies on "mfma" only. The column
             # remainder of a chunk runs on the v_perm tables that the descriptor also carries.
-            if maps is not None or self.bytewise or self.batch > 1:
+            if maps is not None or self.bytewise or (self.batch > 1 and engine != "mfma"):
                 raise ValueError(f"engine={engine!r} needs GF(2^8) coefficients, aligned rows, one stripe")
             if engine == "mfma_i8" and (coeff is None or self.copies is not None):
                 raise ValueError("engine='mfma_i8' needs coeff= and no copies")
@@ -343,7 +355,10 @@ class GemmPlan:
             self.desc.record_stream(stream)
             s = stream.cuda_stream
         h = hip()
-        if self.batch > 1:
+        if self.batch > 1 and self.engine == "mfma" and vec is None and col0 % 2 == 0:
+            h.gemm_fp4_batched(int(self.bitmat.data_ptr()), int(self.desc.data_ptr()), self.k, self.m, self.batch, col0,
+                               ncols, self.mfma_mg, self.in_stride, self.in_bstride, self.out_bstride, self.has_copies, s)
+        elif self.batch > 1:
             if vec is not None:
                 raise ValueError("kernel variants are not selectable on batched plans")
             h.gemm_batched(int(self.desc.data_ptr()), self.k, self.m_pad, self.batch, col0, ncols, self.bytewise, s,
@@ -376,15 +391,48 @@ _MFMA_MIN_K, _MFMA_MIN_M = 64, 16
 _SHORT_ROW, _MID_ROW = 512 << 10, 4 << 20
 
 
-def _auto_engine(k: int, m: int, gf256: bool, bytewise: bool, batch: int, ncols: int | None = None) -> str:
-    if not gf256 or bytewise or batch != 1:
+# Batched wide codes (serving) take the batched FP4 launch from this many columns per stripe (two
+# 128-column chunks of the A-resident kernel): below it the whole batch is a handful of chunks and
+# the k-split v_perm kernel's shorter prologue wins. (scripts/serve_bench.py --code 128:160;
+# GFRS_FP4_BATCH_MIN_COLS overrides, e.g. a huge value keeps every batch on the v_perm kernels.)
+_FP4_BATCH_MIN_COLS = int(__import__("os").environ.get("GFRS_FP4_BATCH_MIN_COLS", 256))
+
+
+def _auto_engine(k: int, m: int, gf256: bool, bytewise: bool, batch: int, ncols: int | None = None,
+                 batch_fp4: bool = False) -> str:
+    if not gf256 or bytewise:
         return "valu"
+    if batch != 1:
+        return "mfma" if (batch_fp4 and ncols is not None and ncols >= _FP4_BATCH_MIN_COLS) else "valu"
     if k >= _MFMA_MIN_K and m >= _MFMA_MIN_M:
         return "mfma"
     if ncols is not None and ((ncols <= _SHORT_ROW and k >= 16 and m >= 4) or
                               (ncols <= _MID_ROW and k >= 32 and m >= 8)):
         return "mfma"
     return "valu"
+
+
+def _batch_strides(stripes_in, stripes_out, stripes_copy=None) -> tuple[int, int] | None:
+    """(input, output) byte strides between consecutive stripes when every stripe's rows are stripe
+    0's shifted by b strides (copy rows at the output stride, the same rows absent in every stripe);
+    None otherwise."""
+    def stride(stripes):
+        base = [int(r.data_ptr()) for r in stripes[0]]
+        d = int(stripes[1][0].data_ptr()) - base[0]
+        for b, st in enumerate(stripes):
+            if any(int(r.data_ptr()) != base[j] + b * d for j, r in enumerate(st)):
+                return None
+        return d
+    d_in, d_out = stride(stripes_in), stride(stripes_out)
+    if d_in is None or d_out is None:
+        return None
+    if stripes_copy is not None:
+        base = [int(c.data_ptr()) if c is not None else 0 for c in stripes_copy[0]]
+        for b, st in enumerate(stripes_copy):
+            for j, c in enumerate(st):
+                if (c is None) != (base[j] == 0) or (c is not None and int(c.data_ptr()) != base[j] + b * d_out):
+                    return None
+    return d_in, d_out
 
 
 def _pack16(coeff) -> bytes:

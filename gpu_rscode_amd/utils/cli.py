@@ -197,7 +197,6 @@ def _dist_run(a, ctx) -> int:
             raise RuntimeError("injected fault (GFRS_DIST_FAULT_RANK)")
         lo, hi = shard_range(C, world, rank)
         kw = dict(st, field_w=a.field_w, col_lo=lo, col_hi=hi, shard=True)
-        t_codec = time.perf_counter()
         if on_gpu:
             r = hip().encode_file_stream(path, k, p, a.matrix, a.cpu_meta, [ctx.local_rank], a.streams, a.slice,
                                          a.grid, zero_copy=a.zero_copy, **kw)
@@ -220,7 +219,7 @@ def _dist_run(a, ctx) -> int:
         _say(a, f"[rank {rank}] encoded columns [{lo}, {hi}) of {C} in {r['windows']} window(s) of {r['window']} B "
                 f"in {1e3 * (time.perf_counter() - t0):.1f}ms (read {r['ms_read']:.1f}, GEMM {r['ms_compute']:.1f}, "
                 f"write {r['ms_write']:.1f} ms, overlapped)")
-        _dist_summary(a, ctx, "encode", total, t0, t_codec)
+        _dist_summary(a, ctx, "encode", total, t0)
         return 0
     if not a.in_file or not a.conf:
         raise ValueError("decode needs -d -i FILE -c CONF")
@@ -250,7 +249,6 @@ def _dist_run(a, ctx) -> int:
         raise RuntimeError("injected fault (GFRS_DIST_FAULT_RANK)")
     lo, hi = shard_range(C, world, rank)
     kw = dict(st, col_lo=lo, col_hi=hi, shard=True, rows=rows)
-    t_codec = time.perf_counter()
     if on_gpu:
         r = hip().decode_file_stream(a.in_file, a.conf, dst, [ctx.local_rank], a.streams, a.slice, a.grid,
                                      zero_copy=a.zero_copy, **kw)
@@ -259,13 +257,15 @@ def _dist_run(a, ctx) -> int:
     barrier()
     _say(a, f"[rank {rank}] decoded columns [{lo}, {hi}) of {C} ({r['erased']} erased native(s)) in "
             f"{r['windows']} window(s) of {r['window']} B in {1e3 * (time.perf_counter() - t0):.1f}ms")
-    _dist_summary(a, ctx, "decode", md.total_size, t0, t_codec)
+    _dist_summary(a, ctx, "decode", md.total_size, t0)
     return 0
 
 
-def _dist_summary(a, ctx, op: str, size: int, t0: float, t_codec: float) -> None:
-    """``--json``: rank 0 prints one line with the job's codec time (max over ranks, from the shard
-    codec call to the final barrier) and its time since the process group existed."""
+def _dist_summary(a, ctx, op: str, size: int, t0: float) -> None:
+    """``--json``: rank 0 prints one line with the job's codec time: max over ranks from the moment
+    the process group exists (outputs created, survivors chosen and CRC-verified, every shard
+    streamed, CRCs combined, METADATA written) to the final barrier — the part bin/RS reports as its
+    file codec time."""
     if not a.json:
         return
     import json
@@ -273,15 +273,13 @@ def _dist_summary(a, ctx, op: str, size: int, t0: float, t_codec: float) -> None
     import torch
     import torch.distributed as dist
 
-    now = time.perf_counter()
-    t = torch.tensor([now - t_codec, now - t0], dtype=torch.float64, device=ctx.device)
+    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=ctx.device)
     if ctx.world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     if ctx.is_root:
-        codec_s, total_s = (float(x) for x in t.tolist())
+        codec_s = float(t.item())
         print(json.dumps({"op": op, "ranks": ctx.world, "bytes": size, "codec_ms": round(codec_s * 1e3, 3),
-                          "codec_GBps": round(size / codec_s / 1e9, 3), "since_pg_ms": round(total_s * 1e3, 3)}),
-              flush=True)
+                          "codec_GBps": round(size / codec_s / 1e9, 3)}), flush=True)
 
 
 def spans_of(world: int, C: int, rank: int) -> tuple[int, int]:

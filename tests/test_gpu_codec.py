@@ -608,3 +608,46 @@ def test_zero_copy_path_is_reported_per_device():
     devs, par = run([host[j] for j in range(k)], 20, wide)
     assert [d["zero_copy"] for d in devs] == [False, False] and all("tile" in d["zero_copy_refused"] for d in devs)
     assert np.array_equal(par, GF256.gemm(wide, host.numpy()))
+
+
+@pytest.mark.parametrize("C,B", [(8_192, 5), (3 * 256 + 77, 3), (1_000, 2)])
+def test_batched_wide_code_on_matrix_cores(C, B):
+    """RS(128,160) objects in one [B, k, C] allocation take the batched FP4 launch (one persistent
+    grid over every stripe's chunks, the A-resident kernel), ragged remainders on the batched v_perm
+    kernel: encode_batch and decode_batch (26 natives + 6 parity lost, survivors copied in the same
+    pass) bit-exact against the oracle on every stripe; scattered stripes stay on the v_perm path."""
+    from gpu_rscode_amd.ops import GemmPlan
+
+    k, n = 128, 160
+    rs = ReedSolomon(k, n, matrix="cauchy")
+    host = np.random.default_rng(C + B).integers(0, 256, size=(B, k, C), dtype=np.uint8)
+    data = torch.from_numpy(host).cuda()
+    parity = rs.encode_batch(data)
+    torch.cuda.synchronize()
+    plan = [p for key, p in rs._plans.items() if key[0] == "encb"][0]
+    assert plan.engine == "mfma" and plan.in_bstride == k * C
+    for b in range(B):
+        assert np.array_equal(parity[b].cpu().numpy(), GF256.gemm(rs.E, host[b])), b
+    lost = set(range(0, 128, 5)) | {128, 133, 140, 149, 155, 159}
+    rows = [r for r in range(n) if r not in lost][:k]
+    stripe = torch.cat([data, parity], dim=1)
+    surv = stripe[:, rows].contiguous()
+    out = rs.decode_batch(surv, rows)
+    torch.cuda.synchronize()
+    dplan = [p for key, p in rs._plans.items() if key[0] == "decb"][0]
+    assert dplan.engine == "mfma" and dplan.has_copies
+    assert torch.equal(out, data)
+    # stripes in separate allocations, not equally spaced: the v_perm batched kernel
+    ins = [alloc_rows(k, C, "cuda") for _ in range(2)]
+    pad = torch.empty(12345, dtype=torch.uint8, device="cuda")  # noqa: F841 (breaks the spacing)
+    ins.append(alloc_rows(k, C, "cuda"))
+    for i in ins:
+        i.copy_(data[0])
+    outs = [alloc_rows(n - k, C, "cuda") for _ in ins]
+    ptrs = [int(x.data_ptr()) for x in ins]
+    p2 = GemmPlan([[r for r in x] for x in ins], [[r for r in o] for o in outs], rs.E)
+    if ptrs[1] - ptrs[0] != ptrs[2] - ptrs[1]:
+        assert p2.engine == "valu"
+    p2.run()
+    torch.cuda.synchronize()
+    assert all(np.array_equal(o.cpu().numpy(), GF256.gemm(rs.E, host[0])) for o in outs)
