@@ -392,18 +392,25 @@ _SHORT_ROW, _MID_ROW = 512 << 10, 4 << 20
 
 
 # Batched wide codes (serving) take the batched FP4 launch from this many columns per stripe (two
-# 128-column chunks of the A-resident kernel): below it the whole batch is a handful of chunks and
-# the k-split v_perm kernel's shorter prologue wins. (scripts/serve_bench.py --code 128:160;
+# 128-column chunks of the A-resident kernel; below it the k-split v_perm kernel's shorter prologue
+# wins) and 16 outputs, or 8..15 outputs up to _FP4_BATCH_MID_COLS columns over the whole batch.
+# Measured on MI355X (profiles/serving/r08_fp4batch, RS(128,160)): encode 256 x 64 KiB 68.9 -> 30.8
+# us, 256 x 1 MiB 419 -> 221 us; decode rebuilding 26 natives (+ 102 fused copies) 256 x 1 MiB
+# 451 -> 256 us; rebuilding 8: 16 x 1 MiB 32.3 -> 28.1 but 256 x 1 MiB 150 -> 166 (v_perm kept);
+# rebuilding 4 (memory-bound beside 124 copies) stays on the v_perm kernels. (scripts/serve_bench.py --code 128:160;
 # GFRS_FP4_BATCH_MIN_COLS overrides, e.g. a huge value keeps every batch on the v_perm kernels.)
 _FP4_BATCH_MIN_COLS = int(__import__("os").environ.get("GFRS_FP4_BATCH_MIN_COLS", 256))
+_FP4_BATCH_MID_COLS = 1 << 20
 
 
 def _auto_engine(k: int, m: int, gf256: bool, bytewise: bool, batch: int, ncols: int | None = None,
                  batch_fp4: bool = False) -> str:
     if not gf256 or bytewise:
         return "valu"
-    if batch != 1:
-        return "mfma" if (batch_fp4 and ncols is not None and ncols >= _FP4_BATCH_MIN_COLS) else "valu"
+    if batch != 1:  # (a narrow decode — few rebuilt rows beside many fused copies — is memory-bound)
+        if not batch_fp4 or ncols is None or ncols < _FP4_BATCH_MIN_COLS:
+            return "valu"
+        return "mfma" if (m >= 16 or (m >= 8 and ncols * batch <= _FP4_BATCH_MID_COLS)) else "valu"
     if k >= _MFMA_MIN_K and m >= _MFMA_MIN_M:
         return "mfma"
     if ncols is not None and ((ncols <= _SHORT_ROW and k >= 16 and m >= 4) or

@@ -48,7 +48,7 @@ def timed(fn, reps: int) -> float:
     return float(np.median(ts))
 
 
-def point(S: int, B: int, reps: int, k: int = 10, n: int = 14) -> dict:
+def point(S: int, B: int, reps: int, k: int = 10, n: int = 14, erase: int = 0) -> dict:
     p = n - k
     C = (S + k - 1) // k
     dev = torch.device("cuda", 0)
@@ -56,7 +56,10 @@ def point(S: int, B: int, reps: int, k: int = 10, n: int = 14) -> dict:
     data, dbase = batch_rows(B, k, C, dev)
     fill_random_(dbase, seed=S + B)
     parity, _ = batch_rows(B, p, C, dev)
-    if (k, n) == (10, 14):
+    if erase:  # natives 0, 2, 4, ... lost, rebuilt from the first `erase` parity rows
+        lost = list(range(0, 2 * erase, 2))[:erase]
+        rows = [r for r in range(k) if r not in lost] + list(range(k, k + len(lost)))
+    elif (k, n) == (10, 14):
         rows = [0, 2, 3, 4, 6, 7, 9, 10, 11, 13]  # natives 1, 5, 8 and parity 12 lost on every object
     else:  # up to three natives and the first parity lost
         lost = sorted({1, k // 2, k - 2})[:max(1, min(3, p - 1))] + ([k] if p > 1 else [])
@@ -82,7 +85,7 @@ def point(S: int, B: int, reps: int, k: int = 10, n: int = 14) -> dict:
     for j, r in enumerate(rows):  # the survivors as the decode reads them
         surv[:, j].copy_(data[:, r] if r < k else parity[:, r - k])
     torch.cuda.synchronize()
-    res = {"object_bytes": S, "batch": B, "k": k, "n": n, "C": C}
+    res = {"object_bytes": S, "batch": B, "k": k, "n": n, "C": C, "erased_natives": sum(1 for r in range(k) if r not in rows)}
     res["enc_batched_us"] = timed(enc_batched, reps)
     res["dec_batched_us"] = timed(dec_batched, reps)
     if B <= 64:
@@ -123,12 +126,13 @@ def main() -> int:
     ap.add_argument("--batches", default="1,16,256")
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--code", default="10:14", help="k:n of the code (default the headline's RS(10,14))")
+    ap.add_argument("--erase", type=int, default=0, help="natives lost per object (0: the default pattern)")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     pts = []
     for S in map(int, a.sizes.split(",")):
         for B in map(int, a.batches.split(",")):
-            r = point(S, B, a.reps, *(int(v) for v in a.code.split(":")))
+            r = point(S, B, a.reps, *(int(v) for v in a.code.split(":")), erase=a.erase)
             print(json.dumps(r), flush=True)
             pts.append(r)
             torch.cuda.empty_cache()

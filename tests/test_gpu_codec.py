@@ -621,18 +621,24 @@ def test_batched_wide_code_on_matrix_cores(C, B):
     k, n = 128, 160
     rs = ReedSolomon(k, n, matrix="cauchy")
     host = np.random.default_rng(C + B).integers(0, 256, size=(B, k, C), dtype=np.uint8)
-    data = torch.from_numpy(host).cuda()
+    P = (C + 255) // 256 * 256  # 16-byte aligned rows (a ragged C pitched up), one allocation
+
+    def pitched(rows):
+        return torch.empty((B, rows, P), dtype=torch.uint8, device="cuda")[:, :, :C]
+    data = pitched(k)
+    data.copy_(torch.from_numpy(host))
     parity = rs.encode_batch(data)
     torch.cuda.synchronize()
     plan = [p for key, p in rs._plans.items() if key[0] == "encb"][0]
-    assert plan.engine == "mfma" and plan.in_bstride == k * C
+    assert plan.engine == "mfma" and plan.in_bstride == k * P
     for b in range(B):
         assert np.array_equal(parity[b].cpu().numpy(), GF256.gemm(rs.E, host[b])), b
     lost = set(range(0, 128, 5)) | {128, 133, 140, 149, 155, 159}
     rows = [r for r in range(n) if r not in lost][:k]
     stripe = torch.cat([data, parity], dim=1)
-    surv = stripe[:, rows].contiguous()
-    out = rs.decode_batch(surv, rows)
+    surv = pitched(k)
+    surv.copy_(stripe[:, rows])
+    out = rs.decode_batch(surv, rows, pitched(k))
     torch.cuda.synchronize()
     dplan = [p for key, p in rs._plans.items() if key[0] == "decb"][0]
     assert dplan.engine == "mfma" and dplan.has_copies
@@ -642,7 +648,7 @@ def test_batched_wide_code_on_matrix_cores(C, B):
     pad = torch.empty(12345, dtype=torch.uint8, device="cuda")  # noqa: F841 (breaks the spacing)
     ins.append(alloc_rows(k, C, "cuda"))
     for i in ins:
-        i.copy_(data[0])
+        i.copy_(torch.from_numpy(host[0]))
     outs = [alloc_rows(n - k, C, "cuda") for _ in ins]
     ptrs = [int(x.data_ptr()) for x in ins]
     p2 = GemmPlan([[r for r in x] for x in ins], [[r for r in o] for o in outs], rs.E)
