@@ -120,6 +120,18 @@ hipError_t launch_fp4_bitmat_sel(const uint8_t* coeff, int ld, const int* sel, i
 hipError_t launch_mfma_bitmat(const uint8_t* coeff, int m, int k, void* bitmat,
                               hipStream_t stream);
 
+// ---- GF(2^16) on the FP4 matrix cores (csrc/kernels/gf_mfma16.hip) -----------------------------
+// desc: a desc_layout16 descriptor (its v_perm records run the columns past the last 512-byte chunk
+// and any start not 4-byte aligned); bitmat from launch_fp16_bitmat with the same (k, m, mg_cap).
+// Rows 4-byte aligned; col0 / ncols even. K is split into passes (one launch each, later passes XOR
+// into the outputs); copies: fused survivor copy (decode), in_stride as launch_gf_gemm_fp4.
+hipError_t launch_gf_gemm16_fp4(const void* bitmat, const void* desc, int k, int m, int64_t col0, int64_t ncols,
+                                int mg_cap, int64_t in_stride, bool copies, hipStream_t stream);
+size_t fp16_bitmat_bytes(int k, int m, int mg_cap);
+// coefficient (o, i) = coeff[row(o) * ld + i] (uint16, device), row(o) = sel ? sel[o] : o
+hipError_t launch_fp16_bitmat(const uint16_t* coeff, int ld, const int* sel, int m, int k, void* bitmat, int mg_cap,
+                              hipStream_t stream);
+
 // FP4 kernels: the bit-matrix allocation ends with a write-only sink of kFp4SinkSlots 1-KiB slots;
 // each wave stores its dummy / destination-less bytes into slot (4 * block + wave) % slots, so the
 // sink writes of concurrent waves land on different L2 lines (one shared 1-KiB sink made every CU of

@@ -1,0 +1,439 @@
+// GF(2^16) GEMM on gfx950 matrix cores: the FP4 (e2m1) GF(2) bit-matrix engine of gf_mfma_fp4.hip
+// (read its header first: operand encoding, K order of the B expansion, biased-float parity
+// epilogue) carried to 16-bit symbols.
+//
+// The reference's generic field code names w = 16 (/root/reference/src/galoisfield.cu:22-32, poly
+// 0210013) but never built it; the v_perm kernel (gf_gemm16.hip) runs it on the VALU at ~0.23 TB/s
+// for wide codes (k=300, m=40: 4.5 ms per GiB). Multiplication by c is a 16 x 16 GF(2) matrix, so
+// a code's whole map is a (16m x 16k) bit-matrix and the GEMM is the same bit-matrix product as in
+// GF(2^8), with twice the bit-MACs per byte.
+//
+// How 16-bit symbols meet the byte engine. A lane reads one dword of each of 4 input rows per
+// K-step: symbols 2c and 2c+1 of its 64-symbol column group, little-endian (lo0 hi0 lo1 hi1). Its
+// B operands are the gf_mfma_fp4.hip bit planes of 4 byte streams: sub-block j (symbol 2c+j) x
+// byte plane t (lo, hi). With A split into the four byte-to-byte blocks of the 16 x 16 maps
+// (f = 2 * src + dst: ll, lh, hl, hh — gfrs/gf65536.h perm_quad's order),
+//     acc[j][lo] += A_ll . B[j][lo] + A_hl . B[j][hi]
+//     acc[j][hi] += A_lh . B[j][lo] + A_hh . B[j][hi]
+// — 4 MFMAs per (M-tile, sub-block, K-step), every A fragment shared by the two sub-blocks. An
+// output dword (lo0 hi0 lo1 hi1 of one row) is packed from the four accumulators of (tile, u).
+//
+// K passes. A whole column of the bit-matrix does not fit the LDS for wide codes (one M-tile of 4
+// output symbols x k=300 is 150 KiB of FP4 nibbles), so the K rows are split into passes of S
+// K-steps (8 input rows each), one launch per pass: pass 0 stores its partial outputs, every later
+// pass XORs into them (launch boundaries order the passes). Within a pass a persistent block holds
+// its M-tile group's A slice (S x MG x 4 KiB) in LDS for all of its chunks; the group's blocks of
+// one chunk share an XCD (the input re-read per group is an L2 hit).
+//
+// Input rows stream through registers (4 dword loads per lane and K-step, D steps in flight
+// across chunk boundaries); rows past k are clamped to row k-1 and meet zero bit-matrix columns.
+// Fused survivor copies (decode): group 0's blocks also store the raw dwords of their rows.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+
+#include "gfrs/desc.h"
+#include "gfrs/device_cache.h"
+#include "gfrs/kernels.h"
+
+namespace gfrs {
+namespace {
+
+using i32x8 = int __attribute__((ext_vector_type(8)));
+using i32x4 = int __attribute__((ext_vector_type(4)));
+using f32x16 = float __attribute__((ext_vector_type(16)));
+template <typename T>
+using cptr = const __attribute__((address_space(4))) T*;
+template <typename T>
+using gptr = __attribute__((address_space(1))) T*;
+
+constexpr int kWaveBytes = 128;            // byte columns per wave: 64 symbols (2 per lane)
+constexpr int kChunkBytes = 4 * kWaveBytes;  // per block and chunk
+constexpr int kDepth = 4;                  // K-steps of input in flight per lane
+constexpr int kSinkBytes16 = 64 * 1024;    // write-only sink after the bit-matrix (padding outputs)
+constexpr uint32_t kPoly16 = 0x1100Bu;
+
+__host__ __device__ constexpr int out_row_of(int r) { return 2 * ((r >> 2) & 1) + (r >> 4); }
+__host__ __device__ constexpr int out_bit_of(int r) { return ((r >> 3) & 1) * 4 + (r & 3); }
+constexpr uint8_t kAOne[4] = {0x4, 0x2, 0x1, 0x1};  // reciprocal weights of the B planes (gf_mfma_fp4.hip)
+
+__device__ __forceinline__ uint32_t xtime16(uint32_t x) {
+  x <<= 1;
+  return (x & 0x10000u) ? (x ^ kPoly16) : x;
+}
+// c * 2^e in GF(2^16)
+__device__ __forceinline__ uint32_t mul_pow2(uint32_t c, int e) {
+  for (int i = 0; i < e; ++i) c = xtime16(c);
+  return c;
+}
+
+// Bit-matrix layout: [pass][group][step < S][mt < MG][f < 4][lane < 64][16 B]; nibble j of a lane's
+// 16 bytes <-> input symbol row row0 + 8 s + 4 h + ((j & 7) >> 1), bit (j >> 3) + 4 (j & 1) of byte
+// plane src; output row 4 (g MG + mt) + out_row_of(r), bit out_bit_of(r) of byte plane dst
+// (f = 2 src + dst). Coefficient (o, i) = coeff[row(o) * ld + i], row(o) = sel ? sel[o] : o.
+__global__ void fp16_bitmat_kernel(const uint16_t* __restrict__ coeff, int ld, const int* __restrict__ sel, int m,
+                                   int k, int S, int mg, int groups, int passes, uint8_t* __restrict__ bitmat) {
+  const int64_t total = int64_t(passes) * groups * S * mg * 4 * 64 * 16;
+  for (int64_t idx = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; idx < total;
+       idx += int64_t(gridDim.x) * blockDim.x) {
+    const int q = int(idx & 15);
+    const int lane = int((idx >> 4) & 63);
+    int64_t rest = idx >> 10;
+    const int f = int(rest & 3);
+    rest >>= 2;
+    const int mt = int(rest % mg);
+    rest /= mg;
+    const int s = int(rest % S);
+    rest /= S;
+    const int g = int(rest % groups);
+    const int pass = int(rest / groups);
+    const int src = f >> 1, dst = f & 1;
+    const int r = lane & 31, h = lane >> 5;
+    const int orow = 4 * (g * mg + mt) + out_row_of(r);
+    const int obit = out_bit_of(r) + 8 * dst;
+    uint8_t v = 0;
+    for (int half = 0; half < 2; ++half) {
+      const int j = 2 * q + half;
+      const int dq = j >> 3, jj = j & 7;
+      const int irow = 8 * (pass * S + s) + 4 * h + (jj >> 1);
+      const int ibit = dq + 4 * (jj & 1) + 8 * src;
+      if (orow < m && irow < k) {
+        const uint32_t c = coeff[size_t(sel ? sel[orow] : orow) * ld + irow];
+        if ((mul_pow2(c, ibit) >> obit) & 1u) v |= uint8_t(kAOne[dq] << (4 * half));
+      }
+    }
+    bitmat[idx] = v;
+  }
+}
+
+__device__ __forceinline__ uint32_t bfi(uint32_t mask, uint32_t a, uint32_t b) {
+  uint32_t r;
+  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "s"(mask), "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ int bias_scale_of_lane(int lane) { return 127 + 23 - out_bit_of(lane & 31); }
+
+// B operands of sub-block j (symbol 2c + j) from the 4 rows' dwords: bytes 2j (lo) and 2j + 1 (hi)
+// of x0..x3 gathered per plane (3 v_perm), then the bit planes masked in place (gf_mfma_fp4.hip).
+template <int J>
+__device__ __forceinline__ void expand16(i32x4 (&bo)[2], const uint32_t (&x)[4]) {
+  constexpr uint32_t sel = J == 0 ? 0x05040100u : 0x07060302u;  // (x_a.b2j, x_a.b2j+1, x_b.b2j, x_b.b2j+1)
+  const uint32_t p01 = __builtin_amdgcn_perm(x[1], x[0], sel);
+  const uint32_t p23 = __builtin_amdgcn_perm(x[3], x[2], sel);
+  const uint32_t w[2] = {__builtin_amdgcn_perm(p23, p01, 0x06040200u), __builtin_amdgcn_perm(p23, p01, 0x07050301u)};
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    bo[t][0] = int(w[t] & 0x11111111u);
+    bo[t][1] = int(w[t] & 0x22222222u);
+    bo[t][2] = int(w[t] & 0x44444444u);
+    bo[t][3] = int((w[t] >> 1) & 0x44444444u);
+  }
+}
+
+// MG: M-tiles (4 output symbol rows each) per block; UNI: input row r at in[0] + r * in_stride (else
+// the row pointers come from an LDS table); COPY: fused survivor copy; ACC: XOR into the outputs
+// (passes after the first).
+template <int MG, bool UNI, bool COPY, bool ACC>
+__global__ __launch_bounds__(256, 1) void gf_gemm16_fp4_kernel(cptr<uint64_t> in, cptr<uint64_t> out,
+                                                               cptr<uint64_t> copy, const i32x4* __restrict__ bitmat,
+                                                               int k, int m, int row0, int S, int groups,
+                                                               int64_t col0, int64_t nchunks, int64_t chunk_slots,
+                                                               int64_t in_stride, uint64_t sink) {
+  extern __shared__ __attribute__((aligned(16))) i32x4 afrag[];  // [S][MG][4][64] | row ptrs | copy ptrs
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7;
+  const int local = bid >> 3;
+  const int g = local % groups;
+  const int64_t slot0 = int64_t(local / groups) * 8 + xcd;
+  if (slot0 >= chunk_slots) return;
+  const int my_chunks = int((nchunks - slot0 + chunk_slots - 1) / chunk_slots);
+  if (my_chunks <= 0) return;
+  const int nrows = 8 * S;  // this pass's input rows (row0 .. row0 + nrows - 1, clamped to k - 1)
+  const size_t a_frags = size_t(S) * MG * 4 * 64;
+  uint64_t* rowptr = reinterpret_cast<uint64_t*>(afrag + a_frags);
+  uint64_t* copyptr = rowptr + nrows;
+  const i32x4* src = bitmat + size_t(g) * a_frags;
+  for (size_t i = threadIdx.x; i < a_frags; i += 256) afrag[i] = src[i];
+  for (int i = threadIdx.x; i < nrows; i += 256) {
+    const int r = min(row0 + i, k - 1);
+    if (!UNI) rowptr[i] = in[r];
+    if (COPY) copyptr[i] = (g == 0 && row0 + i < k) ? copy[r] : 0;
+  }
+  __syncthreads();
+
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5, c = lane & 31;
+  const int scale = 0x7F7F7F7F;  // E8M0 1.0
+  const int bias_scale = bias_scale_of_lane(lane);
+  const i32x8 one_k0 = {h == 0 ? 0x2 : 0, 0, 0, 0, 0, 0, 0, 0};
+  // output rows of this lane: 4 (g MG + mt) + 2h + u (padding rows -> the sink, never read)
+  uint64_t optr[MG][2];
+#pragma unroll
+  for (int mt = 0; mt < MG; ++mt)
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int row = 4 * (g * MG + mt) + 2 * h + u;
+      const uint64_t o = row < m ? out[row] : 0;
+      optr[mt][u] = o;
+    }
+  const uint64_t my_sink = sink + uint64_t(((bid * 4 + wave) % 256) * 256 + 4 * c);
+  const uint64_t in0 = UNI ? in[0] : 0;
+  const int64_t lane_col = int64_t(wave) * kWaveBytes + 4 * c;
+
+  f32x16 acc[MG][2][2];  // [tile][sub-block][plane]
+  auto bias_init = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int mt = 0; mt < MG; ++mt)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          int bs = bias_scale;  // (opaque: identical MFMAs must not be merged or hoisted)
+          asm volatile("" : "+v"(bs));
+          acc[mt][j][t] =
+              __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(one_k0, one_k0, (f32x16)(0.0f), 4, 4, 0, bs, 0, scale);
+        }
+  };
+
+  // flat step sequence over (chunk, step): load cursor (lc, ls) runs kDepth steps ahead
+  int lc = 0, ls = 0;
+  const int total_steps = my_chunks * S;
+  auto load_step = [&](uint32_t (&x)[4], int& cc, int& ss) __attribute__((always_inline)) {
+    const int64_t col = col0 + (slot0 + int64_t(cc) * chunk_slots) * kChunkBytes + lane_col;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int rr = 8 * ss + 4 * h + i;  // pass-relative row
+      uint64_t base;
+      if constexpr (UNI)
+        base = in0 + uint64_t(int64_t(min(row0 + rr, k - 1)) * in_stride);
+      else
+        base = rowptr[rr];
+      x[i] = __builtin_nontemporal_load((gptr<const uint32_t>)(base + uint64_t(col)));
+    }
+    if (++ss == S) {
+      ss = 0;
+      ++cc;
+    }
+  };
+  uint32_t ring[kDepth][4];
+#pragma unroll
+  for (int d = 0; d < kDepth; ++d)
+    if (d < total_steps) load_step(ring[d], lc, ls);
+
+  bias_init();
+  int cc = 0, cs = 0;  // compute cursor
+  for (int t0 = 0; t0 < total_steps; t0 += kDepth) {
+#pragma unroll
+    for (int d = 0; d < kDepth; ++d) {
+      if (t0 + d >= total_steps) break;  // (uniform)
+      uint32_t x[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) x[i] = ring[d][i];
+      if constexpr (COPY) {
+        if (g == 0) {
+          const int64_t col = col0 + (slot0 + int64_t(cc) * chunk_slots) * kChunkBytes + lane_col;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const uint64_t cp = copyptr[8 * cs + 4 * h + i];
+            if (cp) __builtin_nontemporal_store(x[i], (gptr<uint32_t>)(cp + uint64_t(col)));
+          }
+        }
+      }
+      if (t0 + d + kDepth < total_steps) load_step(ring[d], lc, ls);
+      i32x4 b0[2], b1[2];
+      expand16<0>(b0, x);
+      expand16<1>(b1, x);
+      const i32x4* as = afrag + size_t(cs) * MG * 4 * 64 + lane;
+#pragma unroll
+      for (int mt = 0; mt < MG; ++mt) {
+        i32x4 af[4];
+#pragma unroll
+        for (int f = 0; f < 4; ++f) af[f] = as[(mt * 4 + f) * 64];
+#pragma unroll
+        for (int dst = 0; dst < 2; ++dst) {
+          const i32x8 a_lo = {af[dst][0], af[dst][1], af[dst][2], af[dst][3], 0, 0, 0, 0};          // src lo
+          const i32x8 a_hi = {af[2 + dst][0], af[2 + dst][1], af[2 + dst][2], af[2 + dst][3], 0, 0, 0, 0};  // src hi
+          const i32x8 bl0 = {b0[0][0], b0[0][1], b0[0][2], b0[0][3], 0, 0, 0, 0};
+          const i32x8 bh0 = {b0[1][0], b0[1][1], b0[1][2], b0[1][3], 0, 0, 0, 0};
+          const i32x8 bl1 = {b1[0][0], b1[0][1], b1[0][2], b1[0][3], 0, 0, 0, 0};
+          const i32x8 bh1 = {b1[1][0], b1[1][1], b1[1][2], b1[1][3], 0, 0, 0, 0};
+          acc[mt][0][dst] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a_lo, bl0, acc[mt][0][dst], 4, 4, 0, scale, 0, scale);
+          acc[mt][1][dst] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a_lo, bl1, acc[mt][1][dst], 4, 4, 0, scale, 0, scale);
+          acc[mt][0][dst] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a_hi, bh0, acc[mt][0][dst], 4, 4, 0, scale, 0, scale);
+          acc[mt][1][dst] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a_hi, bh1, acc[mt][1][dst], 4, 4, 0, scale, 0, scale);
+        }
+      }
+      if (cs + 1 == S) {  // chunk done: pack, store, restart the accumulators
+        const int64_t col = col0 + (slot0 + int64_t(cc) * chunk_slots) * kChunkBytes + lane_col;
+#pragma unroll
+        for (int mt = 0; mt < MG; ++mt) {
+#pragma unroll
+          for (int u = 0; u < 2; ++u) {
+            uint32_t y[2][2];  // [sub-block][plane]: the byte in bits 0..7
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+              for (int t = 0; t < 2; ++t) {
+                uint32_t v = __float_as_uint(acc[mt][j][t][8 * u]);
+#pragma unroll
+                for (int b = 1; b < 8; ++b) v = bfi(1u << b, __float_as_uint(acc[mt][j][t][8 * u + b]), v);
+                y[j][t] = v;
+              }
+            // (lo0, hi0, lo1, hi1)
+            const uint32_t w = __builtin_amdgcn_perm(__builtin_amdgcn_perm(y[1][1], y[1][0], 0x0c0c0400u),
+                                                     __builtin_amdgcn_perm(y[0][1], y[0][0], 0x0c0c0400u), 0x05040100u);
+            const uint64_t o = optr[mt][u];
+            gptr<uint32_t> dstp = (gptr<uint32_t>)(o ? o + uint64_t(col) : my_sink);
+            if constexpr (ACC) {
+              const uint32_t old = o ? *dstp : 0u;
+              *dstp = old ^ w;
+            } else {
+              *dstp = w;
+            }
+          }
+        }
+        bias_init();
+        cs = 0;
+        ++cc;
+      } else {
+        ++cs;
+      }
+    }
+  }
+}
+
+struct Geo16 {
+  int ksteps, mtiles, mg, groups, passes, S;
+  size_t lds;
+};
+
+// M-tiles per block MG (<= mg_cap, power of two while it pays) and passes of S K-steps so one
+// group's A slice plus its pointer tables fit the LDS.
+Geo16 geometry16(int k, int m, int mg_cap, bool copy) {
+  Geo16 g{};
+  g.ksteps = (k + 7) / 8;
+  g.mtiles = (m + 3) / 4;
+  // MG in {2, 1} (<= mg_cap): the fewest padded M-tiles, then the wider (GFRS_FP16_MG forces one).
+  // (MG = 4 — 256 accumulator registers beside the unrolled input ring — spilled ~2 KiB per lane.)
+  static const int forced = [] {
+    const char* e = std::getenv("GFRS_FP16_MG");
+    return e ? std::atoi(e) : 0;
+  }();
+  g.mg = 1;
+  for (int cand : {2, 1}) {
+    if (cand > mg_cap || (forced && cand != forced)) continue;
+    const int padded = (g.mtiles + cand - 1) / cand * cand;
+    const int best = (g.mtiles + g.mg - 1) / g.mg * g.mg;
+    if (g.mg == 1 || padded < best) g.mg = cand;
+    if (forced) break;
+  }
+  constexpr size_t kLds = 152 * 1024;
+  auto fit_steps = [&](int mg) {
+    // per K-step: A (mg x 4 KiB) + 8 row pointers (+ 8 copy pointers)
+    return int(kLds / (size_t(mg) * 4096 + 64 + (copy ? 64 : 0)));
+  };
+  while (g.mg > 1 && fit_steps(g.mg) < 1) g.mg >>= 1;
+  const int smax = std::max(1, fit_steps(g.mg));
+  g.passes = (g.ksteps + smax - 1) / smax;
+  g.S = (g.ksteps + g.passes - 1) / g.passes;
+  g.groups = (g.mtiles + g.mg - 1) / g.mg;
+  g.lds = size_t(g.S) * g.mg * 4096 + size_t(8 * g.S) * 8 * (copy ? 2 : 1);
+  return g;
+}
+
+size_t bitmat16_matrix_bytes(const Geo16& g) { return size_t(g.passes) * g.groups * g.S * g.mg * 4 * 64 * 16; }
+
+template <int MG, bool UNI, bool COPY, bool ACC>
+hipError_t launch16_pass(const Geo16& geo, cptr<uint64_t> in, cptr<uint64_t> out, cptr<uint64_t> copy,
+                         const uint8_t* bitmat, int k, int m, int pass, int64_t col0, int64_t nchunks, int64_t in_stride,
+                         uint64_t sink, hipStream_t stream) {
+  const void* f = reinterpret_cast<const void*>(&gf_gemm16_fp4_kernel<MG, UNI, COPY, ACC>);
+  hipError_t e = ensure_lds_optin(f);
+  if (e != hipSuccess) return e;
+  static DeviceMemo<size_t, int> occ_memo;
+  const int occ = occ_memo.get_or(geo.lds, [&] {
+    int o = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, f, 256, geo.lds) != hipSuccess) o = 0;
+    return o;
+  });
+  if (occ <= 0) return hipErrorInvalidConfiguration;
+  const int64_t slots = persistent_slots(std::min(occ, 4), geo.groups, nchunks);
+  const unsigned blocks = unsigned(slots * geo.groups);
+  const i32x4* bm = reinterpret_cast<const i32x4*>(bitmat) + size_t(pass) * geo.groups * geo.S * MG * 4 * 64;
+  gf_gemm16_fp4_kernel<MG, UNI, COPY, ACC><<<blocks, 256, geo.lds, stream>>>(
+      in, out, copy, bm, k, m, pass * 8 * geo.S, geo.S, geo.groups, col0, nchunks, slots, in_stride, sink);
+  return hipGetLastError();
+}
+
+template <int MG>
+hipError_t launch16_mg(const Geo16& geo, cptr<uint64_t> in, cptr<uint64_t> out, cptr<uint64_t> copy,
+                       const uint8_t* bitmat, int k, int m, int64_t col0, int64_t nchunks, int64_t in_stride,
+                       uint64_t sink, hipStream_t stream) {
+  for (int p = 0; p < geo.passes; ++p) {
+    hipError_t e;
+    const bool acc = p > 0;
+    if (copy) {
+      e = acc ? launch16_pass<MG, false, true, true>(geo, in, out, copy, bitmat, k, m, p, col0, nchunks, 0, sink, stream)
+              : launch16_pass<MG, false, true, false>(geo, in, out, copy, bitmat, k, m, p, col0, nchunks, 0, sink, stream);
+    } else if (in_stride) {
+      e = acc ? launch16_pass<MG, true, false, true>(geo, in, out, copy, bitmat, k, m, p, col0, nchunks, in_stride, sink,
+                                                     stream)
+              : launch16_pass<MG, true, false, false>(geo, in, out, copy, bitmat, k, m, p, col0, nchunks, in_stride, sink,
+                                                      stream);
+    } else {
+      e = acc ? launch16_pass<MG, false, false, true>(geo, in, out, copy, bitmat, k, m, p, col0, nchunks, 0, sink, stream)
+              : launch16_pass<MG, false, false, false>(geo, in, out, copy, bitmat, k, m, p, col0, nchunks, 0, sink,
+                                                       stream);
+    }
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+}  // namespace
+
+size_t fp16_bitmat_bytes(int k, int m, int mg_cap) {
+  return bitmat16_matrix_bytes(geometry16(k, m, mg_cap, true)) + kSinkBytes16;
+}
+
+hipError_t launch_fp16_bitmat(const uint16_t* coeff, int ld, const int* sel, int m, int k, void* bitmat, int mg_cap,
+                              hipStream_t stream) {
+  if (m <= 0 || k <= 0 || m > 65535 || k > 65535 || mg_cap < 1 || ld < k) return hipErrorInvalidValue;
+  const Geo16 g = geometry16(k, m, mg_cap, true);
+  const int64_t total = int64_t(bitmat16_matrix_bytes(g));
+  const int blocks = int(std::min<int64_t>((total + 255) / 256, 8192));
+  fp16_bitmat_kernel<<<blocks, 256, 0, stream>>>(coeff, ld, sel, m, k, g.S, g.mg, g.groups, g.passes,
+                                                 static_cast<uint8_t*>(bitmat));
+  return hipGetLastError();
+}
+
+hipError_t launch_gf_gemm16_fp4(const void* bitmat, const void* desc, int k, int m, int64_t col0, int64_t ncols,
+                                int mg_cap, int64_t in_stride, bool copies, hipStream_t stream) {
+  if (k <= 0 || m <= 0 || ncols < 0 || ((col0 | ncols) & 1) || mg_cap < 1) return hipErrorInvalidValue;
+  const int m_pad = pad_m(m);
+  const DescLayout l = desc_layout16(k, m_pad);
+  const char* b = static_cast<const char*>(desc);
+  // (the bitmat is built for the copy geometry, whose pointer tables the LDS budget always includes)
+  const Geo16 geo = geometry16(k, m, mg_cap, true);
+  const int64_t nchunks = (col0 & 3) ? 0 : ncols / kChunkBytes;
+  if (nchunks > 0) {
+    cptr<uint64_t> in = (cptr<uint64_t>)(b + l.in_off);
+    cptr<uint64_t> out = (cptr<uint64_t>)(b + l.out_off);
+    cptr<uint64_t> copy = copies ? (cptr<uint64_t>)(b + l.copy_off) : nullptr;
+    const uint64_t sink = reinterpret_cast<uint64_t>(bitmat) + bitmat16_matrix_bytes(geo);
+    const auto* bm = static_cast<const uint8_t*>(bitmat);
+    const int64_t stride = copies ? 0 : in_stride;
+    hipError_t e;
+    switch (geo.mg) {
+      case 2: e = launch16_mg<2>(geo, in, out, copy, bm, k, m, col0, nchunks, stride, sink, stream); break;
+      default: e = launch16_mg<1>(geo, in, out, copy, bm, k, m, col0, nchunks, stride, sink, stream); break;
+    }
+    if (e != hipSuccess) return e;
+  }
+  const int64_t done = nchunks * kChunkBytes;
+  if (done < ncols) return launch_gf_gemm16(desc, k, m_pad, col0 + done, ncols - done, false, 0, stream);
+  return hipSuccess;
+}
+
+}  // namespace gfrs

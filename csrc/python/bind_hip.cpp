@@ -193,6 +193,19 @@ PYBIND11_MODULE(_hip, m) {
     while (mg < mtiles && mg < mg_cap) mg <<= 1;
     return k > 112 && k <= 128 && mtiles <= mg && fp4ar_supported(k, mg);
   });
+  m.def("fp16_bitmat_bytes", &fp16_bitmat_bytes);
+  m.def("fp16_bitmat", [](uint64_t coeff, int ld, uint64_t sel, int mm, int k, uint64_t bitmat, int mg_cap,
+                          uint64_t stream) {
+    check(launch_fp16_bitmat(reinterpret_cast<const uint16_t*>(coeff), ld, reinterpret_cast<const int*>(sel), mm, k,
+                             reinterpret_cast<void*>(bitmat), mg_cap, as_stream(stream)),
+          "fp16_bitmat");
+  });
+  m.def("gemm16_fp4", [](uint64_t bitmat, uint64_t desc, int k, int mm, int64_t col0, int64_t ncols, int mg_cap,
+                         int64_t in_stride, bool copies, uint64_t stream) {
+    check(launch_gf_gemm16_fp4(reinterpret_cast<const void*>(bitmat), reinterpret_cast<const void*>(desc), k, mm, col0,
+                               ncols, mg_cap, in_stride, copies, as_stream(stream)),
+          "gf_gemm16_fp4");
+  });
   m.def("gen_matrix", [](uint64_t e, int k, int p, int kind, uint64_t stream) {
     check(launch_gen_matrix(reinterpret_cast<uint8_t*>(e), k, p, kind, as_stream(stream)), "gen_matrix");
   });

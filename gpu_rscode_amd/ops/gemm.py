@@ -442,6 +442,23 @@ def _batch_strides(stripes_in, stripes_out, stripes_copy=None) -> tuple[int, int
     return d_in, d_out
 
 
+# GF(2^16) codes take the FP4 matrix-core engine from this many coefficients (k x m) with k, m >=
+# 16: the v_perm w = 16 kernel is VALU-bound there (k=300, m=40: 4.5 ms per GiB), narrow codes stay
+# at the memory ceiling on it. (GFRS_GF16_MFMA=0 / 1: never / always where supported.)
+_GF16_MFMA_MIN_KM = 1024
+
+
+def _auto_engine16(k: int, m: int, symwise: bool) -> bool:
+    import os
+
+    forced = os.environ.get("GFRS_GF16_MFMA")
+    if symwise or k > 65535:
+        return False
+    if forced is not None:
+        return forced == "1"
+    return k >= 16 and m >= 16 and k * m >= _GF16_MFMA_MIN_KM
+
+
 def _pack16(coeff) -> bytes:
     """GF(2^16) coefficients as the native pipeline's packed form: little-endian byte pairs
     (``gfrs::pack16``, ``csrc/include/gfrs/host_desc.h``)."""
@@ -472,7 +489,7 @@ class Gemm16Plan:
     """
 
     def __init__(self, inputs, outputs, coeff=None, *, copies=None, device_tables: bool = False,
-                 hold_buffers: bool = True):
+                 engine: str = "auto", mfma_mg: int = 2, hold_buffers: bool = True):
         if coeff is None and not device_tables:
             raise ValueError("need coeff or device_tables=True")
         self.inputs, self.outputs = _rows(inputs), _rows(outputs)
@@ -519,11 +536,56 @@ class Gemm16Plan:
             t[:, : self.m] = np.transpose(gf.perm_quads16(coeff), (1, 0, 2, 3))
             host[self.layout.tab_off:] = np.frombuffer(t.tobytes(), dtype=np.uint8)
         self.desc = torch.from_numpy(host).to(self.device)
-        self.engine = "valu16"
+        if engine == "auto":
+            engine = "mfma" if _auto_engine16(self.k, self.m, self.symwise) else "valu16"
+        if engine == "valu":
+            engine = "valu16"
+        if engine not in ("valu16", "mfma"):
+            raise ValueError(f"unknown GF(2^16) engine {engine!r}")
+        self.engine = engine
+        self.bitmat = None
+        self.has_copies = self.copies is not None
+        if engine == "mfma":
+            # the FP4 matrix-core engine (csrc/kernels/gf_mfma16.hip); the descriptor's v_perm records
+            # run the columns past the last 512-byte chunk
+            if self.symwise:
+                raise ValueError("engine='mfma' needs 16-byte aligned rows")
+            self.mfma_mg = mfma_mg
+            ptrs = [ptr(r) for r in self.inputs]
+            stride = ptrs[1] - ptrs[0] if self.k > 1 else 1
+            self.in_stride = stride if stride != 0 and all(q - ptrs[0] == j * stride for j, q in enumerate(ptrs)) else 0
+            self.bitmat = torch.zeros(hip().fp16_bitmat_bytes(self.k, self.m, mfma_mg), dtype=torch.uint8,
+                                      device=self.device)
+            if coeff is not None:
+                self.set_device_coeff(torch.from_numpy(np.ascontiguousarray(coeff.astype("<u2")).view(np.int16))
+                                      .to(self.device))
         if not hold_buffers:
             self.inputs = self.outputs = self.copies = None
         self._ready = torch.cuda.Event()
         self._ready.record(torch.cuda.current_stream(self.device))
+
+    def set_device_coeff(self, coeff: torch.Tensor, rows=None, stream: torch.cuda.Stream | None = None) -> None:
+        """Rebuild the matrix-core bit-matrix from a DEVICE 16-bit matrix (int16 / uint16, >= k
+        columns): coefficient row i = coeff[rows[i]] (device int32) or coeff[i]. No host round trip
+        (the w = 16 decode feeds it the device-solved decode rows)."""
+        if self.engine != "mfma":
+            raise ValueError("set_device_coeff applies to engine='mfma' plans")
+        if coeff.dtype not in (torch.int16, torch.uint16) or coeff.device != self.device or coeff.dim() != 2 \
+                or coeff.shape[1] < self.k:
+            raise ValueError("coeff must be a 2-D 16-bit tensor on the plan's device with >= k columns")
+        coeff = coeff.contiguous()
+        st = stream or torch.cuda.current_stream(self.device)
+        sel = 0
+        if rows is not None:
+            if rows.dtype != torch.int32 or rows.numel() != self.m:
+                raise ValueError("rows must be an int32 tensor of m row indices")
+            sel = rows.data_ptr()
+        elif coeff.shape[0] < self.m:
+            raise ValueError("coeff needs m rows")
+        hip().fp16_bitmat(coeff.data_ptr(), coeff.stride(0), sel, self.m, self.k, self.bitmat.data_ptr(),
+                          self.mfma_mg, st.cuda_stream)
+        if not torch.cuda.is_current_stream_capturing():
+            coeff.record_stream(st)
 
     def run(self, stream: torch.cuda.Stream | None = None, col0: int = 0, ncols: int | None = None,
             max_blocks: int = 0) -> None:
@@ -538,6 +600,10 @@ class Gemm16Plan:
             self._ready = None
         if stream is not None:
             self.desc.record_stream(stream)
+        if self.engine == "mfma" and max_blocks == 0 and col0 % 4 == 0:
+            hip().gemm16_fp4(int(self.bitmat.data_ptr()), int(self.desc.data_ptr()), self.k, self.m, col0, ncols,
+                             self.mfma_mg, self.in_stride, self.has_copies, st.cuda_stream)
+            return
         hip().gemm16(int(self.desc.data_ptr()), self.k, self.m_pad, col0, ncols, self.symwise, max_blocks,
                      st.cuda_stream)
 

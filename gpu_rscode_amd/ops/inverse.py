@@ -143,9 +143,15 @@ def decode_system16_into_plan(g: torch.Tensor, rows: torch.Tensor, erased: torch
         raise ValueError("dm must be a contiguous [e, k] 16-bit device tensor")
     st = stream or torch.cuda.current_stream(g.device)
     g = g.contiguous()
+    if dm is None and plan.engine == "mfma":  # the bit-matrix is rebuilt from the device-solved rows
+        if getattr(plan, "_dm_buf", None) is None or plan._dm_buf.shape != (e, k):
+            plan._dm_buf = torch.empty((e, k), dtype=torch.int16, device=g.device)
+        dm = plan._dm_buf
     hip().decode_system16(g.data_ptr(), n, k, rows.data_ptr(), erased.data_ptr(), e,
                           0 if dm is None else dm.data_ptr(), status.data_ptr(), plan.desc.data_ptr(), plan.m_pad,
                           st.cuda_stream, 0 if ptrs is None else ptrs.data_ptr())
+    if plan.engine == "mfma":
+        plan.set_device_coeff(dm, stream=st)
     return status
 
 
@@ -187,7 +193,8 @@ class PatternDecoder:
         if self.wide:
             if not hip().decode_system16_supported(n, k, e):
                 raise ValueError(f"GF(2^16) device decode system (n={n}, k={k}, e={e}) does not fit one workgroup")
-            self.plan = Gemm16Plan(chunks[:k], out[:e], copies=out, device_tables=True)
+            self.plan = Gemm16Plan(chunks[:k], out[:e], copies=out, device_tables=True,
+                                   engine="auto" if engine == "auto" else ("mfma" if engine == "mfma" else "valu16"))
         else:
             self.plan = GemmPlan(chunks[:k], out[:e], copies=out, device_tables=True, engine=engine)
         ncols = min(r.numel() for r in rows_all)

@@ -179,3 +179,59 @@ def test_rs_decode_device_invert_w16_matches_host_plan():
     rs.decode([stripe[r] for r in rows], rows, device_invert=True)
     torch.cuda.synchronize()
     assert int(rs.last_status.item()) == 1
+
+
+@pytest.mark.parametrize("k,m,C,col", [(300, 40, 2 * 256 * 37 + 2 * 13, (0, None)), (64, 16, 512 * 9, (0, None)),
+                                       (17, 20, 512 * 3 + 6, (4, 1536)), (300, 40, 512 * 5, (512, 1024))])
+def test_gemm16_fp4_engine_matches_oracle(k, m, C, col):
+    """GF(2^16) on the FP4 matrix cores (gf_mfma16.hip): the 16 x 16 bit-matrix of every coefficient,
+    K split into passes (k = 300: later passes XOR into the outputs), 512-byte chunks on the matrix
+    cores and the ragged tail on the v_perm records; column sub-ranges write only those columns."""
+    rng = np.random.default_rng(k + m + C)
+    coeff = rng.integers(0, 65536, size=(m, k))
+    coeff[0, :3] = [0, 1, 65535]
+    x = alloc_rows(k, C, "cuda")
+    x.copy_(_rand(k, C, C + 1))
+    y = alloc_rows(m, C, "cuda", fill=0x5A)
+    plan = Gemm16Plan(x, y, coeff, engine="mfma")
+    assert plan.engine == "mfma"
+    c0, n = col[0], (C - col[0] if col[1] is None else col[1])
+    plan.run(col0=c0, ncols=n)
+    torch.cuda.synchronize()
+    want = _oracle(coeff, x.cpu().numpy())
+    got = y.cpu().numpy().view("<u2")
+    s0, s1 = c0 // 2, (c0 + n) // 2
+    assert np.array_equal(got[:, s0:s1], want[:, s0:s1])
+    assert (got[:, :s0] == 0x5A5A).all() and (got[:, s1:] == 0x5A5A).all()
+
+
+def test_gemm16_fp4_fused_copies_and_device_decoder():
+    """The matrix-core w = 16 decode: survivors copied in the same pass (group 0 blocks, every pass
+    its own rows), and a PatternDecoder whose plan (tables, row pointers AND bit-matrix) is built
+    on the device from the survivor list (k = 300, 40 erasures)."""
+    from gpu_rscode_amd.ops import PatternDecoder
+
+    k, n, C = 300, 340, 512 * 11 + 2 * 7
+    rs = ReedSolomon(k, n, field="gf65536", matrix="cauchy")
+    data = alloc_rows(k, C, "cuda")
+    data.copy_(_rand(k, C, 5))
+    par = rs.encode(data)
+    torch.cuda.synchronize()
+    assert np.array_equal(par.cpu().numpy().view("<u2"), _oracle(rs.E, data.cpu().numpy()))
+    g = torch.from_numpy(np.ascontiguousarray(rs.G, dtype="<u2").view(np.int16)).cuda()
+    out = alloc_rows(k, C, "cuda")
+    dec = PatternDecoder(g, [data[i] for i in range(k)] + [par[i] for i in range(n - k)], [out[i] for i in range(k)],
+                         40, engine="mfma")
+    assert dec.engine == "mfma"
+    rng = np.random.default_rng(3)
+    for _ in range(2):
+        erased = sorted(rng.choice(k, size=40, replace=False).tolist())
+        rows = [r for r in range(k) if r not in erased] + list(range(k, n))
+        rng.shuffle(rows)
+        out.fill_(0)
+        dec.rows.copy_(torch.tensor(rows, dtype=torch.int32))
+        dec.solve()
+        dec.run()
+        torch.cuda.synchronize()
+        assert int(dec.status.item()) == 0 and dec.erased.tolist() == erased
+        assert torch.equal(out, data)
