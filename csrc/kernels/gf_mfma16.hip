@@ -54,6 +54,8 @@ constexpr int kChunkBytes = 4 * kWaveBytes;  // per block and chunk
 constexpr int kDepth = 4;                  // K-steps of input in flight per lane
 constexpr int kSinkBytes16 = 64 * 1024;    // write-only sink after the bit-matrix (padding outputs)
 constexpr uint32_t kPoly16 = 0x1100Bu;
+constexpr int kRsrcWord3 = 0x00020000;  // raw buffer resource, dword 3 on gfx9 (32-bit data format)
+constexpr int kLoadNT = 2;              // cache policy of the streamed input: slc (non-temporal)
 
 __host__ __device__ constexpr int out_row_of(int r) { return 2 * ((r >> 2) & 1) + (r >> 4); }
 __host__ __device__ constexpr int out_bit_of(int r) { return ((r >> 3) & 1) * 4 + (r & 3); }
@@ -132,16 +134,18 @@ __device__ __forceinline__ void expand16(i32x4 (&bo)[2], const uint32_t (&x)[4])
   }
 }
 
-// MG: M-tiles (4 output symbol rows each) per block; UNI: input row r at in[0] + r * in_stride (else
-// the row pointers come from an LDS table); COPY: fused survivor copy; ACC: XOR into the outputs
-// (passes after the first).
+// MG: M-tiles (4 output symbol rows each) per block; UNI: input row r at in[0] + r * in_stride (4 *
+// in_stride < 2^31: the lane's row-half offset fits a 32-bit voffset), else row pointers from the
+// descriptor; COPY: fused survivor copy; ACC: XOR into the outputs (passes after the first).
+// nchunks counts whole 512-byte chunks plus, when tail_bytes > 0, one last partial chunk of that
+// many bytes (lanes past it load zeros and store nothing).
 template <int MG, bool UNI, bool COPY, bool ACC>
 __global__ __launch_bounds__(256, 1) void gf_gemm16_fp4_kernel(cptr<uint64_t> in, cptr<uint64_t> out,
                                                                cptr<uint64_t> copy, const i32x4* __restrict__ bitmat,
                                                                int k, int m, int row0, int S, int groups,
                                                                int64_t col0, int64_t nchunks, int64_t chunk_slots,
-                                                               int64_t in_stride, uint64_t sink) {
-  extern __shared__ __attribute__((aligned(16))) i32x4 afrag[];  // [S][MG][4][64] | row ptrs | copy ptrs
+                                                               int64_t in_stride, uint64_t sink, int tail_bytes) {
+  extern __shared__ __attribute__((aligned(16))) i32x4 afrag[];  // [S][MG][4][64]
   const int bid = blockIdx.x;
   const int xcd = bid & 7;
   const int local = bid >> 3;
@@ -150,20 +154,13 @@ __global__ __launch_bounds__(256, 1) void gf_gemm16_fp4_kernel(cptr<uint64_t> in
   if (slot0 >= chunk_slots) return;
   const int my_chunks = int((nchunks - slot0 + chunk_slots - 1) / chunk_slots);
   if (my_chunks <= 0) return;
-  const int nrows = 8 * S;  // this pass's input rows (row0 .. row0 + nrows - 1, clamped to k - 1)
   const size_t a_frags = size_t(S) * MG * 4 * 64;
-  uint64_t* rowptr = reinterpret_cast<uint64_t*>(afrag + a_frags);
-  uint64_t* copyptr = rowptr + nrows;
   const i32x4* src = bitmat + size_t(g) * a_frags;
   for (size_t i = threadIdx.x; i < a_frags; i += 256) afrag[i] = src[i];
-  for (int i = threadIdx.x; i < nrows; i += 256) {
-    const int r = min(row0 + i, k - 1);
-    if (!UNI) rowptr[i] = in[r];
-    if (COPY) copyptr[i] = (g == 0 && row0 + i < k) ? copy[r] : 0;
-  }
   __syncthreads();
 
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5, c = lane & 31;
+  const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
+  const int lane = threadIdx.x & 63, h = lane >> 5, c = lane & 31;
   const int scale = 0x7F7F7F7F;  // E8M0 1.0
   const int bias_scale = bias_scale_of_lane(lane);
   const i32x8 one_k0 = {h == 0 ? 0x2 : 0, 0, 0, 0, 0, 0, 0, 0};
@@ -174,12 +171,31 @@ __global__ __launch_bounds__(256, 1) void gf_gemm16_fp4_kernel(cptr<uint64_t> in
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int row = 4 * (g * MG + mt) + 2 * h + u;
-      const uint64_t o = row < m ? out[row] : 0;
-      optr[mt][u] = o;
+      optr[mt][u] = row < m ? out[row] : 0;
     }
   const uint64_t my_sink = sink + uint64_t(((bid * 4 + wave) % 256) * 256 + 4 * c);
   const uint64_t in0 = UNI ? in[0] : 0;
-  const int64_t lane_col = int64_t(wave) * kWaveBytes + 4 * c;
+  const int lane_off = wave * kWaveBytes + 4 * c;  // byte offset inside a chunk
+  const uint32_t voff = UNI ? uint32_t(int64_t(h) * 4 * in_stride) + uint32_t(4 * c) : 0u;
+  const bool has_tail = tail_bytes > 0;
+  // this lane's valid bytes (4, 2 or 0) in a chunk: 4 unless it is the last, partial one
+  const int tail_valid = min(4, max(0, tail_bytes - lane_off));
+  auto chunk_of = [&](int cc) __attribute__((always_inline)) { return slot0 + int64_t(cc) * chunk_slots; };
+  auto wave_col = [&](int cc) __attribute__((always_inline)) {  // uniform: the wave's first column
+    return col0 + chunk_of(cc) * kChunkBytes + int64_t(wave) * kWaveBytes;
+  };
+  auto partial = [&](int cc) __attribute__((always_inline)) { return has_tail && chunk_of(cc) == nchunks - 1; };
+  auto load_masked = [&](uint64_t addr, int nv) __attribute__((always_inline)) -> uint32_t {
+    if (nv == 4) return __builtin_nontemporal_load((gptr<const uint32_t>)addr);
+    if (nv == 2) return uint32_t(*(gptr<const uint16_t>)addr);
+    return 0u;
+  };
+  auto store_masked = [&](uint64_t addr, uint32_t v, int nv) __attribute__((always_inline)) {
+    if (nv == 4)
+      *(gptr<uint32_t>)addr = v;
+    else if (nv == 2)
+      *(gptr<uint16_t>)addr = uint16_t(v);
+  };
 
   f32x16 acc[MG][2][2];  // [tile][sub-block][plane]
   auto bias_init = [&]() __attribute__((always_inline)) {
@@ -196,30 +212,57 @@ __global__ __launch_bounds__(256, 1) void gf_gemm16_fp4_kernel(cptr<uint64_t> in
         }
   };
 
-  // flat step sequence over (chunk, step): load cursor (lc, ls) runs kDepth steps ahead
-  int lc = 0, ls = 0;
-  const int total_steps = my_chunks * S;
-  auto load_step = [&](uint32_t (&x)[4], int& cc, int& ss) __attribute__((always_inline)) {
-    const int64_t col = col0 + (slot0 + int64_t(cc) * chunk_slots) * kChunkBytes + lane_col;
+  // the 4 input dwords of K-step ss of chunk cc: rows row0 + 8 ss + 4h + i
+  auto load_step = [&](uint32_t (&x)[4], int cc, int ss) __attribute__((always_inline)) {
+    const int64_t wcol = wave_col(cc);
+    const int rbase = row0 + 8 * ss;
+    const bool part = partial(cc);
+    if (!part && rbase + 8 <= k) {
+      if constexpr (UNI) {  // raw buffer loads: the row base in the (uniform) resource, the lane's 32-bit offset
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int rr = 8 * ss + 4 * h + i;  // pass-relative row
-      uint64_t base;
-      if constexpr (UNI)
-        base = in0 + uint64_t(int64_t(min(row0 + rr, k - 1)) * in_stride);
-      else
-        base = rowptr[rr];
-      x[i] = __builtin_nontemporal_load((gptr<const uint32_t>)(base + uint64_t(col)));
-    }
-    if (++ss == S) {
-      ss = 0;
-      ++cc;
+        for (int i = 0; i < 4; ++i) {
+          const uint64_t sb = in0 + uint64_t(int64_t(rbase + i) * in_stride + wcol);
+          const __amdgpu_buffer_rsrc_t rs =
+              __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(sb), 0, int(0x7FFFFFFF), kRsrcWord3);
+          x[i] = __builtin_amdgcn_raw_buffer_load_b32(rs, int(voff), 0, kLoadNT);
+        }
+      } else {  // 8 uniform row pointers (scalar loads), the lane's row half selected
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const uint64_t p = h ? in[rbase + 4 + i] : in[rbase + i];
+          x[i] = __builtin_nontemporal_load((gptr<const uint32_t>)(p + uint64_t(wcol) + 4 * c));
+        }
+      }
+    } else {  // the pass's last rows (clamped to k - 1: they meet zero bit-matrix columns) / the partial chunk
+      const int nv = part ? tail_valid : 4;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = min(rbase + 4 * h + i, k - 1);
+        const uint64_t base = UNI ? in0 + uint64_t(int64_t(r) * in_stride) : in[r];
+        x[i] = load_masked(base + uint64_t(wcol) + 4 * c, nv);
+      }
     }
   };
+
+  // flat step sequence over (chunk, step): the load cursor runs kDepth steps ahead
+  const int total_steps = my_chunks * S;
+  int lc = 0, ls = 0;
   uint32_t ring[kDepth][4];
 #pragma unroll
   for (int d = 0; d < kDepth; ++d)
-    if (d < total_steps) load_step(ring[d], lc, ls);
+    if (d < total_steps) {
+      load_step(ring[d], lc, ls);
+      if (++ls == S) {
+        ls = 0;
+        ++lc;
+      }
+    }
+  i32x4 af[MG][4];
+#pragma unroll
+  for (int mt = 0; mt < MG; ++mt)
+#pragma unroll
+    for (int f = 0; f < 4; ++f) af[mt][f] = afrag[(mt * 4 + f) * 64 + lane];
+  [[maybe_unused]] uint32_t old[MG][2] = {};
 
   bias_init();
   int cc = 0, cs = 0;  // compute cursor
@@ -230,42 +273,71 @@ __global__ __launch_bounds__(256, 1) void gf_gemm16_fp4_kernel(cptr<uint64_t> in
       uint32_t x[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) x[i] = ring[d][i];
+      if (t0 + d + kDepth < total_steps) {
+        load_step(ring[d], lc, ls);
+        if (++ls == S) {
+          ls = 0;
+          ++lc;
+        }
+      }
+      const bool part = partial(cc);
+      if constexpr (ACC) {  // the previous passes' outputs of this chunk, read at its first step
+        if (cs == 0) {
+          const int64_t wcol = wave_col(cc);
+          const int nv = part ? tail_valid : 4;
+#pragma unroll
+          for (int mt = 0; mt < MG; ++mt)
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+              old[mt][u] = optr[mt][u] ? load_masked(optr[mt][u] + uint64_t(wcol) + 4 * c, nv) : 0u;
+        }
+      }
       if constexpr (COPY) {
         if (g == 0) {
-          const int64_t col = col0 + (slot0 + int64_t(cc) * chunk_slots) * kChunkBytes + lane_col;
+          const int64_t wcol = wave_col(cc);
+          const int nv = part ? tail_valid : 4;
+          const int rbase = row0 + 8 * cs + 4 * h;
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            const uint64_t cp = copyptr[8 * cs + 4 * h + i];
-            if (cp) __builtin_nontemporal_store(x[i], (gptr<uint32_t>)(cp + uint64_t(col)));
+            const uint64_t cp = rbase + i < k ? copy[rbase + i] : 0;
+            if (cp) store_masked(cp + uint64_t(wcol) + 4 * c, x[i], nv);
           }
         }
       }
-      if (t0 + d + kDepth < total_steps) load_step(ring[d], lc, ls);
-      i32x4 b0[2], b1[2];
-      expand16<0>(b0, x);
-      expand16<1>(b1, x);
-      const i32x4* as = afrag + size_t(cs) * MG * 4 * 64 + lane;
+      // the next step's A fragments under this step's MFMAs
+      const int cs_next = cs + 1 == S ? 0 : cs + 1;
+      i32x4 an[MG][4];
 #pragma unroll
-      for (int mt = 0; mt < MG; ++mt) {
-        i32x4 af[4];
+      for (int mt = 0; mt < MG; ++mt)
 #pragma unroll
-        for (int f = 0; f < 4; ++f) af[f] = as[(mt * 4 + f) * 64];
+        for (int f = 0; f < 4; ++f) an[mt][f] = afrag[((cs_next * MG + mt) * 4 + f) * 64 + lane];
+      i32x4 e[2][2];  // [sub-block][plane]
+      expand16<0>(e[0], x);
+      expand16<1>(e[1], x);
+      // all lo-plane products, then all hi-plane ones: an accumulator's two MFMAs of the step are
+      // 4 MG apart, never back to back
 #pragma unroll
-        for (int dst = 0; dst < 2; ++dst) {
-          const i32x8 a_lo = {af[dst][0], af[dst][1], af[dst][2], af[dst][3], 0, 0, 0, 0};          // src lo
-          const i32x8 a_hi = {af[2 + dst][0], af[2 + dst][1], af[2 + dst][2], af[2 + dst][3], 0, 0, 0, 0};  // src hi
-          const i32x8 bl0 = {b0[0][0], b0[0][1], b0[0][2], b0[0][3], 0, 0, 0, 0};
-          const i32x8 bh0 = {b0[1][0], b0[1][1], b0[1][2], b0[1][3], 0, 0, 0, 0};
-          const i32x8 bl1 = {b1[0][0], b1[0][1], b1[0][2], b1[0][3], 0, 0, 0, 0};
-          const i32x8 bh1 = {b1[1][0], b1[1][1], b1[1][2], b1[1][3], 0, 0, 0, 0};
-          acc[mt][0][dst] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a_lo, bl0, acc[mt][0][dst], 4, 4, 0, scale, 0, scale);
-          acc[mt][1][dst] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a_lo, bl1, acc[mt][1][dst], 4, 4, 0, scale, 0, scale);
-          acc[mt][0][dst] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a_hi, bh0, acc[mt][0][dst], 4, 4, 0, scale, 0, scale);
-          acc[mt][1][dst] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a_hi, bh1, acc[mt][1][dst], 4, 4, 0, scale, 0, scale);
-        }
-      }
+      for (int sp = 0; sp < 2; ++sp)
+#pragma unroll
+        for (int mt = 0; mt < MG; ++mt)
+#pragma unroll
+          for (int dst = 0; dst < 2; ++dst) {
+            const i32x4 a4 = af[mt][2 * sp + dst];
+            const i32x8 a = {a4[0], a4[1], a4[2], a4[3], 0, 0, 0, 0};
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+              const i32x8 b = {e[j][sp][0], e[j][sp][1], e[j][sp][2], e[j][sp][3], 0, 0, 0, 0};
+              acc[mt][j][dst] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b, acc[mt][j][dst], 4, 4, 0, scale,
+                                                                                0, scale);
+            }
+          }
+#pragma unroll
+      for (int mt = 0; mt < MG; ++mt)
+#pragma unroll
+        for (int f = 0; f < 4; ++f) af[mt][f] = an[mt][f];
       if (cs + 1 == S) {  // chunk done: pack, store, restart the accumulators
-        const int64_t col = col0 + (slot0 + int64_t(cc) * chunk_slots) * kChunkBytes + lane_col;
+        const int64_t wcol = wave_col(cc);
+        const int nv = part ? tail_valid : 4;
 #pragma unroll
         for (int mt = 0; mt < MG; ++mt) {
 #pragma unroll
@@ -281,16 +353,11 @@ __global__ __launch_bounds__(256, 1) void gf_gemm16_fp4_kernel(cptr<uint64_t> in
                 y[j][t] = v;
               }
             // (lo0, hi0, lo1, hi1)
-            const uint32_t w = __builtin_amdgcn_perm(__builtin_amdgcn_perm(y[1][1], y[1][0], 0x0c0c0400u),
-                                                     __builtin_amdgcn_perm(y[0][1], y[0][0], 0x0c0c0400u), 0x05040100u);
+            uint32_t w = __builtin_amdgcn_perm(__builtin_amdgcn_perm(y[1][1], y[1][0], 0x0c0c0400u),
+                                               __builtin_amdgcn_perm(y[0][1], y[0][0], 0x0c0c0400u), 0x05040100u);
+            if constexpr (ACC) w ^= old[mt][u];
             const uint64_t o = optr[mt][u];
-            gptr<uint32_t> dstp = (gptr<uint32_t>)(o ? o + uint64_t(col) : my_sink);
-            if constexpr (ACC) {
-              const uint32_t old = o ? *dstp : 0u;
-              *dstp = old ^ w;
-            } else {
-              *dstp = w;
-            }
+            store_masked(o ? o + uint64_t(wcol) + 4 * c : my_sink, w, o ? nv : 4);
           }
         }
         bias_init();
@@ -329,16 +396,14 @@ Geo16 geometry16(int k, int m, int mg_cap, bool copy) {
     if (forced) break;
   }
   constexpr size_t kLds = 152 * 1024;
-  auto fit_steps = [&](int mg) {
-    // per K-step: A (mg x 4 KiB) + 8 row pointers (+ 8 copy pointers)
-    return int(kLds / (size_t(mg) * 4096 + 64 + (copy ? 64 : 0)));
-  };
+  auto fit_steps = [&](int mg) { return int(kLds / (size_t(mg) * 4096)); };  // per K-step: A (mg x 4 KiB)
   while (g.mg > 1 && fit_steps(g.mg) < 1) g.mg >>= 1;
   const int smax = std::max(1, fit_steps(g.mg));
   g.passes = (g.ksteps + smax - 1) / smax;
   g.S = (g.ksteps + g.passes - 1) / g.passes;
   g.groups = (g.mtiles + g.mg - 1) / g.mg;
-  g.lds = size_t(g.S) * g.mg * 4096 + size_t(8 * g.S) * 8 * (copy ? 2 : 1);
+  g.lds = size_t(g.S) * g.mg * 4096;
+  (void)copy;
   return g;
 }
 
@@ -347,7 +412,7 @@ size_t bitmat16_matrix_bytes(const Geo16& g) { return size_t(g.passes) * g.group
 template <int MG, bool UNI, bool COPY, bool ACC>
 hipError_t launch16_pass(const Geo16& geo, cptr<uint64_t> in, cptr<uint64_t> out, cptr<uint64_t> copy,
                          const uint8_t* bitmat, int k, int m, int pass, int64_t col0, int64_t nchunks, int64_t in_stride,
-                         uint64_t sink, hipStream_t stream) {
+                         uint64_t sink, int tail, hipStream_t stream) {
   const void* f = reinterpret_cast<const void*>(&gf_gemm16_fp4_kernel<MG, UNI, COPY, ACC>);
   hipError_t e = ensure_lds_optin(f);
   if (e != hipSuccess) return e;
@@ -362,29 +427,29 @@ hipError_t launch16_pass(const Geo16& geo, cptr<uint64_t> in, cptr<uint64_t> out
   const unsigned blocks = unsigned(slots * geo.groups);
   const i32x4* bm = reinterpret_cast<const i32x4*>(bitmat) + size_t(pass) * geo.groups * geo.S * MG * 4 * 64;
   gf_gemm16_fp4_kernel<MG, UNI, COPY, ACC><<<blocks, 256, geo.lds, stream>>>(
-      in, out, copy, bm, k, m, pass * 8 * geo.S, geo.S, geo.groups, col0, nchunks, slots, in_stride, sink);
+      in, out, copy, bm, k, m, pass * 8 * geo.S, geo.S, geo.groups, col0, nchunks, slots, in_stride, sink, tail);
   return hipGetLastError();
 }
 
 template <int MG>
 hipError_t launch16_mg(const Geo16& geo, cptr<uint64_t> in, cptr<uint64_t> out, cptr<uint64_t> copy,
                        const uint8_t* bitmat, int k, int m, int64_t col0, int64_t nchunks, int64_t in_stride,
-                       uint64_t sink, hipStream_t stream) {
+                       uint64_t sink, int tail, hipStream_t stream) {
   for (int p = 0; p < geo.passes; ++p) {
     hipError_t e;
     const bool acc = p > 0;
     if (copy) {
-      e = acc ? launch16_pass<MG, false, true, true>(geo, in, out, copy, bitmat, k, m, p, col0, nchunks, 0, sink, stream)
-              : launch16_pass<MG, false, true, false>(geo, in, out, copy, bitmat, k, m, p, col0, nchunks, 0, sink, stream);
+      e = acc ? launch16_pass<MG, false, true, true>(geo, in, out, copy, bitmat, k, m, p, col0, nchunks, 0, sink, tail, stream)
+              : launch16_pass<MG, false, true, false>(geo, in, out, copy, bitmat, k, m, p, col0, nchunks, 0, sink, tail, stream);
     } else if (in_stride) {
       e = acc ? launch16_pass<MG, true, false, true>(geo, in, out, copy, bitmat, k, m, p, col0, nchunks, in_stride, sink,
-                                                     stream)
+                                                     tail, stream)
               : launch16_pass<MG, true, false, false>(geo, in, out, copy, bitmat, k, m, p, col0, nchunks, in_stride, sink,
-                                                      stream);
+                                                      tail, stream);
     } else {
-      e = acc ? launch16_pass<MG, false, false, true>(geo, in, out, copy, bitmat, k, m, p, col0, nchunks, 0, sink, stream)
+      e = acc ? launch16_pass<MG, false, false, true>(geo, in, out, copy, bitmat, k, m, p, col0, nchunks, 0, sink, tail, stream)
               : launch16_pass<MG, false, false, false>(geo, in, out, copy, bitmat, k, m, p, col0, nchunks, 0, sink,
-                                                       stream);
+                                                       tail, stream);
     }
     if (e != hipSuccess) return e;
   }
@@ -414,25 +479,28 @@ hipError_t launch_gf_gemm16_fp4(const void* bitmat, const void* desc, int k, int
   const int m_pad = pad_m(m);
   const DescLayout l = desc_layout16(k, m_pad);
   const char* b = static_cast<const char*>(desc);
-  // (the bitmat is built for the copy geometry, whose pointer tables the LDS budget always includes)
   const Geo16 geo = geometry16(k, m, mg_cap, true);
-  const int64_t nchunks = (col0 & 3) ? 0 : ncols / kChunkBytes;
+  // whole 512-byte chunks plus the ragged rest as one partial chunk, all on the matrix cores (a
+  // start off a 4-byte boundary: the v_perm records)
+  const int64_t full = (col0 & 3) ? 0 : ncols / kChunkBytes;
+  const int tail = (col0 & 3) ? 0 : int(ncols % kChunkBytes);
+  const int64_t nchunks = full + (tail ? 1 : 0);
   if (nchunks > 0) {
     cptr<uint64_t> in = (cptr<uint64_t>)(b + l.in_off);
     cptr<uint64_t> out = (cptr<uint64_t>)(b + l.out_off);
     cptr<uint64_t> copy = copies ? (cptr<uint64_t>)(b + l.copy_off) : nullptr;
     const uint64_t sink = reinterpret_cast<uint64_t>(bitmat) + bitmat16_matrix_bytes(geo);
     const auto* bm = static_cast<const uint8_t*>(bitmat);
-    const int64_t stride = copies ? 0 : in_stride;
+    // uniform-stride inputs address rows as row base + 32-bit lane offset (4 rows apart at most)
+    const int64_t stride = (copies || in_stride <= 0 || in_stride >= (int64_t(1) << 29)) ? 0 : in_stride;
     hipError_t e;
     switch (geo.mg) {
-      case 2: e = launch16_mg<2>(geo, in, out, copy, bm, k, m, col0, nchunks, stride, sink, stream); break;
-      default: e = launch16_mg<1>(geo, in, out, copy, bm, k, m, col0, nchunks, stride, sink, stream); break;
+      case 2: e = launch16_mg<2>(geo, in, out, copy, bm, k, m, col0, nchunks, stride, sink, tail, stream); break;
+      default: e = launch16_mg<1>(geo, in, out, copy, bm, k, m, col0, nchunks, stride, sink, tail, stream); break;
     }
-    if (e != hipSuccess) return e;
+    return e;
   }
-  const int64_t done = nchunks * kChunkBytes;
-  if (done < ncols) return launch_gf_gemm16(desc, k, m_pad, col0 + done, ncols - done, false, 0, stream);
+  if (ncols > 0) return launch_gf_gemm16(desc, k, m_pad, col0, ncols, false, 0, stream);
   return hipSuccess;
 }
 

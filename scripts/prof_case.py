@@ -29,8 +29,10 @@ def main():
     ap.add_argument("--pf", type=int, default=2)
     ap.add_argument("--nt", type=int, default=1)
     ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--field", type=int, default=8, choices=[8, 16], help="16: a GF(2^16) plan (Gemm16Plan)")
     a = ap.parse_args()
     C = (a.bytes + a.k - 1) // a.k
+    C += C % 2 if a.field == 16 else 0
     data = alloc_rows(a.k, C, "cuda")
     fill_random_(flat_rows(data), seed=1)
     out = alloc_rows(a.m, C, "cuda")
@@ -38,9 +40,16 @@ def main():
     if a.copies:
         dst = alloc_rows(a.copies, C, "cuda")
         copies = [dst[j] if j < a.copies else None for j in range(a.k)]
-    coeff = np.random.default_rng(0).integers(1, 256, size=(a.m, a.k), dtype=np.uint8)
-    plan = GemmPlan(data, out, coeff, copies=copies, engine=a.engine)
-    kw = {} if a.vec is None else dict(vec=a.vec, pf=a.pf, nt=bool(a.nt))
+    if a.field == 16:
+        from gpu_rscode_amd.ops import Gemm16Plan
+
+        coeff = np.random.default_rng(0).integers(1, 65536, size=(a.m, a.k))
+        plan = Gemm16Plan(data, out, coeff, copies=copies, engine=a.engine)
+        kw = {}
+    else:
+        coeff = np.random.default_rng(0).integers(1, 256, size=(a.m, a.k), dtype=np.uint8)
+        plan = GemmPlan(data, out, coeff, copies=copies, engine=a.engine)
+        kw = {} if a.vec is None else dict(vec=a.vec, pf=a.pf, nt=bool(a.nt))
     for _ in range(a.iters):
         plan.run(**kw)
     torch.cuda.synchronize()
