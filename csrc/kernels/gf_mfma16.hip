@@ -25,9 +25,12 @@
 // its M-tile group's A slice (S x MG x 4 KiB) in LDS for all of its chunks; the group's blocks of
 // one chunk share an XCD (the input re-read per group is an L2 hit).
 //
-// Input rows stream through registers (4 dword loads per lane and K-step, D steps in flight
-// across chunk boundaries); rows past k are clamped to row k-1 and meet zero bit-matrix columns.
-// Fused survivor copies (decode): group 0's blocks also store the raw dwords of their rows.
+// Input rows stream through registers (4 dword loads per lane and K-step, kDepth steps in flight
+// across chunk boundaries); rows past k read zeros (buffer bounds) or are clamped to row k-1, and
+// meet zero bit-matrix columns either way. Eight waves per block (two per SIMD) share the A slice:
+// one wave's bookkeeping and load waits issue under the other's MFMAs. Fused survivor copies
+// (decode): the store of K-step s's raw dwords goes to group s mod groups, so no group's blocks
+// carry all of them.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -49,8 +52,10 @@ using cptr = const __attribute__((address_space(4))) T*;
 template <typename T>
 using gptr = __attribute__((address_space(1))) T*;
 
-constexpr int kWaveBytes = 128;            // byte columns per wave: 64 symbols (2 per lane)
-constexpr int kChunkBytes = 4 * kWaveBytes;  // per block and chunk
+constexpr int kWaveBytes = 128;  // byte columns per wave: 64 symbols (2 per lane)
+constexpr int kWaves = 8;        // per block: two per SIMD, sharing the LDS A slice
+constexpr int kThreads = 64 * kWaves;
+constexpr int kChunkBytes = kWaves * kWaveBytes;  // per block and chunk
 constexpr int kDepth = 4;                  // K-steps of input in flight per lane
 constexpr int kSinkBytes16 = 64 * 1024;    // write-only sink after the bit-matrix (padding outputs)
 constexpr uint32_t kPoly16 = 0x1100Bu;
@@ -115,6 +120,14 @@ __device__ __forceinline__ uint32_t bfi(uint32_t mask, uint32_t a, uint32_t b) {
   asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "s"(mask), "v"(a), "v"(b));
   return r;
 }
+// The epilogue's v_bfi (inline asm) reads accumulator VGPRs, and the compiler's hazard recognizer
+// does not look into inline asm: nothing crosses this point, and the last 16-pass MFMA gets its
+// wait states before the first read (scripts/mfma_hazard_check.py lints the emitted code).
+__device__ __forceinline__ void mfma_result_fence() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7");
+  __builtin_amdgcn_sched_barrier(0);
+}
 __device__ __forceinline__ int bias_scale_of_lane(int lane) { return 127 + 23 - out_bit_of(lane & 31); }
 
 // B operands of sub-block j (symbol 2c + j) from the 4 rows' dwords: bytes 2j (lo) and 2j + 1 (hi)
@@ -134,17 +147,24 @@ __device__ __forceinline__ void expand16(i32x4 (&bo)[2], const uint32_t (&x)[4])
   }
 }
 
-// MG: M-tiles (4 output symbol rows each) per block; UNI: input row r at in[0] + r * in_stride (4 *
-// in_stride < 2^31: the lane's row-half offset fits a 32-bit voffset), else row pointers from the
-// descriptor; COPY: fused survivor copy; ACC: XOR into the outputs (passes after the first).
-// nchunks counts whole 512-byte chunks plus, when tail_bytes > 0, one last partial chunk of that
-// many bytes (lanes past it load zeros and store nothing).
+// MG: M-tiles (4 output symbol rows each) per block; UNI: input row r at in[0] + r * in_stride (8 *
+// in_stride <= 2^31: a lane's rows sit at 32-bit offsets from the step's first row), else row
+// pointers from the descriptor (columns below 2^32); COPY: fused survivor copies; ACC: XOR into the
+// outputs (passes after the first). nchunks counts whole chunks plus, when tail_bytes > 0, one last
+// partial chunk of that many bytes (lanes past it load zeros and store nothing).
+//
+// Issue budget. A wave's step is 8 MG MFMAs (32 cycles each); with two waves per SIMD every
+// instruction the step issues besides them costs issue slots, so the per-step bookkeeping is a few
+// scalar adds on uniform cursors (no 64-bit multiplies, one buffer resource per step), the
+// bounds of the pass's last rows come from the resource's num_records (rows past k read zeros),
+// and only the partial chunk takes the per-lane masked path.
 template <int MG, bool UNI, bool COPY, bool ACC>
-__global__ __launch_bounds__(256, 1) void gf_gemm16_fp4_kernel(cptr<uint64_t> in, cptr<uint64_t> out,
-                                                               cptr<uint64_t> copy, const i32x4* __restrict__ bitmat,
-                                                               int k, int m, int row0, int S, int groups,
-                                                               int64_t col0, int64_t nchunks, int64_t chunk_slots,
-                                                               int64_t in_stride, uint64_t sink, int tail_bytes) {
+__global__ __launch_bounds__(kThreads, 1) void gf_gemm16_fp4_kernel(cptr<uint64_t> in, cptr<uint64_t> out,
+                                                                    cptr<uint64_t> copy,
+                                                                    const i32x4* __restrict__ bitmat, int k, int m,
+                                                                    int row0, int S, int groups, int64_t col0,
+                                                                    int64_t nchunks, int64_t chunk_slots,
+                                                                    int64_t in_stride, uint64_t sink, int tail_bytes) {
   extern __shared__ __attribute__((aligned(16))) i32x4 afrag[];  // [S][MG][4][64]
   const int bid = blockIdx.x;
   const int xcd = bid & 7;
@@ -156,7 +176,7 @@ __global__ __launch_bounds__(256, 1) void gf_gemm16_fp4_kernel(cptr<uint64_t> in
   if (my_chunks <= 0) return;
   const size_t a_frags = size_t(S) * MG * 4 * 64;
   const i32x4* src = bitmat + size_t(g) * a_frags;
-  for (size_t i = threadIdx.x; i < a_frags; i += 256) afrag[i] = src[i];
+  for (size_t i = threadIdx.x; i < a_frags; i += kThreads) afrag[i] = src[i];
   __syncthreads();
 
   const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
@@ -173,18 +193,20 @@ __global__ __launch_bounds__(256, 1) void gf_gemm16_fp4_kernel(cptr<uint64_t> in
       const int row = 4 * (g * MG + mt) + 2 * h + u;
       optr[mt][u] = row < m ? out[row] : 0;
     }
-  const uint64_t my_sink = sink + uint64_t(((bid * 4 + wave) % 256) * 256 + 4 * c);
+  const uint64_t my_sink = sink + uint64_t(((bid * kWaves + wave) % 256) * 256 + 4 * c);
   const uint64_t in0 = UNI ? in[0] : 0;
   const int lane_off = wave * kWaveBytes + 4 * c;  // byte offset inside a chunk
-  const uint32_t voff = UNI ? uint32_t(int64_t(h) * 4 * in_stride) + uint32_t(4 * c) : 0u;
-  const bool has_tail = tail_bytes > 0;
-  // this lane's valid bytes (4, 2 or 0) in a chunk: 4 unless it is the last, partial one
+  // this lane's valid bytes (4, 2 or 0) in the partial chunk
   const int tail_valid = min(4, max(0, tail_bytes - lane_off));
-  auto chunk_of = [&](int cc) __attribute__((always_inline)) { return slot0 + int64_t(cc) * chunk_slots; };
-  auto wave_col = [&](int cc) __attribute__((always_inline)) {  // uniform: the wave's first column
-    return col0 + chunk_of(cc) * kChunkBytes + int64_t(wave) * kWaveBytes;
-  };
-  auto partial = [&](int cc) __attribute__((always_inline)) { return has_tail && chunk_of(cc) == nchunks - 1; };
+  // the partial chunk's index among this block's chunks (-1: none of them)
+  const int part_rel =
+      (tail_bytes > 0 && (nchunks - 1 - slot0) % chunk_slots == 0) ? int((nchunks - 1 - slot0) / chunk_slots) : -1;
+  const int64_t chunk_step = chunk_slots * kChunkBytes;  // column advance between this block's chunks
+  const int64_t wave_col0 = col0 + slot0 * kChunkBytes + int64_t(wave) * kWaveBytes;
+  // UNI: the lane's 4 rows as 32-bit offsets from the step's first row
+  uint32_t voff[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) voff[i] = uint32_t((4 * h + i) * in_stride) + uint32_t(4 * c);
   auto load_masked = [&](uint64_t addr, int nv) __attribute__((always_inline)) -> uint32_t {
     if (nv == 4) return __builtin_nontemporal_load((gptr<const uint32_t>)addr);
     if (nv == 2) return uint32_t(*(gptr<const uint16_t>)addr);
@@ -212,160 +234,183 @@ __global__ __launch_bounds__(256, 1) void gf_gemm16_fp4_kernel(cptr<uint64_t> in
         }
   };
 
-  // the 4 input dwords of K-step ss of chunk cc: rows row0 + 8 ss + 4h + i
-  auto load_step = [&](uint32_t (&x)[4], int cc, int ss) __attribute__((always_inline)) {
-    const int64_t wcol = wave_col(cc);
-    const int rbase = row0 + 8 * ss;
-    const bool part = partial(cc);
-    if (!part && rbase + 8 <= k) {
-      if constexpr (UNI) {  // raw buffer loads: the row base in the (uniform) resource, the lane's 32-bit offset
+  // The block's whole chunks run through a software pipeline whose loads never sit in a branch
+  // (a conditional load makes the ring slots merge values, and every merge copy waits for all
+  // loads in flight): loads past the last whole chunk read zeros (UNI: num_records 0) or the sink.
+  // The partial chunk, if the block has it (always its last), follows with per-lane masked loads.
+  const int my_full = my_chunks - (part_rel >= 0 ? 1 : 0);
+  constexpr int RW = UNI ? 4 : 8;  // ring dwords per step (pointer inputs: both row halves)
+  // load cursor (uniform): chunk lc, step ls; rows row0 + 8 ls + 4h + i; UNI: lbase = the step's
+  // first row at the wave's column
+  int lc = 0, ls = 0;
+  int64_t lcol = wave_col0;
+  uint64_t lbase = UNI ? in0 + uint64_t(int64_t(row0) * in_stride + lcol) : 0;
+  const uint64_t step_bytes = UNI ? uint64_t(8 * in_stride) : 0;
+  auto load_step = [&](uint32_t (&x)[RW]) __attribute__((always_inline)) {
+    const int rbase = row0 + 8 * ls;
+    const bool live = lc < my_full;
+    if constexpr (UNI) {  // one raw buffer resource; rows past k fall outside num_records and read 0
+      // (readfirstlane: the resource is provably uniform, no waterfall)
+      const int rem = live ? k - rbase : 0;
+      const int nrec = __builtin_amdgcn_readfirstlane(
+          rem >= 8 ? int(uint32_t(8) * uint32_t(in_stride)) : rem > 0 ? int(uint32_t(rem) * uint32_t(in_stride)) : 0);
+      const uint64_t b = (uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(int(lbase >> 32)))) << 32) |
+                         uint32_t(__builtin_amdgcn_readfirstlane(int(uint32_t(lbase))));
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(b), 0, nrec, kRsrcWord3);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const uint64_t sb = in0 + uint64_t(int64_t(rbase + i) * in_stride + wcol);
-          const __amdgpu_buffer_rsrc_t rs =
-              __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(sb), 0, int(0x7FFFFFFF), kRsrcWord3);
-          x[i] = __builtin_amdgcn_raw_buffer_load_b32(rs, int(voff), 0, kLoadNT);
-        }
-      } else {  // 8 uniform row pointers (scalar loads), the lane's row half selected
+      for (int i = 0; i < 4; ++i) x[i] = __builtin_amdgcn_raw_buffer_load_b32(rs, int(voff[i]), 0, kLoadNT);
+      lbase += step_bytes;
+    } else {  // 8 uniform row pointers, each row read by the whole wave (both halves kept)
+      uint64_t p[8];
+      if (rbase + 8 <= k) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const uint64_t p = h ? in[rbase + 4 + i] : in[rbase + i];
-          x[i] = __builtin_nontemporal_load((gptr<const uint32_t>)(p + uint64_t(wcol) + 4 * c));
-        }
+        for (int j = 0; j < 8; ++j) p[j] = in[rbase + j];
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) p[j] = in[min(rbase + j, k - 1)];
       }
-    } else {  // the pass's last rows (clamped to k - 1: they meet zero bit-matrix columns) / the partial chunk
-      const int nv = part ? tail_valid : 4;
+      const uint32_t vo = uint32_t(live ? lcol : 0) + uint32_t(4 * c);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int r = min(rbase + 4 * h + i, k - 1);
-        const uint64_t base = UNI ? in0 + uint64_t(int64_t(r) * in_stride) : in[r];
-        x[i] = load_masked(base + uint64_t(wcol) + 4 * c, nv);
-      }
+      for (int j = 0; j < 8; ++j)
+        x[j] = __builtin_nontemporal_load((gptr<const uint32_t>)((live ? p[j] : sink) + vo));
+    }
+    if (++ls == S) {
+      ls = 0;
+      ++lc;
+      lcol += chunk_step;
+      if constexpr (UNI) lbase = in0 + uint64_t(int64_t(row0) * in_stride + lcol);
     }
   };
 
-  // flat step sequence over (chunk, step): the load cursor runs kDepth steps ahead
-  const int total_steps = my_chunks * S;
-  int lc = 0, ls = 0;
-  uint32_t ring[kDepth][4];
-#pragma unroll
-  for (int d = 0; d < kDepth; ++d)
-    if (d < total_steps) {
-      load_step(ring[d], lc, ls);
-      if (++ls == S) {
-        ls = 0;
-        ++lc;
-      }
-    }
-  i32x4 af[MG][4];
-#pragma unroll
-  for (int mt = 0; mt < MG; ++mt)
-#pragma unroll
-    for (int f = 0; f < 4; ++f) af[mt][f] = afrag[(mt * 4 + f) * 64 + lane];
+  // compute cursor (uniform): chunk cc, step cs, wave column ccol
+  int cc = 0, cs = 0;
+  int64_t ccol = wave_col0;
+  [[maybe_unused]] int cturn = 0;  // COPY: this group stores step cs's copies when cturn == g
   [[maybe_unused]] uint32_t old[MG][2] = {};
+  auto chunk_start = [&]() __attribute__((always_inline)) {
+    if constexpr (ACC) {  // the previous passes' outputs of the chunk, read S steps ahead of their use
+      const bool live = cc < my_full;
+#pragma unroll
+      for (int mt = 0; mt < MG; ++mt)
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const uint64_t o = optr[mt][u];
+          old[mt][u] = __builtin_nontemporal_load((gptr<const uint32_t>)(live && o ? o + uint64_t(ccol) + 4 * c : my_sink));
+        }
+    }
+    if constexpr (COPY) cturn = 0;
+  };
+  // one K-step on the 4 input dwords x (nv: the lane's valid bytes of the chunk, for the stores)
+  auto consume = [&](const uint32_t (&x)[4], int nv) __attribute__((always_inline)) {
+    i32x4 af[MG][4];
+#pragma unroll
+    for (int mt = 0; mt < MG; ++mt)
+#pragma unroll
+      for (int f = 0; f < 4; ++f) af[mt][f] = afrag[((cs * MG + mt) * 4 + f) * 64 + lane];
+    if constexpr (COPY) {  // the steps' survivor copies, spread round-robin over the groups
+      if (cturn == g) {
+        const int rbase = row0 + 8 * cs;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const uint64_t c0 = rbase + i < k ? copy[rbase + i] : 0;
+          const uint64_t c1 = rbase + 4 + i < k ? copy[rbase + 4 + i] : 0;
+          const uint64_t cb = h ? c1 : c0;
+          if (cb) store_masked(cb + uint64_t(ccol) + 4 * c, x[i], nv);
+        }
+      }
+      cturn = cturn + 1 == groups ? 0 : cturn + 1;
+    }
+    i32x4 e[2][2];  // [sub-block][plane]
+    expand16<0>(e[0], x);
+    expand16<1>(e[1], x);
+    // all lo-plane products, then all hi-plane ones: an accumulator's two MFMAs of the step are
+    // 4 MG apart, never back to back
+#pragma unroll
+    for (int sp = 0; sp < 2; ++sp)
+#pragma unroll
+      for (int mt = 0; mt < MG; ++mt)
+#pragma unroll
+        for (int dst = 0; dst < 2; ++dst) {
+          const i32x4 a4 = af[mt][2 * sp + dst];
+          const i32x8 a = {a4[0], a4[1], a4[2], a4[3], 0, 0, 0, 0};
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const i32x8 b = {e[j][sp][0], e[j][sp][1], e[j][sp][2], e[j][sp][3], 0, 0, 0, 0};
+            acc[mt][j][dst] =
+                __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b, acc[mt][j][dst], 4, 4, 0, scale, 0, scale);
+          }
+        }
+    if (++cs == S) {  // chunk done: pack, store, restart the accumulators
+      mfma_result_fence();
+#pragma unroll
+      for (int mt = 0; mt < MG; ++mt) {
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          uint32_t y[2][2];  // [sub-block][plane]: the byte in bits 0..7
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+              uint32_t v = __float_as_uint(acc[mt][j][t][8 * u]);
+#pragma unroll
+              for (int b = 1; b < 8; ++b) v = bfi(1u << b, __float_as_uint(acc[mt][j][t][8 * u + b]), v);
+              y[j][t] = v;
+            }
+          // (lo0, hi0, lo1, hi1)
+          uint32_t w = __builtin_amdgcn_perm(__builtin_amdgcn_perm(y[1][1], y[1][0], 0x0c0c0400u),
+                                             __builtin_amdgcn_perm(y[0][1], y[0][0], 0x0c0c0400u), 0x05040100u);
+          if constexpr (ACC) w ^= old[mt][u];
+          const uint64_t o = optr[mt][u];
+          store_masked(o ? o + uint64_t(ccol) + 4 * c : my_sink, w, o ? nv : 4);
+        }
+      }
+      bias_init();
+      cs = 0;
+      ++cc;
+      ccol += chunk_step;
+      chunk_start();
+    }
+  };
 
   bias_init();
-  int cc = 0, cs = 0;  // compute cursor
+  chunk_start();
+  const int total_steps = my_full * S;
+  uint32_t ring[kDepth][RW];
+#pragma unroll
+  for (int d = 0; d < kDepth; ++d) load_step(ring[d]);
   for (int t0 = 0; t0 < total_steps; t0 += kDepth) {
 #pragma unroll
     for (int d = 0; d < kDepth; ++d) {
       if (t0 + d >= total_steps) break;  // (uniform)
       uint32_t x[4];
+      if constexpr (UNI) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) x[i] = ring[d][i];
-      if (t0 + d + kDepth < total_steps) {
-        load_step(ring[d], lc, ls);
-        if (++ls == S) {
-          ls = 0;
-          ++lc;
-        }
-      }
-      const bool part = partial(cc);
-      if constexpr (ACC) {  // the previous passes' outputs of this chunk, read at its first step
-        if (cs == 0) {
-          const int64_t wcol = wave_col(cc);
-          const int nv = part ? tail_valid : 4;
-#pragma unroll
-          for (int mt = 0; mt < MG; ++mt)
-#pragma unroll
-            for (int u = 0; u < 2; ++u)
-              old[mt][u] = optr[mt][u] ? load_masked(optr[mt][u] + uint64_t(wcol) + 4 * c, nv) : 0u;
-        }
-      }
-      if constexpr (COPY) {
-        if (g == 0) {
-          const int64_t wcol = wave_col(cc);
-          const int nv = part ? tail_valid : 4;
-          const int rbase = row0 + 8 * cs + 4 * h;
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const uint64_t cp = rbase + i < k ? copy[rbase + i] : 0;
-            if (cp) store_masked(cp + uint64_t(wcol) + 4 * c, x[i], nv);
-          }
-        }
-      }
-      // the next step's A fragments under this step's MFMAs
-      const int cs_next = cs + 1 == S ? 0 : cs + 1;
-      i32x4 an[MG][4];
-#pragma unroll
-      for (int mt = 0; mt < MG; ++mt)
-#pragma unroll
-        for (int f = 0; f < 4; ++f) an[mt][f] = afrag[((cs_next * MG + mt) * 4 + f) * 64 + lane];
-      i32x4 e[2][2];  // [sub-block][plane]
-      expand16<0>(e[0], x);
-      expand16<1>(e[1], x);
-      // all lo-plane products, then all hi-plane ones: an accumulator's two MFMAs of the step are
-      // 4 MG apart, never back to back
-#pragma unroll
-      for (int sp = 0; sp < 2; ++sp)
-#pragma unroll
-        for (int mt = 0; mt < MG; ++mt)
-#pragma unroll
-          for (int dst = 0; dst < 2; ++dst) {
-            const i32x4 a4 = af[mt][2 * sp + dst];
-            const i32x8 a = {a4[0], a4[1], a4[2], a4[3], 0, 0, 0, 0};
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-              const i32x8 b = {e[j][sp][0], e[j][sp][1], e[j][sp][2], e[j][sp][3], 0, 0, 0, 0};
-              acc[mt][j][dst] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b, acc[mt][j][dst], 4, 4, 0, scale,
-                                                                                0, scale);
-            }
-          }
-#pragma unroll
-      for (int mt = 0; mt < MG; ++mt)
-#pragma unroll
-        for (int f = 0; f < 4; ++f) af[mt][f] = an[mt][f];
-      if (cs + 1 == S) {  // chunk done: pack, store, restart the accumulators
-        const int64_t wcol = wave_col(cc);
-        const int nv = part ? tail_valid : 4;
-#pragma unroll
-        for (int mt = 0; mt < MG; ++mt) {
-#pragma unroll
-          for (int u = 0; u < 2; ++u) {
-            uint32_t y[2][2];  // [sub-block][plane]: the byte in bits 0..7
-#pragma unroll
-            for (int j = 0; j < 2; ++j)
-#pragma unroll
-              for (int t = 0; t < 2; ++t) {
-                uint32_t v = __float_as_uint(acc[mt][j][t][8 * u]);
-#pragma unroll
-                for (int b = 1; b < 8; ++b) v = bfi(1u << b, __float_as_uint(acc[mt][j][t][8 * u + b]), v);
-                y[j][t] = v;
-              }
-            // (lo0, hi0, lo1, hi1)
-            uint32_t w = __builtin_amdgcn_perm(__builtin_amdgcn_perm(y[1][1], y[1][0], 0x0c0c0400u),
-                                               __builtin_amdgcn_perm(y[0][1], y[0][0], 0x0c0c0400u), 0x05040100u);
-            if constexpr (ACC) w ^= old[mt][u];
-            const uint64_t o = optr[mt][u];
-            store_masked(o ? o + uint64_t(wcol) + 4 * c : my_sink, w, o ? nv : 4);
-          }
-        }
-        bias_init();
-        cs = 0;
-        ++cc;
+        for (int i = 0; i < 4; ++i) x[i] = ring[d][i];
       } else {
-        ++cs;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) x[i] = h ? ring[d][4 + i] : ring[d][i];
       }
+      load_step(ring[d]);  // kDepth steps ahead (past the whole chunks: zeros / the sink)
+      consume(x, 4);
+    }
+  }
+  if (part_rel >= 0) {  // the partial chunk (cc == my_full): per-lane masked loads, no pipeline
+    if constexpr (ACC) {
+#pragma unroll
+      for (int mt = 0; mt < MG; ++mt)
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+          old[mt][u] = optr[mt][u] ? load_masked(optr[mt][u] + uint64_t(ccol) + 4 * c, tail_valid) : 0u;
+    }
+    for (int s = 0; s < S; ++s) {
+      uint32_t x[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = min(row0 + 8 * s + 4 * h + i, k - 1);  // rows past k meet zero bit-matrix columns
+        const uint64_t base = UNI ? in0 + uint64_t(int64_t(r) * in_stride) : in[r];
+        x[i] = load_masked(base + uint64_t(ccol) + 4 * c, tail_valid);
+      }
+      consume(x, tail_valid);
     }
   }
 }
@@ -419,14 +464,14 @@ hipError_t launch16_pass(const Geo16& geo, cptr<uint64_t> in, cptr<uint64_t> out
   static DeviceMemo<size_t, int> occ_memo;
   const int occ = occ_memo.get_or(geo.lds, [&] {
     int o = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, f, 256, geo.lds) != hipSuccess) o = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, f, kThreads, geo.lds) != hipSuccess) o = 0;
     return o;
   });
   if (occ <= 0) return hipErrorInvalidConfiguration;
   const int64_t slots = persistent_slots(std::min(occ, 4), geo.groups, nchunks);
   const unsigned blocks = unsigned(slots * geo.groups);
   const i32x4* bm = reinterpret_cast<const i32x4*>(bitmat) + size_t(pass) * geo.groups * geo.S * MG * 4 * 64;
-  gf_gemm16_fp4_kernel<MG, UNI, COPY, ACC><<<blocks, 256, geo.lds, stream>>>(
+  gf_gemm16_fp4_kernel<MG, UNI, COPY, ACC><<<blocks, kThreads, geo.lds, stream>>>(
       in, out, copy, bm, k, m, pass * 8 * geo.S, geo.S, geo.groups, col0, nchunks, slots, in_stride, sink, tail);
   return hipGetLastError();
 }
@@ -480,7 +525,7 @@ hipError_t launch_gf_gemm16_fp4(const void* bitmat, const void* desc, int k, int
   const DescLayout l = desc_layout16(k, m_pad);
   const char* b = static_cast<const char*>(desc);
   const Geo16 geo = geometry16(k, m, mg_cap, true);
-  // whole 512-byte chunks plus the ragged rest as one partial chunk, all on the matrix cores (a
+  // whole chunks plus the ragged rest as one partial chunk, all on the matrix cores (a
   // start off a 4-byte boundary: the v_perm records)
   const int64_t full = (col0 & 3) ? 0 : ncols / kChunkBytes;
   const int tail = (col0 & 3) ? 0 : int(ncols % kChunkBytes);
@@ -491,8 +536,11 @@ hipError_t launch_gf_gemm16_fp4(const void* bitmat, const void* desc, int k, int
     cptr<uint64_t> copy = copies ? (cptr<uint64_t>)(b + l.copy_off) : nullptr;
     const uint64_t sink = reinterpret_cast<uint64_t>(bitmat) + bitmat16_matrix_bytes(geo);
     const auto* bm = static_cast<const uint8_t*>(bitmat);
-    // uniform-stride inputs address rows as row base + 32-bit lane offset (4 rows apart at most)
-    const int64_t stride = (copies || in_stride <= 0 || in_stride >= (int64_t(1) << 29)) ? 0 : in_stride;
+    // uniform-stride inputs address rows as the step's first row + 32-bit lane offsets (8 rows);
+    // pointer inputs as row pointer + 32-bit column
+    const int64_t stride = (copies || in_stride <= 0 || in_stride > (int64_t(1) << 28)) ? 0 : in_stride;
+    if (!stride && col0 + ncols + kChunkBytes > (int64_t(1) << 32))
+      return launch_gf_gemm16(desc, k, m_pad, col0, ncols, false, 0, stream);
     hipError_t e;
     switch (geo.mg) {
       case 2: e = launch16_mg<2>(geo, in, out, copy, bm, k, m, col0, nchunks, stride, sink, tail, stream); break;

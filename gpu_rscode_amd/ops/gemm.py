@@ -546,8 +546,8 @@ class Gemm16Plan:
         self.bitmat = None
         self.has_copies = self.copies is not None
         if engine == "mfma":
-            # the FP4 matrix-core engine (csrc/kernels/gf_mfma16.hip); the descriptor's v_perm records
-            # run the columns past the last 512-byte chunk
+            # the FP4 matrix-core engine (csrc/kernels/gf_mfma16.hip), ragged tail included; the
+            # descriptor's v_perm records serve starts off a 4-byte boundary
             if self.symwise:
                 raise ValueError("engine='mfma' needs 16-byte aligned rows")
             self.mfma_mg = mfma_mg

@@ -182,11 +182,13 @@ def test_rs_decode_device_invert_w16_matches_host_plan():
 
 
 @pytest.mark.parametrize("k,m,C,col", [(300, 40, 2 * 256 * 37 + 2 * 13, (0, None)), (64, 16, 512 * 9, (0, None)),
-                                       (17, 20, 512 * 3 + 6, (4, 1536)), (300, 40, 512 * 5, (512, 1024))])
+                                       (17, 20, 512 * 3 + 6, (4, 1536)), (300, 40, 512 * 5, (512, 1024)),
+                                       (300, 35, 2 * 20_011, (0, None)), (150, 35, 1024 * 40, (1024, 1024 * 37 + 6))])
 def test_gemm16_fp4_engine_matches_oracle(k, m, C, col):
     """GF(2^16) on the FP4 matrix cores (gf_mfma16.hip): the 16 x 16 bit-matrix of every coefficient,
-    K split into passes (k = 300: later passes XOR into the outputs), 512-byte chunks on the matrix
-    cores and the ragged tail on the v_perm records; column sub-ranges write only those columns."""
+    K split into passes (k = 300: later passes XOR into the outputs), 1 KiB chunks on the matrix
+    cores (the ragged tail as a partial chunk); column sub-ranges write only those columns. m = 35
+    takes one M-tile per block (MG = 1), whose epilogue follows its last MFMA closely."""
     rng = np.random.default_rng(k + m + C)
     coeff = rng.integers(0, 65536, size=(m, k))
     coeff[0, :3] = [0, 1, 65535]
@@ -206,7 +208,7 @@ def test_gemm16_fp4_engine_matches_oracle(k, m, C, col):
 
 
 def test_gemm16_fp4_fused_copies_and_device_decoder():
-    """The matrix-core w = 16 decode: survivors copied in the same pass (group 0 blocks, every pass
+    """The matrix-core w = 16 decode: survivors copied in the same pass (K-steps spread over the groups, every pass
     its own rows), and a PatternDecoder whose plan (tables, row pointers AND bit-matrix) is built
     on the device from the survivor list (k = 300, 40 erasures)."""
     from gpu_rscode_amd.ops import PatternDecoder
