@@ -177,6 +177,19 @@ __global__ __launch_bounds__(kThreads, 1) void gf_gemm16_fp4_kernel(cptr<uint64_
   const size_t a_frags = size_t(S) * MG * 4 * 64;
   const i32x4* src = bitmat + size_t(g) * a_frags;
   for (size_t i = threadIdx.x; i < a_frags; i += kThreads) afrag[i] = src[i];
+  // pointer inputs / copies: the pass's row pointers as per-step tables after the A slice (a lane
+  // reads its row half's 4 pointers with two LDS loads instead of 8 scalar loads whose latency
+  // every step would wait out): itab[s][j] = in[min(row, k - 1)], ctab[s][j] = copy[row] or 0
+  // for row = row0 + 8 s + j
+  uint64_t* itab = reinterpret_cast<uint64_t*>(afrag + a_frags);
+  uint64_t* ctab = itab + (UNI ? 0 : 8 * S);
+  if constexpr (!UNI || COPY) {
+    for (int i = threadIdx.x; i < 8 * S; i += kThreads) {
+      const int row = row0 + i;
+      if constexpr (!UNI) itab[i] = in[min(row, k - 1)];
+      if constexpr (COPY) ctab[i] = row < k ? copy[row] : 0;
+    }
+  }
   __syncthreads();
 
   const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
@@ -239,14 +252,14 @@ __global__ __launch_bounds__(kThreads, 1) void gf_gemm16_fp4_kernel(cptr<uint64_
   // loads in flight): loads past the last whole chunk read zeros (UNI: num_records 0) or the sink.
   // The partial chunk, if the block has it (always its last), follows with per-lane masked loads.
   const int my_full = my_chunks - (part_rel >= 0 ? 1 : 0);
-  constexpr int RW = UNI ? 4 : 8;  // ring dwords per step (pointer inputs: both row halves)
   // load cursor (uniform): chunk lc, step ls; rows row0 + 8 ls + 4h + i; UNI: lbase = the step's
   // first row at the wave's column
   int lc = 0, ls = 0;
   int64_t lcol = wave_col0;
   uint64_t lbase = UNI ? in0 + uint64_t(int64_t(row0) * in_stride + lcol) : 0;
   const uint64_t step_bytes = UNI ? uint64_t(8 * in_stride) : 0;
-  auto load_step = [&](uint32_t (&x)[RW]) __attribute__((always_inline)) {
+  [[maybe_unused]] uint64_t loff = uint64_t(lcol) + 4 * c;  // pointer inputs: the lane's byte in the row
+  auto load_step = [&](uint32_t (&x)[4]) __attribute__((always_inline)) {
     const int rbase = row0 + 8 * ls;
     const bool live = lc < my_full;
     if constexpr (UNI) {  // one raw buffer resource; rows past k fall outside num_records and read 0
@@ -260,25 +273,23 @@ __global__ __launch_bounds__(kThreads, 1) void gf_gemm16_fp4_kernel(cptr<uint64_
 #pragma unroll
       for (int i = 0; i < 4; ++i) x[i] = __builtin_amdgcn_raw_buffer_load_b32(rs, int(voff[i]), 0, kLoadNT);
       lbase += step_bytes;
-    } else {  // 8 uniform row pointers, each row read by the whole wave (both halves kept)
-      uint64_t p[8];
-      if (rbase + 8 <= k) {
+    } else {  // the lane's 4 row pointers from the LDS table (two 16-byte reads)
+      const i32x4* tp = reinterpret_cast<const i32x4*>(itab + 8 * ls + 4 * h);
+      const i32x4 q0 = tp[0], q1 = tp[1];
+      const uint64_t p[4] = {uint64_t(uint32_t(q0[0])) | (uint64_t(uint32_t(q0[1])) << 32),
+                             uint64_t(uint32_t(q0[2])) | (uint64_t(uint32_t(q0[3])) << 32),
+                             uint64_t(uint32_t(q1[0])) | (uint64_t(uint32_t(q1[1])) << 32),
+                             uint64_t(uint32_t(q1[2])) | (uint64_t(uint32_t(q1[3])) << 32)};
 #pragma unroll
-        for (int j = 0; j < 8; ++j) p[j] = in[rbase + j];
-      } else {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) p[j] = in[min(rbase + j, k - 1)];
-      }
-      const uint32_t vo = uint32_t(live ? lcol : 0) + uint32_t(4 * c);
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        x[j] = __builtin_nontemporal_load((gptr<const uint32_t>)((live ? p[j] : sink) + vo));
+      for (int i = 0; i < 4; ++i)
+        x[i] = __builtin_nontemporal_load((gptr<const uint32_t>)(live ? p[i] + loff : my_sink));
     }
     if (++ls == S) {
       ls = 0;
       ++lc;
       lcol += chunk_step;
       if constexpr (UNI) lbase = in0 + uint64_t(int64_t(row0) * in_stride + lcol);
+      if constexpr (!UNI) loff = uint64_t(lcol) + 4 * c;
     }
   };
 
@@ -309,14 +320,15 @@ __global__ __launch_bounds__(kThreads, 1) void gf_gemm16_fp4_kernel(cptr<uint64_
       for (int f = 0; f < 4; ++f) af[mt][f] = afrag[((cs * MG + mt) * 4 + f) * 64 + lane];
     if constexpr (COPY) {  // the steps' survivor copies, spread round-robin over the groups
       if (cturn == g) {
-        const int rbase = row0 + 8 * cs;
+        const i32x4* tp = reinterpret_cast<const i32x4*>(ctab + 8 * cs + 4 * h);
+        const i32x4 q0 = tp[0], q1 = tp[1];
+        const uint64_t cp[4] = {uint64_t(uint32_t(q0[0])) | (uint64_t(uint32_t(q0[1])) << 32),
+                                uint64_t(uint32_t(q0[2])) | (uint64_t(uint32_t(q0[3])) << 32),
+                                uint64_t(uint32_t(q1[0])) | (uint64_t(uint32_t(q1[1])) << 32),
+                                uint64_t(uint32_t(q1[2])) | (uint64_t(uint32_t(q1[3])) << 32)};
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const uint64_t c0 = rbase + i < k ? copy[rbase + i] : 0;
-          const uint64_t c1 = rbase + 4 + i < k ? copy[rbase + 4 + i] : 0;
-          const uint64_t cb = h ? c1 : c0;
-          if (cb) store_masked(cb + uint64_t(ccol) + 4 * c, x[i], nv);
-        }
+        for (int i = 0; i < 4; ++i)
+          if (cp[i]) store_masked(cp[i] + uint64_t(ccol) + 4 * c, x[i], nv);
       }
       cturn = cturn + 1 == groups ? 0 : cturn + 1;
     }
@@ -375,7 +387,7 @@ __global__ __launch_bounds__(kThreads, 1) void gf_gemm16_fp4_kernel(cptr<uint64_
   bias_init();
   chunk_start();
   const int total_steps = my_full * S;
-  uint32_t ring[kDepth][RW];
+  uint32_t ring[kDepth][4];
 #pragma unroll
   for (int d = 0; d < kDepth; ++d) load_step(ring[d]);
   for (int t0 = 0; t0 < total_steps; t0 += kDepth) {
@@ -383,13 +395,8 @@ __global__ __launch_bounds__(kThreads, 1) void gf_gemm16_fp4_kernel(cptr<uint64_
     for (int d = 0; d < kDepth; ++d) {
       if (t0 + d >= total_steps) break;  // (uniform)
       uint32_t x[4];
-      if constexpr (UNI) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) x[i] = ring[d][i];
-      } else {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) x[i] = h ? ring[d][4 + i] : ring[d][i];
-      }
+      for (int i = 0; i < 4; ++i) x[i] = ring[d][i];
       load_step(ring[d]);  // kDepth steps ahead (past the whole chunks: zeros / the sink)
       consume(x, 4);
     }
@@ -407,7 +414,7 @@ __global__ __launch_bounds__(kThreads, 1) void gf_gemm16_fp4_kernel(cptr<uint64_
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int r = min(row0 + 8 * s + 4 * h + i, k - 1);  // rows past k meet zero bit-matrix columns
-        const uint64_t base = UNI ? in0 + uint64_t(int64_t(r) * in_stride) : in[r];
+        const uint64_t base = UNI ? in0 + uint64_t(int64_t(r) * in_stride) : itab[r - row0];
         x[i] = load_masked(base + uint64_t(ccol) + 4 * c, tail_valid);
       }
       consume(x, tail_valid);
@@ -440,14 +447,15 @@ Geo16 geometry16(int k, int m, int mg_cap, bool copy) {
     if (g.mg == 1 || padded < best) g.mg = cand;
     if (forced) break;
   }
-  constexpr size_t kLds = 152 * 1024;
-  auto fit_steps = [&](int mg) { return int(kLds / (size_t(mg) * 4096)); };  // per K-step: A (mg x 4 KiB)
+  constexpr size_t kLds = 160 * 1024;
+  // per K-step: A (mg x 4 KiB) and 8 row + 8 copy pointers
+  auto fit_steps = [&](int mg) { return int(kLds / (size_t(mg) * 4096 + 128)); };
   while (g.mg > 1 && fit_steps(g.mg) < 1) g.mg >>= 1;
   const int smax = std::max(1, fit_steps(g.mg));
   g.passes = (g.ksteps + smax - 1) / smax;
   g.S = (g.ksteps + g.passes - 1) / g.passes;
   g.groups = (g.mtiles + g.mg - 1) / g.mg;
-  g.lds = size_t(g.S) * g.mg * 4096;
+  g.lds = size_t(g.S) * g.mg * 4096 + 2 * 64 * size_t(g.S);  // A slice + row / copy pointer tables
   (void)copy;
   return g;
 }

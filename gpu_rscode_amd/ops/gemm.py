@@ -442,13 +442,17 @@ def _batch_strides(stripes_in, stripes_out, stripes_copy=None) -> tuple[int, int
     return d_in, d_out
 
 
-# GF(2^16) codes take the FP4 matrix-core engine from this many coefficients (k x m) with k, m >=
-# 16: the v_perm w = 16 kernel is VALU-bound there (k=300, m=40: 4.5 ms per GiB), narrow codes stay
-# at the memory ceiling on it. (GFRS_GF16_MFMA=0 / 1: never / always where supported.)
-_GF16_MFMA_MIN_KM = 1024
+# GF(2^16) codes on the FP4 matrix-core engine (csrc/kernels/gf_mfma16.hip) against the v_perm
+# w = 16 kernel, 1 GiB stripes (profiles/gf65536/r08_mfma16): encodes win from k = 16 at any m
+# (k=16, m=4: 0.30 vs 0.40 ms; k=300, m=40: 1.98 vs 4.49), k = 10 loses (0.55 vs 0.48). Decodes,
+# which also copy the survivors, lose at m = 4 (k=16: 0.51 vs 0.43) and win from m = 8 on wider
+# codes (k=64, m=8: 0.62 vs 0.73; k=300, m=40: 2.43 vs 4.52). (GFRS_GF16_MFMA=0 / 1: never /
+# always where supported.)
+_GF16_MFMA_MIN_K = 16
+_GF16_MFMA_COPY_MIN_M, _GF16_MFMA_COPY_MIN_KM = 8, 256
 
 
-def _auto_engine16(k: int, m: int, symwise: bool) -> bool:
+def _auto_engine16(k: int, m: int, symwise: bool, copies: bool = False) -> bool:
     import os
 
     forced = os.environ.get("GFRS_GF16_MFMA")
@@ -456,7 +460,9 @@ def _auto_engine16(k: int, m: int, symwise: bool) -> bool:
         return False
     if forced is not None:
         return forced == "1"
-    return k >= 16 and m >= 16 and k * m >= _GF16_MFMA_MIN_KM
+    if k < _GF16_MFMA_MIN_K or m < 4:
+        return False
+    return not copies or (m >= _GF16_MFMA_COPY_MIN_M and k * m >= _GF16_MFMA_COPY_MIN_KM)
 
 
 def _pack16(coeff) -> bytes:
@@ -537,7 +543,7 @@ class Gemm16Plan:
             host[self.layout.tab_off:] = np.frombuffer(t.tobytes(), dtype=np.uint8)
         self.desc = torch.from_numpy(host).to(self.device)
         if engine == "auto":
-            engine = "mfma" if _auto_engine16(self.k, self.m, self.symwise) else "valu16"
+            engine = "mfma" if _auto_engine16(self.k, self.m, self.symwise, self.copies is not None) else "valu16"
         if engine == "valu":
             engine = "valu16"
         if engine not in ("valu16", "mfma"):
