@@ -16,6 +16,12 @@
 
 namespace {
 
+// A device setup running on a helper thread (gfrs/async_prepare.h), handed to a later file-codec
+// call: `--dist` starts it before its file creation / survivor choice so it overlaps them.
+struct PrepareHandle {
+  std::unique_ptr<gfrs::AsyncPrepare> prep;
+};
+
 void check(hipError_t e, const char* what) {
   if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
 }
@@ -336,19 +342,67 @@ PYBIND11_MODULE(_hip, m) {
       py::arg("file"), py::arg("conf"), py::arg("out") = "", py::arg("devices") = std::vector<int>{0},
       py::arg("streams") = 2, py::arg("slice") = 16 << 20, py::arg("max_blocks") = 0, py::arg("zero_copy") = false);
   m.def("release_workspaces", [] { check(release_workspaces(), "release_workspaces"); });
+  py::class_<PrepareHandle>(m, "PrepareHandle")
+      .def("wait", [](PrepareHandle& h) {
+        double ms = 0;
+        if (h.prep) {
+          py::gil_scoped_release nogil;
+          ms = h.prep->wait();
+        }
+        return ms;
+      });
+  // the setup an encode / decode of `file` will need, started now on a helper thread
+  m.def(
+      "prepare_encode_async",
+      [](const std::string& file, int k, int p, const std::vector<int>& devices, int streams, int64_t slice,
+         int max_blocks, int field_w, bool zero_copy, int64_t window) {
+        PipelineOptions popt = pipeline_options(streams, slice, max_blocks);
+        popt.field_w = field_w;
+        popt.zero_copy = zero_copy;
+        StreamOptions so;
+        so.window = window;
+        so.field_w = field_w;
+        return PrepareHandle{prepare_for_encode(devices, popt, file, k, p, &so)};
+      },
+      py::arg("file"), py::arg("k"), py::arg("p"), py::arg("devices") = std::vector<int>{0}, py::arg("streams") = 2,
+      py::arg("slice") = 16 << 20, py::arg("max_blocks") = 0, py::arg("field_w") = 8, py::arg("zero_copy") = false,
+      py::arg("window") = 0);
+  m.def(
+      "prepare_decode_async",
+      [](const std::string& file, const std::vector<int>& devices, int streams, int64_t slice, int max_blocks,
+         bool zero_copy, int64_t window) {
+        PipelineOptions popt = pipeline_options(streams, slice, max_blocks);
+        popt.zero_copy = zero_copy;
+        StreamOptions so;
+        so.window = window;
+        return PrepareHandle{prepare_for_decode(devices, popt, file, &so)};
+      },
+      py::arg("file"), py::arg("devices") = std::vector<int>{0}, py::arg("streams") = 2, py::arg("slice") = 16 << 20,
+      py::arg("max_blocks") = 0, py::arg("zero_copy") = false, py::arg("window") = 0);
+  // (prep: a PrepareHandle from prepare_*_async, consumed; None: the call starts its own)
+  auto take_prep = [](py::object prep) -> std::unique_ptr<AsyncPrepare> {
+    if (prep.is_none()) return nullptr;
+    return std::move(prep.cast<PrepareHandle&>().prep);
+  };
   m.def(
       "encode_file_stream",
-      [gpu_gemm](const std::string& file, int k, int p, const std::string& matrix, bool cpu_meta,
-                 const std::vector<int>& devices, int streams, int64_t slice, int max_blocks, int64_t window,
-                 bool resume, bool durable, int stop_after, int field_w, int64_t col_lo, int64_t col_hi, bool shard,
-                 bool zero_copy) {
-        const GemmFn g = gpu_gemm(devices, streams, slice, max_blocks, nullptr, zero_copy);
+      [gpu_gemm, take_prep](const std::string& file, int k, int p, const std::string& matrix, bool cpu_meta,
+                            const std::vector<int>& devices, int streams, int64_t slice, int max_blocks,
+                            int64_t window, bool resume, bool durable, int stop_after, int field_w, int64_t col_lo,
+                            int64_t col_hi, bool shard, bool zero_copy, py::object prep_handle) {
         StreamReport r;
+        std::unique_ptr<AsyncPrepare> given = take_prep(prep_handle);
+        const bool have = bool(given) || !prep_handle.is_none();
         {
           py::gil_scoped_release nogil;
-          r = encode_file_stream(file, k, p, parse_matrix_kind(matrix), g, pinned_alloc(),
-                                 stream_options(window, resume, durable, stop_after, field_w, col_lo, col_hi, shard),
-                                 cpu_meta);
+          // device setup on a helper thread during the first window's reads, as bin/RS does
+          const StreamOptions so = stream_options(window, resume, durable, stop_after, field_w, col_lo, col_hi, shard);
+          PipelineOptions popt = pipeline_options(streams, slice, max_blocks);
+          popt.field_w = field_w;
+          popt.zero_copy = zero_copy;
+          auto prep = have ? std::move(given) : prepare_for_encode(devices, popt, file, k, p, &so);
+          const GemmFn g = gpu_gemm(devices, streams, slice, max_blocks, &prep, zero_copy);
+          r = encode_file_stream(file, k, p, parse_matrix_kind(matrix), g, pinned_alloc(), so, cpu_meta);
         }
         return stream_report(r);
       },
@@ -356,19 +410,25 @@ PYBIND11_MODULE(_hip, m) {
       py::arg("devices") = std::vector<int>{0}, py::arg("streams") = 2, py::arg("slice") = 16 << 20,
       py::arg("max_blocks") = 0, py::arg("window") = 0, py::arg("resume") = true, py::arg("durable") = true,
       py::arg("stop_after") = -1, py::arg("field_w") = 8, py::arg("col_lo") = 0, py::arg("col_hi") = -1,
-      py::arg("shard") = false, py::arg("zero_copy") = false);
+      py::arg("shard") = false, py::arg("zero_copy") = false, py::arg("prep") = py::none());
   m.def(
       "decode_file_stream",
-      [gpu_gemm](const std::string& file, const std::string& conf, const std::string& out,
-                 const std::vector<int>& devices, int streams, int64_t slice, int max_blocks, int64_t window,
-                 bool resume, bool durable, int stop_after, int64_t col_lo, int64_t col_hi, bool shard,
-                 const std::vector<int>& rows, bool zero_copy) {
-        const GemmFn g = gpu_gemm(devices, streams, slice, max_blocks, nullptr, zero_copy);
+      [gpu_gemm, take_prep](const std::string& file, const std::string& conf, const std::string& out,
+                            const std::vector<int>& devices, int streams, int64_t slice, int max_blocks,
+                            int64_t window, bool resume, bool durable, int stop_after, int64_t col_lo,
+                            int64_t col_hi, bool shard, const std::vector<int>& rows, bool zero_copy,
+                            py::object prep_handle) {
         StreamReport r;
+        std::unique_ptr<AsyncPrepare> given = take_prep(prep_handle);
+        const bool have = bool(given) || !prep_handle.is_none();
         {
           py::gil_scoped_release nogil;
-          r = decode_file_stream(file, conf, out, g, pinned_alloc(),
-                                 stream_options(window, resume, durable, stop_after, 8, col_lo, col_hi, shard, rows));
+          const StreamOptions so = stream_options(window, resume, durable, stop_after, 8, col_lo, col_hi, shard, rows);
+          PipelineOptions popt = pipeline_options(streams, slice, max_blocks);
+          popt.zero_copy = zero_copy;
+          auto prep = have ? std::move(given) : prepare_for_decode(devices, popt, file, &so);
+          const GemmFn g = gpu_gemm(devices, streams, slice, max_blocks, &prep, zero_copy);
+          r = decode_file_stream(file, conf, out, g, pinned_alloc(), so);
         }
         return stream_report(r);
       },
@@ -376,5 +436,5 @@ PYBIND11_MODULE(_hip, m) {
       py::arg("streams") = 2, py::arg("slice") = 16 << 20, py::arg("max_blocks") = 0, py::arg("window") = 0,
       py::arg("resume") = true, py::arg("durable") = true, py::arg("stop_after") = -1, py::arg("col_lo") = 0,
       py::arg("col_hi") = -1, py::arg("shard") = false, py::arg("rows") = std::vector<int>{},
-      py::arg("zero_copy") = false);
+      py::arg("zero_copy") = false, py::arg("prep") = py::none());
 }

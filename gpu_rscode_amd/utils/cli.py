@@ -189,6 +189,10 @@ def _dist_run(a, ctx) -> int:
         total = os.path.getsize(path)
         k, p, n = a.k, a.n - a.k, a.n
         C = max(2 if a.field_w == 16 else 1, ff.chunk_size(total, k, a.field_w))
+        # the device setup (streams, buffers, code object) runs on a helper thread from here on,
+        # under the output creation, the barrier and the first window's reads (as bin/RS overlaps it)
+        prep = (hip().prepare_encode_async(path, k, p, [ctx.local_rank], a.streams, a.slice, a.grid, a.field_w,
+                                           a.zero_copy, a.window or 0) if on_gpu else None)
         if ctx.is_root:
             for i in range(n):
                 _create(ff.chunk_path(path, i), C)
@@ -199,7 +203,7 @@ def _dist_run(a, ctx) -> int:
         kw = dict(st, field_w=a.field_w, col_lo=lo, col_hi=hi, shard=True)
         if on_gpu:
             r = hip().encode_file_stream(path, k, p, a.matrix, a.cpu_meta, [ctx.local_rank], a.streams, a.slice,
-                                         a.grid, zero_copy=a.zero_copy, **kw)
+                                         a.grid, zero_copy=a.zero_copy, prep=prep, **kw)
         else:
             r = cpu().encode_file_stream(path, k, p, a.matrix, a.cpu_meta, a.mul, a.threads, **kw)
         # every rank's shard CRCs (and width) to rank 0, combined in column order
@@ -226,6 +230,9 @@ def _dist_run(a, ctx) -> int:
     md = ff.read_metadata(ff.metadata_path(a.in_file))
     C = max(2 if md.w == 16 else 1, ff.chunk_size(md.total_size, md.k, md.w))
     dst = a.out or a.in_file
+    # device setup under rank 0's survivor choice (it reads and CRC-checks every survivor)
+    prep = (hip().prepare_decode_async(a.in_file, [ctx.local_rank], a.streams, a.slice, a.grid, a.zero_copy,
+                                       a.window or 0) if on_gpu else None)
     # rank 0 picks (and CRC-verifies) the survivors; status first: a failure there stops every rank
     pick = torch.zeros(md.k + 1, dtype=torch.int64, device=ctx.device)
     if ctx.is_root:
@@ -251,7 +258,7 @@ def _dist_run(a, ctx) -> int:
     kw = dict(st, col_lo=lo, col_hi=hi, shard=True, rows=rows)
     if on_gpu:
         r = hip().decode_file_stream(a.in_file, a.conf, dst, [ctx.local_rank], a.streams, a.slice, a.grid,
-                                     zero_copy=a.zero_copy, **kw)
+                                     zero_copy=a.zero_copy, prep=prep, **kw)
     else:
         r = cpu().decode_file_stream(a.in_file, a.conf, dst, a.mul, a.threads, **kw)
     barrier()
