@@ -16,6 +16,7 @@ import argparse
 import json
 import os
 import socket
+import statistics
 import subprocess
 import sys
 import tempfile
@@ -123,8 +124,11 @@ def main() -> int:
             out[f"{op}_{what}_GBps_rs"] = round(a.size / best_rs / 1e9, 3)
             out[f"{op}_{what}_GBps_dist"] = round(a.size / best_dist / 1e9, 3)
             out[f"{op}_{what}_dist_vs_rs"] = round(best_rs / best_dist, 3)
+            # medians too: the first rep writes into fresh chunk files, later ones overwrite them
+            med_rs, med_dist = statistics.median(res[f"rs_{op}_{what}_s"]), statistics.median(res[f"dist_{op}_{what}_s"])
+            out[f"{op}_{what}_median_dist_vs_rs"] = round(med_rs / med_dist, 3)
     out["pipeline"] = "staged -s 2" if a.staged else "zero-copy"
-    out["what"] = ("best of reps, page cache warm, --no-sync, GB/s = input bytes / time. codec: the file codec call "
+    out["what"] = ("best of reps (and median ratios), page cache warm, --no-sync, GB/s = input bytes / time. codec: the file codec call "
                    "inside the process (bin/RS: encode/decode_file_stream; --dist: max over ranks from the shard "
                    "codec call to the final barrier). wall: the whole process (torchrun + interpreter + torch "
                    "import + process group for --dist)")
