@@ -234,6 +234,7 @@ class GemmPlan:
                                   and hip().fp4_batched_supported(self.k, self.m, mfma_mg))
         self.engine = engine
         self.bitmat = None
+        self.fp4_form = None
         if engine == "mfma" and self.batch > 1 and (
                 self.in_bstride is None or not hip().fp4_batched_supported(self.k, self.m, mfma_mg)):
             raise ValueError("batched engine='mfma' needs k in (112, 128], m <= 32 and stripes at fixed strides")
@@ -255,11 +256,15 @@ class GemmPlan:
             stride = ptrs[1] - ptrs[0] if self.k > 1 else 1
             uniform = stride != 0 and all(p - ptrs[0] == j * stride for j, p in enumerate(ptrs))
             self.in_stride = stride if uniform else 0
+            # FP4 kernel family: "lds" (gf_mfma_fp4.hip / gf_mfma_fp4ar.hip: LDS-DMA input rings, one
+            # wave per SIMD) or "r" (gf_mfma8r.hip: register-streamed input, two waves per SIMD);
+            # each has its own bit-matrix layout
+            self.fp4_form = _fp4_form(self.k, self.m, self.batch, self.copies is not None) if engine == "mfma" else None
+            self.fp4r_mg = hip().fp4r_choose_mg(self.k, self.m) if self.fp4_form == "r" else 0
             if coeff is not None:
                 self._build_bitmat(coeff)
             else:  # filled on device later (set_device_coeff / invert_into_plan)
-                self.bitmat = torch.zeros(hip().fp4_bitmat_bytes(self.k, self.m, self.mfma_mg), dtype=torch.uint8,
-                                          device=self.device)
+                self.bitmat = torch.zeros(self._bitmat_bytes(), dtype=torch.uint8, device=self.device)
         elif engine == "lut":  # LDS nibble-table ablation (csrc/kernels/gf_gemm_lut.hip)
             if self.bytewise or self.batch > 1:
                 raise ValueError("engine='lut' needs 16-byte aligned rows and one stripe")
@@ -271,13 +276,24 @@ class GemmPlan:
             self._stripes_in = self._stripes_out = self._stripes_copy = None
         self._mark_ready()
 
+    def _bitmat_bytes(self) -> int:
+        if self.engine == "mfma" and self.fp4_form == "r":
+            return hip().fp4r_bitmat_bytes(self.k, self.m, self.fp4r_mg)
+        if self.engine == "mfma":
+            return hip().fp4_bitmat_bytes(self.k, self.m, self.mfma_mg)
+        return hip().mfma_bitmat_bytes(self.k, self.m)
+
     def _build_bitmat(self, coeff) -> None:
         """Bit-matrix operand of the matrix-core engines, built on device from the m x k coefficients."""
         c = torch.from_numpy(np.ascontiguousarray(np.asarray(coeff, dtype=np.uint8).reshape(self.m, self.k)))
         c = c.to(self.device)
         h = hip()
         st = torch.cuda.current_stream(self.device).cuda_stream
-        if self.engine == "mfma":
+        if self.engine == "mfma" and self.fp4_form == "r":
+            if self.bitmat is None:
+                self.bitmat = torch.empty(self._bitmat_bytes(), dtype=torch.uint8, device=self.device)
+            h.fp4r_bitmat(c.data_ptr(), self.k, 0, self.m, self.k, self.bitmat.data_ptr(), self.fp4r_mg, st)
+        elif self.engine == "mfma":
             if self.bitmat is None:
                 self.bitmat = torch.empty(h.fp4_bitmat_bytes(self.k, self.m, self.mfma_mg), dtype=torch.uint8,
                                           device=self.device)
@@ -305,8 +321,12 @@ class GemmPlan:
             sel = rows.data_ptr()
         elif coeff.shape[0] < self.m:
             raise ValueError("coeff needs m rows")
-        hip().fp4_bitmat_sel(coeff.data_ptr(), coeff.stride(0), sel, self.m, self.k, self.bitmat.data_ptr(),
-                             self.mfma_mg, st.cuda_stream)
+        if self.fp4_form == "r":
+            hip().fp4r_bitmat(coeff.data_ptr(), coeff.stride(0), sel, self.m, self.k, self.bitmat.data_ptr(),
+                              self.fp4r_mg, st.cuda_stream)
+        else:
+            hip().fp4_bitmat_sel(coeff.data_ptr(), coeff.stride(0), sel, self.m, self.k, self.bitmat.data_ptr(),
+                                 self.mfma_mg, st.cuda_stream)
         if not torch.cuda.is_current_stream_capturing():
             coeff.record_stream(st)
 
@@ -363,6 +383,9 @@ class GemmPlan:
                 raise ValueError("kernel variants are not selectable on batched plans")
             h.gemm_batched(int(self.desc.data_ptr()), self.k, self.m_pad, self.batch, col0, ncols, self.bytewise, s,
                            self.has_copies)
+        elif self.engine == "mfma" and vec is None and col0 % 2 == 0 and self.fp4_form == "r":
+            h.gemm_fp4r(int(self.bitmat.data_ptr()), int(self.desc.data_ptr()), self.k, self.m, col0, ncols,
+                        self.fp4r_mg, self.in_stride, self.has_copies, s)
         elif self.engine == "mfma" and vec is None and col0 % 2 == 0:
             h.gemm_fp4(int(self.bitmat.data_ptr()), int(self.desc.data_ptr()), self.k, self.m, col0, ncols,
                        self.mfma_mg, self.in_stride, self.has_copies, s)
@@ -376,6 +399,22 @@ class GemmPlan:
             h.gemm(int(self.desc.data_ptr()), self.k, self.m_pad, col0, ncols, False, max_blocks, s, self.has_copies)
         else:
             h.gemm_variant(int(self.desc.data_ptr()), self.k, self.m_pad, col0, ncols, vec, pf, nt, max_blocks, s)
+
+
+def _fp4_form(k: int, m: int, batch: int, copies: bool) -> str:
+    """Which FP4 kernel family a single-stripe ``engine="mfma"`` plan runs: ``GFRS_FP4_FORM=r|lds``
+    forces one; batched plans always take the LDS family's batched kernel. The LDS ring is the
+    default everywhere: the register-streamed form lost at every measured GF(2^8) shape
+    (k = 128: 906-918 vs 794-804 us plain, 1331-1366 vs 911-993 with copies;
+    profiles/wide_stripe/r08_fp4r), unlike its GF(2^16) sibling."""
+    import os
+
+    forced = os.environ.get("GFRS_FP4_FORM")
+    if batch > 1:
+        return "lds"
+    if forced in ("r", "lds"):
+        return forced
+    return "lds"
 
 
 # wide stripes go to the FP4 matrix-core kernel: measured on MI355X (profiles/archive/r01_kbench5) it wins
