@@ -50,8 +50,8 @@ constexpr DescLayout desc_layout(int k, int m_pad, int batch = 1) {
 // GF(2^16) descriptor (csrc/kernels/gf_gemm16.hip): the same header and pointer arrays (rows are
 // byte rows holding little-endian 16-bit symbols), and FOUR records per coefficient, tab[j][i][q]
 // with q = 2 * src_byte + dst_byte (gfrs/gf65536.h perm_quad).
-constexpr DescLayout desc_layout16(int k, int m_pad) {
-  DescLayout l = desc_layout(k, m_pad, 1);
+constexpr DescLayout desc_layout16(int k, int m_pad, int batch = 1) {
+  DescLayout l = desc_layout(k, m_pad, batch);
   l.bytes = l.tab_off + 4 * sizeof(PermTable) * size_t(k) * size_t(m_pad);
   return l;
 }

@@ -25,6 +25,9 @@ hipError_t launch_gf_gemm(const void* desc, int k, int m_pad, int64_t col0, int6
 // inputs cross PCIe once per tile; short rows otherwise run one output per tile).
 hipError_t launch_gf_gemm16(const void* desc, int k, int m_pad, int64_t col0, int64_t ncols, bool symwise,
                             int max_blocks, hipStream_t stream, bool one_tile = false);
+// batched: `batch` stripes (grid.y), desc built with desc_layout16(k, m_pad, batch)
+hipError_t launch_gf_gemm16_batched(const void* desc, int k, int m_pad, int batch, int64_t col0, int64_t ncols,
+                                    bool symwise, int max_blocks, hipStream_t stream, bool one_tile = false);
 
 // Batched form: `batch` stripes of identical shape share the coefficient tables (small-object
 // serving: one launch for many objects). desc built with desc_layout(k, m_pad, batch).
@@ -127,6 +130,12 @@ hipError_t launch_mfma_bitmat(const uint8_t* coeff, int m, int k, void* bitmat,
 // into the outputs); copies: fused survivor copy (decode), in_stride as launch_gf_gemm_fp4.
 hipError_t launch_gf_gemm16_fp4(const void* bitmat, const void* desc, int k, int m, int64_t col0, int64_t ncols,
                                 int mg_cap, int64_t in_stride, bool copies, hipStream_t stream);
+// Batched: `batch` stripes whose rows are stripe 0's plus b * in_bstride (inputs) / b * out_bstride
+// (outputs, copies), desc built with desc_layout16(k, m_pad, batch). Every stripe's whole chunks run
+// in one persistent launch per K pass; the ragged remainders on the batched v_perm kernel.
+hipError_t launch_gf_gemm16_fp4_batched(const void* bitmat, const void* desc, int k, int m, int batch, int64_t col0,
+                                        int64_t ncols, int mg_cap, int64_t in_stride, int64_t in_bstride,
+                                        int64_t out_bstride, bool copies, hipStream_t stream);
 size_t fp16_bitmat_bytes(int k, int m, int mg_cap);
 // coefficient (o, i) = coeff[row(o) * ld + i] (uint16, device), row(o) = sel ? sel[o] : o
 hipError_t launch_fp16_bitmat(const uint16_t* coeff, int ld, const int* sel, int m, int k, void* bitmat, int mg_cap,

@@ -42,11 +42,20 @@ constexpr uint32_t kSelHi = 0x07050301u;  // [h0 h1 h2 h3]
 constexpr uint32_t kSelW0 = 0x05010400u;  // [l0 h0 l1 h1] from lo=[l0..l3], hi=[h0..h3]
 constexpr uint32_t kSelW1 = 0x07030602u;  // [l2 h2 l3 h3]
 
-inline DescView view16(const void* desc, int k, int m_pad) {
-  const DescLayout l = desc_layout16(k, m_pad);
+inline DescView view16(const void* desc, int k, int m_pad, int batch = 1) {
+  const DescLayout l = desc_layout16(k, m_pad, batch);
   const char* b = static_cast<const char*>(desc);
   return {(cptr<uint64_t>)(b + l.in_off), (cptr<uint64_t>)(b + l.copy_off), (cptr<uint64_t>)(b + l.out_off),
           (cptr<uint32_t>)(b + l.tab_off)};
+}
+
+// Stripe b of a batched descriptor (blockIdx.y): its own row pointers, the shared table block.
+__device__ __forceinline__ DescView stripe16(DescView d, int k, int m_pad) {
+  const int b = blockIdx.y;
+  d.in += size_t(b) * k;
+  d.copy += size_t(b) * k;
+  d.out += size_t(b) * m_pad;
+  return d;
 }
 
 // One symbol column (2 bytes at `off`), one lane: k symbols loaded 8 at a time before use (see
@@ -90,6 +99,7 @@ template <int MT, int PF>
 __global__ __launch_bounds__(kBlock) void gf_gemm16_vec_kernel(DescView d, int k, int m_pad, int ntiles, int64_t col0,
                                                                int64_t ngroups, int64_t nblk, int64_t ncb,
                                                                int tail_syms) {
+  d = stripe16(d, k, m_pad);
   const TileMap tm = map_block(ntiles);
   const int i0 = sgpr_int(tm.tile * MT);  // (first, with every lane active)
   if (tm.cb0 >= ncb) return;
@@ -154,6 +164,7 @@ __global__ __launch_bounds__(kBlock) void gf_gemm16_vec_kernel(DescView d, int k
 template <int MT>
 __global__ __launch_bounds__(kBlock) void gf_gemm16_sym_kernel(DescView d, int k, int m_pad, int ntiles, int64_t col0,
                                                                int64_t nsyms, int64_t nblk, int64_t ncb) {
+  d = stripe16(d, k, m_pad);
   const TileMap tm = map_block(ntiles);
   const int i0 = sgpr_int(tm.tile * MT);  // (first, with every lane active)
   if (tm.cb0 >= ncb) return;
@@ -198,10 +209,15 @@ hipError_t dispatch16(int m_pad, int mt_cap, F&& f) {
 
 hipError_t launch_gf_gemm16(const void* desc, int k, int m_pad, int64_t col0, int64_t ncols, bool symwise,
                             int max_blocks, hipStream_t stream, bool one_tile) {
+  return launch_gf_gemm16_batched(desc, k, m_pad, 1, col0, ncols, symwise, max_blocks, stream, one_tile);
+}
+
+hipError_t launch_gf_gemm16_batched(const void* desc, int k, int m_pad, int batch, int64_t col0, int64_t ncols,
+                                    bool symwise, int max_blocks, hipStream_t stream, bool one_tile) {
   if (k <= 0 || m_pad <= 0 || ncols <= 0) return ncols < 0 ? hipErrorInvalidValue : hipSuccess;
   if ((col0 | ncols) & 1) return hipErrorInvalidValue;  // whole 16-bit symbols only
-  if (m_pad % tile_for(m_pad) != 0) return hipErrorInvalidValue;
-  const DescView d = view16(desc, k, m_pad);
+  if (m_pad % tile_for(m_pad) != 0 || batch < 1 || batch > 65535) return hipErrorInvalidValue;
+  const DescView d = view16(desc, k, m_pad, batch);
   // Short rows: one output per tile. The kernel parallelises over columns and output tiles only,
   // so a row of a few KiB is a handful of blocks each walking all k rows for 8 outputs (k = 300,
   // m = 40, 3.4 KiB: 5 blocks). One output per tile puts m times as many blocks on the chip; the
@@ -213,20 +229,22 @@ hipError_t launch_gf_gemm16(const void* desc, int k, int m_pad, int64_t col0, in
     const char* e = std::getenv("GFRS_GF16_SHORT_GROUPS");
     return e ? std::max<int64_t>(0, std::atoll(e)) : int64_t(32768);
   }();
-  const int mt_cap = (ncols / 16 < short_groups && !one_tile) ? 1 : 8;
+  // (a batch fills the chip with its own grid rows: the cut counts the groups of every stripe)
+  const int mt_cap = (ncols / 16 * batch < short_groups && !one_tile) ? 1 : 8;
   return dispatch16(m_pad, mt_cap, [&](auto mt) -> hipError_t {
     constexpr int MT = decltype(mt)::value;
     const int ntiles = m_pad / MT;
     if (symwise || (col0 & 15)) {
       const Grid g = make_grid(ncols / 2, ntiles, max_blocks);
-      gf_gemm16_sym_kernel<MT><<<g.blocks, kBlock, 0, stream>>>(d, k, m_pad, ntiles, col0, ncols / 2, g.nblk, g.ncb);
+      gf_gemm16_sym_kernel<MT>
+          <<<dim3(g.blocks, batch), kBlock, 0, stream>>>(d, k, m_pad, ntiles, col0, ncols / 2, g.nblk, g.ncb);
       return hipGetLastError();
     }
     const int64_t ngroups = ncols / 16;
     const int tail_syms = int((ncols - ngroups * 16) / 2);
     const Grid g = make_grid(ngroups + tail_syms, ntiles, max_blocks);
     gf_gemm16_vec_kernel<MT, 2>
-        <<<g.blocks, kBlock, 0, stream>>>(d, k, m_pad, ntiles, col0, ngroups, g.nblk, g.ncb, tail_syms);
+        <<<dim3(g.blocks, batch), kBlock, 0, stream>>>(d, k, m_pad, ntiles, col0, ngroups, g.nblk, g.ncb, tail_syms);
     return hipGetLastError();
   });
 }

@@ -164,7 +164,9 @@ __global__ __launch_bounds__(kThreads, 1) void gf_gemm16_fp4_kernel(cptr<uint64_
                                                                     const i32x4* __restrict__ bitmat, int k, int m,
                                                                     int row0, int S, int groups, int64_t col0,
                                                                     int64_t nchunks, int64_t chunk_slots,
-                                                                    int64_t in_stride, uint64_t sink, int tail_bytes) {
+                                                                    int64_t in_stride, uint64_t sink, int tail_bytes,
+                                                                    int64_t fps, int64_t in_bstride,
+                                                                    int64_t out_bstride) {
   extern __shared__ __attribute__((aligned(16))) i32x4 afrag[];  // [S][MG][4][64]
   const int bid = blockIdx.x;
   const int xcd = bid & 7;
@@ -209,22 +211,39 @@ __global__ __launch_bounds__(kThreads, 1) void gf_gemm16_fp4_kernel(cptr<uint64_
   const uint64_t my_sink = sink + uint64_t(((bid * kWaves + wave) % 256) * 256 + 4 * c);
   const uint64_t in0 = UNI ? in[0] : 0;
   const int lane_off = wave * kWaveBytes + 4 * c;  // byte offset inside a chunk
-  // this lane's valid bytes (4, 2 or 0) in the partial chunk
+  // this lane's valid bytes (4, 2 or 0) in a partial chunk (the last of each stripe when the
+  // columns end tail_bytes into a chunk)
   const int tail_valid = min(4, max(0, tail_bytes - lane_off));
-  // the partial chunk's index among this block's chunks (-1: none of them)
-  const int part_rel =
-      (tail_bytes > 0 && (nchunks - 1 - slot0) % chunk_slots == 0) ? int((nchunks - 1 - slot0) / chunk_slots) : -1;
-  const int64_t chunk_step = chunk_slots * kChunkBytes;  // column advance between this block's chunks
-  const int64_t wave_col0 = col0 + slot0 * kChunkBytes + int64_t(wave) * kWaveBytes;
-  // UNI: the lane's 4 rows as 32-bit offsets from the step's first row
+  // chunk q of the launch is chunk q % fps of stripe q / fps (batched launches: fps chunks per
+  // stripe, rows at fixed strides from stripe 0's). A cursor keeps (stripe, chunk) and steps by
+  // chunk_slots without dividing (one division, here).
+  const int64_t db = chunk_slots / fps, dch = chunk_slots - db * fps;
+  const int64_t b_first = slot0 / fps, ch_first = slot0 - b_first * fps;
+  // a cursor: chunk ch of stripe b, its wave column col and stripe byte offset soff (at stride
+  // bstride); one step adds chunk_slots chunks with adds and one compare
+  const int64_t dcol = dch * kChunkBytes, fcol = fps * kChunkBytes;
+  auto advance = [&](int64_t& ch, int64_t& col, int64_t& soff, int64_t bstride) __attribute__((always_inline)) {
+    ch += dch;
+    col += dcol;
+    soff += db * bstride;
+    if (ch >= fps) {
+      ch -= fps;
+      col -= fcol;
+      soff += bstride;
+    }
+  };
+  auto col_of = [&](int64_t ch) __attribute__((always_inline)) {  // the wave's first byte column
+    return col0 + ch * kChunkBytes + int64_t(wave) * kWaveBytes;
+  };
+  // the lane's valid bytes of chunk ch of a stripe: 4, or tail_valid in the partial chunk
+  auto valid_of = [&](int64_t ch) __attribute__((always_inline)) {
+    return (tail_bytes > 0 && ch == fps - 1) ? tail_valid : 4;
+  };
+  // UNI: the lane's 4 rows as 32-bit offsets from the step's first row (a lane past the columns of
+  // a partial chunk: an offset past num_records, so it reads zeros)
   uint32_t voff[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) voff[i] = uint32_t((4 * h + i) * in_stride) + uint32_t(4 * c);
-  auto load_masked = [&](uint64_t addr, int nv) __attribute__((always_inline)) -> uint32_t {
-    if (nv == 4) return __builtin_nontemporal_load((gptr<const uint32_t>)addr);
-    if (nv == 2) return uint32_t(*(gptr<const uint16_t>)addr);
-    return 0u;
-  };
   auto store_masked = [&](uint64_t addr, uint32_t v, int nv) __attribute__((always_inline)) {
     if (nv == 4)
       *(gptr<uint32_t>)addr = v;
@@ -247,21 +266,27 @@ __global__ __launch_bounds__(kThreads, 1) void gf_gemm16_fp4_kernel(cptr<uint64_
         }
   };
 
-  // The block's whole chunks run through a software pipeline whose loads never sit in a branch
-  // (a conditional load makes the ring slots merge values, and every merge copy waits for all
-  // loads in flight): loads past the last whole chunk read zeros (UNI: num_records 0) or the sink.
-  // The partial chunk, if the block has it (always its last), follows with per-lane masked loads.
-  const int my_full = my_chunks - (part_rel >= 0 ? 1 : 0);
+  // Every chunk runs through one software pipeline whose loads never sit in a branch (a
+  // conditional load makes the ring slots merge values, and every merge copy waits for all loads
+  // in flight): loads past the block's last chunk read zeros (UNI: num_records 0) or the sink, and
+  // a partial chunk's lanes past the columns read zeros / the sink through per-lane state set once
+  // per chunk (a dword holding 2 valid bytes is read whole: its other 2 lie in the same word).
   // load cursor (uniform): chunk lc, step ls; rows row0 + 8 ls + 4h + i; UNI: lbase = the step's
   // first row at the wave's column
   int lc = 0, ls = 0;
-  int64_t lcol = wave_col0;
-  uint64_t lbase = UNI ? in0 + uint64_t(int64_t(row0) * in_stride + lcol) : 0;
+  int64_t lch = ch_first, lcol = col_of(lch), lsoff = b_first * in_bstride;
+  const uint64_t lrow0 = UNI ? in0 + uint64_t(int64_t(row0) * in_stride) : 0;
+  uint64_t lbase = UNI ? lrow0 + uint64_t(lsoff + lcol) : 0;
   const uint64_t step_bytes = UNI ? uint64_t(8 * in_stride) : 0;
-  [[maybe_unused]] uint64_t loff = uint64_t(lcol) + 4 * c;  // pointer inputs: the lane's byte in the row
+  // pointer inputs: the lane's byte in stripe 0's row pointers
+  [[maybe_unused]] uint64_t loff = uint64_t(lsoff + lcol) + 4 * c;
+  bool lok = valid_of(lch) > 0;  // this lane reads the load cursor's chunk
+  uint32_t voffc[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) voffc[i] = lok ? voff[i] : 0x80000000u;
   auto load_step = [&](uint32_t (&x)[4]) __attribute__((always_inline)) {
     const int rbase = row0 + 8 * ls;
-    const bool live = lc < my_full;
+    const bool live = lc < my_chunks;
     if constexpr (UNI) {  // one raw buffer resource; rows past k fall outside num_records and read 0
       // (readfirstlane: the resource is provably uniform, no waterfall)
       const int rem = live ? k - rbase : 0;
@@ -271,7 +296,7 @@ __global__ __launch_bounds__(kThreads, 1) void gf_gemm16_fp4_kernel(cptr<uint64_
                          uint32_t(__builtin_amdgcn_readfirstlane(int(uint32_t(lbase))));
       const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(b), 0, nrec, kRsrcWord3);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) x[i] = __builtin_amdgcn_raw_buffer_load_b32(rs, int(voff[i]), 0, kLoadNT);
+      for (int i = 0; i < 4; ++i) x[i] = __builtin_amdgcn_raw_buffer_load_b32(rs, int(voffc[i]), 0, kLoadNT);
       lbase += step_bytes;
     } else {  // the lane's 4 row pointers from the LDS table (two 16-byte reads)
       const i32x4* tp = reinterpret_cast<const i32x4*>(itab + 8 * ls + 4 * h);
@@ -282,37 +307,44 @@ __global__ __launch_bounds__(kThreads, 1) void gf_gemm16_fp4_kernel(cptr<uint64_
                              uint64_t(uint32_t(q1[2])) | (uint64_t(uint32_t(q1[3])) << 32)};
 #pragma unroll
       for (int i = 0; i < 4; ++i)
-        x[i] = __builtin_nontemporal_load((gptr<const uint32_t>)(live ? p[i] + loff : my_sink));
+        x[i] = __builtin_nontemporal_load((gptr<const uint32_t>)(live && lok ? p[i] + loff : my_sink));
     }
     if (++ls == S) {
       ls = 0;
       ++lc;
-      lcol += chunk_step;
-      if constexpr (UNI) lbase = in0 + uint64_t(int64_t(row0) * in_stride + lcol);
-      if constexpr (!UNI) loff = uint64_t(lcol) + 4 * c;
+      advance(lch, lcol, lsoff, in_bstride);
+      if constexpr (UNI) lbase = lrow0 + uint64_t(lsoff + lcol);
+      if constexpr (!UNI) loff = uint64_t(lsoff + lcol) + 4 * c;
+      lok = valid_of(lch) > 0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) voffc[i] = lok ? voff[i] : 0x80000000u;
     }
   };
 
-  // compute cursor (uniform): chunk cc, step cs, wave column ccol
+  // compute cursor (uniform): chunk cc, step cs, wave column ccol, the lane's valid bytes cnv
   int cc = 0, cs = 0;
-  int64_t ccol = wave_col0;
+  int64_t cch = ch_first, ccol = col_of(cch);
+  int64_t csoff = b_first * out_bstride;  // the chunk's stripe offset of outputs and copies
+  uint64_t cout = uint64_t(csoff);
+  int cnv = valid_of(cch);
   [[maybe_unused]] int cturn = 0;  // COPY: this group stores step cs's copies when cturn == g
   [[maybe_unused]] uint32_t old[MG][2] = {};
   auto chunk_start = [&]() __attribute__((always_inline)) {
     if constexpr (ACC) {  // the previous passes' outputs of the chunk, read S steps ahead of their use
-      const bool live = cc < my_full;
+      const bool live = cc < my_chunks && cnv > 0;
 #pragma unroll
       for (int mt = 0; mt < MG; ++mt)
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
           const uint64_t o = optr[mt][u];
-          old[mt][u] = __builtin_nontemporal_load((gptr<const uint32_t>)(live && o ? o + uint64_t(ccol) + 4 * c : my_sink));
+          old[mt][u] =
+              __builtin_nontemporal_load((gptr<const uint32_t>)(live && o ? o + cout + uint64_t(ccol) + 4 * c : my_sink));
         }
     }
     if constexpr (COPY) cturn = 0;
   };
-  // one K-step on the 4 input dwords x (nv: the lane's valid bytes of the chunk, for the stores)
-  auto consume = [&](const uint32_t (&x)[4], int nv) __attribute__((always_inline)) {
+  // one K-step on the 4 input dwords x
+  auto consume = [&](const uint32_t (&x)[4]) __attribute__((always_inline)) {
     i32x4 af[MG][4];
 #pragma unroll
     for (int mt = 0; mt < MG; ++mt)
@@ -328,7 +360,7 @@ __global__ __launch_bounds__(kThreads, 1) void gf_gemm16_fp4_kernel(cptr<uint64_
                                 uint64_t(uint32_t(q1[2])) | (uint64_t(uint32_t(q1[3])) << 32)};
 #pragma unroll
         for (int i = 0; i < 4; ++i)
-          if (cp[i]) store_masked(cp[i] + uint64_t(ccol) + 4 * c, x[i], nv);
+          if (cp[i]) store_masked(cp[i] + cout + uint64_t(ccol) + 4 * c, x[i], cnv);
       }
       cturn = cturn + 1 == groups ? 0 : cturn + 1;
     }
@@ -373,20 +405,22 @@ __global__ __launch_bounds__(kThreads, 1) void gf_gemm16_fp4_kernel(cptr<uint64_
                                              __builtin_amdgcn_perm(y[0][1], y[0][0], 0x0c0c0400u), 0x05040100u);
           if constexpr (ACC) w ^= old[mt][u];
           const uint64_t o = optr[mt][u];
-          store_masked(o ? o + uint64_t(ccol) + 4 * c : my_sink, w, o ? nv : 4);
+          store_masked(o ? o + cout + uint64_t(ccol) + 4 * c : my_sink, w, o ? cnv : 4);
         }
       }
       bias_init();
       cs = 0;
       ++cc;
-      ccol += chunk_step;
+      advance(cch, ccol, csoff, out_bstride);
+      cout = uint64_t(csoff);
+      cnv = valid_of(cch);
       chunk_start();
     }
   };
 
   bias_init();
   chunk_start();
-  const int total_steps = my_full * S;
+  const int total_steps = my_chunks * S;
   uint32_t ring[kDepth][4];
 #pragma unroll
   for (int d = 0; d < kDepth; ++d) load_step(ring[d]);
@@ -397,27 +431,8 @@ __global__ __launch_bounds__(kThreads, 1) void gf_gemm16_fp4_kernel(cptr<uint64_
       uint32_t x[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) x[i] = ring[d][i];
-      load_step(ring[d]);  // kDepth steps ahead (past the whole chunks: zeros / the sink)
-      consume(x, 4);
-    }
-  }
-  if (part_rel >= 0) {  // the partial chunk (cc == my_full): per-lane masked loads, no pipeline
-    if constexpr (ACC) {
-#pragma unroll
-      for (int mt = 0; mt < MG; ++mt)
-#pragma unroll
-        for (int u = 0; u < 2; ++u)
-          old[mt][u] = optr[mt][u] ? load_masked(optr[mt][u] + uint64_t(ccol) + 4 * c, tail_valid) : 0u;
-    }
-    for (int s = 0; s < S; ++s) {
-      uint32_t x[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int r = min(row0 + 8 * s + 4 * h + i, k - 1);  // rows past k meet zero bit-matrix columns
-        const uint64_t base = UNI ? in0 + uint64_t(int64_t(r) * in_stride) : itab[r - row0];
-        x[i] = load_masked(base + uint64_t(ccol) + 4 * c, tail_valid);
-      }
-      consume(x, tail_valid);
+      load_step(ring[d]);  // kDepth steps ahead (past the block's chunks: zeros / the sink)
+      consume(x);
     }
   }
 }
@@ -462,10 +477,18 @@ Geo16 geometry16(int k, int m, int mg_cap, bool copy) {
 
 size_t bitmat16_matrix_bytes(const Geo16& g) { return size_t(g.passes) * g.groups * g.S * g.mg * 4 * 64 * 16; }
 
+struct Args16 {
+  cptr<uint64_t> in, out, copy;
+  const uint8_t* bitmat;
+  int k, m;
+  int64_t col0, nchunks, in_stride;
+  uint64_t sink;
+  int tail;
+  int64_t fps, in_bstride, out_bstride;  // batched: whole chunks per stripe, stripe strides
+};
+
 template <int MG, bool UNI, bool COPY, bool ACC>
-hipError_t launch16_pass(const Geo16& geo, cptr<uint64_t> in, cptr<uint64_t> out, cptr<uint64_t> copy,
-                         const uint8_t* bitmat, int k, int m, int pass, int64_t col0, int64_t nchunks, int64_t in_stride,
-                         uint64_t sink, int tail, hipStream_t stream) {
+hipError_t launch16_pass(const Geo16& geo, const Args16& a, int pass, hipStream_t stream) {
   const void* f = reinterpret_cast<const void*>(&gf_gemm16_fp4_kernel<MG, UNI, COPY, ACC>);
   hipError_t e = ensure_lds_optin(f);
   if (e != hipSuccess) return e;
@@ -476,37 +499,62 @@ hipError_t launch16_pass(const Geo16& geo, cptr<uint64_t> in, cptr<uint64_t> out
     return o;
   });
   if (occ <= 0) return hipErrorInvalidConfiguration;
-  const int64_t slots = persistent_slots(std::min(occ, 4), geo.groups, nchunks);
+  const int64_t slots = persistent_slots(std::min(occ, 4), geo.groups, a.nchunks);
   const unsigned blocks = unsigned(slots * geo.groups);
-  const i32x4* bm = reinterpret_cast<const i32x4*>(bitmat) + size_t(pass) * geo.groups * geo.S * MG * 4 * 64;
+  const i32x4* bm = reinterpret_cast<const i32x4*>(a.bitmat) + size_t(pass) * geo.groups * geo.S * MG * 4 * 64;
   gf_gemm16_fp4_kernel<MG, UNI, COPY, ACC><<<blocks, kThreads, geo.lds, stream>>>(
-      in, out, copy, bm, k, m, pass * 8 * geo.S, geo.S, geo.groups, col0, nchunks, slots, in_stride, sink, tail);
+      a.in, a.out, a.copy, bm, a.k, a.m, pass * 8 * geo.S, geo.S, geo.groups, a.col0, a.nchunks, slots,
+      UNI ? a.in_stride : 0, a.sink, a.tail, a.fps, a.in_bstride, a.out_bstride);
   return hipGetLastError();
 }
 
 template <int MG>
-hipError_t launch16_mg(const Geo16& geo, cptr<uint64_t> in, cptr<uint64_t> out, cptr<uint64_t> copy,
-                       const uint8_t* bitmat, int k, int m, int64_t col0, int64_t nchunks, int64_t in_stride,
-                       uint64_t sink, int tail, hipStream_t stream) {
+hipError_t launch16_mg(const Geo16& geo, const Args16& a, hipStream_t stream) {
   for (int p = 0; p < geo.passes; ++p) {
     hipError_t e;
     const bool acc = p > 0;
-    if (copy) {
-      e = acc ? launch16_pass<MG, false, true, true>(geo, in, out, copy, bitmat, k, m, p, col0, nchunks, 0, sink, tail, stream)
-              : launch16_pass<MG, false, true, false>(geo, in, out, copy, bitmat, k, m, p, col0, nchunks, 0, sink, tail, stream);
-    } else if (in_stride) {
-      e = acc ? launch16_pass<MG, true, false, true>(geo, in, out, copy, bitmat, k, m, p, col0, nchunks, in_stride, sink,
-                                                     tail, stream)
-              : launch16_pass<MG, true, false, false>(geo, in, out, copy, bitmat, k, m, p, col0, nchunks, in_stride, sink,
-                                                      tail, stream);
+    if (a.copy) {
+      e = acc ? launch16_pass<MG, false, true, true>(geo, a, p, stream)
+              : launch16_pass<MG, false, true, false>(geo, a, p, stream);
+    } else if (a.in_stride) {
+      e = acc ? launch16_pass<MG, true, false, true>(geo, a, p, stream)
+              : launch16_pass<MG, true, false, false>(geo, a, p, stream);
     } else {
-      e = acc ? launch16_pass<MG, false, false, true>(geo, in, out, copy, bitmat, k, m, p, col0, nchunks, 0, sink, tail, stream)
-              : launch16_pass<MG, false, false, false>(geo, in, out, copy, bitmat, k, m, p, col0, nchunks, 0, sink,
-                                                       tail, stream);
+      e = acc ? launch16_pass<MG, false, false, true>(geo, a, p, stream)
+              : launch16_pass<MG, false, false, false>(geo, a, p, stream);
     }
     if (e != hipSuccess) return e;
   }
   return hipSuccess;
+}
+
+// The matrix-core launch over `batch` stripes' chunks: each stripe's whole chunks plus its ragged
+// rest as one partial chunk
+hipError_t launch16(const void* bitmat, const void* desc, int k, int m, int batch, int64_t col0, int64_t full,
+                    int tail, int mg_cap, int64_t in_stride, int64_t in_bstride, int64_t out_bstride, bool copies,
+                    hipStream_t stream) {
+  const int m_pad = pad_m(m);
+  const DescLayout l = desc_layout16(k, m_pad, batch);
+  const char* b = static_cast<const char*>(desc);
+  const Geo16 geo = geometry16(k, m, mg_cap, true);
+  Args16 a{};
+  a.in = (cptr<uint64_t>)(b + l.in_off);
+  a.out = (cptr<uint64_t>)(b + l.out_off);
+  a.copy = copies ? (cptr<uint64_t>)(b + l.copy_off) : nullptr;
+  a.bitmat = static_cast<const uint8_t*>(bitmat);
+  a.k = k;
+  a.m = m;
+  a.col0 = col0;
+  a.fps = full + (tail ? 1 : 0);
+  a.nchunks = a.fps * batch;
+  // uniform-stride inputs address rows as the step's first row + 32-bit lane offsets (8 rows)
+  a.in_stride = (copies || in_stride <= 0 || in_stride > (int64_t(1) << 28)) ? 0 : in_stride;
+  a.sink = reinterpret_cast<uint64_t>(bitmat) + bitmat16_matrix_bytes(geo);
+  a.tail = tail;
+  a.in_bstride = in_bstride;
+  a.out_bstride = out_bstride;
+  if (a.nchunks == 0) return hipSuccess;
+  return geo.mg == 2 ? launch16_mg<2>(geo, a, stream) : launch16_mg<1>(geo, a, stream);
 }
 
 }  // namespace
@@ -529,35 +577,24 @@ hipError_t launch_fp16_bitmat(const uint16_t* coeff, int ld, const int* sel, int
 hipError_t launch_gf_gemm16_fp4(const void* bitmat, const void* desc, int k, int m, int64_t col0, int64_t ncols,
                                 int mg_cap, int64_t in_stride, bool copies, hipStream_t stream) {
   if (k <= 0 || m <= 0 || ncols < 0 || ((col0 | ncols) & 1) || mg_cap < 1) return hipErrorInvalidValue;
-  const int m_pad = pad_m(m);
-  const DescLayout l = desc_layout16(k, m_pad);
-  const char* b = static_cast<const char*>(desc);
-  const Geo16 geo = geometry16(k, m, mg_cap, true);
-  // whole chunks plus the ragged rest as one partial chunk, all on the matrix cores (a
-  // start off a 4-byte boundary: the v_perm records)
-  const int64_t full = (col0 & 3) ? 0 : ncols / kChunkBytes;
-  const int tail = (col0 & 3) ? 0 : int(ncols % kChunkBytes);
-  const int64_t nchunks = full + (tail ? 1 : 0);
-  if (nchunks > 0) {
-    cptr<uint64_t> in = (cptr<uint64_t>)(b + l.in_off);
-    cptr<uint64_t> out = (cptr<uint64_t>)(b + l.out_off);
-    cptr<uint64_t> copy = copies ? (cptr<uint64_t>)(b + l.copy_off) : nullptr;
-    const uint64_t sink = reinterpret_cast<uint64_t>(bitmat) + bitmat16_matrix_bytes(geo);
-    const auto* bm = static_cast<const uint8_t*>(bitmat);
-    // uniform-stride inputs address rows as the step's first row + 32-bit lane offsets (8 rows);
-    // pointer inputs as row pointer + 32-bit column
-    const int64_t stride = (copies || in_stride <= 0 || in_stride > (int64_t(1) << 28)) ? 0 : in_stride;
-    if (!stride && col0 + ncols + kChunkBytes > (int64_t(1) << 32))
-      return launch_gf_gemm16(desc, k, m_pad, col0, ncols, false, 0, stream);
-    hipError_t e;
-    switch (geo.mg) {
-      case 2: e = launch16_mg<2>(geo, in, out, copy, bm, k, m, col0, nchunks, stride, sink, tail, stream); break;
-      default: e = launch16_mg<1>(geo, in, out, copy, bm, k, m, col0, nchunks, stride, sink, tail, stream); break;
-    }
-    return e;
-  }
-  if (ncols > 0) return launch_gf_gemm16(desc, k, m_pad, col0, ncols, false, 0, stream);
-  return hipSuccess;
+  if (col0 & 3)  // a start off a 4-byte boundary: the v_perm records
+    return ncols > 0 ? launch_gf_gemm16(desc, k, pad_m(m), col0, ncols, false, 0, stream) : hipSuccess;
+  // whole chunks plus the ragged rest as one partial chunk, all on the matrix cores
+  return launch16(bitmat, desc, k, m, 1, col0, ncols / kChunkBytes, int(ncols % kChunkBytes), mg_cap, in_stride, 0, 0,
+                  copies, stream);
+}
+
+hipError_t launch_gf_gemm16_fp4_batched(const void* bitmat, const void* desc, int k, int m, int batch, int64_t col0,
+                                        int64_t ncols, int mg_cap, int64_t in_stride, int64_t in_bstride,
+                                        int64_t out_bstride, bool copies, hipStream_t stream) {
+  if (k <= 0 || m <= 0 || ncols < 0 || ((col0 | ncols) & 1) || mg_cap < 1 || batch < 1 || batch > 65535)
+    return hipErrorInvalidValue;
+  if (batch == 1) return launch_gf_gemm16_fp4(bitmat, desc, k, m, col0, ncols, mg_cap, in_stride, copies, stream);
+  if (col0 & 3)  // a start off a 4-byte boundary: the batched v_perm kernel
+    return launch_gf_gemm16_batched(desc, k, pad_m(m), batch, col0, ncols, false, 0, stream);
+  // every stripe's whole chunks and its partial one, all in one launch per K pass
+  return launch16(bitmat, desc, k, m, batch, col0, ncols / kChunkBytes, int(ncols % kChunkBytes), mg_cap, in_stride,
+                  in_bstride, out_bstride, copies, stream);
 }
 
 }  // namespace gfrs

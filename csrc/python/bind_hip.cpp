@@ -220,6 +220,20 @@ PYBIND11_MODULE(_hip, m) {
                              reinterpret_cast<void*>(bitmat), mg_cap, as_stream(stream)),
           "fp16_bitmat");
   });
+  m.def("gemm16_batched", [](uint64_t desc, int k, int m_pad, int batch, int64_t col0, int64_t ncols, bool symwise,
+                             uint64_t stream) {
+    check(launch_gf_gemm16_batched(reinterpret_cast<const void*>(desc), k, m_pad, batch, col0, ncols, symwise, 0,
+                                   as_stream(stream)),
+          "gf_gemm16_batched");
+  });
+  m.def("gemm16_fp4_batched", [](uint64_t bitmat, uint64_t desc, int k, int mm, int batch, int64_t col0, int64_t ncols,
+                                 int mg_cap, int64_t in_stride, int64_t in_bstride, int64_t out_bstride, bool copies,
+                                 uint64_t stream) {
+    check(launch_gf_gemm16_fp4_batched(reinterpret_cast<const void*>(bitmat), reinterpret_cast<const void*>(desc), k,
+                                       mm, batch, col0, ncols, mg_cap, in_stride, in_bstride, out_bstride, copies,
+                                       as_stream(stream)),
+          "gf_gemm16_fp4_batched");
+  });
   m.def("gemm16_fp4", [](uint64_t bitmat, uint64_t desc, int k, int mm, int64_t col0, int64_t ncols, int mg_cap,
                          int64_t in_stride, bool copies, uint64_t stream) {
     check(launch_gf_gemm16_fp4(reinterpret_cast<const void*>(bitmat), reinterpret_cast<const void*>(desc), k, mm, col0,

@@ -292,8 +292,6 @@ class ReedSolomon:
         batched descriptor (grid.y = stripe) amortises it (serving path)."""
         if data.dim() != 3 or data.shape[1] != self.k:
             raise ValueError(f"expected [B, {self.k}, C]")
-        if self.wide:
-            raise ValueError("batched launches run GF(2^8) / GF(16) codes; encode GF(2^16) stripes one at a time")
         B, _, C = data.shape
         if parity is None:
             pitch = row_pitch(C, data.device)
@@ -308,8 +306,11 @@ class ReedSolomon:
         key = ("encb", int(data.data_ptr()), tuple(data.stride()), tuple(data.shape), int(parity.data_ptr()))
         plan = self._plans.get(key)
         if plan is None:
-            maps = self._maps(self.E)
-            plan = GemmPlan(data, parity, None if maps is not None else self.E, maps=maps, hold_buffers=False)
+            if self.wide:  # GF(2^16): matrix cores for stripes at fixed strides, else batched v_perm
+                plan = Gemm16Plan(data, parity, self.E, hold_buffers=False)
+            else:
+                maps = self._maps(self.E)
+                plan = GemmPlan(data, parity, None if maps is not None else self.E, maps=maps, hold_buffers=False)
             self._plans[key] = plan
         plan.run(stream)
         return parity
@@ -321,8 +322,6 @@ class ReedSolomon:
         surviving natives are copied in the same pass (batched fused copy) and the plan is cached
         per (buffers, pattern), so a repeated call is one kernel launch."""
         rows = [int(r) for r in rows]
-        if self.wide:
-            raise ValueError("batched launches run GF(2^8) / GF(16) codes; decode GF(2^16) stripes one at a time")
         B, k, C = survivors.shape
         if k != self.k:
             raise ValueError(f"expected [B, {self.k}, C]")
@@ -346,12 +345,16 @@ class ReedSolomon:
                int(out.data_ptr()), tuple(out.stride()))
         plan = self._plans.get(key)
         if plan is None:
-            dm = self.decode_matrix(rows)[erased]
-            maps = self._maps(dm)
             outs = [[out[b, i] for i in erased] for b in range(B)]
             ins = [[survivors[b, j] for j in range(self.k)] for b in range(B)]
             copies = [[out[b, r] if r < self.k else None for r in rows] for b in range(B)]
-            plan = GemmPlan(ins, outs, None if maps is not None else dm, maps=maps, copies=copies, hold_buffers=False)
+            if self.wide:
+                plan = Gemm16Plan(ins, outs, self._erased_rows(rows, erased), copies=copies, hold_buffers=False)
+            else:
+                dm = self.decode_matrix(rows)[erased]
+                maps = self._maps(dm)
+                plan = GemmPlan(ins, outs, None if maps is not None else dm, maps=maps, copies=copies,
+                                hold_buffers=False)
             self._plans[key] = plan
         plan.run(stream)
         return out

@@ -510,9 +510,9 @@ def _pack16(coeff) -> bytes:
     return np.ascontiguousarray(np.asarray(coeff, dtype=np.int64).astype("<u2")).tobytes()
 
 
-def desc_layout16(k: int, m_pad: int) -> DescLayout:
+def desc_layout16(k: int, m_pad: int, batch: int = 1) -> DescLayout:
     """Mirror of ``gfrs::desc_layout16``: four 32-byte records per coefficient."""
-    lay = desc_layout(k, m_pad)
+    lay = desc_layout(k, m_pad, batch)
     return DescLayout(lay.in_off, lay.copy_off, lay.out_off, lay.tab_off, lay.tab_off + 4 * 32 * k * m_pad)
 
 
@@ -524,12 +524,17 @@ class Gemm16Plan:
     GF(2^8) was ever built; here it runs on the same v_perm engine as four byte maps per coefficient.
 
     Args:
-        inputs: k byte rows (2-D uint8 tensor or list of 1-D tensors) on one GPU, 2-byte aligned.
-        outputs: m byte rows on the same GPU.
+        inputs: k byte rows (2-D uint8 tensor or list of 1-D tensors) on one GPU, 2-byte aligned;
+            or B stripes ([B, k, C] tensor or list of row lists) for one batched launch.
+        outputs: m byte rows on the same GPU (batched: [B, m, C] or B row lists).
         coeff: (m, k) GF(2^16) coefficients (uint16-valued); or None with ``device_tables=True``
             (the tables are written later on the device, :func:`~gpu_rscode_amd.ops.inverse.PatternDecoder`).
-        copies: optional k destination rows (or None entries): fused survivor copy of decode.
+        copies: optional k destination rows (or None entries): fused survivor copy of decode
+            (batched: one such list per stripe).
         hold_buffers: as :class:`GemmPlan`.
+    Batched stripes whose rows sit at fixed strides from stripe 0's run the matrix-core engine in one
+    persistent launch; otherwise (and with ``engine="valu16"``) the v_perm kernels take grid.y =
+    stripe.
     Rows shorter than the others bound the column range, which must be a whole number of symbols.
     """
 
@@ -537,14 +542,38 @@ class Gemm16Plan:
                  engine: str = "auto", mfma_mg: int = 2, hold_buffers: bool = True):
         if coeff is None and not device_tables:
             raise ValueError("need coeff or device_tables=True")
+        bi, bo = _batched_rows(inputs), _batched_rows(outputs)
+        if (bi is None) != (bo is None):
+            raise ValueError("inputs and outputs must both be batched ([B, rows, C]) or both not")
+        self.batch = 1
+        stripes_copy = None
+        if bi is not None:
+            if len(bi) != len(bo) or not 1 <= len(bi) <= 65535:
+                raise ValueError("batched plan needs 1..65535 stripes in inputs and outputs")
+            if any(len(st) != len(bi[0]) for st in bi) or any(len(st) != len(bo[0]) for st in bo):
+                raise ValueError("every stripe needs the same number of input / output rows")
+            self.batch = len(bi)
+            if copies is not None:
+                if len(copies) != self.batch or any(len(c) != len(bi[0]) for c in copies):
+                    raise ValueError("batched copies need one list of k destinations per stripe")
+                stripes_copy = [list(c) for c in copies]
+                copies = stripes_copy[0]
+            inputs, outputs = bi[0], bo[0]
+        else:
+            bi, bo = [_rows(inputs)], [_rows(outputs)]
+            if copies is not None:
+                stripes_copy = [list(copies)]
         self.inputs, self.outputs = _rows(inputs), _rows(outputs)
         self.copies = None if copies is None else list(copies)
-        dev = _check_rows(self.inputs, "input", None)
-        dev = _check_rows(self.outputs, "output", dev)
-        if self.copies is not None:
-            if len(self.copies) != len(self.inputs):
-                raise ValueError("copies must have one entry per input row")
-            dev = _check_rows([c for c in self.copies if c is not None], "copy", dev)
+        if self.copies is not None and len(self.copies) != len(self.inputs):
+            raise ValueError("copies must have one entry per input row")
+        all_in = [r for st in bi for r in st]
+        all_out = [r for st in bo for r in st]
+        all_copy = [c for st in (stripes_copy or []) for c in st if c is not None]
+        dev = _check_rows(all_in, "input", None)
+        dev = _check_rows(all_out, "output", dev)
+        if all_copy:
+            dev = _check_rows(all_copy, "copy", dev)
         if dev.type != "cuda":
             raise ValueError("Gemm16Plan runs on a GPU; use the CPU codec for host tensors")
         self.device = dev
@@ -552,7 +581,7 @@ class Gemm16Plan:
         if not (1 <= self.k <= 65535 and 1 <= self.m <= 65535):
             raise ValueError("GF(2^16) GEMM supports 1 <= k, m <= 65535")
         self.m_pad = pad_m(self.m)
-        rows = self.inputs + self.outputs + [c for c in (self.copies or []) if c is not None]
+        rows = all_in + all_out + all_copy
         self.ncols = min(r.numel() for r in rows)
         if self.ncols % 2:
             raise ValueError("GF(2^16) rows hold 16-bit symbols: the column range must be an even byte count")
@@ -564,18 +593,25 @@ class Gemm16Plan:
             coeff = np.asarray(coeff, dtype=np.int64).reshape(self.m, self.k)
             if coeff.min() < 0 or coeff.max() > 65535:
                 raise ValueError("GF(2^16) coefficients must be in [0, 65535]")
-        self.layout = desc_layout16(self.k, self.m_pad)
+        self.layout = desc_layout16(self.k, self.m_pad, self.batch)
         lay = self.layout
         host = np.zeros(lay.bytes, dtype=np.uint8)
-        host[0:16] = np.frombuffer(np.array([self.k, self.m, self.m_pad, 1], dtype="<i4").tobytes(), dtype=np.uint8)
+        host[0:16] = np.frombuffer(np.array([self.k, self.m, self.m_pad, self.batch], dtype="<i4").tobytes(),
+                                   dtype=np.uint8)
 
         def put(off, vals):
             b = np.frombuffer(np.array(vals, dtype="<u8").tobytes(), dtype=np.uint8)
             host[off: off + b.size] = b
-        put(lay.in_off, [ptr(r) for r in self.inputs])
-        if self.copies is not None:
-            put(lay.copy_off, [ptr(c) if c is not None else 0 for c in self.copies])
-        put(lay.out_off, [ptr(r) for r in self.outputs] + [0] * (self.m_pad - self.m))
+        put(lay.in_off, [ptr(r) for r in all_in])
+        if stripes_copy is not None:
+            put(lay.copy_off, [ptr(c) if c is not None else 0 for st in stripes_copy for c in st])
+        put(lay.out_off, [v for st in bo for v in [ptr(r) for r in st] + [0] * (self.m_pad - self.m)])
+        # batched matrix-core launches address stripe b's rows as stripe 0's plus b fixed strides
+        self.in_bstride = self.out_bstride = None
+        if self.batch > 1:
+            strides = _batch_strides(bi, bo, stripes_copy)
+            if strides is not None:
+                self.in_bstride, self.out_bstride = strides
         if coeff is not None:  # else written on the device (decode_system16_into_plan)
             t = np.zeros((self.k, self.m_pad, 4, 8), dtype="<u4")
             t[:, : self.m] = np.transpose(gf.perm_quads16(coeff), (1, 0, 2, 3))
@@ -583,10 +619,14 @@ class Gemm16Plan:
         self.desc = torch.from_numpy(host).to(self.device)
         if engine == "auto":
             engine = "mfma" if _auto_engine16(self.k, self.m, self.symwise, self.copies is not None) else "valu16"
+            if self.batch > 1 and self.in_bstride is None:
+                engine = "valu16"  # scattered stripes: the batched v_perm kernel (per-stripe pointers)
         if engine == "valu":
             engine = "valu16"
         if engine not in ("valu16", "mfma"):
             raise ValueError(f"unknown GF(2^16) engine {engine!r}")
+        if engine == "mfma" and self.batch > 1 and self.in_bstride is None:
+            raise ValueError("batched engine='mfma' needs stripes at fixed strides (one [B, rows, C] allocation)")
         self.engine = engine
         self.bitmat = None
         self.has_copies = self.copies is not None
@@ -604,6 +644,7 @@ class Gemm16Plan:
             if coeff is not None:
                 self.set_device_coeff(torch.from_numpy(np.ascontiguousarray(coeff.astype("<u2")).view(np.int16))
                                       .to(self.device))
+        self._stripes = (bi, bo, stripes_copy) if hold_buffers else None
         if not hold_buffers:
             self.inputs = self.outputs = self.copies = None
         self._ready = torch.cuda.Event()
@@ -645,6 +686,15 @@ class Gemm16Plan:
             self._ready = None
         if stream is not None:
             self.desc.record_stream(stream)
+        if self.batch > 1:
+            if self.engine == "mfma":
+                hip().gemm16_fp4_batched(int(self.bitmat.data_ptr()), int(self.desc.data_ptr()), self.k, self.m,
+                                         self.batch, col0, ncols, self.mfma_mg, self.in_stride, self.in_bstride,
+                                         self.out_bstride, self.has_copies, st.cuda_stream)
+            else:
+                hip().gemm16_batched(int(self.desc.data_ptr()), self.k, self.m_pad, self.batch, col0, ncols,
+                                     self.symwise, st.cuda_stream)
+            return
         if self.engine == "mfma" and max_blocks == 0 and col0 % 4 == 0:
             hip().gemm16_fp4(int(self.bitmat.data_ptr()), int(self.desc.data_ptr()), self.k, self.m, col0, ncols,
                              self.mfma_mg, self.in_stride, self.has_copies, st.cuda_stream)

@@ -48,11 +48,13 @@ def timed(fn, reps: int) -> float:
     return float(np.median(ts))
 
 
-def point(S: int, B: int, reps: int, k: int = 10, n: int = 14, erase: int = 0) -> dict:
+def point(S: int, B: int, reps: int, k: int = 10, n: int = 14, erase: int = 0, field: int = 8) -> dict:
     p = n - k
     C = (S + k - 1) // k
+    if field == 16:
+        C += C % 2  # whole 16-bit symbols
     dev = torch.device("cuda", 0)
-    rs = ReedSolomon(k, n)
+    rs = ReedSolomon(k, n, **({"field": "gf65536", "matrix": "cauchy"} if field == 16 else {}))
     data, dbase = batch_rows(B, k, C, dev)
     fill_random_(dbase, seed=S + B)
     parity, _ = batch_rows(B, p, C, dev)
@@ -85,7 +87,8 @@ def point(S: int, B: int, reps: int, k: int = 10, n: int = 14, erase: int = 0) -
     for j, r in enumerate(rows):  # the survivors as the decode reads them
         surv[:, j].copy_(data[:, r] if r < k else parity[:, r - k])
     torch.cuda.synchronize()
-    res = {"object_bytes": S, "batch": B, "k": k, "n": n, "C": C, "erased_natives": sum(1 for r in range(k) if r not in rows)}
+    res = {"object_bytes": S, "batch": B, "k": k, "n": n, "field": field, "C": C,
+           "erased_natives": sum(1 for r in range(k) if r not in rows)}
     res["enc_batched_us"] = timed(enc_batched, reps)
     res["dec_batched_us"] = timed(dec_batched, reps)
     if B <= 64:
@@ -104,8 +107,12 @@ def point(S: int, B: int, reps: int, k: int = 10, n: int = 14, erase: int = 0) -
     res["enc_dec_graph_us"] = timed(g.replay, reps)
     ok = True
     for b in (0, B - 1):
-        want = gf.GF256.gemm(rs.E, data[b].cpu().numpy())
-        ok = ok and np.array_equal(parity[b].cpu().numpy(), want)
+        if field == 16:
+            want = gf.field(16).gemm(rs.E, np.ascontiguousarray(data[b].cpu().numpy()).view("<u2"))
+            ok = ok and np.array_equal(parity[b].cpu().numpy().view("<u2"), want)
+        else:
+            want = gf.GF256.gemm(rs.E, data[b].cpu().numpy())
+            ok = ok and np.array_equal(parity[b].cpu().numpy(), want)
     ok = ok and torch.equal(out, data)
     res["verified"] = bool(ok)
     obj = B / 1e6
@@ -127,12 +134,13 @@ def main() -> int:
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--code", default="10:14", help="k:n of the code (default the headline's RS(10,14))")
     ap.add_argument("--erase", type=int, default=0, help="natives lost per object (0: the default pattern)")
+    ap.add_argument("--field", type=int, default=8, choices=[8, 16], help="16: GF(2^16) symbols (Cauchy code)")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     pts = []
     for S in map(int, a.sizes.split(",")):
         for B in map(int, a.batches.split(",")):
-            r = point(S, B, a.reps, *(int(v) for v in a.code.split(":")), erase=a.erase)
+            r = point(S, B, a.reps, *(int(v) for v in a.code.split(":")), erase=a.erase, field=a.field)
             print(json.dumps(r), flush=True)
             pts.append(r)
             torch.cuda.empty_cache()

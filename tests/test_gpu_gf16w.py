@@ -237,3 +237,46 @@ def test_gemm16_fp4_fused_copies_and_device_decoder():
         torch.cuda.synchronize()
         assert int(dec.status.item()) == 0 and dec.erased.tolist() == erased
         assert torch.equal(out, data)
+
+
+@pytest.mark.parametrize("engine_env", ["0", "1"])
+@pytest.mark.parametrize("k,n,C,B", [(300, 340, 1024 * 3 + 208, 5), (64, 80, 1024 * 3, 9), (16, 20, 2 * 333, 17)])
+def test_batched_w16_encode_decode(k, n, C, B, engine_env, monkeypatch):
+    """GF(2^16) batched launches (ReedSolomon.encode_batch / decode_batch): B stripes in one call,
+    on the matrix cores (stripes at fixed strides; every stripe's ragged rest on the batched v_perm
+    kernel) and on the batched v_perm kernel alone; decode copies the survivors in the same pass."""
+    monkeypatch.setenv("GFRS_GF16_MFMA", engine_env)
+    rs = ReedSolomon(k, n, field="gf65536", matrix="cauchy")
+    data = torch.stack([_rand(k, C, 100 + b) for b in range(B)]).cuda()
+    par = rs.encode_batch(data)
+    torch.cuda.synchronize()
+    d_host = data.cpu().numpy()
+    for b in (0, B // 2, B - 1):
+        assert np.array_equal(par[b].cpu().numpy().view("<u2"), _oracle(rs.E, d_host[b]))
+    rng = np.random.default_rng(k + B)
+    erased = sorted(rng.choice(k, size=min(n - k, k), replace=False).tolist())
+    rows = [r for r in range(n) if r not in set(erased)][:k]
+    surv = torch.stack([torch.stack([data[b, r] if r < k else par[b, r - k] for r in rows]) for b in range(B)])
+    out = rs.decode_batch(surv, rows)
+    torch.cuda.synchronize()
+    assert torch.equal(out, data)
+
+
+def test_batched_w16_scattered_stripes_fall_back_to_vperm():
+    """Stripes that are not at fixed strides cannot take the batched matrix-core launch: the plan
+    keeps the per-stripe pointer tables of the batched v_perm kernel."""
+    k, m, C, B = 64, 16, 2048, 4
+    rng = np.random.default_rng(4)
+    coeff = rng.integers(0, 65536, size=(m, k))
+    ins = [[alloc_rows(k, C, "cuda")[j] for j in range(k)] for _ in range(B)]  # separate allocations
+    for st in ins:
+        for r in st:
+            r.copy_(torch.from_numpy(rng.integers(0, 256, C, dtype=np.uint8)))
+    outs = [[alloc_rows(m, C, "cuda", fill=0)[i] for i in range(m)] for _ in range(B)]
+    plan = Gemm16Plan(ins, outs, coeff)
+    assert plan.batch == B and plan.in_bstride is None and plan.engine == "valu16"
+    plan.run()
+    torch.cuda.synchronize()
+    for b in range(B):
+        x = torch.stack(ins[b]).cpu().numpy()
+        assert np.array_equal(torch.stack(outs[b]).cpu().numpy().view("<u2"), _oracle(coeff, x))
