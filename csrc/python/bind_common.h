@@ -100,6 +100,16 @@ inline void bind_common(py::module_& m) {
     d["bytes"] = l.bytes;
     return d;
   }, py::arg("k"), py::arg("m_pad"), py::arg("batch") = 1);
+  m.def("desc_layout16", [](int k, int m_pad, int batch) {
+    const gfrs::DescLayout l = gfrs::desc_layout16(k, m_pad, batch);
+    py::dict d;
+    d["in_off"] = l.in_off;
+    d["copy_off"] = l.copy_off;
+    d["out_off"] = l.out_off;
+    d["tab_off"] = l.tab_off;
+    d["bytes"] = l.bytes;
+    return d;
+  }, py::arg("k"), py::arg("m_pad"), py::arg("batch") = 1);
   m.def(
       "build_desc",
       [](int k, int mm, const std::vector<uint64_t>& in, const std::vector<uint64_t>& copy,

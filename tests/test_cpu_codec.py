@@ -51,6 +51,17 @@ def test_desc_layout_python_equals_native(k, m, batch):
         nat["in_off"], nat["copy_off"], nat["out_off"], nat["tab_off"], nat["bytes"])
 
 
+@pytest.mark.parametrize("k,m,batch", [(10, 4, 1), (300, 40, 1), (300, 40, 256), (7, 3, 5), (64, 16, 9)])
+def test_desc_layout16_python_equals_native(k, m, batch):
+    from gpu_rscode_amd.ops.gemm import desc_layout16
+
+    mp = pad_m(m)
+    lay = desc_layout16(k, mp, batch)
+    nat = cpu().desc_layout16(k, mp, batch)
+    assert (lay.in_off, lay.copy_off, lay.out_off, lay.tab_off, lay.bytes) == (
+        nat["in_off"], nat["copy_off"], nat["out_off"], nat["tab_off"], nat["bytes"])
+
+
 def test_build_desc_python_equals_native():
     k, m = 10, 3
     coeff = np.random.default_rng(0).integers(0, 256, size=(m, k), dtype=np.uint8)
