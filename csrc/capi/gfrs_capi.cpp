@@ -85,6 +85,8 @@ struct DevBuf {
 };
 
 constexpr int kMfmaMinK = 64, kMfmaMinM = 16, kMgCap = 8;  // as ops/gemm.py _auto_engine
+// GF(2^16): as ops/gemm.py _auto_engine16 (profiles/gf65536/r08_mfma16)
+constexpr int kMfma16MinK = 16, kMfma16MinM = 4, kMfma16CopyMinM = 8, kMfma16CopyMinKM = 256, kMg16Cap = 2;
 
 class DeviceGuard {  // restores the calling thread's current device
  public:
@@ -207,6 +209,22 @@ std::vector<uint64_t> addrs(const void* const* rows, int n) {
 
 }  // namespace
 
+// ---- GF(2^16) plan ----------------------------------------------------------------------------
+struct gfrs_plan16 {
+  int device = 0, k = 0, m = 0, m_pad = 0, engine = GFRS_ENGINE_VALU;
+  int64_t ncols = 0, in_stride = 0;
+  bool symwise = false, copies = false;
+  DevBuf desc, bitmat, coeff;
+
+  void run(hipStream_t s) const {
+    if (engine == GFRS_ENGINE_MFMA)
+      hip_check(gfrs::launch_gf_gemm16_fp4(bitmat.p, desc.p, k, m, 0, ncols, kMg16Cap, copies ? 0 : in_stride, copies, s),
+                "gf_gemm16_fp4");
+    else
+      hip_check(gfrs::launch_gf_gemm16(desc.p, k, m_pad, 0, ncols, symwise, 0, s), "gf_gemm16");
+  }
+};
+
 // ---- decoder --------------------------------------------------------------------------------
 struct gfrs_decoder {
   int k = 0, n = 0, e = 0;
@@ -255,6 +273,101 @@ int gfrs_encoding_matrix(int kind, int k, int p, uint8_t* e) {
     const gfrs::Mat m = gfrs::encoding_matrix(static_cast<gfrs::MatrixKind>(kind), k, p);
     std::memcpy(e, m.data(), m.size());
   });
+}
+
+int gfrs_encoding_matrix16(int kind, int k, int p, uint16_t* e) {
+  return guarded([&] {
+    need(e && k >= 1 && p >= 1 && k + p <= 65535, "encoding_matrix16: 1 <= k, p and k + p <= 65535");
+    need(kind >= 0 && kind <= 2, "encoding_matrix16: bad kind");
+    const gfrs::gf16w::Mat m = gfrs::encoding_matrix16(static_cast<gfrs::MatrixKind>(kind), k, p);
+    std::copy(m.begin(), m.end(), e);
+  });
+}
+
+int gfrs_decode_rows16(const uint16_t* e, int k, int p, const int* survivors, const int* erased, int n_erased,
+                       uint16_t* rows_out) {
+  return guarded([&] {
+    need(e && survivors && erased && rows_out && k >= 1 && p >= 1 && k + p <= 65535 && n_erased >= 1 &&
+             n_erased <= k,
+         "decode_rows16: bad arguments");
+    std::vector<int> rows(survivors, survivors + k), want(erased, erased + n_erased);
+    for (int r : rows) need(r >= 0 && r < k + p, "decode_rows16: survivor id out of range");
+    for (int w : want) need(w >= 0 && w < k, "decode_rows16: erased native id out of range");
+    const gfrs::gf16w::Mat g = gfrs::gf16w::generator(gfrs::gf16w::Mat(e, e + size_t(p) * k), k, p);
+    gfrs::gf16w::Mat out;
+    if (!gfrs::gf16w::decode_rows(g, k, rows, want, out)) throw Error(GFRS_ESINGULAR, "decode_rows16: pattern not recoverable");
+    std::copy(out.begin(), out.end(), rows_out);
+  });
+}
+
+int gfrs_plan16_create(gfrs_plan16** plan, int device, int k, int m, const uint16_t* coeff, const void* const* in,
+                       void* const* out, void* const* copy, int64_t ncols, int engine) {
+  return guarded([&] {
+    need(plan && coeff && in && out, "plan16_create: plan, coeff, in and out are required");
+    need(k >= 1 && k <= 65535 && m >= 1 && m <= 65535, "plan16_create: 1 <= k, m <= 65535");
+    need(ncols >= 0 && ncols % 2 == 0, "plan16_create: ncols must be an even byte count");
+    need(engine == GFRS_ENGINE_AUTO || engine == GFRS_ENGINE_VALU || engine == GFRS_ENGINE_MFMA,
+         "plan16_create: bad engine");
+    auto p = std::make_unique<gfrs_plan16>();
+    p->device = device;
+    p->k = k;
+    p->m = m;
+    p->m_pad = gfrs::pad_m(m);
+    p->ncols = ncols;
+    const std::vector<uint64_t> iv = addrs(in, k), ov = addrs(const_cast<const void* const*>(out), m);
+    std::vector<uint64_t> cv;
+    if (copy) cv = addrs(const_cast<const void* const*>(copy), k);
+    p->copies = !cv.empty();
+    auto odd = [](uint64_t a) { return a % 2 != 0; };
+    need(std::none_of(iv.begin(), iv.end(), odd) && std::none_of(ov.begin(), ov.end(), odd) &&
+             std::none_of(cv.begin(), cv.end(), odd),
+         "plan16_create: rows must be 2-byte aligned");
+    auto mis16 = [](uint64_t a) { return a % 16 != 0; };
+    p->symwise = std::any_of(iv.begin(), iv.end(), mis16) || std::any_of(ov.begin(), ov.end(), mis16) ||
+                 std::any_of(cv.begin(), cv.end(), [](uint64_t a) { return a && a % 16; });
+    if (engine == GFRS_ENGINE_AUTO) {
+      const bool wide = k >= kMfma16MinK && m >= kMfma16MinM &&
+                        (!p->copies || (m >= kMfma16CopyMinM && int64_t(k) * m >= kMfma16CopyMinKM));
+      engine = (!p->symwise && wide) ? GFRS_ENGINE_MFMA : GFRS_ENGINE_VALU;
+    }
+    need(!(engine == GFRS_ENGINE_MFMA && p->symwise), "plan16_create: the matrix-core engine needs 16-byte aligned rows");
+    p->engine = engine;
+    const gfrs::Mat packed = gfrs::pack16(gfrs::gf16w::Mat(coeff, coeff + size_t(m) * k));
+    const std::vector<uint8_t> host = gfrs::build_desc(k, m, iv, cv, ov, packed, 16);
+    DeviceGuard g(device);
+    p->desc.alloc(host.size());
+    hip_check(hipMemcpy(p->desc.p, host.data(), host.size(), hipMemcpyHostToDevice), "hipMemcpy desc");
+    if (engine == GFRS_ENGINE_MFMA) {
+      const int64_t stride = k > 1 ? int64_t(iv[1] - iv[0]) : 1;
+      bool uniform = stride != 0;
+      for (int j = 0; j < k && uniform; ++j) uniform = int64_t(iv[j] - iv[0]) == j * stride;
+      p->in_stride = uniform ? stride : 0;
+      p->coeff.alloc(size_t(m) * k * 2);
+      hip_check(hipMemcpy(p->coeff.p, coeff, size_t(m) * k * 2, hipMemcpyHostToDevice), "hipMemcpy coeff");
+      p->bitmat.alloc(gfrs::fp16_bitmat_bytes(k, m, kMg16Cap));
+      hip_check(gfrs::launch_fp16_bitmat(static_cast<const uint16_t*>(p->coeff.p), k, nullptr, m, k, p->bitmat.p,
+                                         kMg16Cap, nullptr),
+                "fp16_bitmat");
+      hip_check(hipStreamSynchronize(nullptr), "hipStreamSynchronize");
+    }
+    *plan = p.release();
+  });
+}
+
+int gfrs_plan16_run(gfrs_plan16* p, void* stream) {
+  return guarded([&] {
+    need(p != nullptr, "plan16_run: null plan");
+    DeviceGuard g(p->device);
+    p->run(as_stream(stream));
+  });
+}
+
+int gfrs_plan16_engine(const gfrs_plan16* p) { return p ? p->engine : GFRS_EINVAL; }
+
+void gfrs_plan16_destroy(gfrs_plan16* p) {
+  if (!p) return;
+  DeviceGuard g(p->device, DeviceGuard::NoThrow{});
+  delete p;
 }
 
 int gfrs_decode_matrix(const uint8_t* e, int k, int p, const int* survivors, uint8_t* dm) {

@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define GFRS_API_VERSION 2
+#define GFRS_API_VERSION 3
 
 enum {
   GFRS_OK = 0,
@@ -65,6 +65,24 @@ int gfrs_plan_set_coeff(gfrs_plan* plan, const uint8_t* coeff); /* synchronous *
 int gfrs_plan_run(gfrs_plan* plan, void* stream);
 int gfrs_plan_engine(const gfrs_plan* plan); /* GFRS_ENGINE_VALU or GFRS_ENGINE_MFMA */
 void gfrs_plan_destroy(gfrs_plan* plan);
+
+/* ---- GF(2^16) (API version 3): 16-bit little-endian symbols, poly 0x1100B --------------------- */
+/* e: p x k row-major uint16 (k + p <= 65535); kind as gfrs_encoding_matrix. */
+int gfrs_encoding_matrix16(int kind, int k, int p, uint16_t* e);
+/* rows_out: the erased natives' rows of the decode matrix (len(erased) x k) for survivors[0..k) of
+ * G = [I_k; E] (the e x e systematic solve, not a k x k inverse). GFRS_ESINGULAR if not recoverable. */
+int gfrs_decode_rows16(const uint16_t* e, int k, int p, const int* survivors, const int* erased, int n_erased,
+                       uint16_t* rows_out);
+/* The GF(2^16) device GEMM plan: out[i] = XOR_j coeff[i][j] * in[j] over ncols bytes (even; rows
+ * 2-byte aligned). coeff: m x k host uint16. Engine AUTO picks the FP4 matrix-core kernel (each
+ * coefficient's 16 x 16 GF(2) map) for codes from k = 16 and the v_perm kernel for narrower ones;
+ * copy as gfrs_plan_create (fused survivor copy). */
+typedef struct gfrs_plan16 gfrs_plan16;
+int gfrs_plan16_create(gfrs_plan16** plan, int device, int k, int m, const uint16_t* coeff, const void* const* in,
+                       void* const* out, void* const* copy, int64_t ncols, int engine);
+int gfrs_plan16_run(gfrs_plan16* plan, void* stream);
+int gfrs_plan16_engine(const gfrs_plan16* plan); /* GFRS_ENGINE_VALU or GFRS_ENGINE_MFMA */
+void gfrs_plan16_destroy(gfrs_plan16* plan);
 
 /* ---- decoder with a device-resident erasure pattern ------------------------------------------ */
 /* chunks: the stripe's n = k + p device rows (natives, then parity), out: k device rows, all

@@ -128,7 +128,7 @@ def test_gpu_capi_file_codec_ex_gf65536_zero_copy(lib, tmp_path):
     f = tmp_path / "obj.bin"
     f.write_bytes(data)
     lib.gfrs_last_error.restype = ctypes.c_char_p
-    assert lib.gfrs_api_version() == 2
+    assert lib.gfrs_api_version() >= 2
     assert lib.gfrs_encode_file_ex(str(f).encode(), 300, 40, 1, 16, 1, None, 0, 2, None) == 0, lib.gfrs_last_error()
     assert open(str(f) + ".METADATA").readline() == "GFRS-METADATA 2 16\n"
     conf = tmp_path / "conf"
@@ -139,3 +139,65 @@ def test_gpu_capi_file_codec_ex_gf65536_zero_copy(lib, tmp_path):
     assert out.read_bytes() == data
     assert lib.gfrs_encode_file_ex(str(f).encode(), 4, 2, 0, 12, 0, None, 0, 2, None) == -1  # bad field width
     assert lib.gfrs_release() == 0
+
+
+def test_gf65536_matrices_match_the_oracle(lib):
+    """API version 3: gfrs_encoding_matrix16 equals ReedSolomon(field="gf65536")'s E for every kind,
+    and gfrs_decode_rows16 rebuilds the erased natives (oracle: rows of G applied to the data)."""
+    F = gf.field(16)
+    k, p = 12, 5
+    for kind, name in ((0, "vandermonde"), (1, "cauchy"), (2, "sys_vandermonde")):
+        e = np.zeros((p, k), dtype=np.uint16)
+        assert lib.gfrs_encoding_matrix16(kind, k, p, e.ctypes.data_as(ctypes.POINTER(ctypes.c_uint16))) == 0
+        assert np.array_equal(e.astype(np.int64), np.asarray(ReedSolomon(k, k + p, field="gf65536", matrix=name).E))
+    e = np.zeros((p, k), dtype=np.uint16)
+    assert lib.gfrs_encoding_matrix16(1, k, p, e.ctypes.data_as(ctypes.POINTER(ctypes.c_uint16))) == 0
+    data = np.random.default_rng(2).integers(0, 65536, size=(k, 33)).astype(np.int64)
+    chunks = np.concatenate([data, F.gemm(e.astype(np.int64), data)])
+    erased = [1, 4, 9]
+    rows = [r for r in range(k + p) if r not in erased][:k]
+    out = np.zeros((len(erased), k), dtype=np.uint16)
+    rc = lib.gfrs_decode_rows16(e.ctypes.data_as(ctypes.POINTER(ctypes.c_uint16)), k, p,
+                                np.asarray(rows, dtype=np.int32).ctypes.data_as(ctypes.POINTER(ctypes.c_int)),
+                                np.asarray(erased, dtype=np.int32).ctypes.data_as(ctypes.POINTER(ctypes.c_int)),
+                                len(erased), out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint16)))
+    assert rc == 0
+    assert np.array_equal(F.gemm(out.astype(np.int64), chunks[rows]), data[erased])
+    bad = np.asarray([0] * k, dtype=np.int32)  # repeated survivor: not recoverable
+    assert lib.gfrs_decode_rows16(e.ctypes.data_as(ctypes.POINTER(ctypes.c_uint16)), k, p,
+                                  bad.ctypes.data_as(ctypes.POINTER(ctypes.c_int)),
+                                  np.asarray(erased, dtype=np.int32).ctypes.data_as(ctypes.POINTER(ctypes.c_int)),
+                                  len(erased), out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint16))) in (-1, -2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k,m,C,engine", [(300, 40, 2 * 4096 + 100, 0), (10, 4, 2 * 5000, 0), (64, 16, 8192, 1),
+                                          (64, 16, 8192, 2)])
+def test_gpu_capi_plan16_matches_oracle(lib, k, m, C, engine):
+    """gfrs_plan16_*: the GF(2^16) device GEMM through the C API, on the matrix cores (AUTO for
+    k >= 16, or MFMA) and the v_perm kernel (AUTO at k = 10, or VALU), against the numpy oracle."""
+    import torch
+
+    from gpu_rscode_amd.models import alloc_rows
+
+    F = gf.field(16)
+    rng = np.random.default_rng(k + m)
+    coeff = rng.integers(0, 65536, size=(m, k)).astype(np.uint16)
+    x = alloc_rows(k, C, "cuda")
+    x.copy_(torch.from_numpy(rng.integers(0, 256, size=(k, C), dtype=np.uint8)))
+    y = alloc_rows(m, C, "cuda", fill=0)
+    ins = (ctypes.c_void_p * k)(*[int(x[i].data_ptr()) for i in range(k)])
+    outs = (ctypes.c_void_p * m)(*[int(y[i].data_ptr()) for i in range(m)])
+    plan = ctypes.c_void_p()
+    lib.gfrs_last_error.restype = ctypes.c_char_p
+    torch.cuda.synchronize()
+    rc = lib.gfrs_plan16_create(ctypes.byref(plan), 0, k, m, coeff.ctypes.data_as(ctypes.POINTER(ctypes.c_uint16)),
+                                ins, outs, None, ctypes.c_int64(C), engine)
+    assert rc == 0, lib.gfrs_last_error()
+    want_engine = engine or (2 if k >= 16 else 1)
+    assert lib.gfrs_plan16_engine(plan) == want_engine
+    assert lib.gfrs_plan16_run(plan, None) == 0
+    assert lib.gfrs_sync(0) == 0
+    got = y.cpu().numpy().view("<u2").astype(np.int64)
+    assert np.array_equal(got, F.gemm(coeff.astype(np.int64), np.ascontiguousarray(x.cpu().numpy()).view("<u2")))
+    lib.gfrs_plan16_destroy(plan)
