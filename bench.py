@@ -104,7 +104,7 @@ METRIC = "encode+decode throughput (GB/s) at k=10,n=14 on 1 GiB; 1/2/4/8-GPU sca
 COMM_MODES = ("bcast", "owners", "root", "none")
 # BASELINE.json's other configs (#4, #5, #1's shape at GPU scale) and the w = 16 field, timed by the
 # headline run itself (N = 1) so the driver's record carries them
-CONFIG_PRESETS = ("k128n160", "k16n20_8g", "k4n6", "k10n14_w16")
+CONFIG_PRESETS = ("k128n160", "k16n20_8g", "k4n6", "k10n14_w16", "k4n6_cpu")
 
 # BASELINE.json configs. Weak presets are per GPU; strong presets are the whole job's bytes.
 PRESETS = {
@@ -117,6 +117,8 @@ PRESETS = {
     "k4n6": dict(k=4, n=6, bytes=1_096_310_784, erasures=2),
     # the reference's w = 16 field (src/galoisfield.cu:22-32), same stripe shape as the headline
     "k10n14_w16": dict(k=10, n=14, bytes=1 << 30, erasures=4, field="gf65536"),
+    # BASELINE config #1: k=4, n=6 on the CPU, 1 MiB (the C++ CPU codec; src/cpu-rs.c's shape)
+    "k4n6_cpu": dict(k=4, n=6, bytes=1 << 20, erasures=2, device="cpu"),
 }
 
 
@@ -189,6 +191,7 @@ def parse(argv=None):
                     help="seconds for all --configs children together (each gets what is left, at most 75)")
     a = ap.parse_args(argv)
     pr = {"scaling": "weak", "gather": "step", "lanes": 2, "field": "gf256", **PRESETS[a.preset]}
+    pr.pop("device", None)  # (selects the config child's --device; the command line decides here)
     for key, val in pr.items():
         if getattr(a, key) is None:
             setattr(a, key, val)
@@ -750,8 +753,9 @@ def run_config_child(a, preset: str, timeout_s: float) -> dict:
     """``bench.py --preset <preset>`` as a CHILD process (never an exec of this one) with its own
     timeout and process group; its one JSON line, condensed. A crash, a hang or a bad record gives
     ``{"error": ..., "rc": ...}`` — the caller's headline record is never touched."""
+    device = PRESETS[preset].get("device", a.device)  # (a CPU preset runs on the CPU codec)
     cmd = [sys.executable, os.path.abspath(__file__), "--preset", preset, "--steps", str(a.config_steps),
-           "--warmup", str(a.config_warmup), "--no-e2e", "--configs", "none", "--device", a.device,
+           "--warmup", str(a.config_warmup), "--no-e2e", "--configs", "none", "--device", device,
            "--headline-budget", str(max(10.0, timeout_s - 5))]
     env = dict(os.environ, GFRS_CONFIG_CHILD=preset)
     t0 = time.perf_counter()
