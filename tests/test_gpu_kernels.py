@@ -317,6 +317,34 @@ def test_fp4_fused_copy_and_device_coeff(k, m, ncols):
         assert np.array_equal(got[j], perm_host[j] if j % 3 else np.full(ncols, 0x44, np.uint8)), j
 
 
+@pytest.mark.parametrize("m", [26, 20, 32, 12])
+def test_fp4_fused_copy_decode_shape(m):
+    """The wide decode's shape: k = 128 scattered survivors, m rebuilt rows, and copies for the first
+    128 - m inputs only (the surviving natives; the parity survivors have no destination). Whole
+    16-row ring slots then hold no destination at all, so every wave takes the fused-copy store's
+    lane-0 sink path there, and the rows around the boundary take the masked path. Bit-exact outputs
+    and copies, and the copy buffers of destination-less rows stay untouched."""
+    _native_loaded()
+    k = 128
+    ncols = 256 * (256 * 2 + 3) + 41  # several chunks per persistent block + a v_perm remainder
+    rng = np.random.default_rng(1000 + m)
+    host, dev = _rand_rows(k, ncols, 7 * m)
+    inputs = [dev[j].clone() for j in range(k)]
+    coeff = rng.integers(0, 256, size=(m, k), dtype=np.uint8)
+    out = alloc_rows(m, ncols, "cuda", fill=0x5A)
+    cdst = alloc_rows(k, ncols, "cuda", fill=0x44)
+    ncopy = k - m
+    copies = [cdst[j] if j < ncopy else None for j in range(k)]
+    plan = GemmPlan(inputs, out, coeff, copies=copies, engine="mfma")
+    assert plan.engine == "mfma"
+    plan.run()
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), GF256.gemm(coeff, host))
+    got = cdst.cpu().numpy()
+    assert np.array_equal(got[:ncopy], host[:ncopy])
+    assert (got[ncopy:] == 0x44).all()
+
+
 @pytest.mark.parametrize("k,n,matrix", [(10, 14, "vandermonde"), (128, 160, "cauchy"), (4, 6, "vandermonde"),
                                         (200, 255, "sys_vandermonde")])
 def test_decode_system_matches_host_decode_matrix(k, n, matrix):
