@@ -43,6 +43,35 @@ __device__ __forceinline__ uint32_t mac_pair(uint32_t acc, P t0, const Sel& s0, 
   return xor3(xor3(xor3(acc, a0, b0), c0, a1), b1, c1);
 }
 
+// A byte map's five table words with two of them copied to VGPRs once: a v_perm can read only one
+// SGPR (the gfx9 constant bus), and left to itself the compiler re-copies a table word before every
+// v_perm that reads it (0.6 v_mov per v_perm in the w = 16 kernel). The asm copy is opaque, so it
+// is made once and shared by every word the map is applied to.
+struct MapV {
+  uint32_t s1, s3, s4;  // (scalar)
+  uint32_t v0, v2;      // (vector copies)
+};
+__device__ __forceinline__ uint32_t vcopy(uint32_t s) {
+  uint32_t v;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(v) : "s"(s));
+  return v;
+}
+template <typename P>
+__device__ __forceinline__ MapV map_v(P t) {
+  return {t[1], t[3], t[4], vcopy(t[0]), vcopy(t[2])};
+}
+// acc ^= L0(x0) ^ L1(x1) for two rows, tables in MapV form: 6 v_perm_b32 + 3 v_bitop3.
+__device__ __forceinline__ uint32_t mac_pair_v(uint32_t acc, const MapV& t0, const Sel& s0, const MapV& t1,
+                                               const Sel& s1) {
+  const uint32_t a0 = __builtin_amdgcn_perm(t0.s1, t0.v0, s0.s0);
+  const uint32_t b0 = __builtin_amdgcn_perm(t0.s3, t0.v2, s0.s1);
+  const uint32_t c0 = __builtin_amdgcn_perm(0u, t0.s4, s0.s2);
+  const uint32_t a1 = __builtin_amdgcn_perm(t1.s1, t1.v0, s1.s0);
+  const uint32_t b1 = __builtin_amdgcn_perm(t1.s3, t1.v2, s1.s1);
+  const uint32_t c1 = __builtin_amdgcn_perm(0u, t1.s4, s1.s2);
+  return xor3(xor3(xor3(acc, a0, b0), c0, a1), b1, c1);
+}
+
 // acc ^= L(x) for one GF(2)-linear byte map L on 4 packed bytes: 3 v_perm_b32 + 2 v_bitop3.
 template <typename P>
 __device__ __forceinline__ uint32_t mac_map(uint32_t acc, P t, const Sel& s) {

@@ -24,6 +24,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdlib>
 
 #include "gfrs/desc.h"
 #include "gfrs/kernels.h"
@@ -93,9 +94,14 @@ __device__ void tail_sym(const DescView& d, int k, int m_pad, int i0, bool do_co
       *(gptr<uint16_t>)(d.out[i0 + i] + uint64_t(off)) = static_cast<uint16_t>((lo[i] & 0xFFu) | ((hi[i] & 0xFFu) << 8));
 }
 
-// Vector kernel: each lane owns one 16-byte group (8 symbols) of every row, PF rows in flight.
-// Lanes ngroups .. ngroups + tail_syms - 1 take one ragged tail symbol each.
-template <int MT, int PF>
+// Vector kernel: each lane owns G 16-byte groups (8 symbols each, kBlock groups apart so every load
+// stays coalesced) of every row, PF rows in flight. The perm tables of a (row, output) pair are
+// scalar loads, and a v_perm can read only one SGPR (the gfx9 constant-bus limit), so each table
+// pair is first copied to a VGPR: with G = 2 that copy, the row's pointer and loop bookkeeping
+// serve twice the symbols (profiles/gf65536/r08_k10: the w = 16 kernel is VALU-bound). A group
+// past the row end reads group 0's bytes and stores nothing; lanes past the groups take one ragged
+// tail symbol each.
+template <int MT, int PF, int G>
 __global__ __launch_bounds__(kBlock) void gf_gemm16_vec_kernel(DescView d, int k, int m_pad, int ntiles, int64_t col0,
                                                                int64_t ngroups, int64_t nblk, int64_t ncb,
                                                                int tail_syms) {
@@ -106,56 +112,94 @@ __global__ __launch_bounds__(kBlock) void gf_gemm16_vec_kernel(DescView d, int k
   const bool do_copy = (tm.tile == 0);
 
   for (int64_t cb = tm.cb0; cb < nblk; cb += ncb) {
-    const int64_t g = cb * kBlock + threadIdx.x;
-    if (g >= ngroups) {
-      if (g - ngroups < tail_syms) tail_sym<MT>(d, k, m_pad, i0, do_copy, col0 + ngroups * 16 + 2 * (g - ngroups));
-      continue;
+    const int64_t g0 = cb * (G * kBlock) + threadIdx.x;
+    bool live[G];
+    int64_t off[G];
+#pragma unroll
+    for (int u = 0; u < G; ++u) {
+      live[u] = g0 + u * kBlock < ngroups;
+      off[u] = col0 + (live[u] ? g0 + u * kBlock : g0) * 16;
     }
-    const int64_t off = col0 + g * 16;
-    uint32_t lo[MT][2], hi[MT][2];
+    if (live[0]) {
+      uint32_t lo[G][MT][2], hi[G][MT][2];
 #pragma unroll
-    for (int i = 0; i < MT; ++i) lo[i][0] = lo[i][1] = hi[i][0] = hi[i][1] = 0;
+      for (int v = 0; v < G; ++v)
+#pragma unroll
+        for (int i = 0; i < MT; ++i) lo[v][i][0] = lo[v][i][1] = hi[v][i][0] = hi[v][i][1] = 0;
 
-    u32x4 ring[PF];
+      u32x4 ring[PF][G];
 #pragma unroll
-    for (int u = 0; u < PF; ++u)
-      if (u < k) ring[u] = ld16<true>(row_vec(d.in[u], off));
+      for (int u = 0; u < PF; ++u)
+        if (u < k)
+#pragma unroll
+          for (int v = 0; v < G; ++v) ring[u][v] = ld16<true>(row_vec(d.in[u], off[v]));
 
-    for (int j0 = 0; j0 < k; j0 += PF) {
+      for (int j0 = 0; j0 < k; j0 += PF) {
 #pragma unroll
-      for (int u = 0; u < PF; ++u) {
-        const int j = j0 + u;
-        if (j >= k) break;
-        const u32x4 x = ring[u];
-        if (j + PF < k) ring[u] = ld16<true>(row_vec(d.in[j + PF], off));
-        if (do_copy) {
-          const uint64_t cp = d.copy[j];
-          if (cp) st16<true>(row_vec_w(cp, off), x);
+        for (int u = 0; u < PF; ++u) {
+          const int j = j0 + u;
+          if (j >= k) break;
+          u32x4 x[G];
+#pragma unroll
+          for (int v = 0; v < G; ++v) {
+            x[v] = ring[u][v];
+            if (j + PF < k) ring[u][v] = ld16<true>(row_vec(d.in[j + PF], off[v]));
+          }
+          if (do_copy) {
+            const uint64_t cp = d.copy[j];
+            if (cp)
+#pragma unroll
+              for (int v = 0; v < G; ++v)
+                if (live[v]) st16<true>(row_vec_w(cp, off[v]), x[v]);
+          }
+          const auto t = d.tab + (size_t(j) * m_pad + i0) * kQuad;
+          MapV mv[MT][4];  // this row's tables, shared by the G groups and both plane words
+#pragma unroll
+          for (int i = 0; i < MT; ++i)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) mv[i][e] = map_v(t + i * kQuad + e * kPermStride);
+#pragma unroll
+          for (int v = 0; v < G; ++v) {
+            const uint32_t L0 = __builtin_amdgcn_perm(x[v][1], x[v][0], kSelLo);
+            const uint32_t H0 = __builtin_amdgcn_perm(x[v][1], x[v][0], kSelHi);
+            const uint32_t L1 = __builtin_amdgcn_perm(x[v][3], x[v][2], kSelLo);
+            const uint32_t H1 = __builtin_amdgcn_perm(x[v][3], x[v][2], kSelHi);
+            const Sel sl0 = make_sel(L0), sh0 = make_sel(H0), sl1 = make_sel(L1), sh1 = make_sel(H1);
+#pragma unroll
+            for (int i = 0; i < MT; ++i) {
+              const MapV& ll = mv[i][0];
+              const MapV& lh = mv[i][1];
+              const MapV& hl = mv[i][2];
+              const MapV& hh = mv[i][3];
+              lo[v][i][0] = mac_pair_v(lo[v][i][0], ll, sl0, hl, sh0);
+              hi[v][i][0] = mac_pair_v(hi[v][i][0], lh, sl0, hh, sh0);
+              lo[v][i][1] = mac_pair_v(lo[v][i][1], ll, sl1, hl, sh1);
+              hi[v][i][1] = mac_pair_v(hi[v][i][1], lh, sl1, hh, sh1);
+            }
+          }
         }
-        const uint32_t L0 = __builtin_amdgcn_perm(x[1], x[0], kSelLo);
-        const uint32_t H0 = __builtin_amdgcn_perm(x[1], x[0], kSelHi);
-        const uint32_t L1 = __builtin_amdgcn_perm(x[3], x[2], kSelLo);
-        const uint32_t H1 = __builtin_amdgcn_perm(x[3], x[2], kSelHi);
-        const Sel sl0 = make_sel(L0), sh0 = make_sel(H0), sl1 = make_sel(L1), sh1 = make_sel(H1);
-        const auto t = d.tab + (size_t(j) * m_pad + i0) * kQuad;
+      }
+
 #pragma unroll
-        for (int i = 0; i < MT; ++i) {
-          const auto q = t + i * kQuad;
-          lo[i][0] = mac_pair(lo[i][0], q, sl0, q + 2 * kPermStride, sh0);
-          hi[i][0] = mac_pair(hi[i][0], q + kPermStride, sl0, q + 3 * kPermStride, sh0);
-          lo[i][1] = mac_pair(lo[i][1], q, sl1, q + 2 * kPermStride, sh1);
-          hi[i][1] = mac_pair(hi[i][1], q + kPermStride, sl1, q + 3 * kPermStride, sh1);
+      for (int i = 0; i < MT; ++i) {
+        const uint64_t op = d.out[i0 + i];
+        if (!op) continue;
+#pragma unroll
+        for (int v = 0; v < G; ++v) {
+          if (!live[v]) continue;
+          const u32x4 w{__builtin_amdgcn_perm(hi[v][i][0], lo[v][i][0], kSelW0),
+                        __builtin_amdgcn_perm(hi[v][i][0], lo[v][i][0], kSelW1),
+                        __builtin_amdgcn_perm(hi[v][i][1], lo[v][i][1], kSelW0),
+                        __builtin_amdgcn_perm(hi[v][i][1], lo[v][i][1], kSelW1)};
+          st16<true>(row_vec_w(op, off[v]), w);
         }
       }
     }
-
+    // ragged tail symbols: virtual groups ngroups .. ngroups + tail_syms - 1, one symbol each
 #pragma unroll
-    for (int i = 0; i < MT; ++i) {
-      const uint64_t op = d.out[i0 + i];
-      if (!op) continue;
-      const u32x4 w{__builtin_amdgcn_perm(hi[i][0], lo[i][0], kSelW0), __builtin_amdgcn_perm(hi[i][0], lo[i][0], kSelW1),
-                    __builtin_amdgcn_perm(hi[i][1], lo[i][1], kSelW0), __builtin_amdgcn_perm(hi[i][1], lo[i][1], kSelW1)};
-      st16<true>(row_vec_w(op, off), w);
+    for (int u = 0; u < G; ++u) {
+      const int64_t t = g0 + u * kBlock - ngroups;
+      if (t >= 0 && t < tail_syms) tail_sym<MT>(d, k, m_pad, i0, do_copy, col0 + ngroups * 16 + 2 * t);
     }
   }
 }
@@ -191,6 +235,16 @@ inline Grid make_grid(int64_t items, int ntiles, int max_blocks) {
   if (g.ncb > cap) g.ncb = cap;
   g.blocks = static_cast<unsigned>((g.ncb < 8 ? g.ncb : (g.ncb + 7) / 8 * 8) * ntiles);  // see map_block
   return g;
+}
+
+// 16-byte groups per lane of the vector kernel where it may take two (GFRS_GF16_VEC_G=1: always one,
+// for A/B measurements)
+int vec_groups() {
+  static const int v = [] {
+    const char* e = std::getenv("GFRS_GF16_VEC_G");
+    return e && std::atoi(e) == 1 ? 1 : 2;
+  }();
+  return v;
 }
 
 // Output tile of the w = 16 kernel: the GF(2^8) tile (gfrs/desc.h tile_for) capped at 8, since
@@ -242,9 +296,19 @@ hipError_t launch_gf_gemm16_batched(const void* desc, int k, int m_pad, int batc
     }
     const int64_t ngroups = ncols / 16;
     const int tail_syms = int((ncols - ngroups * 16) / 2);
-    const Grid g = make_grid(ngroups + tail_syms, ntiles, max_blocks);
-    gf_gemm16_vec_kernel<MT, 2>
-        <<<dim3(g.blocks, batch), kBlock, 0, stream>>>(d, k, m_pad, ntiles, col0, ngroups, g.nblk, g.ncb, tail_syms);
+    // (a Grid item is one lane's G groups) Two groups per lane where the tile is small enough to
+    // keep the registers low (MT <= 4: 111 VGPRs, against 177 at MT = 8) and the rows are long
+    // (the short-row regime wants as many blocks as it can get). k = 10, m = 4, 1 GiB: 208 M VALU
+    // instructions against 232 M, kernel 401 vs 431 us (profiles/gf65536/r08_k10).
+    if (MT <= 4 && mt_cap > 1 && vec_groups() == 2) {
+      const Grid g = make_grid((ngroups + tail_syms + 1) / 2, ntiles, max_blocks);
+      gf_gemm16_vec_kernel<MT, 2, 2>
+          <<<dim3(g.blocks, batch), kBlock, 0, stream>>>(d, k, m_pad, ntiles, col0, ngroups, g.nblk, g.ncb, tail_syms);
+    } else {
+      const Grid g = make_grid(ngroups + tail_syms, ntiles, max_blocks);
+      gf_gemm16_vec_kernel<MT, 2, 1>
+          <<<dim3(g.blocks, batch), kBlock, 0, stream>>>(d, k, m_pad, ntiles, col0, ngroups, g.nblk, g.ncb, tail_syms);
+    }
     return hipGetLastError();
   });
 }

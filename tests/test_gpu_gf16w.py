@@ -40,6 +40,41 @@ def test_gemm16_matches_oracle(k, m, C):
     assert np.array_equal(y.cpu().numpy().view("<u2"), _oracle(coeff, x.cpu().numpy()))
 
 
+@pytest.mark.parametrize("extra_groups,tail", [(100, 5), (300, 7), (256, 7), (511, 1), (0, 3)])
+@pytest.mark.parametrize("m,B", [(4, 1), (2, 2), (1, 1)])
+def test_gemm16_two_groups_per_lane(extra_groups, tail, m, B):
+    """Long rows (>= 32768 16-byte groups) run the vector kernel with two groups per lane, 256
+    groups apart. The last block's second group is live for some lanes only, and the ragged tail
+    symbols land on the first or the second group slot (extra_groups < 256 or >= 256). Fused copies
+    and a batch of stripes run through the same kernel. Bit-exact against the oracle, and
+    destination-less rows and columns are left untouched."""
+    k = 6
+    C = 16 * (512 * 70 + extra_groups) + 2 * tail
+    rng = np.random.default_rng(extra_groups * 31 + tail + 7 * m + B)
+    coeff = rng.integers(0, 65536, size=(m, k))
+    if B == 1:
+        x = alloc_rows(k, C, "cuda")
+        x.copy_(_rand(k, C, C + m))
+        y = alloc_rows(m, C, "cuda", fill=0xAB)
+        z = alloc_rows(k, C, "cuda", fill=0x44)
+        copies = [z[j] if j % 2 else None for j in range(k)]
+        Gemm16Plan(x, y, coeff, copies=copies, engine="valu16").run()
+        torch.cuda.synchronize()
+        xh = x.cpu().numpy()
+        assert np.array_equal(y.cpu().numpy().view("<u2"), _oracle(coeff, xh))
+        zh = z.cpu().numpy()
+        for j in range(k):
+            assert np.array_equal(zh[j], xh[j] if j % 2 else np.full(C, 0x44, np.uint8)), j
+    else:
+        x = _rand(B * k, C, C + m).view(B, k, C).cuda()
+        y = torch.zeros((B, m, C), dtype=torch.uint8, device="cuda")
+        Gemm16Plan(x, y, coeff, engine="valu16").run()
+        torch.cuda.synchronize()
+        xh, yh = x.cpu().numpy(), y.cpu().numpy()
+        for b in range(B):
+            assert np.array_equal(yh[b].view("<u2"), _oracle(coeff, xh[b])), b
+
+
 def test_gemm16_unaligned_rows_and_column_ranges():
     """Rows 2 bytes off a 16-byte boundary take the symbol kernel; a sub-range [col0, col0 + n) only
     writes those columns."""
