@@ -1250,6 +1250,14 @@ bool use_ar(const Fp4Geometry& geo, int k, bool copies) {
   return geo.mg == 4 || (!copies && (geo.mg == 6 || geo.mg == 8));
 }
 
+// The tile-major kernel (gf_mfma_fp4tm.hip) for one group of 5..7 M-tiles at k in (112, 128]:
+// GFRS_FP4_KERNEL=tm selects it (A/B measurements).
+bool use_tm(const Fp4Geometry& geo, int k) {
+  if (geo.groups != 1 || !fp4tm_supported(k, geo.mg)) return false;
+  const char* env = std::getenv("GFRS_FP4_KERNEL");
+  return env && std::strcmp(env, "tm") == 0;
+}
+
 }  // namespace
 
 size_t fp4_bitmat_bytes(int k, int m, int mg_cap) {
@@ -1279,6 +1287,24 @@ hipError_t launch_gf_gemm_fp4(const void* bitmat, const void* desc, int k, int m
   const DescLayout l = desc_layout(k, m_pad);
   const char* b = static_cast<const char*>(desc);
   const Fp4Geometry geo = geometry(k, m, mg_cap, copies);
+  if (use_tm(geo, k)) {  // the tile-major form (gf_mfma_fp4tm.hip)
+    Fp4ArLaunch a{};
+    a.in = reinterpret_cast<const uint64_t*>(b + l.in_off);
+    a.out = reinterpret_cast<const uint64_t*>(b + l.out_off);
+    a.copy = copies ? reinterpret_cast<const uint64_t*>(b + l.copy_off) : nullptr;
+    a.bitmat = bitmat;
+    a.k = k;
+    a.m = m;
+    a.mg = geo.mg;
+    a.col0 = col0;
+    a.ncols = ncols;
+    a.in_stride = copies ? 0 : in_stride;
+    int64_t done = 0;
+    const hipError_t e = launch_gf_gemm_fp4tm(a, &done, stream);
+    if (e != hipSuccess) return e;
+    if (done < ncols) return launch_gf_gemm(desc, k, m_pad, col0 + done, ncols - done, false, 0, stream);
+    return hipSuccess;
+  }
   // split copy (GFRS_FP4_COPY=split, measured and not the default: split_copy_mode)
   if (use_ar(geo, k, copies) && !(copies && split_copy_mode())) {  // the A-resident form (gf_mfma_fp4ar.hip)
     Fp4ArLaunch a{};

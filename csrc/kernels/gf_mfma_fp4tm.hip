@@ -1,0 +1,469 @@
+// GF(2^8) GEMM on gfx950 matrix cores, FP4 bit-matrix form — TILE-MAJOR variant ("tm").
+//
+// Same algebra, bit-matrix layout, B expansion and biased-float parity as gf_mfma_fp4.hip (read its
+// header first); what changes is the loop order. The LDS kernels there walk a chunk K-step by
+// K-step with every M-tile's accumulator live (224 AGPRs at 7 tiles), so a chunk ends with all
+// tiles finishing at once: 224 accumulator reads and 196 bit inserts that the matrix pipe waits out,
+// plus one bias MFMA per tile (56 % MFMA pipe on the k = 128 decode, profiles/wide_stripe/r07_pmc).
+//
+// Here a wave keeps its chunk's B operand resident instead — all 16 K-steps x 2 N-tiles, 128
+// registers, in the AGPRs (this file is compiled with -amdgpu-mfma-vgpr-form, so the scaled MFMA
+// reads B from AGPRs and keeps its accumulators in arch VGPRs) — and runs the tiles one after the
+// other, 16 K-steps each:
+//   * only two tiles' accumulators are live: the one accumulating and the previous one, whose
+//     epilogue (28 bit inserts straight from VGPRs, 2 stores) runs under this tile's 32 MFMAs;
+//   * the bias is the C operand of a tile's first MFMA (a constant VGPR block), no extra MFMA;
+//   * the next chunk's 8 ring slots are DMA'd during tile 1 and expanded into the B registers during
+//     the last tile, step by step right after the last MFMA that reads each step's old value; the
+//     fused survivor copy of a slot is stored from the ring at the same time.
+// Per 256-column chunk at 7 tiles: 224 MFMAs, ~560 VALU (v1: 238 MFMAs, ~1140 VALU).
+//
+// Accumulator sets alternate by global tile number; with an odd tile count the chunk loop is
+// unrolled by two so the set a tile writes is never the one still waiting to be packed. An odd
+// chunk count ends with a phantom chunk (its loads are dummies, its stores go to the sink) whose
+// first tile packs the last real one.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <type_traits>
+#include <utility>
+
+#include "gfrs/desc.h"
+#include "gfrs/device_cache.h"
+#include "gfrs/kernels.h"
+
+namespace gfrs {
+namespace {
+
+using i32x8 = int __attribute__((ext_vector_type(8)));
+using i32x4 = int __attribute__((ext_vector_type(4)));
+using u32x4 = unsigned __attribute__((ext_vector_type(4)));
+using f32x16 = float __attribute__((ext_vector_type(16)));
+template <typename T>
+using cptr = const __attribute__((address_space(4))) T*;
+template <typename T>
+using gptr = __attribute__((address_space(1))) T*;
+using lds_u8 = __attribute__((address_space(3))) uint8_t;
+
+constexpr int kSlotBytes = 1024;  // one ring slot: 16 input rows x the wave's 64 columns
+constexpr int kCW = 64;           // columns per wave (two 32-column N-tiles, interleaved 2c + t)
+constexpr int kNS = 16;           // K-steps per chunk (k in (112, 128]: 128 rows = 1024 bits)
+constexpr int kKS = 8;            // ring slots per chunk (2 K-steps each) = the ring depth
+constexpr int kRS = 16;           // input rows per ring slot
+constexpr int kQ = 4;             // K-steps per super-step (LDS reads one super-step ahead)
+constexpr int kBlockCols = 256;   // 4 waves x 64 columns
+constexpr int kPtrBytes = 8 * (256 + 32 + 256);  // LDS: row, output-row and copy pointer tables
+
+__device__ __forceinline__ void lgkm_wait() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+template <typename T>
+__device__ __forceinline__ void tie(T& v) {
+  asm volatile("" : "+v"(v));
+}
+template <typename F, int... I>
+__device__ __forceinline__ void static_for_impl(F& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+// mask ? a : b per bit, one v_bitop3 (a builtin, so the compiler sees the accumulator reads and
+// inserts the MFMA -> VALU wait states itself)
+__device__ __forceinline__ uint32_t bfi(uint32_t mask, uint32_t a, uint32_t b) {
+  return __builtin_amdgcn_bitop3_b32(mask, a, b, 0xCA);
+}
+
+// accumulator set of tile t in chunk parity P (alternating over the global tile sequence)
+template <int MG>
+__host__ __device__ constexpr int acc_set(int P, int t) {
+  return (P * MG + t) & 1;
+}
+
+template <int MG, bool UNI, bool COPY>
+__global__ __launch_bounds__(256, 1) void gf_gemm_fp4tm_kernel(cptr<uint64_t> in, cptr<uint64_t> out,
+                                                               cptr<uint64_t> copy, const i32x4* __restrict__ bitmat,
+                                                               int k, int m, int64_t col0, int64_t nchunks,
+                                                               int64_t chunk_slots, int64_t in_stride,
+                                                               int sink_spread) {
+  static_assert(MG >= 4 && MG <= 7, "DMAs in tile 1 must land before the expansion in tile MG-1");
+  constexpr size_t kA = size_t(MG) * kNS * 1024;  // LDS A slice [kstep][tile][lane] x 16 B
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  i32x4* afrag = reinterpret_cast<i32x4*>(smem);
+  uint64_t* rowptr = reinterpret_cast<uint64_t*>(smem + kA);
+  uint64_t* outptr = rowptr + 256;
+  uint64_t* copyptr = outptr + 32;
+  const int bid = blockIdx.x;
+  const int64_t slot0 = int64_t(bid >> 3) * 8 + (bid & 7);  // slot -> one XCD (blocks round-robin)
+  if (slot0 >= chunk_slots) return;
+  const int my_chunks = int((nchunks - slot0 + chunk_slots - 1) / chunk_slots);
+  if (my_chunks <= 0) return;
+
+  for (int i = threadIdx.x; i < MG * kNS * 64; i += 256) afrag[i] = bitmat[i];
+  if (!UNI)
+    for (int i = threadIdx.x; i < k; i += 256) rowptr[i] = in[i];
+  for (int i = threadIdx.x; i < 32; i += 256) outptr[i] = i < m ? out[i] : 0;
+  if (COPY)
+    for (int i = threadIdx.x; i < k; i += 256) copyptr[i] = copy[i];
+  __syncthreads();
+
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 31, h = lane >> 5;
+  const uint32_t lds0 = uint32_t(reinterpret_cast<uintptr_t>((lds_u8*)smem));
+  lds_u8* ring = (lds_u8*)(smem + kA + kPtrBytes) + size_t(wave) * kKS * kSlotBytes;
+  const uint32_t ring_base = uint32_t(reinterpret_cast<uintptr_t>(ring));
+  const uint32_t ring_x = ring_base + uint32_t(4 * h * kCW + 2 * c);  // rows 4h.., column pair (2c, 2c+1)
+  const uint32_t ring_lane = ring_base + 16u * lane;                   // this lane's DMA'd 16 B
+  const uint32_t a_lo = lds0 + 16u * lane, a_hi = a_lo + 65536u;
+  const uint32_t optr_addr = lds0 + uint32_t(kA) + 2048u + 16u * h;  // outptr[4t + 2h + u]: + 32t + 8u
+  const unsigned sslot = sink_spread ? (blockIdx.x * 4u + unsigned(wave)) % unsigned(kFp4SinkSlots) : 0u;
+  const uint64_t sink = uint64_t(bitmat + size_t(MG) * kNS * 64) + uint64_t(sslot) * 1024u + 16 * lane;
+  const int scale = 0x7F7F7F7F;  // E8M0 1.0 for every block of 32
+  const uint64_t in0 = UNI ? in[0] : 0;
+  const int drow = lane >> 2;                      // this lane's row within a DMA'd slot
+  const int dcol = wave * kCW + 16 * (lane & 3);   // and its 16 columns (block-relative)
+  // the slot rows are the same in every chunk: their input and copy row pointers stay in registers
+  uint64_t rp[kKS], cpv[kKS];
+#pragma unroll
+  for (int p = 0; p < kKS; ++p) {
+    const int r = kRS * p + drow;
+    rp[p] = UNI ? in0 + uint64_t(int64_t(r < k ? r : k - 1) * in_stride) : rowptr[r < k ? r : k - 1];
+    cpv[p] = COPY && r < k ? copyptr[r] : 0;
+  }
+  auto cbase = [&](int ci) __attribute__((always_inline)) {
+    return col0 + (slot0 + int64_t(ci) * chunk_slots) * kBlockCols;
+  };
+  // DMA of ring slot p for chunk cn (past my chunks: chunk 0's bytes, never used)
+  auto dma = [&](int cn, int p) __attribute__((always_inline)) {
+    const int64_t col = cbase(cn < my_chunks ? cn : 0) + dcol;
+    __builtin_amdgcn_global_load_lds((gptr<const void>)(rp[p] + uint64_t(col)), ring + p * kSlotBytes, 16, 0, 0);
+  };
+  // fused copy of ring slot p (chunk cn's bytes) from this lane's 16 B
+  auto copy_store = [&](int cn, int p, u32x4 v) __attribute__((always_inline)) {
+    const uint64_t cp = cpv[p];
+    const bool live = cn < my_chunks && cp;
+    __builtin_nontemporal_store(v, (gptr<u32x4>)(live ? cp + uint64_t(cbase(cn) + dcol) : sink));
+  };
+  // rows 4h+i of K-step s (slot s / 2, half s % 2), this lane's column pair
+  auto read_x = [&](uint32_t (&x)[4], auto s_tag) __attribute__((always_inline)) {
+    constexpr int S = decltype(s_tag)::value;
+    constexpr int off = (S / 2) * kSlotBytes + (S % 2) * 8 * kCW;
+    const uint32_t addr = ring_x;
+    uint32_t x0, x1, x2, x3;
+    asm volatile(
+        "ds_read_u16 %0, %4 offset:%5\n\t"
+        "ds_read_u16 %1, %4 offset:%6\n\t"
+        "ds_read_u16 %2, %4 offset:%7\n\t"
+        "ds_read_u16 %3, %4 offset:%8"
+        : "=&v"(x0), "=&v"(x1), "=&v"(x2), "=&v"(x3)
+        : "v"(addr), "n"(off), "n"(off + 64), "n"(off + 128), "n"(off + 192)
+        : "memory");
+    x[0] = x0;
+    x[1] = x1;
+    x[2] = x2;
+    x[3] = x3;
+  };
+  // A fragment of (tile T, K-step S)
+  auto read_a = [&](i32x4& a, auto t_tag, auto s_tag) __attribute__((always_inline)) {
+    constexpr int off = (decltype(s_tag)::value * MG + decltype(t_tag)::value) * 1024;
+    const uint32_t base = off >= 65536 ? a_hi : a_lo;
+    i32x4 v;
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=&v"(v) : "v"(base), "n"(off % 65536) : "memory");
+    a = v;
+  };
+  auto read_slot = [&](u32x4& v, auto p_tag) __attribute__((always_inline)) {
+    constexpr int off = decltype(p_tag)::value * kSlotBytes;
+    const uint32_t addr = ring_lane;
+    u32x4 r;
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=&v"(r) : "v"(addr), "n"(off) : "memory");
+    v = r;
+  };
+  auto read_op = [&](uint64_t (&o)[2], auto t_tag) __attribute__((always_inline)) {
+    constexpr int T = decltype(t_tag)::value;
+    const uint32_t addr = optr_addr;
+    uint64_t o0, o1;
+    asm volatile("ds_read_b64 %0, %2 offset:%3\n\tds_read_b64 %1, %2 offset:%4"
+                 : "=&v"(o0), "=&v"(o1)
+                 : "v"(addr), "n"(32 * T), "n"(32 * T + 8)
+                 : "memory");
+    o[0] = o0;
+    o[1] = o1;
+  };
+  // B operands of a K-step from its 4 raw ring words (gf_mfma_fp4.hip expand, kAOne order)
+  auto expand = [&](i32x4 (&bo)[2], const uint32_t (&x)[4]) __attribute__((always_inline)) {
+    const uint32_t p01 = x[0] | (x[1] << 16), p23 = x[2] | (x[3] << 16);
+    const uint32_t w[2] = {__builtin_amdgcn_perm(p23, p01, 0x06040200u), __builtin_amdgcn_perm(p23, p01, 0x07050301u)};
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      bo[t][0] = int(w[t] & 0x11111111u);
+      bo[t][1] = int(w[t] & 0x22222222u);
+      bo[t][2] = int(w[t] & 0x44444444u);
+      bo[t][3] = int((w[t] >> 1) & 0x44444444u);
+    }
+  };
+
+  i32x4 Bc[kNS][2];  // B of the chunk being multiplied, resident in AGPRs
+  f32x16 acc[2][2];  // two accumulator sets x two N-tiles
+  f32x16 bias;       // start value 2^(23 - b) on output bit b = accumulator register & 7
+#pragma unroll
+  for (int v = 0; v < 16; ++v) bias[v] = float(1u << (23 - (v & 7)));
+#pragma unroll
+  for (int i = 0; i < 2; ++i) acc[i][0] = acc[i][1] = bias;
+
+  // prologue: chunk 0's slots, expanded into B and copied
+#pragma unroll
+  for (int p = 0; p < kKS; ++p) dma(0, p);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  static_for<kNS>([&](auto s_tag) {
+    constexpr int S = decltype(s_tag)::value;
+    uint32_t x[4];
+    read_x(x, s_tag);
+    lgkm_wait();
+#pragma unroll
+    for (int i = 0; i < 4; ++i) tie(x[i]);
+    expand(Bc[S], x);
+#pragma unroll
+    for (int n = 0; n < 2; ++n) asm volatile("" : "+a"(Bc[S][n]));
+  });
+  if constexpr (COPY) {
+    static_for<kKS>([&](auto p_tag) {
+      u32x4 v;
+      read_slot(v, p_tag);
+      lgkm_wait();
+      tie(v);
+      copy_store(0, decltype(p_tag)::value, v);
+    });
+  }
+  using I0 = std::integral_constant<int, 0>;
+  i32x4 Acur[kQ];  // A of the current super-step
+  static_for<kQ>([&](auto j) { read_a(Acur[decltype(j)::value], I0{}, j); });
+  uint64_t opc[2];  // output row pointers of the tile packed next (MG-1 of "chunk -1": discarded)
+  read_op(opc, std::integral_constant<int, MG - 1>{});
+  lgkm_wait();
+#pragma unroll
+  for (int j = 0; j < kQ; ++j) tie(Acur[j]);
+  tie(opc[0]);
+  tie(opc[1]);
+  uint32_t xc[kQ][4] = {};  // raw bytes of the next chunk's K-steps of this super-step (last tile)
+
+  // One chunk ci with chunk parity P (ci == my_chunks: the phantom).
+  auto chunk_body = [&](int ci, auto p_tag) __attribute__((always_inline)) {
+    constexpr int P = decltype(p_tag)::value;
+    const bool live = ci < my_chunks;
+    const int64_t colw = cbase(ci) + wave * kCW + 2 * c;                                  // this chunk
+    const int64_t pcolw = colw - chunk_slots * kBlockCols;                                  // previous chunk
+    static_for<MG>([&](auto t_tag) {
+      constexpr int T = decltype(t_tag)::value;
+      constexpr int PT = T == 0 ? MG - 1 : T - 1;                 // the tile packed during tile T
+      constexpr int kSet = acc_set<MG>(P, T);
+      constexpr int kPSet = T == 0 ? acc_set<MG>(P ^ 1, MG - 1) : acc_set<MG>(P, T - 1);
+      static_assert(kSet != kPSet, "a tile must not write the set still waiting to be packed");
+      static_for<kQ>([&](auto q_tag) {
+        constexpr int Q = decltype(q_tag)::value;
+        // ---- LDS reads for the next super-step (retired by this one's closing lgkmcnt(0))
+        constexpr int NT = Q + 1 < kQ ? T : (T + 1 < MG ? T + 1 : 0);
+        constexpr int NQ = Q + 1 < kQ ? Q + 1 : 0;
+        i32x4 An[kQ];
+        static_for<kQ>([&](auto j) {
+          read_a(An[decltype(j)::value], std::integral_constant<int, NT>{},
+                 std::integral_constant<int, kQ * NQ + decltype(j)::value>{});
+        });
+        // the next chunk's raw bytes for the expansion in the last tile, one super-step ahead
+        constexpr bool kXn = (T == MG - 1 && Q + 1 < kQ) || (T == MG - 2 && Q + 1 == kQ);
+        if constexpr (T == MG - 2 && Q + 1 == kQ) {
+          // the next chunk's 8 DMAs (tile 1) have landed: younger are the 2 epilogue stores of each
+          // of tiles 2 .. MG-2 (vmcnt retires in issue order)
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (MG - 3)) : "memory");
+        }
+        uint32_t xn[kQ][4];
+        if constexpr (kXn) {
+          static_for<kQ>([&](auto j) {
+            read_x(xn[decltype(j)::value], std::integral_constant<int, kQ * NQ + decltype(j)::value>{});
+          });
+        }
+        // fused copy: this super-step's two slots of the next chunk (last tile)
+        [[maybe_unused]] u32x4 cd[2];
+        if constexpr (COPY && T == MG - 1) {
+          read_slot(cd[0], std::integral_constant<int, 2 * Q>{});
+          read_slot(cd[1], std::integral_constant<int, 2 * Q + 1>{});
+        }
+        uint64_t opn[2];
+        if constexpr (Q + 1 == kQ) read_op(opn, t_tag);  // tile T is packed during the next tile
+        __builtin_amdgcn_sched_barrier(0);
+
+        // ---- 4 K-steps x 2 N-tiles of tile T, from the resident B
+        static_for<kQ>([&](auto j_tag) {
+          constexpr int J = decltype(j_tag)::value;
+          constexpr int S = kQ * Q + J;
+          const i32x8 a = {Acur[J][0], Acur[J][1], Acur[J][2], Acur[J][3], 0, 0, 0, 0};
+#pragma unroll
+          for (int n = 0; n < 2; ++n) {
+            const i32x8 bb = {Bc[S][n][0], Bc[S][n][1], Bc[S][n][2], Bc[S][n][3], 0, 0, 0, 0};
+            acc[kSet][n] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, bb, S == 0 ? bias : acc[kSet][n], 4,
+                                                                            4, 0, scale, 0, scale);
+          }
+        });
+        // ---- VALU under the MFMAs: the next chunk's B (last tile), the previous tile's epilogue
+        if constexpr (T == MG - 1) {
+          static_for<kQ>([&](auto j_tag) {
+            constexpr int J = decltype(j_tag)::value;
+            expand(Bc[kQ * Q + J], xc[J]);
+#pragma unroll
+            for (int n = 0; n < 2; ++n) asm volatile("" : "+a"(Bc[kQ * Q + J][n]));
+          });
+        }
+        [[maybe_unused]] uint32_t w[2];
+        if constexpr (Q == 0) {
+          // output bytes of tile PT: 7 bit inserts per byte, straight from the accumulator VGPRs
+          uint32_t y[2][2];
+#pragma unroll
+          for (int b = 0; b < 8; ++b)
+#pragma unroll
+            for (int n = 0; n < 2; ++n)
+#pragma unroll
+              for (int u = 0; u < 2; ++u) {
+                const uint32_t v = __float_as_uint(acc[kPSet][n][8 * u + b]);
+                y[n][u] = b == 0 ? v : bfi(1u << b, v, y[n][u]);
+              }
+#pragma unroll
+          for (int u = 0; u < 2; ++u) w[u] = __builtin_amdgcn_perm(y[1][u], y[0][u], 0x0c0c0400u);
+        }
+        constexpr int kValu = (T == MG - 1 ? kQ * 22 : 0) + (Q == 0 ? 30 : 0);  // (22: 14 + 8 AGPR writes)
+        constexpr int kPer = (kValu + 2 * kQ - 1) / (2 * kQ);
+#pragma unroll
+        for (int i = 0; i < 2 * kQ; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);     // MFMA
+          __builtin_amdgcn_sched_group_barrier(0x002, kPer, 0);  // VALU
+        }
+        __builtin_amdgcn_sched_barrier(0);
+
+        // ---- stores and the next chunk's DMAs
+        if constexpr (Q == 0) {
+          // (tile 0 packs the previous chunk's last tile; the phantom's own tiles go to the sink)
+          const bool plive = T == 0 ? ci > 0 : live;
+          const int64_t pc = T == 0 ? pcolw : colw;
+#pragma unroll
+          for (int u = 0; u < 2; ++u) {
+            const uint64_t o = opc[u];
+            *(gptr<uint16_t>)(plive && o ? o + uint64_t(pc) : sink) = uint16_t(w[u]);
+          }
+        }
+        if constexpr (T == 1) {
+          dma(ci + 1, 2 * Q);
+          dma(ci + 1, 2 * Q + 1);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        lgkm_wait();
+#pragma unroll
+        for (int j = 0; j < kQ; ++j) {
+          tie(An[j]);
+          Acur[j] = An[j];
+        }
+        if constexpr (kXn) {
+#pragma unroll
+          for (int j = 0; j < kQ; ++j)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              tie(xn[j][i]);
+              xc[j][i] = xn[j][i];
+            }
+        }
+        if constexpr (Q + 1 == kQ) {
+          tie(opn[0]);
+          tie(opn[1]);
+          opc[0] = opn[0];
+          opc[1] = opn[1];
+        }
+        if constexpr (COPY && T == MG - 1) {
+          tie(cd[0]);
+          tie(cd[1]);
+          copy_store(ci + 1, 2 * Q, cd[0]);
+          copy_store(ci + 1, 2 * Q + 1, cd[1]);
+        }
+      });
+    });
+  };
+
+  using P0 = std::integral_constant<int, 0>;
+  using P1 = std::integral_constant<int, 1>;
+  // chunk pairs; with an odd count the last pair's second chunk is the phantom, whose first tile
+  // packs the last real chunk's last tile
+  int ci = 0;
+  for (; ci < my_chunks; ci += 2) {
+    chunk_body(ci, P0{});
+    chunk_body(ci + 1, P1{});
+  }
+  if (ci == my_chunks) {
+    // an even count: pack the last real chunk's last tile here (parity 1)
+    constexpr int kLast = acc_set<MG>(1, MG - 1);
+    const int64_t pcolw = cbase(ci - 1) + wave * kCW + 2 * c;
+    uint32_t y[2][2];
+#pragma unroll
+    for (int b = 0; b < 8; ++b)
+#pragma unroll
+      for (int n = 0; n < 2; ++n)
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const uint32_t v = __float_as_uint(acc[kLast][n][8 * u + b]);
+          y[n][u] = b == 0 ? v : bfi(1u << b, v, y[n][u]);
+        }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const uint32_t w = __builtin_amdgcn_perm(y[1][u], y[0][u], 0x0c0c0400u);
+      const uint64_t o = opc[u];
+      *(gptr<uint16_t>)(o ? o + uint64_t(pcolw) : sink) = uint16_t(w);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA (dummy or not) outlives the wave
+}
+
+template <int MG, bool UNI, bool COPY>
+hipError_t launch_tm(const Fp4ArLaunch& a, int64_t* done, hipStream_t stream) {
+  const void* f = reinterpret_cast<const void*>(&gf_gemm_fp4tm_kernel<MG, UNI, COPY>);
+  const size_t lds = size_t(MG) * kNS * 1024 + kPtrBytes + size_t(4) * kKS * kSlotBytes;
+  if (lds > 160 * 1024) return hipErrorInvalidConfiguration;
+  hipError_t e = ensure_lds_optin(f, int(lds));
+  if (e != hipSuccess) return e;
+  static DeviceMemo<int, int> occ_memo;
+  const int occ = occ_memo.get_or(0, [&] {
+    int o = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, f, 256, lds) != hipSuccess) o = 0;
+    return o;
+  });
+  if (occ <= 0) return hipErrorInvalidConfiguration;
+  const int64_t nchunks = a.ncols / kBlockCols;
+  *done = nchunks * kBlockCols;
+  if (nchunks == 0) return hipSuccess;
+  static const int sink_spread = [] {  // GFRS_FP4_SINK=1: one shared sink slot (A/B only)
+    const char* env = std::getenv("GFRS_FP4_SINK");
+    return (env && std::atoi(env) == 1) ? 0 : 1;
+  }();
+  const int64_t slots = persistent_slots(occ, 1, nchunks);
+  gf_gemm_fp4tm_kernel<MG, UNI, COPY><<<unsigned(slots), 256, lds, stream>>>(
+      (cptr<uint64_t>)a.in, (cptr<uint64_t>)a.out, (cptr<uint64_t>)a.copy, static_cast<const i32x4*>(a.bitmat), a.k,
+      a.m, a.col0, nchunks, slots, a.in_stride, sink_spread);
+  return hipGetLastError();
+}
+
+template <int MG>
+hipError_t launch_tm_var(const Fp4ArLaunch& a, int64_t* done, hipStream_t stream) {
+  if (a.copy) return launch_tm<MG, false, true>(a, done, stream);
+  return a.in_stride ? launch_tm<MG, true, false>(a, done, stream) : launch_tm<MG, false, false>(a, done, stream);
+}
+
+}  // namespace
+
+bool fp4tm_supported(int k, int mg) { return k > 112 && k <= 128 && mg >= 5 && mg <= 7; }
+
+hipError_t launch_gf_gemm_fp4tm(const Fp4ArLaunch& a, int64_t* done, hipStream_t stream) {
+  *done = 0;
+  if (!fp4tm_supported(a.k, a.mg) || a.m > 4 * a.mg || a.ncols < 0 || (a.col0 & 1) || a.batch != 1)
+    return hipErrorInvalidValue;
+  switch (a.mg) {
+    case 5: return launch_tm_var<5>(a, done, stream);
+    case 6: return launch_tm_var<6>(a, done, stream);
+    default: return launch_tm_var<7>(a, done, stream);
+  }
+}
+
+}  // namespace gfrs

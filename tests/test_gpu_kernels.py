@@ -345,6 +345,42 @@ def test_fp4_fused_copy_decode_shape(m):
     assert (got[ncopy:] == 0x44).all()
 
 
+@pytest.mark.parametrize("k,m", [(128, 26), (128, 20), (128, 24), (120, 21), (113, 17)])
+@pytest.mark.parametrize("variant", ["uniform", "scattered", "copy"])
+@pytest.mark.parametrize("nblk", [256 * 3 + 5, 256 * 2, 40])
+def test_fp4_tile_major_kernel_matches_oracle(k, m, variant, nblk, monkeypatch):
+    """The tile-major FP4 kernel (gf_gemm_fp4tm_kernel, GFRS_FP4_KERNEL=tm: the chunk's B resident
+    in AGPRs, tiles in turn, 5..7 M-tiles). Column counts give the persistent blocks an odd or an
+    even number of chunks (the phantom chunk and the drain after the loop) or a single one, plus a
+    v_perm remainder. The fused copy covers the first inputs only (the decode layout). Bit-exact
+    against the oracle, and nothing is written outside the outputs' and copies' columns."""
+    _native_loaded()
+    monkeypatch.setenv("GFRS_FP4_KERNEL", "tm")
+    ncols = 256 * nblk + 77
+    rng = np.random.default_rng(k * 131 + m * 7 + nblk)
+    coeff = rng.integers(0, 256, size=(m, k), dtype=np.uint8)
+    host, dev = _rand_rows(k, ncols, k + m + nblk)
+    inputs, want_in = dev, host
+    copies = None
+    if variant in ("scattered", "copy"):
+        perm = rng.permutation(k)
+        inputs = [dev[j].clone() for j in perm]
+        want_in = host[perm]
+    ncopy = k - m
+    if variant == "copy":
+        cdst = alloc_rows(k, ncols, "cuda", fill=0x44)
+        copies = [cdst[j] if j < ncopy else None for j in range(k)]
+    out = alloc_rows(m, ncols, "cuda", fill=0x5A)
+    plan = GemmPlan(inputs, out, coeff, copies=copies, engine="mfma")
+    plan.run()
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), GF256.gemm(coeff, want_in))
+    if copies is not None:
+        c = cdst.cpu().numpy()
+        assert np.array_equal(c[:ncopy], want_in[:ncopy])
+        assert (c[ncopy:] == 0x44).all()
+
+
 @pytest.mark.parametrize("k,n,matrix", [(10, 14, "vandermonde"), (128, 160, "cauchy"), (4, 6, "vandermonde"),
                                         (200, 255, "sys_vandermonde")])
 def test_decode_system_matches_host_decode_matrix(k, n, matrix):

@@ -17,10 +17,12 @@ HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 
 
 @pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
-@pytest.mark.parametrize("name", ["gf_mfma16", "gf_mfma8r", "gf_mfma_fp4", "gf_mfma_fp4ar"])
+@pytest.mark.parametrize("name", ["gf_mfma16", "gf_mfma8r", "gf_mfma_fp4", "gf_mfma_fp4ar", "gf_mfma_fp4tm"])
 def test_no_unguarded_accumulator_reads(name, tmp_path):
     asm = tmp_path / f"{name}.s"
-    subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-S", "--offload-device-only",
+    # (compiled as csrc/Makefile does: the A-resident and tile-major kernels in MFMA VGPR form)
+    extra = ["-mllvm", "-amdgpu-mfma-vgpr-form=1"] if name in ("gf_mfma_fp4ar", "gf_mfma_fp4tm") else []
+    subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-S", "--offload-device-only", *extra,
                     "-I", os.path.join(ROOT, "csrc", "include"), os.path.join(ROOT, "csrc", "kernels", f"{name}.hip"),
                     "-o", str(asm)], check=True, capture_output=True, timeout=600)
     r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "mfma_hazard_check.py"), str(asm)],
