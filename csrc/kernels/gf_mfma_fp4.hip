@@ -1250,12 +1250,17 @@ bool use_ar(const Fp4Geometry& geo, int k, bool copies) {
   return geo.mg == 4 || (!copies && (geo.mg == 6 || geo.mg == 8));
 }
 
-// The tile-major kernel (gf_mfma_fp4tm.hip) for one group of 5..7 M-tiles at k in (112, 128]:
-// GFRS_FP4_KERNEL=tm selects it (A/B measurements).
-bool use_tm(const Fp4Geometry& geo, int k) {
-  if (geo.groups != 1 || !fp4tm_supported(k, geo.mg)) return false;
+// The tile-major kernel (gf_mfma_fp4tm.hip) for one group of 5..7 M-tiles at k in (112, 128], where
+// it measured faster (profiles/wide_stripe/r08_tm, k = 128, 1 GiB, medians): plain GEMMs at 5..7
+// tiles (m = 26: 728-744 vs 784-790 us on v1; m = 24: 646-648 vs 668-677 on the A-resident kernel;
+// m = 20: 569-608 vs 625) and the 7-tile GEMM with fused copies (the k = 128 decode: 888-904 vs
+// 902-908). With copies at 5 tiles it only ties v1, at 6 it does not fit the registers.
+// GFRS_FP4_KERNEL=tm forces it wherever supported; =v1 / =sk / =ar never.
+bool use_tm(const Fp4Geometry& geo, int k, bool copies) {
+  if (geo.groups != 1 || !fp4tm_supported(k, geo.mg, copies)) return false;
   const char* env = std::getenv("GFRS_FP4_KERNEL");
-  return env && std::strcmp(env, "tm") == 0;
+  if (env && *env) return std::strcmp(env, "tm") == 0;
+  return !copies || geo.mg == 7;
 }
 
 }  // namespace
@@ -1287,7 +1292,7 @@ hipError_t launch_gf_gemm_fp4(const void* bitmat, const void* desc, int k, int m
   const DescLayout l = desc_layout(k, m_pad);
   const char* b = static_cast<const char*>(desc);
   const Fp4Geometry geo = geometry(k, m, mg_cap, copies);
-  if (use_tm(geo, k)) {  // the tile-major form (gf_mfma_fp4tm.hip)
+  if (use_tm(geo, k, copies) && !(copies && split_copy_mode())) {  // the tile-major form (gf_mfma_fp4tm.hip)
     Fp4ArLaunch a{};
     a.in = reinterpret_cast<const uint64_t*>(b + l.in_off);
     a.out = reinterpret_cast<const uint64_t*>(b + l.out_off);

@@ -52,7 +52,7 @@ constexpr int kCW = 64;           // columns per wave (two 32-column N-tiles, in
 constexpr int kNS = 16;           // K-steps per chunk (k in (112, 128]: 128 rows = 1024 bits)
 constexpr int kKS = 8;            // ring slots per chunk (2 K-steps each) = the ring depth
 constexpr int kRS = 16;           // input rows per ring slot
-constexpr int kQ = 4;             // K-steps per super-step (LDS reads one super-step ahead)
+constexpr int kQ = 2;             // K-steps per super-step (LDS reads one super-step ahead)
 constexpr int kBlockCols = 256;   // 4 waves x 64 columns
 constexpr int kPtrBytes = 8 * (256 + 32 + 256);  // LDS: row, output-row and copy pointer tables
 
@@ -75,10 +75,10 @@ __device__ __forceinline__ uint32_t bfi(uint32_t mask, uint32_t a, uint32_t b) {
   return __builtin_amdgcn_bitop3_b32(mask, a, b, 0xCA);
 }
 
-// accumulator set of tile t in chunk parity P (alternating over the global tile sequence)
-template <int MG>
-__host__ __device__ constexpr int acc_set(int P, int t) {
-  return (P * MG + t) & 1;
+// accumulator set of tile group g in chunk parity P (alternating over the global group sequence)
+template <int NG>
+__host__ __device__ constexpr int acc_set(int P, int g) {
+  return (P * NG + g) & 1;
 }
 
 template <int MG, bool UNI, bool COPY>
@@ -87,7 +87,7 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4tm_kernel(cptr<uint64_t> in
                                                                int k, int m, int64_t col0, int64_t nchunks,
                                                                int64_t chunk_slots, int64_t in_stride,
                                                                int sink_spread) {
-  static_assert(MG >= 4 && MG <= 7, "DMAs in tile 1 must land before the expansion in tile MG-1");
+  static_assert(MG >= 5 && MG <= 7, "three tile groups at least: DMAs in group 0, the wait in group NG-2");
   constexpr size_t kA = size_t(MG) * kNS * 1024;  // LDS A slice [kstep][tile][lane] x 16 B
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   i32x4* afrag = reinterpret_cast<i32x4*>(smem);
@@ -116,35 +116,36 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4tm_kernel(cptr<uint64_t> in
   const uint32_t ring_lane = ring_base + 16u * lane;                   // this lane's DMA'd 16 B
   const uint32_t a_lo = lds0 + 16u * lane, a_hi = a_lo + 65536u;
   const uint32_t optr_addr = lds0 + uint32_t(kA) + 2048u + 16u * h;  // outptr[4t + 2h + u]: + 32t + 8u
-  const unsigned sslot = sink_spread ? (blockIdx.x * 4u + unsigned(wave)) % unsigned(kFp4SinkSlots) : 0u;
+  const unsigned sslot = (sink_spread & 1) ? (blockIdx.x * 4u + unsigned(wave)) % unsigned(kFp4SinkSlots) : 0u;
   const uint64_t sink = uint64_t(bitmat + size_t(MG) * kNS * 64) + uint64_t(sslot) * 1024u + 16 * lane;
   const int scale = 0x7F7F7F7F;  // E8M0 1.0 for every block of 32
   const uint64_t in0 = UNI ? in[0] : 0;
   const int drow = lane >> 2;                      // this lane's row within a DMA'd slot
   const int dcol = wave * kCW + 16 * (lane & 3);   // and its 16 columns (block-relative)
-  // the slot rows are the same in every chunk: their input and copy row pointers stay in registers
-  uint64_t rp[kKS], cpv[kKS];
-#pragma unroll
-  for (int p = 0; p < kKS; ++p) {
-    const int r = kRS * p + drow;
-    rp[p] = UNI ? in0 + uint64_t(int64_t(r < k ? r : k - 1) * in_stride) : rowptr[r < k ? r : k - 1];
-    cpv[p] = COPY && r < k ? copyptr[r] : 0;
-  }
+  const uint32_t rowptr_addr = lds0 + uint32_t(kA);
+  const uint32_t cptr_addr = rowptr_addr + 8u * (256u + 32u);
+  auto slot_row = [&](int p) __attribute__((always_inline)) { return kRS * p + drow < k ? kRS * p + drow : k - 1; };
   auto cbase = [&](int ci) __attribute__((always_inline)) {
     return col0 + (slot0 + int64_t(ci) * chunk_slots) * kBlockCols;
   };
-  // DMA of ring slot p for chunk cn (past my chunks: chunk 0's bytes, never used)
-  auto dma = [&](int cn, int p) __attribute__((always_inline)) {
+  // DMA of ring slot p for chunk cn (past my chunks: chunk 0's bytes, never used); rowp: the slot
+  // row's input pointer (scattered rows) read from LDS beforehand
+  auto dma = [&](int cn, int p, uint64_t rowp) __attribute__((always_inline)) {
     const int64_t col = cbase(cn < my_chunks ? cn : 0) + dcol;
-    __builtin_amdgcn_global_load_lds((gptr<const void>)(rp[p] + uint64_t(col)), ring + p * kSlotBytes, 16, 0, 0);
+    const uint64_t base = UNI ? in0 + uint64_t(int64_t(slot_row(p)) * in_stride) : rowp;
+    __builtin_amdgcn_global_load_lds((gptr<const void>)(base + uint64_t(col)), ring + p * kSlotBytes, 16, 0, 0);
   };
-  // fused copy of ring slot p (chunk cn's bytes) from this lane's 16 B
-  auto copy_store = [&](int cn, int p, u32x4 v) __attribute__((always_inline)) {
-    const uint64_t cp = cpv[p];
-    const bool live = cn < my_chunks && cp;
+  // fused copy of ring slot p (chunk cn's bytes) from this lane's 16 B; cp: the row's copy pointer
+  auto copy_store = [&](int cn, int p, uint64_t cp, u32x4 v) __attribute__((always_inline)) {
+    const bool live = cn < my_chunks && kRS * p + drow < k && cp && !(sink_spread & 2);
     __builtin_nontemporal_store(v, (gptr<u32x4>)(live ? cp + uint64_t(cbase(cn) + dcol) : sink));
   };
-  // rows 4h+i of K-step s (slot s / 2, half s % 2), this lane's column pair
+  auto read_ptr = [&](uint64_t& v, uint32_t addr) __attribute__((always_inline)) {
+    uint64_t r;
+    asm volatile("ds_read_b64 %0, %1" : "=&v"(r) : "v"(addr) : "memory");
+    v = r;
+  };
+  // rows 4h+i of K-step S (slot S / 2, half S % 2), this lane's column pair
   auto read_x = [&](uint32_t (&x)[4], auto s_tag) __attribute__((always_inline)) {
     constexpr int S = decltype(s_tag)::value;
     constexpr int off = (S / 2) * kSlotBytes + (S % 2) * 8 * kCW;
@@ -178,6 +179,7 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4tm_kernel(cptr<uint64_t> in
     asm volatile("ds_read_b128 %0, %1 offset:%2" : "=&v"(r) : "v"(addr), "n"(off) : "memory");
     v = r;
   };
+  // output row pointers of tile T: rows 4T + 2h + u
   auto read_op = [&](uint64_t (&o)[2], auto t_tag) __attribute__((always_inline)) {
     constexpr int T = decltype(t_tag)::value;
     const uint32_t addr = optr_addr;
@@ -201,18 +203,35 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4tm_kernel(cptr<uint64_t> in
       bo[t][3] = int((w[t] >> 1) & 0x44444444u);
     }
   };
+  // the two output words (byte rows 2h, 2h + 1 of the tile, both N-tiles) of one accumulator tile
+  auto pack = [&](uint32_t (&w)[2], const f32x16 (&a)[2]) __attribute__((always_inline)) {
+    uint32_t y[2][2];
+#pragma unroll
+    for (int b = 0; b < 8; ++b)
+#pragma unroll
+      for (int n = 0; n < 2; ++n)
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const uint32_t v = __float_as_uint(a[n][8 * u + b]);
+          y[n][u] = b == 0 ? v : bfi(1u << b, v, y[n][u]);
+        }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) w[u] = __builtin_amdgcn_perm(y[1][u], y[0][u], 0x0c0c0400u);
+  };
 
-  i32x4 Bc[kNS][2];  // B of the chunk being multiplied, resident in AGPRs
-  f32x16 acc[2][2];  // two accumulator sets x two N-tiles
-  f32x16 bias;       // start value 2^(23 - b) on output bit b = accumulator register & 7
+  i32x4 Bc[kNS][2];     // B of the chunk being multiplied, resident in AGPRs
+  f32x16 acc[2][2][2];  // [set][tile of the group][N-tile]
+  f32x16 bias;          // start value 2^(23 - b) on output bit b = accumulator register & 7
 #pragma unroll
   for (int v = 0; v < 16; ++v) bias[v] = float(1u << (23 - (v & 7)));
 #pragma unroll
-  for (int i = 0; i < 2; ++i) acc[i][0] = acc[i][1] = bias;
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int e = 0; e < 2; ++e) acc[i][e][0] = acc[i][e][1] = bias;
 
   // prologue: chunk 0's slots, expanded into B and copied
 #pragma unroll
-  for (int p = 0; p < kKS; ++p) dma(0, p);
+  for (int p = 0; p < kKS; ++p) dma(0, p, UNI ? 0 : rowptr[slot_row(p)]);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   static_for<kNS>([&](auto s_tag) {
     constexpr int S = decltype(s_tag)::value;
@@ -227,53 +246,79 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4tm_kernel(cptr<uint64_t> in
   });
   if constexpr (COPY) {
     static_for<kKS>([&](auto p_tag) {
+      constexpr int Pp = decltype(p_tag)::value;
       u32x4 v;
+      uint64_t cp;
       read_slot(v, p_tag);
+      read_ptr(cp, cptr_addr + 8u * uint32_t(slot_row(Pp)));
       lgkm_wait();
       tie(v);
-      copy_store(0, decltype(p_tag)::value, v);
+      tie(cp);
+      copy_store(0, Pp, cp, v);
     });
   }
+  // tile groups: pairs (2g, 2g + 1), the last one single when MG is odd
+  constexpr int NG = (MG + 1) / 2;
   using I0 = std::integral_constant<int, 0>;
-  i32x4 Acur[kQ];  // A of the current super-step
-  static_for<kQ>([&](auto j) { read_a(Acur[decltype(j)::value], I0{}, j); });
-  uint64_t opc[2];  // output row pointers of the tile packed next (MG-1 of "chunk -1": discarded)
-  read_op(opc, std::integral_constant<int, MG - 1>{});
+  i32x4 Acur[2][kQ];  // A of the current super-step: [tile of the group][K-step]
+  static_for<kQ>([&](auto j) {
+    read_a(Acur[0][decltype(j)::value], I0{}, j);
+    read_a(Acur[1][decltype(j)::value], std::integral_constant<int, 1>{}, j);
+  });
+  uint64_t opc[2][2];  // output row pointers of the group packed next (the last of "chunk -1": discarded)
+  read_op(opc[0], std::integral_constant<int, 2 * (NG - 1)>{});
+  if constexpr (MG % 2 == 0) read_op(opc[1], std::integral_constant<int, MG - 1>{});
   lgkm_wait();
 #pragma unroll
-  for (int j = 0; j < kQ; ++j) tie(Acur[j]);
-  tie(opc[0]);
-  tie(opc[1]);
-  uint32_t xc[kQ][4] = {};  // raw bytes of the next chunk's K-steps of this super-step (last tile)
+  for (int j = 0; j < kQ; ++j) {
+    tie(Acur[0][j]);
+    tie(Acur[1][j]);
+  }
+  tie(opc[0][0]);
+  tie(opc[0][1]);
+  if constexpr (MG % 2 == 0) {
+    tie(opc[1][0]);
+    tie(opc[1][1]);
+  }
+  uint32_t xc[kQ][4] = {};  // raw bytes of the next chunk's K-steps of this super-step (last group)
 
   // One chunk ci with chunk parity P (ci == my_chunks: the phantom).
   auto chunk_body = [&](int ci, auto p_tag) __attribute__((always_inline)) {
     constexpr int P = decltype(p_tag)::value;
     const bool live = ci < my_chunks;
-    const int64_t colw = cbase(ci) + wave * kCW + 2 * c;                                  // this chunk
-    const int64_t pcolw = colw - chunk_slots * kBlockCols;                                  // previous chunk
-    static_for<MG>([&](auto t_tag) {
-      constexpr int T = decltype(t_tag)::value;
-      constexpr int PT = T == 0 ? MG - 1 : T - 1;                 // the tile packed during tile T
-      constexpr int kSet = acc_set<MG>(P, T);
-      constexpr int kPSet = T == 0 ? acc_set<MG>(P ^ 1, MG - 1) : acc_set<MG>(P, T - 1);
-      static_assert(kSet != kPSet, "a tile must not write the set still waiting to be packed");
-      static_for<kQ>([&](auto q_tag) {
+    const int64_t colw = cbase(ci) + wave * kCW + 2 * c;  // this chunk
+    const int64_t pcolw = colw - chunk_slots * kBlockCols;  // previous chunk
+    static_for<NG>([&](auto g_tag) {
+      constexpr int G = decltype(g_tag)::value;
+      constexpr int T0 = 2 * G;
+      constexpr int GS = T0 + 1 < MG ? 2 : 1;  // tiles in this group
+      constexpr int PG = G == 0 ? NG - 1 : G - 1;  // the group packed during this one
+      constexpr int PGS = 2 * PG + 1 < MG ? 2 : 1;
+      constexpr int kSet = acc_set<NG>(P, G);
+      constexpr int kPSet = G == 0 ? acc_set<NG>(P ^ 1, NG - 1) : acc_set<NG>(P, G - 1);
+      static_assert(kSet != kPSet, "a group must not write the set still waiting to be packed");
+      constexpr int kSS = kNS / kQ;  // super-steps per group
+      static_for<kSS>([&](auto q_tag) {
         constexpr int Q = decltype(q_tag)::value;
         // ---- LDS reads for the next super-step (retired by this one's closing lgkmcnt(0))
-        constexpr int NT = Q + 1 < kQ ? T : (T + 1 < MG ? T + 1 : 0);
-        constexpr int NQ = Q + 1 < kQ ? Q + 1 : 0;
-        i32x4 An[kQ];
+        constexpr int NGi = Q + 1 < kSS ? G : (G + 1 < NG ? G + 1 : 0);
+        constexpr int NQ = Q + 1 < kSS ? Q + 1 : 0;
+        constexpr int NT0 = 2 * NGi;
+        constexpr int NGS = NT0 + 1 < MG ? 2 : 1;
+        i32x4 An[2][kQ];
         static_for<kQ>([&](auto j) {
-          read_a(An[decltype(j)::value], std::integral_constant<int, NT>{},
-                 std::integral_constant<int, kQ * NQ + decltype(j)::value>{});
+          constexpr int J = decltype(j)::value;
+          read_a(An[0][J], std::integral_constant<int, NT0>{}, std::integral_constant<int, kQ * NQ + J>{});
+          if constexpr (NGS == 2)
+            read_a(An[1][J], std::integral_constant<int, NT0 + 1>{}, std::integral_constant<int, kQ * NQ + J>{});
         });
-        // the next chunk's raw bytes for the expansion in the last tile, one super-step ahead
-        constexpr bool kXn = (T == MG - 1 && Q + 1 < kQ) || (T == MG - 2 && Q + 1 == kQ);
-        if constexpr (T == MG - 2 && Q + 1 == kQ) {
-          // the next chunk's 8 DMAs (tile 1) have landed: younger are the 2 epilogue stores of each
-          // of tiles 2 .. MG-2 (vmcnt retires in issue order)
-          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (MG - 3)) : "memory");
+        constexpr bool kLastG = G == NG - 1;
+        // the next chunk's raw bytes for the expansion in the last group, one super-step ahead
+        constexpr bool kXn = (kLastG && Q + 1 < kSS) || (G == NG - 2 && Q + 1 == kSS);
+        if constexpr (G == NG - 2 && Q + 1 == kSS) {
+          // the next chunk's 8 DMAs (group 0) have landed: younger are the 4 epilogue stores of each
+          // of groups 1 .. NG-2 (pairs; vmcnt retires in issue order)
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (NG - 2)) : "memory");
         }
         uint32_t xn[kQ][4];
         if constexpr (kXn) {
@@ -281,30 +326,38 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4tm_kernel(cptr<uint64_t> in
             read_x(xn[decltype(j)::value], std::integral_constant<int, kQ * NQ + decltype(j)::value>{});
           });
         }
-        // fused copy: this super-step's two slots of the next chunk (last tile)
-        [[maybe_unused]] u32x4 cd[2];
-        if constexpr (COPY && T == MG - 1) {
-          read_slot(cd[0], std::integral_constant<int, 2 * Q>{});
-          read_slot(cd[1], std::integral_constant<int, 2 * Q + 1>{});
+        // fused copy: slot Q of the next chunk (last group); the DMA row pointer of slot Q (group 0)
+        [[maybe_unused]] u32x4 cd;
+        [[maybe_unused]] uint64_t cpp = 0, rpp = 0;
+        if constexpr (COPY && kLastG) {
+          read_slot(cd, q_tag);
+          read_ptr(cpp, cptr_addr + 8u * uint32_t(slot_row(Q)));
         }
-        uint64_t opn[2];
-        if constexpr (Q + 1 == kQ) read_op(opn, t_tag);  // tile T is packed during the next tile
+        if constexpr (!UNI && G == 0) read_ptr(rpp, rowptr_addr + 8u * uint32_t(slot_row(Q)));
+        uint64_t opn[2][2];
+        if constexpr (Q + 1 == kSS) {  // this group's output pointers: it is packed during the next
+          read_op(opn[0], std::integral_constant<int, T0>{});
+          if constexpr (GS == 2) read_op(opn[1], std::integral_constant<int, T0 + 1>{});
+        }
         __builtin_amdgcn_sched_barrier(0);
 
-        // ---- 4 K-steps x 2 N-tiles of tile T, from the resident B
+        // ---- kQ K-steps x GS tiles x 2 N-tiles from the resident B (GS x 2 independent chains)
         static_for<kQ>([&](auto j_tag) {
           constexpr int J = decltype(j_tag)::value;
           constexpr int S = kQ * Q + J;
-          const i32x8 a = {Acur[J][0], Acur[J][1], Acur[J][2], Acur[J][3], 0, 0, 0, 0};
 #pragma unroll
-          for (int n = 0; n < 2; ++n) {
-            const i32x8 bb = {Bc[S][n][0], Bc[S][n][1], Bc[S][n][2], Bc[S][n][3], 0, 0, 0, 0};
-            acc[kSet][n] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, bb, S == 0 ? bias : acc[kSet][n], 4,
-                                                                            4, 0, scale, 0, scale);
+          for (int e = 0; e < GS; ++e) {
+            const i32x8 a = {Acur[e][J][0], Acur[e][J][1], Acur[e][J][2], Acur[e][J][3], 0, 0, 0, 0};
+#pragma unroll
+            for (int n = 0; n < 2; ++n) {
+              const i32x8 bb = {Bc[S][n][0], Bc[S][n][1], Bc[S][n][2], Bc[S][n][3], 0, 0, 0, 0};
+              acc[kSet][e][n] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(
+                  a, bb, S == 0 ? bias : acc[kSet][e][n], 4, 4, 0, scale, 0, scale);
+            }
           }
         });
-        // ---- VALU under the MFMAs: the next chunk's B (last tile), the previous tile's epilogue
-        if constexpr (T == MG - 1) {
+        // ---- VALU under the MFMAs: the next chunk's B (last group), the previous group's epilogue
+        if constexpr (kLastG) {
           static_for<kQ>([&](auto j_tag) {
             constexpr int J = decltype(j_tag)::value;
             expand(Bc[kQ * Q + J], xc[J]);
@@ -312,52 +365,44 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4tm_kernel(cptr<uint64_t> in
             for (int n = 0; n < 2; ++n) asm volatile("" : "+a"(Bc[kQ * Q + J][n]));
           });
         }
-        [[maybe_unused]] uint32_t w[2];
+        [[maybe_unused]] uint32_t w[2][2];
         if constexpr (Q == 0) {
-          // output bytes of tile PT: 7 bit inserts per byte, straight from the accumulator VGPRs
-          uint32_t y[2][2];
-#pragma unroll
-          for (int b = 0; b < 8; ++b)
-#pragma unroll
-            for (int n = 0; n < 2; ++n)
-#pragma unroll
-              for (int u = 0; u < 2; ++u) {
-                const uint32_t v = __float_as_uint(acc[kPSet][n][8 * u + b]);
-                y[n][u] = b == 0 ? v : bfi(1u << b, v, y[n][u]);
-              }
-#pragma unroll
-          for (int u = 0; u < 2; ++u) w[u] = __builtin_amdgcn_perm(y[1][u], y[0][u], 0x0c0c0400u);
+          pack(w[0], acc[kPSet][0]);
+          if constexpr (PGS == 2) pack(w[1], acc[kPSet][1]);
         }
-        constexpr int kValu = (T == MG - 1 ? kQ * 22 : 0) + (Q == 0 ? 30 : 0);  // (22: 14 + 8 AGPR writes)
-        constexpr int kPer = (kValu + 2 * kQ - 1) / (2 * kQ);
+        constexpr int kMfma = kQ * GS * 2;
+        constexpr int kValu = (kLastG ? kQ * 22 : 0) + (Q == 0 ? 30 * PGS : 0);  // (22: 14 + 8 AGPR writes)
+        constexpr int kPer = (kValu + kMfma - 1) / kMfma;
 #pragma unroll
-        for (int i = 0; i < 2 * kQ; ++i) {
+        for (int i = 0; i < kMfma; ++i) {
           __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);     // MFMA
           __builtin_amdgcn_sched_group_barrier(0x002, kPer, 0);  // VALU
         }
         __builtin_amdgcn_sched_barrier(0);
 
-        // ---- stores and the next chunk's DMAs
+        // ---- stores
         if constexpr (Q == 0) {
-          // (tile 0 packs the previous chunk's last tile; the phantom's own tiles go to the sink)
-          const bool plive = T == 0 ? ci > 0 : live;
-          const int64_t pc = T == 0 ? pcolw : colw;
+          // (group 0 packs the previous chunk's last group; the phantom's own groups go to the sink)
+          const bool plive = G == 0 ? ci > 0 : live;
+          const int64_t pc = G == 0 ? pcolw : colw;
 #pragma unroll
-          for (int u = 0; u < 2; ++u) {
-            const uint64_t o = opc[u];
-            *(gptr<uint16_t>)(plive && o ? o + uint64_t(pc) : sink) = uint16_t(w[u]);
-          }
-        }
-        if constexpr (T == 1) {
-          dma(ci + 1, 2 * Q);
-          dma(ci + 1, 2 * Q + 1);
+          for (int e = 0; e < PGS; ++e)
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+              const uint64_t o = opc[e][u];
+              *(gptr<uint16_t>)(plive && o ? o + uint64_t(pc) : sink) = uint16_t(w[e][u]);
+            }
         }
         __builtin_amdgcn_sched_barrier(0);
         lgkm_wait();
 #pragma unroll
         for (int j = 0; j < kQ; ++j) {
-          tie(An[j]);
-          Acur[j] = An[j];
+          tie(An[0][j]);
+          Acur[0][j] = An[0][j];
+          if constexpr (NGS == 2) {
+            tie(An[1][j]);
+            Acur[1][j] = An[1][j];
+          }
         }
         if constexpr (kXn) {
 #pragma unroll
@@ -368,17 +413,24 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4tm_kernel(cptr<uint64_t> in
               xc[j][i] = xn[j][i];
             }
         }
-        if constexpr (Q + 1 == kQ) {
-          tie(opn[0]);
-          tie(opn[1]);
-          opc[0] = opn[0];
-          opc[1] = opn[1];
+        if constexpr (Q + 1 == kSS) {
+#pragma unroll
+          for (int e = 0; e < GS; ++e) {
+            tie(opn[e][0]);
+            tie(opn[e][1]);
+            opc[e][0] = opn[e][0];
+            opc[e][1] = opn[e][1];
+          }
         }
-        if constexpr (COPY && T == MG - 1) {
-          tie(cd[0]);
-          tie(cd[1]);
-          copy_store(ci + 1, 2 * Q, cd[0]);
-          copy_store(ci + 1, 2 * Q + 1, cd[1]);
+        // the next chunk's DMA of slot Q (group 0: its ring slot was consumed in the last group)
+        if constexpr (G == 0) {
+          if constexpr (!UNI) tie(rpp);
+          dma(ci + 1, Q, rpp);
+        }
+        if constexpr (COPY && kLastG) {
+          tie(cd);
+          tie(cpp);
+          copy_store(ci + 1, Q, cpp, cd);
         }
       });
     });
@@ -386,32 +438,27 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4tm_kernel(cptr<uint64_t> in
 
   using P0 = std::integral_constant<int, 0>;
   using P1 = std::integral_constant<int, 1>;
-  // chunk pairs; with an odd count the last pair's second chunk is the phantom, whose first tile
-  // packs the last real chunk's last tile
+  // chunk pairs; with an odd count the last pair's second chunk is the phantom, whose first group
+  // packs the last real chunk's last group
   int ci = 0;
   for (; ci < my_chunks; ci += 2) {
     chunk_body(ci, P0{});
     chunk_body(ci + 1, P1{});
   }
   if (ci == my_chunks) {
-    // an even count: pack the last real chunk's last tile here (parity 1)
-    constexpr int kLast = acc_set<MG>(1, MG - 1);
+    // an even count: pack the last real chunk's last group here (parity 1)
+    constexpr int kLast = acc_set<NG>(1, NG - 1);
     const int64_t pcolw = cbase(ci - 1) + wave * kCW + 2 * c;
-    uint32_t y[2][2];
+    constexpr int LGS = 2 * (NG - 1) + 1 < MG ? 2 : 1;
 #pragma unroll
-    for (int b = 0; b < 8; ++b)
+    for (int e = 0; e < LGS; ++e) {
+      uint32_t w[2];
+      pack(w, acc[kLast][e]);
 #pragma unroll
-      for (int n = 0; n < 2; ++n)
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          const uint32_t v = __float_as_uint(acc[kLast][n][8 * u + b]);
-          y[n][u] = b == 0 ? v : bfi(1u << b, v, y[n][u]);
-        }
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const uint32_t w = __builtin_amdgcn_perm(y[1][u], y[0][u], 0x0c0c0400u);
-      const uint64_t o = opc[u];
-      *(gptr<uint16_t>)(o ? o + uint64_t(pcolw) : sink) = uint16_t(w);
+      for (int u = 0; u < 2; ++u) {
+        const uint64_t o = opc[e][u];
+        *(gptr<uint16_t>)(o ? o + uint64_t(pcolw) : sink) = uint16_t(w[u]);
+      }
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA (dummy or not) outlives the wave
@@ -434,9 +481,12 @@ hipError_t launch_tm(const Fp4ArLaunch& a, int64_t* done, hipStream_t stream) {
   const int64_t nchunks = a.ncols / kBlockCols;
   *done = nchunks * kBlockCols;
   if (nchunks == 0) return hipSuccess;
-  static const int sink_spread = [] {  // GFRS_FP4_SINK=1: one shared sink slot (A/B only)
+  // flags: bit 0 = spread the sink (GFRS_FP4_SINK=1 clears it: one shared slot); bit 1 = every
+  // fused copy stored to the sink instead (GFRS_FP4_TM_ABL=1: an ablation, copies are wrong). A/B only.
+  static const int sink_spread = [] {
     const char* env = std::getenv("GFRS_FP4_SINK");
-    return (env && std::atoi(env) == 1) ? 0 : 1;
+    const char* abl = std::getenv("GFRS_FP4_TM_ABL");
+    return ((env && std::atoi(env) == 1) ? 0 : 1) | ((abl && std::atoi(abl) == 1) ? 2 : 0);
   }();
   const int64_t slots = persistent_slots(occ, 1, nchunks);
   gf_gemm_fp4tm_kernel<MG, UNI, COPY><<<unsigned(slots), 256, lds, stream>>>(
@@ -447,17 +497,24 @@ hipError_t launch_tm(const Fp4ArLaunch& a, int64_t* done, hipStream_t stream) {
 
 template <int MG>
 hipError_t launch_tm_var(const Fp4ArLaunch& a, int64_t* done, hipStream_t stream) {
-  if (a.copy) return launch_tm<MG, false, true>(a, done, stream);
+  if (a.copy) {
+    // (6 tiles with fused copies need more than the 512 registers: no such build)
+    if constexpr (MG == 6) return hipErrorNotSupported;
+    else return launch_tm<MG, false, true>(a, done, stream);
+  }
   return a.in_stride ? launch_tm<MG, true, false>(a, done, stream) : launch_tm<MG, false, false>(a, done, stream);
 }
 
 }  // namespace
 
-bool fp4tm_supported(int k, int mg) { return k > 112 && k <= 128 && mg >= 5 && mg <= 7; }
+bool fp4tm_supported(int k, int mg, bool copies) {
+  return k > 112 && k <= 128 && mg >= 5 && mg <= 7 && !(copies && mg == 6);
+}
 
 hipError_t launch_gf_gemm_fp4tm(const Fp4ArLaunch& a, int64_t* done, hipStream_t stream) {
   *done = 0;
-  if (!fp4tm_supported(a.k, a.mg) || a.m > 4 * a.mg || a.ncols < 0 || (a.col0 & 1) || a.batch != 1)
+  if (!fp4tm_supported(a.k, a.mg, a.copy != nullptr) || a.m > 4 * a.mg || a.ncols < 0 || (a.col0 & 1) ||
+      a.batch != 1)
     return hipErrorInvalidValue;
   switch (a.mg) {
     case 5: return launch_tm_var<5>(a, done, stream);
