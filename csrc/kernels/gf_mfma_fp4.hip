@@ -1254,7 +1254,7 @@ bool use_ar(const Fp4Geometry& geo, int k, bool copies) {
 // it measured faster (profiles/wide_stripe/r08_tm, k = 128, 1 GiB, medians): plain GEMMs at 5..7
 // tiles (m = 26: 728-744 vs 784-790 us on v1; m = 24: 646-648 vs 668-677 on the A-resident kernel;
 // m = 20: 569-608 vs 625) and the 7-tile GEMM with fused copies (the k = 128 decode: 888-904 vs
-// 902-908). With copies at 5 tiles it only ties v1, at 6 it does not fit the registers.
+// 902-908). With copies at 5 or 6 tiles it trails v1 (819-824 vs 773-780, 849-866 vs 831-832 us).
 // GFRS_FP4_KERNEL=tm forces it wherever supported; =v1 / =sk / =ar never.
 bool use_tm(const Fp4Geometry& geo, int k, bool copies) {
   if (geo.groups != 1 || !fp4tm_supported(k, geo.mg, copies)) return false;

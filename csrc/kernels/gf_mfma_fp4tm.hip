@@ -8,18 +8,21 @@
 //
 // Here a wave keeps its chunk's B operand resident instead — all 16 K-steps x 2 N-tiles, 128
 // registers, in the AGPRs (this file is compiled with -amdgpu-mfma-vgpr-form, so the scaled MFMA
-// reads B from AGPRs and keeps its accumulators in arch VGPRs) — and runs the tiles one after the
-// other, 16 K-steps each:
-//   * only two tiles' accumulators are live: the one accumulating and the previous one, whose
-//     epilogue (28 bit inserts straight from VGPRs, 2 stores) runs under this tile's 32 MFMAs;
+// reads B from AGPRs and keeps its accumulators in arch VGPRs) — and runs the M-tiles in pairs,
+// 16 K-steps per pair (a pair is four independent accumulator chains; one tile alone is two, and
+// the matrix pipe then waits on every other MFMA: profiles/wide_stripe/r08_tm):
+//   * only two groups' accumulators are live: the pair accumulating and the previous one, whose
+//     epilogue (bit inserts straight from VGPRs, 4 stores) runs under this pair's MFMAs;
 //   * the bias is the C operand of a tile's first MFMA (a constant VGPR block), no extra MFMA;
-//   * the next chunk's 8 ring slots are DMA'd during tile 1 and expanded into the B registers during
-//     the last tile, step by step right after the last MFMA that reads each step's old value; the
-//     fused survivor copy of a slot is stored from the ring at the same time.
-// Per 256-column chunk at 7 tiles: 224 MFMAs, ~560 VALU (v1: 238 MFMAs, ~1140 VALU).
+//   * the next chunk's 8 ring slots are DMA'd during the first tile pair and expanded into the B
+//     registers during the last group, step by step right after the last MFMA that reads each step's
+//     old value; a slot's fused survivor copy is stored from the ring in the next chunk's first
+//     group, just before that slot's next DMA.
+// With an odd tile count the last group is one tile: the next chunk's B expansion fills its stalls.
+// Per 256-column chunk at 7 tiles: 224 MFMAs and ~680 VALU (v1: 238 MFMAs, ~840 VALU).
 //
-// Accumulator sets alternate by global tile number; with an odd tile count the chunk loop is
-// unrolled by two so the set a tile writes is never the one still waiting to be packed. An odd
+// Accumulator sets alternate by global group number; with an odd group count the chunk loop is
+// unrolled by two so the set a group writes is never the one still waiting to be packed. An odd
 // chunk count ends with a phantom chunk (its loads are dummies, its stores go to the sink) whose
 // first tile packs the last real one.
 #include <hip/hip_runtime.h>
@@ -244,19 +247,6 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4tm_kernel(cptr<uint64_t> in
 #pragma unroll
     for (int n = 0; n < 2; ++n) asm volatile("" : "+a"(Bc[S][n]));
   });
-  if constexpr (COPY) {
-    static_for<kKS>([&](auto p_tag) {
-      constexpr int Pp = decltype(p_tag)::value;
-      u32x4 v;
-      uint64_t cp;
-      read_slot(v, p_tag);
-      read_ptr(cp, cptr_addr + 8u * uint32_t(slot_row(Pp)));
-      lgkm_wait();
-      tie(v);
-      tie(cp);
-      copy_store(0, Pp, cp, v);
-    });
-  }
   // tile groups: pairs (2g, 2g + 1), the last one single when MG is odd
   constexpr int NG = (MG + 1) / 2;
   using I0 = std::integral_constant<int, 0>;
@@ -326,10 +316,11 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4tm_kernel(cptr<uint64_t> in
             read_x(xn[decltype(j)::value], std::integral_constant<int, kQ * NQ + decltype(j)::value>{});
           });
         }
-        // fused copy: slot Q of the next chunk (last group); the DMA row pointer of slot Q (group 0)
+        // fused copy of this chunk's slot Q, from the ring before the next chunk's DMA refills it,
+        // and that DMA's row pointer (group 0: a pair of tiles with little VALU work)
         [[maybe_unused]] u32x4 cd;
         [[maybe_unused]] uint64_t cpp = 0, rpp = 0;
-        if constexpr (COPY && kLastG) {
+        if constexpr (COPY && G == 0) {
           read_slot(cd, q_tag);
           read_ptr(cpp, cptr_addr + 8u * uint32_t(slot_row(Q)));
         }
@@ -422,15 +413,16 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4tm_kernel(cptr<uint64_t> in
             opc[e][1] = opn[e][1];
           }
         }
-        // the next chunk's DMA of slot Q (group 0: its ring slot was consumed in the last group)
+        // group 0: this chunk's copy of slot Q, then the next chunk's DMA into it (the slot's bytes
+        // were expanded in the previous chunk's last group and copied just now)
+        if constexpr (COPY && G == 0) {
+          tie(cd);
+          tie(cpp);
+          copy_store(ci, Q, cpp, cd);
+        }
         if constexpr (G == 0) {
           if constexpr (!UNI) tie(rpp);
           dma(ci + 1, Q, rpp);
-        }
-        if constexpr (COPY && kLastG) {
-          tie(cd);
-          tie(cpp);
-          copy_store(ci + 1, Q, cpp, cd);
         }
       });
     });
@@ -497,18 +489,15 @@ hipError_t launch_tm(const Fp4ArLaunch& a, int64_t* done, hipStream_t stream) {
 
 template <int MG>
 hipError_t launch_tm_var(const Fp4ArLaunch& a, int64_t* done, hipStream_t stream) {
-  if (a.copy) {
-    // (6 tiles with fused copies need more than the 512 registers: no such build)
-    if constexpr (MG == 6) return hipErrorNotSupported;
-    else return launch_tm<MG, false, true>(a, done, stream);
-  }
+  if (a.copy) return launch_tm<MG, false, true>(a, done, stream);
   return a.in_stride ? launch_tm<MG, true, false>(a, done, stream) : launch_tm<MG, false, false>(a, done, stream);
 }
 
 }  // namespace
 
 bool fp4tm_supported(int k, int mg, bool copies) {
-  return k > 112 && k <= 128 && mg >= 5 && mg <= 7 && !(copies && mg == 6);
+  (void)copies;
+  return k > 112 && k <= 128 && mg >= 5 && mg <= 7;
 }
 
 hipError_t launch_gf_gemm_fp4tm(const Fp4ArLaunch& a, int64_t* done, hipStream_t stream) {
