@@ -16,8 +16,9 @@
 //   * the bias is the C operand of a tile's first MFMA (a constant VGPR block), no extra MFMA;
 //   * the next chunk's 8 ring slots are DMA'd during the first tile pair and expanded into the B
 //     registers during the last group, step by step right after the last MFMA that reads each step's
-//     old value; a slot's fused survivor copy is stored from the ring in the next chunk's first
-//     group, just before that slot's next DMA.
+//     old value; the fused survivor copies are stored in the same group, block-wide: each store
+//     instruction writes 4 rows x 256 B out of the four waves' rings (two barriers per chunk), which
+//     the memory system takes at 1.7x the rate of one wave's 16 rows x 64 B.
 // With an odd tile count the last group is one tile: the next chunk's B expansion fills its stalls.
 // Per 256-column chunk at 7 tiles: 224 MFMAs and ~680 VALU (v1: 238 MFMAs, ~840 VALU).
 //
@@ -116,7 +117,12 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4tm_kernel(cptr<uint64_t> in
   lds_u8* ring = (lds_u8*)(smem + kA + kPtrBytes) + size_t(wave) * kKS * kSlotBytes;
   const uint32_t ring_base = uint32_t(reinterpret_cast<uintptr_t>(ring));
   const uint32_t ring_x = ring_base + uint32_t(4 * h * kCW + 2 * c);  // rows 4h.., column pair (2c, 2c+1)
-  const uint32_t ring_lane = ring_base + 16u * lane;                   // this lane's DMA'd 16 B
+  // block-wide fused copy: this lane stores row 4 * wave + lane / 16 of a slot, the block's columns
+  // 16 * (lane % 16) .. + 15, which wave (lane % 16) / 4 DMA'd into its ring (4 rows x 256 B per
+  // store instruction: 1.7x the copy bandwidth of 16 rows x 64 B, scripts/fp4_pattern_probe.hip)
+  const int wrow = 4 * wave + (lane >> 4), wcol = 16 * (lane & 15);
+  const uint32_t wring = uint32_t(reinterpret_cast<uintptr_t>((lds_u8*)(smem + kA + kPtrBytes))) +
+                         uint32_t(((lane & 15) >> 2) * kKS * kSlotBytes + wrow * kCW + 16 * (lane & 3));
   const uint32_t a_lo = lds0 + 16u * lane, a_hi = a_lo + 65536u;
   const uint32_t optr_addr = lds0 + uint32_t(kA) + 2048u + 16u * h;  // outptr[4t + 2h + u]: + 32t + 8u
   const unsigned sslot = (sink_spread & 1) ? (blockIdx.x * 4u + unsigned(wave)) % unsigned(kFp4SinkSlots) : 0u;
@@ -138,11 +144,12 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4tm_kernel(cptr<uint64_t> in
     const uint64_t base = UNI ? in0 + uint64_t(int64_t(slot_row(p)) * in_stride) : rowp;
     __builtin_amdgcn_global_load_lds((gptr<const void>)(base + uint64_t(col)), ring + p * kSlotBytes, 16, 0, 0);
   };
-  // fused copy of ring slot p (chunk cn's bytes) from this lane's 16 B; cp: the row's copy pointer
+  // fused copy of ring slot p (chunk cn's bytes), block-wide (wrow, wcol); cp: the row's copy pointer
   auto copy_store = [&](int cn, int p, uint64_t cp, u32x4 v) __attribute__((always_inline)) {
-    const bool live = cn < my_chunks && kRS * p + drow < k && cp && !(sink_spread & 2);
-    __builtin_nontemporal_store(v, (gptr<u32x4>)(live ? cp + uint64_t(cbase(cn) + dcol) : sink));
+    const bool live = cn < my_chunks && kRS * p + wrow < k && cp && !(sink_spread & 2);
+    __builtin_nontemporal_store(v, (gptr<u32x4>)(live ? cp + uint64_t(cbase(cn) + wcol) : sink));
   };
+  auto copy_row = [&](int p) __attribute__((always_inline)) { return kRS * p + wrow < k ? kRS * p + wrow : k - 1; };
   auto read_ptr = [&](uint64_t& v, uint32_t addr) __attribute__((always_inline)) {
     uint64_t r;
     asm volatile("ds_read_b64 %0, %1" : "=&v"(r) : "v"(addr) : "memory");
@@ -177,7 +184,7 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4tm_kernel(cptr<uint64_t> in
   };
   auto read_slot = [&](u32x4& v, auto p_tag) __attribute__((always_inline)) {
     constexpr int off = decltype(p_tag)::value * kSlotBytes;
-    const uint32_t addr = ring_lane;
+    const uint32_t addr = wring;
     u32x4 r;
     asm volatile("ds_read_b128 %0, %1 offset:%2" : "=&v"(r) : "v"(addr), "n"(off) : "memory");
     v = r;
@@ -236,6 +243,21 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4tm_kernel(cptr<uint64_t> in
 #pragma unroll
   for (int p = 0; p < kKS; ++p) dma(0, p, UNI ? 0 : rowptr[slot_row(p)]);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if constexpr (COPY) {  // chunk 0's copies, block-wide: every wave's ring has landed
+    __builtin_amdgcn_s_barrier();
+    static_for<kKS>([&](auto p_tag) {
+      constexpr int Pp = decltype(p_tag)::value;
+      u32x4 v;
+      uint64_t cp;
+      read_slot(v, p_tag);
+      read_ptr(cp, cptr_addr + 8u * uint32_t(copy_row(Pp)));
+      lgkm_wait();
+      tie(v);
+      tie(cp);
+      copy_store(0, Pp, cp, v);
+    });
+    __builtin_amdgcn_s_barrier();  // (no wave refills its ring before every copy has read it)
+  }
   static_for<kNS>([&](auto s_tag) {
     constexpr int S = decltype(s_tag)::value;
     uint32_t x[4];
@@ -316,13 +338,14 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4tm_kernel(cptr<uint64_t> in
             read_x(xn[decltype(j)::value], std::integral_constant<int, kQ * NQ + decltype(j)::value>{});
           });
         }
-        // fused copy of this chunk's slot Q, from the ring before the next chunk's DMA refills it,
-        // and that DMA's row pointer (group 0: a pair of tiles with little VALU work)
+        // fused copy of the next chunk's slot Q (last group, block-wide: the first super-step waits
+        // at a barrier until every wave's DMAs have landed), and group 0's DMA row pointer
         [[maybe_unused]] u32x4 cd;
         [[maybe_unused]] uint64_t cpp = 0, rpp = 0;
-        if constexpr (COPY && G == 0) {
+        if constexpr (COPY && kLastG) {
+          if constexpr (Q == 0) __builtin_amdgcn_s_barrier();
           read_slot(cd, q_tag);
-          read_ptr(cpp, cptr_addr + 8u * uint32_t(slot_row(Q)));
+          read_ptr(cpp, cptr_addr + 8u * uint32_t(copy_row(Q)));
         }
         if constexpr (!UNI && G == 0) read_ptr(rpp, rowptr_addr + 8u * uint32_t(slot_row(Q)));
         uint64_t opn[2][2];
@@ -413,13 +436,15 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4tm_kernel(cptr<uint64_t> in
             opc[e][1] = opn[e][1];
           }
         }
-        // group 0: this chunk's copy of slot Q, then the next chunk's DMA into it (the slot's bytes
-        // were expanded in the previous chunk's last group and copied just now)
-        if constexpr (COPY && G == 0) {
+        if constexpr (COPY && kLastG) {
           tie(cd);
           tie(cpp);
-          copy_store(ci, Q, cpp, cd);
+          copy_store(ci + 1, Q, cpp, cd);
+          // every wave has read its copies out of the rings before any refills them (group 0)
+          if constexpr (Q + 1 == kSS) __builtin_amdgcn_s_barrier();
         }
+        // group 0: the next chunk's DMA of slot Q (its bytes were expanded and copied in the
+        // previous chunk's last group)
         if constexpr (G == 0) {
           if constexpr (!UNI) tie(rpp);
           dma(ci + 1, Q, rpp);
