@@ -125,7 +125,7 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4tm_kernel(cptr<uint64_t> in
                          uint32_t(((lane & 15) >> 2) * kKS * kSlotBytes + wrow * kCW + 16 * (lane & 3));
   const uint32_t a_lo = lds0 + 16u * lane, a_hi = a_lo + 65536u;
   const uint32_t optr_addr = lds0 + uint32_t(kA) + 2048u + 16u * h;  // outptr[4t + 2h + u]: + 32t + 8u
-  const unsigned sslot = (sink_spread & 1) ? (blockIdx.x * 4u + unsigned(wave)) % unsigned(kFp4SinkSlots) : 0u;
+  const unsigned sslot = sink_spread ? (blockIdx.x * 4u + unsigned(wave)) % unsigned(kFp4SinkSlots) : 0u;
   const uint64_t sink = uint64_t(bitmat + size_t(MG) * kNS * 64) + uint64_t(sslot) * 1024u + 16 * lane;
   const int scale = 0x7F7F7F7F;  // E8M0 1.0 for every block of 32
   const uint64_t in0 = UNI ? in[0] : 0;
@@ -146,7 +146,7 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4tm_kernel(cptr<uint64_t> in
   };
   // fused copy of ring slot p (chunk cn's bytes), block-wide (wrow, wcol); cp: the row's copy pointer
   auto copy_store = [&](int cn, int p, uint64_t cp, u32x4 v) __attribute__((always_inline)) {
-    const bool live = cn < my_chunks && kRS * p + wrow < k && cp && !(sink_spread & 2);
+    const bool live = cn < my_chunks && kRS * p + wrow < k && cp;
     __builtin_nontemporal_store(v, (gptr<u32x4>)(live ? cp + uint64_t(cbase(cn) + wcol) : sink));
   };
   auto copy_row = [&](int p) __attribute__((always_inline)) { return kRS * p + wrow < k ? kRS * p + wrow : k - 1; };
@@ -498,12 +498,11 @@ hipError_t launch_tm(const Fp4ArLaunch& a, int64_t* done, hipStream_t stream) {
   const int64_t nchunks = a.ncols / kBlockCols;
   *done = nchunks * kBlockCols;
   if (nchunks == 0) return hipSuccess;
-  // flags: bit 0 = spread the sink (GFRS_FP4_SINK=1 clears it: one shared slot); bit 1 = every
-  // fused copy stored to the sink instead (GFRS_FP4_TM_ABL=1: an ablation, copies are wrong). A/B only.
+  // GFRS_FP4_SINK=1: one shared sink slot (A/B only). (The copy-to-sink ablation of
+  // profiles/wide_stripe/r08_tm was a temporary flag here; it made the copies wrong and is gone.)
   static const int sink_spread = [] {
     const char* env = std::getenv("GFRS_FP4_SINK");
-    const char* abl = std::getenv("GFRS_FP4_TM_ABL");
-    return ((env && std::atoi(env) == 1) ? 0 : 1) | ((abl && std::atoi(abl) == 1) ? 2 : 0);
+    return (env && std::atoi(env) == 1) ? 0 : 1;
   }();
   const int64_t slots = persistent_slots(occ, 1, nchunks);
   gf_gemm_fp4tm_kernel<MG, UNI, COPY><<<unsigned(slots), 256, lds, stream>>>(
