@@ -25,7 +25,7 @@
 // Accumulator sets alternate by global group number; with an odd group count the chunk loop is
 // unrolled by two so the set a group writes is never the one still waiting to be packed. An odd
 // chunk count ends with a phantom chunk (its loads are dummies, its stores go to the sink) whose
-// first tile packs the last real one.
+// first group packs the last real chunk's last group.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
