@@ -30,3 +30,14 @@ def test_sweep_table_renders_committed_points():
 def test_tools_parse_arguments_on_a_host(script):
     r = _run(script, "--help")
     assert r.returncode == 0 and "usage" in r.stdout.lower(), r.stderr[-2000:]
+
+
+@pytest.mark.skipif(not os.path.exists("/opt/rocm/bin/hipcc"), reason="hipcc not available")
+@pytest.mark.parametrize("src", ["scripts/membench.hip", "scripts/fp4_pattern_probe.hip"])
+def test_hip_probes_compile_for_gfx950(src, tmp_path):
+    """The standalone HIP probes behind profiles/ (memory ceilings, the wide decode's access pattern)
+    still build for gfx950 (cross-compiled on the host; they run only on the GPU box)."""
+    r = subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-o",
+                        str(tmp_path / "probe"), os.path.join(ROOT, src)], capture_output=True, text=True,
+                       timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
