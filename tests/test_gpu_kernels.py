@@ -381,6 +381,38 @@ def test_fp4_tile_major_kernel_matches_oracle(k, m, variant, nblk, monkeypatch):
         assert (c[ncopy:] == 0x44).all()
 
 
+@pytest.mark.parametrize("m,copy", [(26, True), (26, False), (20, False)])
+def test_fp4_tile_major_column_windows(m, copy):
+    """Windowed launches on the tile-major kernel (its default shapes): three column windows with
+    ragged starts and lengths, as the windowed codecs issue them, fill exactly their columns.
+    Outputs and copies are bit-exact inside each window and untouched outside."""
+    _native_loaded()
+    k, ncols = 128, 256 * 700 + 90
+    rng = np.random.default_rng(m * 17 + copy)
+    coeff = rng.integers(0, 256, size=(m, k), dtype=np.uint8)
+    host, dev = _rand_rows(k, ncols, 3 * m + copy)
+    inputs = [dev[j].clone() for j in range(k)]
+    out = alloc_rows(m, ncols, "cuda", fill=0x5A)
+    cdst = alloc_rows(k, ncols, "cuda", fill=0x44) if copy else None
+    copies = [cdst[j] if j < k - m else None for j in range(k)] if copy else None
+    plan = GemmPlan(inputs, out, coeff, copies=copies, engine="mfma")
+    windows = [(0, 256 * 100), (256 * 100 + 2, 256 * 333 + 46), (256 * 500, ncols - 256 * 500)]
+    for c0, n in windows:
+        plan.run(col0=c0, ncols=n)
+    torch.cuda.synchronize()
+    want = GF256.gemm(coeff, host)
+    got = out.cpu().numpy()
+    mask = np.zeros(ncols, dtype=bool)
+    for c0, n in windows:
+        mask[c0:c0 + n] = True
+    assert np.array_equal(got[:, mask], want[:, mask])
+    assert (got[:, ~mask] == 0x5A).all()
+    if copy:
+        c = cdst.cpu().numpy()
+        assert np.array_equal(c[: k - m][:, mask], host[: k - m][:, mask])
+        assert (c[: k - m][:, ~mask] == 0x44).all() and (c[k - m:] == 0x44).all()
+
+
 @pytest.mark.parametrize("k,n,matrix", [(10, 14, "vandermonde"), (128, 160, "cauchy"), (4, 6, "vandermonde"),
                                         (200, 255, "sys_vandermonde")])
 def test_decode_system_matches_host_decode_matrix(k, n, matrix):
