@@ -16,8 +16,11 @@
 //     reference can read is still written the reference's way.
 #pragma once
 
+#include <algorithm>
+#include <atomic>
 #include <cstdint>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "gfrs/gf65536.h"
@@ -45,6 +48,27 @@ uint32_t crc32(const uint8_t* data, int64_t len, uint32_t crc = 0);
 // 32 x 32 GF(2) operator raised to 8 len(B) by repeated squaring). Column shards of a chunk, each
 // CRC'd by its own rank, combine into the chunk's METADATA CRC this way (multi-GPU file codec).
 uint32_t crc32_combine(uint32_t crc_a, uint32_t crc_b, int64_t len_b);
+
+// fn(i) for every i in [0, n) on up to max_threads threads, each taking the next index in turn
+// (the decode's survivor check: k chunk files read and CRC-checked at once). fn must not throw.
+template <typename F>
+void parallel_indices(int n, int max_threads, F&& fn) {
+  const int nt = std::max(1, std::min(n, max_threads));
+  if (nt <= 1) {
+    for (int i = 0; i < n; ++i) fn(i);
+    return;
+  }
+  std::atomic<int> next{0};
+  std::vector<std::thread> th;
+  th.reserve(size_t(nt));
+  for (int t = 0; t < nt; ++t)
+    th.emplace_back([&] {
+      for (int i = next.fetch_add(1); i < n; i = next.fetch_add(1)) fn(i);
+    });
+  for (auto& x : th) x.join();
+}
+// threads for the survivor check (GFRS_VERIFY_THREADS, default 16; 1 = serial)
+int verify_threads();
 
 std::string chunk_path(const std::string& file, int index);
 std::string metadata_path(const std::string& file);

@@ -240,9 +240,38 @@ FileReport decode_file(const std::string& file, const std::string& conf, const s
     }
     return true;
   };
-  // fill k slots in conf order, then search for a recoverable subset among the verified chunks
+  // fill k slots in conf order, then search for a recoverable subset among the verified chunks.
+  // The first k candidates (all a clean decode needs) are read into slots 0..k-1 and checked at
+  // once; a failed one leaves a gap that the verified rows after it close by moving down.
+  const int first = std::min(int(cand_idx.size()), k);
+  std::vector<signed char> pre(size_t(first), 0);
+  std::vector<int> rej(size_t(first), 0);
+  {
+    const int r0 = r.rejected;
+    parallel_indices(first, verify_threads(), [&](int ci) {
+      try {
+        if (file_size(cand_path[size_t(ci)]) < C && md.total_size > 0) return;
+        read_into(cand_path[size_t(ci)], 0, surv.p + size_t(ci) * P, C);
+      } catch (const std::exception&) {
+        return;  // missing chunk
+      }
+      if (!md.crc.empty() && crc32(surv.p + size_t(ci) * P, C) != md.crc[size_t(cand_idx[size_t(ci)])]) {
+        rej[size_t(ci)] = 1;
+        return;
+      }
+      pre[size_t(ci)] = 1;
+    });
+    r.rejected = r0;
+    for (int ci = 0; ci < first; ++ci) r.rejected += rej[size_t(ci)];
+  }
   std::vector<int> verified;
-  for (int ci = 0; ci < int(cand_idx.size()); ++ci) {
+  for (int ci = 0; ci < first; ++ci) {
+    if (!pre[size_t(ci)]) continue;
+    const size_t slot = verified.size();
+    if (slot != size_t(ci)) std::memcpy(surv.p + slot * P, surv.p + size_t(ci) * P, size_t(C));
+    verified.push_back(ci);
+  }
+  for (int ci = first; ci < int(cand_idx.size()); ++ci) {
     if (int(verified.size()) < k) {
       if (row_ok(ci, surv.p + size_t(verified.size()) * P)) verified.push_back(ci);
     } else {

@@ -4,6 +4,10 @@
 
 #include <sys/stat.h>
 
+#if defined(__x86_64__)
+#include <immintrin.h>
+#endif
+
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -50,8 +54,10 @@ int chunk_index(const std::string& name) {
   return int(v);
 }
 
-uint32_t crc32(const uint8_t* data, int64_t len, uint32_t crc) {
-  // slicing-by-8 CRC-32 (IEEE 802.3, reflected 0xEDB88320)
+namespace {
+
+// slicing-by-8 CRC-32 (IEEE 802.3, reflected 0xEDB88320) on the inverted register value
+uint32_t crc32_slice8(const uint8_t* data, int64_t len, uint32_t state) {
   static uint32_t t[8][256];
   static bool init = [] {
     for (uint32_t i = 0; i < 256; ++i) {
@@ -64,7 +70,7 @@ uint32_t crc32(const uint8_t* data, int64_t len, uint32_t crc) {
     return true;
   }();
   (void)init;
-  crc = ~crc;
+  uint32_t crc = state;
   int64_t i = 0;
   for (; i + 8 <= len; i += 8) {
     uint32_t lo, hi;
@@ -75,7 +81,99 @@ uint32_t crc32(const uint8_t* data, int64_t len, uint32_t crc) {
           t[2][(hi >> 8) & 0xFF] ^ t[1][(hi >> 16) & 0xFF] ^ t[0][hi >> 24];
   }
   for (; i < len; ++i) crc = (crc >> 8) ^ t[0][(crc ^ data[i]) & 0xFF];
-  return ~crc;
+  return crc;
+}
+
+#if defined(__x86_64__)
+// Carry-less-multiply folding (the method of Intel's "Fast CRC Computation for Generic Polynomials
+// Using PCLMULQDQ"): four 128-bit lanes folded 64 bytes at a time, then into one lane, then 128 ->
+// 64 -> 32 bits with a Barrett reduction. The constants are x^k mod P for the bit-reflected
+// CRC-32 polynomial (k1/k2: the 512-bit fold, k3/k4: 128-bit, k5: 64-bit; P' and mu for Barrett).
+// len >= 64 and a multiple of 16; works on the inverted register value like crc32_slice8. The
+// survivor check of a decode reads and checks up to k whole chunks before any GPU work, so it is
+// on the critical path of every file decode.
+#define GFRS_CLMUL __attribute__((target("pclmul,sse4.1")))
+GFRS_CLMUL inline __m128i ld128(const uint8_t* p) { return _mm_loadu_si128(reinterpret_cast<const __m128i*>(p)); }
+// acc folded across 128 bits by the constant pair k (low x low, high x high) into next
+GFRS_CLMUL inline __m128i fold128(__m128i acc, __m128i next, __m128i k) {
+  const __m128i lo = _mm_clmulepi64_si128(acc, k, 0x00);
+  return _mm_xor_si128(_mm_xor_si128(_mm_clmulepi64_si128(acc, k, 0x11), next), lo);
+}
+GFRS_CLMUL uint32_t crc32_clmul(const uint8_t* buf, int64_t len, uint32_t state) {
+  alignas(16) static const uint64_t k1k2[2] = {0x0154442bd4ull, 0x01c6e41596ull};
+  alignas(16) static const uint64_t k3k4[2] = {0x01751997d0ull, 0x00ccaa009eull};
+  alignas(16) static const uint64_t k5k0[2] = {0x0163cd6124ull, 0x0000000000ull};
+  alignas(16) static const uint64_t poly[2] = {0x01db710641ull, 0x01f7011641ull};
+  __m128i x1 = ld128(buf), x2 = ld128(buf + 16), x3 = ld128(buf + 32), x4 = ld128(buf + 48);
+  x1 = _mm_xor_si128(x1, _mm_cvtsi32_si128(int(state)));
+  __m128i x0 = _mm_load_si128(reinterpret_cast<const __m128i*>(k1k2));
+  buf += 64;
+  len -= 64;
+  while (len >= 64) {
+    x1 = fold128(x1, ld128(buf), x0);
+    x2 = fold128(x2, ld128(buf + 16), x0);
+    x3 = fold128(x3, ld128(buf + 32), x0);
+    x4 = fold128(x4, ld128(buf + 48), x0);
+    buf += 64;
+    len -= 64;
+  }
+  x0 = _mm_load_si128(reinterpret_cast<const __m128i*>(k3k4));
+  x1 = fold128(x1, x2, x0);
+  x1 = fold128(x1, x3, x0);
+  x1 = fold128(x1, x4, x0);
+  while (len >= 16) {
+    x1 = fold128(x1, ld128(buf), x0);
+    buf += 16;
+    len -= 16;
+  }
+  // 128 -> 64 bits
+  __m128i x2b = _mm_clmulepi64_si128(x1, x0, 0x10);
+  const __m128i mask = _mm_setr_epi32(~0, 0, ~0, 0);
+  x1 = _mm_xor_si128(_mm_srli_si128(x1, 8), x2b);
+  x0 = _mm_loadl_epi64(reinterpret_cast<const __m128i*>(k5k0));
+  x2b = _mm_srli_si128(x1, 4);
+  x1 = _mm_xor_si128(_mm_clmulepi64_si128(_mm_and_si128(x1, mask), x0, 0x00), x2b);
+  // Barrett reduction to 32 bits
+  x0 = _mm_load_si128(reinterpret_cast<const __m128i*>(poly));
+  x2b = _mm_clmulepi64_si128(_mm_and_si128(x1, mask), x0, 0x10);
+  x2b = _mm_clmulepi64_si128(_mm_and_si128(x2b, mask), x0, 0x00);
+  x1 = _mm_xor_si128(x1, x2b);
+  return uint32_t(_mm_extract_epi32(x1, 1));
+}
+
+bool have_clmul() {
+  static const bool v = [] {
+    if (const char* e = std::getenv("GFRS_CRC_SCALAR"))  // (tests: the table path on the same machine)
+      if (std::atoi(e) == 1) return false;
+    __builtin_cpu_init();
+    return __builtin_cpu_supports("pclmul") && __builtin_cpu_supports("sse4.1");
+  }();
+  return v;
+}
+#endif
+
+}  // namespace
+
+int verify_threads() {
+  static const int v = [] {
+    const char* e = std::getenv("GFRS_VERIFY_THREADS");
+    const int n = e ? std::atoi(e) : 16;
+    return n < 1 ? 1 : n;
+  }();
+  return v;
+}
+
+uint32_t crc32(const uint8_t* data, int64_t len, uint32_t crc) {
+  uint32_t state = ~crc;
+#if defined(__x86_64__)
+  if (len >= 64 && have_clmul()) {
+    const int64_t n = len & ~int64_t(15);
+    state = crc32_clmul(data, n, state);
+    data += n;
+    len -= n;
+  }
+#endif
+  return ~crc32_slice8(data, len, state);
 }
 
 namespace {

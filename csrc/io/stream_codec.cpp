@@ -363,27 +363,48 @@ int64_t stripe_chunk(const Metadata& md) {
 // positions into the candidate list.
 std::vector<int> pick_survivors(const Metadata& md, const Candidates& cand, int64_t C, int* rejected) {
   const int k = md.k;
-  std::vector<uint8_t> scratch(size_t(std::min<int64_t>(std::max<int64_t>(C, 1), int64_t(16) << 20)));
-  auto verified_ok = [&](int ci) -> bool {
-    const std::string& path = cand.path[size_t(ci)];
-    if (!file_at_least(path, md.total_size > 0 ? C : 0)) return false;
-    if (md.crc.empty()) return true;
-    Fd f(::open(path.c_str(), O_RDONLY | O_CLOEXEC));
-    if (f.fd < 0) return false;
-    uint32_t c = 0;
-    for (int64_t off = 0; off < C; off += int64_t(scratch.size())) {
-      const int64_t len = std::min<int64_t>(int64_t(scratch.size()), C - off);
-      pread_full(f.fd, scratch.data(), len, off);
-      c = crc32(scratch.data(), len, c);
-    }
-    if (c != md.crc[size_t(cand.idx[size_t(ci)])]) {
-      if (rejected) ++*rejected;
+  const size_t scratch_bytes = size_t(std::min<int64_t>(std::max<int64_t>(C, 1), int64_t(16) << 20));
+  // 1 = intact, 0 = missing, short or failing its CRC (*rej counts the CRC failures)
+  auto check = [&](int ci, std::vector<uint8_t>& scratch, int* rej) -> bool {
+    try {
+      const std::string& path = cand.path[size_t(ci)];
+      if (!file_at_least(path, md.total_size > 0 ? C : 0)) return false;
+      if (md.crc.empty()) return true;
+      Fd f(::open(path.c_str(), O_RDONLY | O_CLOEXEC));
+      if (f.fd < 0) return false;
+      scratch.resize(scratch_bytes);
+      uint32_t c = 0;
+      for (int64_t off = 0; off < C; off += int64_t(scratch.size())) {
+        const int64_t len = std::min<int64_t>(int64_t(scratch.size()), C - off);
+        pread_full(f.fd, scratch.data(), len, off);
+        c = crc32(scratch.data(), len, c);
+      }
+      if (c != md.crc[size_t(cand.idx[size_t(ci)])]) {
+        ++*rej;
+        return false;
+      }
+      return true;
+    } catch (const std::exception&) {
       return false;
     }
-    return true;
+  };
+  // the first k candidates (all a clean decode needs) are read and checked at once
+  const int ncand = int(cand.idx.size());
+  const int first = std::min(ncand, k);
+  std::vector<signed char> pre(size_t(ncand), -1);
+  std::vector<int> rej(size_t(ncand), 0);
+  parallel_indices(first, verify_threads(), [&](int ci) {
+    std::vector<uint8_t> scratch;
+    pre[size_t(ci)] = check(ci, scratch, &rej[size_t(ci)]) ? 1 : 0;
+  });
+  std::vector<uint8_t> scratch;
+  auto verified_ok = [&](int ci) -> bool {
+    const bool ok = pre[size_t(ci)] >= 0 ? pre[size_t(ci)] == 1 : check(ci, scratch, &rej[size_t(ci)]);
+    if (rejected) *rejected += rej[size_t(ci)];
+    return ok;
   };
   std::vector<int> verified;
-  for (int ci = 0; ci < int(cand.idx.size()); ++ci) {
+  for (int ci = 0; ci < ncand; ++ci) {
     if (!verified_ok(ci)) continue;
     verified.push_back(ci);
     if (int(verified.size()) < k) continue;

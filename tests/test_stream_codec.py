@@ -6,12 +6,15 @@ a run stopped after N windows (simulated crash) must resume from its checkpoint.
 """
 import os
 import subprocess
+import sys
 
 import pytest
 
 from gpu_rscode_amd._build import binary
 from gpu_rscode_amd._native import cpu
 from gpu_rscode_amd.utils import fileformat as ff
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _files(d, name, n):
@@ -147,6 +150,43 @@ def test_crc32_combine_matches_zlib():
         a, b = rng(la), rng(lb)
         assert cpu().crc32(a) == zlib.crc32(a)
         assert cpu().crc32_combine(cpu().crc32(a), cpu().crc32(b), lb) == zlib.crc32(a + b)
+
+
+def test_crc32_fast_path_matches_zlib_and_the_table_path():
+    """The carry-less-multiply CRC-32 (64-byte folds, then 16-byte folds, then the table for the
+    tail) equals zlib for every length around its block sizes, unaligned starts and chained seeds;
+    the slicing-by-8 table path (GFRS_CRC_SCALAR=1, a fresh process) gives the same values."""
+    import zlib
+
+    buf = os.urandom(1 << 18)
+    cases = [(n, off, seed) for n in list(range(0, 200)) + [1023, 1024, 1025, 4096 + 15, 65_599, 200_000]
+             for off, seed in ((0, 0), (3, 0x12345678), (13, 0xFFFFFFFF))]
+    want = [zlib.crc32(buf[off:off + n], seed) for n, off, seed in cases]
+    assert [cpu().crc32(buf[off:off + n], seed) for n, off, seed in cases] == want
+    code = ("import sys, zlib, os; sys.path.insert(0, sys.argv[1]); from gpu_rscode_amd._native import cpu; "
+            "b = os.urandom(70_001); assert cpu().crc32(b, 7) == zlib.crc32(b, 7); print('ok')")
+    r = subprocess.run([sys.executable, "-c", code, ROOT], env=dict(os.environ, GFRS_CRC_SCALAR="1"),
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]
+
+
+def test_stream_decode_skips_corrupt_and_missing_survivors(tmp_path):
+    """The windowed decoder's survivor check (the first k candidates read and CRC-checked at once):
+    a corrupted chunk and a missing chunk among the first k are skipped, the next listed chunks take
+    their place, and the file comes back byte-exact."""
+    f = tmp_path / "f.bin"
+    payload = os.urandom(500_001)
+    f.write_bytes(payload)
+    cpu().encode_file(str(f), 6, 3)
+    bad = bytearray((tmp_path / "_2_f.bin").read_bytes())
+    bad[7] ^= 0x40
+    (tmp_path / "_2_f.bin").write_bytes(bytes(bad))
+    os.remove(tmp_path / "_4_f.bin")
+    ff.write_conf(str(tmp_path / "conf"), [ff.chunk_path(str(f), i) for i in range(9)])
+    rows, rejected = cpu().choose_survivors(str(f), str(tmp_path / "conf"))
+    assert rejected == 1 and rows == [0, 1, 3, 5, 6, 7]
+    r = cpu().decode_file_stream(str(f), str(tmp_path / "conf"), str(tmp_path / "o"), window=70_000, durable=False)
+    assert r["rejected"] == 1 and (tmp_path / "o").read_bytes() == payload
 
 
 @pytest.mark.parametrize("size,k,p,w,cuts", [(3_000_017, 10, 4, 8, (0, 100_000, 222_224, None)),
