@@ -56,6 +56,20 @@ struct StreamReport : FileReport {
 // candidate through its CRC in bounded windows. `rejected` counts CRC mismatches.
 std::vector<int> choose_survivors(const std::string& file, const std::string& conf, int* rejected = nullptr);
 
+// A survivor check split over ranks (the multi-GPU decode): each rank reads only its column range
+// [lo, hi) of every conf candidate (on parallel threads) and reports whether the chunk file is there
+// in full and the CRC-32 of those bytes; the coordinator combines the ranks' CRCs in column order
+// (crc32_combine), compares them with the METADATA, and picks the survivors from the verdicts.
+struct ShardCrc {
+  int index = -1;        // chunk index of the candidate (conf order)
+  bool present = false;  // the file exists and holds the whole chunk
+  uint32_t crc = 0;      // CRC-32 of its bytes [lo, hi)
+};
+std::vector<ShardCrc> shard_crcs(const std::string& file, const std::string& conf, int64_t lo, int64_t hi);
+// choose_survivors with every candidate's verdict known (intact[ci] != 0: usable), conf order
+std::vector<int> choose_survivors_given(const std::string& file, const std::string& conf,
+                                        const std::vector<int>& intact);
+
 StreamReport encode_file_stream(const std::string& file, int k, int p, MatrixKind kind, const GemmFn& gemm,
                                 const HostAlloc& alloc, const StreamOptions& opt, bool cpu_meta = false);
 

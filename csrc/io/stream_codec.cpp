@@ -361,7 +361,8 @@ int64_t stripe_chunk(const Metadata& md) {
 
 // First recoverable k-subset (conf order) of the candidates that exist and pass their CRC; returns
 // positions into the candidate list.
-std::vector<int> pick_survivors(const Metadata& md, const Candidates& cand, int64_t C, int* rejected) {
+std::vector<int> pick_survivors(const Metadata& md, const Candidates& cand, int64_t C, int* rejected,
+                                const std::vector<int>* given = nullptr) {
   const int k = md.k;
   const size_t scratch_bytes = size_t(std::min<int64_t>(std::max<int64_t>(C, 1), int64_t(16) << 20));
   // 1 = intact, 0 = missing, short or failing its CRC (*rej counts the CRC failures)
@@ -393,10 +394,14 @@ std::vector<int> pick_survivors(const Metadata& md, const Candidates& cand, int6
   const int first = std::min(ncand, k);
   std::vector<signed char> pre(size_t(ncand), -1);
   std::vector<int> rej(size_t(ncand), 0);
-  parallel_indices(first, verify_threads(), [&](int ci) {
-    std::vector<uint8_t> scratch;
-    pre[size_t(ci)] = check(ci, scratch, &rej[size_t(ci)]) ? 1 : 0;
-  });
+  if (given) {  // verdicts known already (a distributed check: combined shard CRCs)
+    for (int ci = 0; ci < ncand; ++ci) pre[size_t(ci)] = ci < int(given->size()) && (*given)[size_t(ci)] ? 1 : 0;
+  } else {
+    parallel_indices(first, verify_threads(), [&](int ci) {
+      std::vector<uint8_t> scratch;
+      pre[size_t(ci)] = check(ci, scratch, &rej[size_t(ci)]) ? 1 : 0;
+    });
+  }
   std::vector<uint8_t> scratch;
   auto verified_ok = [&](int ci) -> bool {
     const bool ok = pre[size_t(ci)] >= 0 ? pre[size_t(ci)] == 1 : check(ci, scratch, &rej[size_t(ci)]);
@@ -439,6 +444,47 @@ std::vector<int> choose_survivors(const std::string& file, const std::string& co
   const Metadata md = read_metadata(metadata_path(file));
   const Candidates cand = conf_candidates(file, conf, md);
   const std::vector<int> pos = pick_survivors(md, cand, stripe_chunk(md), rejected);
+  std::vector<int> rows;
+  for (int ci : pos) rows.push_back(cand.idx[size_t(ci)]);
+  return rows;
+}
+
+std::vector<ShardCrc> shard_crcs(const std::string& file, const std::string& conf, int64_t lo, int64_t hi) {
+  const Metadata md = read_metadata(metadata_path(file));
+  const Candidates cand = conf_candidates(file, conf, md);
+  const int64_t C = stripe_chunk(md);
+  lo = std::max<int64_t>(0, std::min(lo, C));
+  hi = std::max<int64_t>(lo, std::min(hi, C));
+  std::vector<ShardCrc> out(cand.idx.size());
+  parallel_indices(int(cand.idx.size()), verify_threads(), [&](int ci) {
+    ShardCrc& r = out[size_t(ci)];
+    r.index = cand.idx[size_t(ci)];
+    try {
+      const std::string& path = cand.path[size_t(ci)];
+      if (!file_at_least(path, md.total_size > 0 ? C : 0)) return;
+      Fd f(::open(path.c_str(), O_RDONLY | O_CLOEXEC));
+      if (f.fd < 0) return;
+      std::vector<uint8_t> scratch(size_t(std::min<int64_t>(std::max<int64_t>(hi - lo, 1), int64_t(16) << 20)));
+      uint32_t c = 0;
+      for (int64_t off = lo; off < hi; off += int64_t(scratch.size())) {
+        const int64_t len = std::min<int64_t>(int64_t(scratch.size()), hi - off);
+        pread_full(f.fd, scratch.data(), len, off);
+        c = crc32(scratch.data(), len, c);
+      }
+      r.crc = c;
+      r.present = true;
+    } catch (const std::exception&) {
+      r.present = false;
+    }
+  });
+  return out;
+}
+
+std::vector<int> choose_survivors_given(const std::string& file, const std::string& conf,
+                                        const std::vector<int>& intact) {
+  const Metadata md = read_metadata(metadata_path(file));
+  const Candidates cand = conf_candidates(file, conf, md);
+  const std::vector<int> pos = pick_survivors(md, cand, stripe_chunk(md), nullptr, &intact);
   std::vector<int> rows;
   for (int ci : pos) rows.push_back(cand.idx[size_t(ci)]);
   return rows;

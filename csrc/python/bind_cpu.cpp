@@ -173,6 +173,29 @@ PYBIND11_MODULE(_cpu, m) {
     return crc32(reinterpret_cast<const uint8_t*>(s.data()), int64_t(s.size()), crc);
   }, py::arg("data"), py::arg("crc") = 0);
   m.def("crc32_combine", &crc32_combine);
+  m.def(
+      "shard_crcs",
+      [](const std::string& file, const std::string& conf, int64_t lo, int64_t hi) {
+        std::vector<ShardCrc> r;
+        {
+          py::gil_scoped_release nogil;
+          r = shard_crcs(file, conf, lo, hi);
+        }
+        py::list out;
+        for (const auto& x : r) out.append(py::make_tuple(x.index, x.present, x.crc));
+        return out;
+      },
+      py::arg("file"), py::arg("conf"), py::arg("lo"), py::arg("hi"),
+      "One rank's part of a split survivor check: (chunk index, present, CRC-32 of bytes [lo, hi)) per conf "
+      "candidate");
+  m.def(
+      "choose_survivors_given",
+      [](const std::string& file, const std::string& conf, const std::vector<int>& intact) {
+        py::gil_scoped_release nogil;
+        return choose_survivors_given(file, conf, intact);
+      },
+      py::arg("file"), py::arg("conf"), py::arg("intact"),
+      "The decode survivors (chunk indices) given every conf candidate's verdict (1 = intact)");
 
   m.def("chunk_path", &chunk_path);
   m.def("chunk_index", &chunk_index);

@@ -138,8 +138,9 @@ def _main_dist(a) -> int:
     ``csrc/io/stream_codec.cpp`` with pinned buffers on its own GPU, checkpointed per shard — reading
     its columns straight from the input file and pwriting them straight into the outputs. What
     crosses the process group is tiny: rank 0 creates the outputs at their final size, picks and
-    CRC-verifies the decode survivors (broadcast), and combines every rank's per-chunk CRC-32s
-    (``crc32_combine`` in column order) into the METADATA.
+    combines every rank's per-chunk CRC-32s (``crc32_combine`` in column order) into the METADATA
+    (encode), and checks the decode survivors the same way: each rank CRCs only its column shard of
+    every candidate, rank 0 combines and picks, and the choice is broadcast.
 
     A rank that fails exits non-zero at once, issuing no further collective: its peers' next one
     fails (gloo) or is aborted by the process group's bounded timeout (``--pg-timeout``), and torchrun
@@ -230,14 +231,34 @@ def _dist_run(a, ctx) -> int:
     md = ff.read_metadata(ff.metadata_path(a.in_file))
     C = max(2 if md.w == 16 else 1, ff.chunk_size(md.total_size, md.k, md.w))
     dst = a.out or a.in_file
-    # device setup under rank 0's survivor choice (it reads and CRC-checks every survivor)
+    # device setup under the survivor choice (the survivors' bytes are read and CRC-checked first)
     prep = (hip().prepare_decode_async(a.in_file, [ctx.local_rank], a.streams, a.slice, a.grid, a.zero_copy,
                                        a.window or 0) if on_gpu else None)
-    # rank 0 picks (and CRC-verifies) the survivors; status first: a failure there stops every rank
+    lo, hi = shard_range(C, world, rank)
+    # the survivor check, split over the ranks: each reads and CRCs only its column shard of every
+    # conf candidate; rank 0 combines the CRCs in column order, compares them with the METADATA and
+    # picks (one rank: the whole check in-process)
+    shard = None
+    if world > 1:
+        n = md.k + md.p
+        shard = torch.zeros(n + 1, 3, dtype=torch.int64, device=ctx.device)  # row 0: status, count, width
+        try:
+            got = cpu().shard_crcs(a.in_file, a.conf, lo, hi)
+            shard[0] = torch.tensor([0, len(got), hi - lo], dtype=torch.int64)
+            for i, (idx, present, crc) in enumerate(got[:n]):
+                shard[1 + i] = torch.tensor([idx, int(present), crc], dtype=torch.int64)
+        except Exception:  # noqa: BLE001 — rank 0 reports (it hits the same conf / METADATA)
+            shard[0, 0] = 1
+        parts = [torch.zeros_like(shard) for _ in range(world)]
+        dist.all_gather(parts, shard)
+    # rank 0 picks the survivors; status first: a failure there stops every rank
     pick = torch.zeros(md.k + 1, dtype=torch.int64, device=ctx.device)
     if ctx.is_root:
         try:
-            rows, _ = cpu().choose_survivors(a.in_file, a.conf)
+            if shard is None:
+                rows, _ = cpu().choose_survivors(a.in_file, a.conf)
+            else:
+                rows = cpu().choose_survivors_given(a.in_file, a.conf, _combine_shard_crcs(parts, md))
             pick[1:] = torch.tensor(rows, dtype=torch.int64)
         except Exception as ex:  # noqa: BLE001 — told to every rank through the broadcast
             pick[0] = 1
@@ -254,7 +275,6 @@ def _dist_run(a, ctx) -> int:
     barrier()
     if fault is not None and int(fault) == rank:
         raise RuntimeError("injected fault (GFRS_DIST_FAULT_RANK)")
-    lo, hi = shard_range(C, world, rank)
     kw = dict(st, col_lo=lo, col_hi=hi, shard=True, rows=rows)
     if on_gpu:
         r = hip().decode_file_stream(a.in_file, a.conf, dst, [ctx.local_rank], a.streams, a.slice, a.grid,
@@ -266,6 +286,30 @@ def _dist_run(a, ctx) -> int:
             f"{r['windows']} window(s) of {r['window']} B in {1e3 * (time.perf_counter() - t0):.1f}ms")
     _dist_summary(a, ctx, "decode", md.total_size, t0)
     return 0
+
+
+def _combine_shard_crcs(parts, md) -> list:
+    """Every conf candidate's verdict (1 = usable) from the ranks' shard reports (``shard_crcs``:
+    row 0 = status, candidate count, shard width; then chunk index, present, CRC-32 of the shard):
+    present on every rank, and the shard CRCs combined in rank (= column) order equal to the
+    METADATA's (METADATA without CRCs: present is enough)."""
+    from .._native import cpu
+
+    heads = [p[0].tolist() for p in parts]
+    if any(h[0] for h in heads):
+        raise RuntimeError("a rank could not read the survivors' configuration or METADATA")
+    ncand = int(heads[0][1])
+    rows = [p[1:1 + ncand].tolist() for p in parts]
+    intact = []
+    for ci in range(ncand):
+        idx = int(rows[0][ci][0])
+        present = all(int(r[ci][1]) for r in rows)
+        crc = 0
+        for r, h in zip(rows, heads):
+            crc = cpu().crc32_combine(crc, int(r[ci][2]), int(h[2]))
+        ok = present and (not md.crc or crc == md.crc[idx])
+        intact.append(1 if ok else 0)
+    return intact
 
 
 def _dist_summary(a, ctx, op: str, size: int, t0: float) -> None:

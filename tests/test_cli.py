@@ -62,6 +62,30 @@ def test_torchrun_dist_cli_matches_single_process(tmp_path, w):
     assert (d1 / "o.bin").read_bytes() == payload
 
 
+def test_torchrun_dist_cli_split_survivor_check(tmp_path):
+    """The multi-GPU decode checks its survivors split over the ranks: each rank CRCs only its
+    column shard of every listed chunk, and rank 0 combines the CRCs and picks. A chunk corrupted
+    only inside the last rank's shard, and a chunk that is missing, are both skipped (3 ranks,
+    gloo), and the file comes back byte-exact."""
+    payload = os.urandom(5 * 4096 * 10 + 777)
+    (tmp_path / "f.bin").write_bytes(payload)
+    env = dict(os.environ, PYTHONPATH=ROOT, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    r = _py(["-k", "10", "-n", "14", "-e", "f.bin", "--backend", "cpu"], tmp_path)
+    assert r.returncode == 0, r.stderr
+    chunk = (tmp_path / "_1_f.bin").read_bytes()
+    bad = bytearray(chunk)
+    bad[len(bad) - 3] ^= 0x21  # last columns: the last rank's shard only
+    (tmp_path / "_1_f.bin").write_bytes(bytes(bad))
+    os.remove(tmp_path / "_4_f.bin")
+    ff.write_conf(str(tmp_path / "conf"), [f"_{i}_f.bin" for i in range(14)])
+    base = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=3",
+            "--master-addr=127.0.0.1", f"--master-port={_port()}", "-m", "gpu_rscode_amd", "--dist"]
+    r = subprocess.run(base + ["-d", "-i", "f.bin", "-c", "conf", "-o", "o.bin"], cwd=tmp_path,
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert (tmp_path / "o.bin").read_bytes() == payload
+
+
 def test_torchrun_dist_cli_windows_world3_and_stale_outputs(tmp_path):
     """3 ranks walking their shards in 4 KiB windows (uneven shard sizes, so some ranks run out of
     columns while the window collective continues), over stale, longer chunk / output files."""
