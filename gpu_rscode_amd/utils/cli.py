@@ -241,14 +241,15 @@ def _dist_run(a, ctx) -> int:
     shard = None
     if world > 1:
         n = md.k + md.p
-        shard = torch.zeros(n + 1, 3, dtype=torch.int64, device=ctx.device)  # row 0: status, count, width
+        rows_h = [[1, 0, 0]] + [[0, 0, 0]] * n  # row 0: status, candidate count, shard width
         try:
             got = cpu().shard_crcs(a.in_file, a.conf, lo, hi)
-            shard[0] = torch.tensor([0, len(got), hi - lo], dtype=torch.int64)
+            rows_h[0] = [0, len(got), hi - lo]
             for i, (idx, present, crc) in enumerate(got[:n]):
-                shard[1 + i] = torch.tensor([idx, int(present), crc], dtype=torch.int64)
+                rows_h[1 + i] = [idx, int(present), crc]
         except Exception:  # noqa: BLE001 — rank 0 reports (it hits the same conf / METADATA)
-            shard[0, 0] = 1
+            rows_h[0][0] = 1
+        shard = torch.tensor(rows_h, dtype=torch.int64).to(ctx.device)
         parts = [torch.zeros_like(shard) for _ in range(world)]
         dist.all_gather(parts, shard)
     # rank 0 picks the survivors; status first: a failure there stops every rank
