@@ -74,6 +74,22 @@ std::string chunk_path(const std::string& file, int index);
 std::string metadata_path(const std::string& file);
 int chunk_index(const std::string& name);  // atoi(basename + 1); -1 if malformed
 
+// Durable commit of a small file: written to "<path>.gfrs-tmp", checked at every write and at
+// close, fsync'ed, renamed over `path`, and the directory fsync'ed (durable = true). A failure
+// (ENOSPC, EFBIG, EIO) throws and leaves `path` as it was — never a partial file. METADATA is always
+// written this way: a stripe whose METADATA exists was completely written before it
+// (the reference fopen/fprintf's it in place, src/encode.cu:61-101).
+void commit_file(const std::string& path, const uint8_t* data, int64_t len, bool durable = true);
+// the same for a file made of consecutive pieces (a decoded file: k rows, the last one cut)
+struct Piece {
+  const uint8_t* data;
+  int64_t len;
+};
+void commit_file(const std::string& path, const std::vector<Piece>& pieces, bool durable = true);
+// unlink (missing is fine) and, durable, fsync the directory: an encode removes an older METADATA
+// before its first chunk byte so a crash mid-way cannot leave a METADATA describing other chunks
+void remove_file(const std::string& path, bool durable = true);
+
 void write_metadata(const std::string& path, int64_t total_size, int p, int k, const Mat& e, bool with_matrix = true,
                     const std::vector<uint32_t>& crc = {});
 // GF(2^16): the versioned form (always with the matrix).
@@ -93,7 +109,9 @@ inline int64_t chunk_size(int64_t total, int k, int field_w) {
 int64_t file_size(const std::string& path);
 // Reads up to `len` bytes at `offset` into dst; zero-fills what the file does not cover.
 void read_into(const std::string& path, int64_t offset, uint8_t* dst, int64_t len);
-void write_from(const std::string& path, const uint8_t* src, int64_t len);
+// Writes `len` bytes to `path` (created / truncated); every write and the close are checked and
+// throw with errno's text (ENOSPC, EFBIG), durable: fdatasync'ed before the close.
+void write_from(const std::string& path, const uint8_t* src, int64_t len, bool durable = false);
 // Resolve a chunk name from a conf: as given (relative to the CWD, like the reference), else
 // relative to the directory of `anchor`.
 std::string resolve_chunk(const std::string& name, const std::string& anchor);

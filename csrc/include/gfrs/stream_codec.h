@@ -27,13 +27,18 @@ struct StreamOptions {
   bool resume = true;   // continue from a matching <target>.PROGRESS
   bool durable = true;  // fdatasync the outputs before each checkpoint
   int stop_after = -1;  // testing: return after this many windows of this call (simulated crash)
+  // testing: return after the last window, before the commit (chunk sizes, METADATA, checkpoint
+  // removal): a crash at the last step, which a later call with resume completes
+  bool stop_before_commit = false;
   int field_w = 8;      // encode: GF(2^8) or GF(2^16) symbols (decode reads it from METADATA)
   // Column shard (the multi-GPU file codec, one rank per GPU: the reference's per-device column
   // split, src/encode.cu:368-381): process chunk columns [col_lo, col_hi) only (col_hi < 0: to C;
   // GF(2^16): even offsets). With `shard`, the outputs must already exist at their full size (one
   // coordinator creates them): they are neither truncated nor resized, no METADATA is written, the
-  // checkpoint is "<target>.PROGRESS.<lo>-<hi>", and StreamReport::crc holds the shard's per-chunk
-  // CRC-32s (crc32_combine them in column order for the METADATA).
+  // checkpoint is "<target>.PROGRESS.<lo>-<hi>" (shard_progress_path) and is NOT removed when the
+  // shard completes (the coordinator removes it once its METADATA is committed, so a job that dies
+  // before that resumes finished shards at their end), and StreamReport::crc holds the shard's
+  // per-chunk CRC-32s (crc32_combine them in column order for the METADATA).
   int64_t col_lo = 0, col_hi = -1;
   bool shard = false;
   // decode: decode from exactly these survivor chunk ids, in this order (chosen and CRC-verified by
@@ -65,7 +70,11 @@ struct ShardCrc {
   bool present = false;  // the file exists and holds the whole chunk
   uint32_t crc = 0;      // CRC-32 of its bytes [lo, hi)
 };
-std::vector<ShardCrc> shard_crcs(const std::string& file, const std::string& conf, int64_t lo, int64_t hi);
+// Only candidates [first, first + count) are read (count < 0: to the end); the others are reported
+// absent. The coordinator asks for the first k (all a clean decode needs) and reads further ones only
+// when those are short of a recoverable set.
+std::vector<ShardCrc> shard_crcs(const std::string& file, const std::string& conf, int64_t lo, int64_t hi,
+                                 int first = 0, int count = -1);
 // choose_survivors with every candidate's verdict known (intact[ci] != 0: usable), conf order
 std::vector<int> choose_survivors_given(const std::string& file, const std::string& conf,
                                         const std::vector<int>& intact);
@@ -77,6 +86,8 @@ StreamReport decode_file_stream(const std::string& file, const std::string& conf
                                 const GemmFn& gemm, const HostAlloc& alloc, const StreamOptions& opt);
 
 std::string progress_path(const std::string& target);
+// a column shard's checkpoint: "<target>.PROGRESS.<lo>-<hi>"
+std::string shard_progress_path(const std::string& target, int64_t lo, int64_t hi);
 
 // Column window (bytes per chunk row) the streaming codecs use for `rows` buffered rows per window
 // (encode: n, decode: 2k) of C-byte chunks.

@@ -173,6 +173,9 @@ FileReport encode_file(const std::string& file, int k, int p, MatrixKind kind, c
       });
     for (auto& x : th) x.join();
   }
+  // commit order: an older METADATA goes first, then the chunks, then the new METADATA (atomic) — a
+  // failure anywhere (ENOSPC at a chunk, at the METADATA) leaves no METADATA claiming the stripe
+  remove_file(metadata_path(file));
   for (int i = 0; i < k; ++i) write_from(chunk_path(file, i), data.p + size_t(i) * P, C);
   for (int i = 0; i < p; ++i) write_from(chunk_path(file, k + i), parity.p + size_t(i) * P, C);
   if (field_w == 16)
@@ -346,26 +349,20 @@ FileReport decode_file(const std::string& file, const std::string& conf, const s
 
   t = Clock::now();
   const std::string dst = out.empty() ? file : out;
-  FILE* fp = std::fopen(dst.c_str(), "wb");
-  if (!fp) throw std::runtime_error("cannot open output file " + dst);
+  // the decoded file is written next to its target and renamed over it (a failed write, e.g. ENOSPC,
+  // leaves the target as it was; decoding in place over the input file never truncates it first).
+  // Not fsync'ed: the reference's decode writes without a sync too (src/decode.cu:410-427); the
+  // windowed codec is the durable path (--window).
+  std::vector<Piece> pieces;
   int64_t left = md.total_size;
   size_t e_idx = 0;
   for (int i = 0; i < k && left > 0; ++i) {
-    const uint8_t* row;
-    if (pos_of_native[i] >= 0) {
-      row = surv.p + size_t(pos_of_native[i]) * P;
-    } else {
-      row = rec.p + e_idx * P;
-      ++e_idx;
-    }
+    const uint8_t* row = pos_of_native[i] >= 0 ? surv.p + size_t(pos_of_native[i]) * P : rec.p + (e_idx++) * P;
     const int64_t w = std::min(C, left);
-    if (std::fwrite(row, 1, size_t(w), fp) != size_t(w)) {
-      std::fclose(fp);
-      throw std::runtime_error("short write to " + dst);
-    }
+    pieces.push_back({row, w});
     left -= w;
   }
-  std::fclose(fp);
+  commit_file(dst, pieces, false);
   r.ms_write = ms_since(t);
   return r;
 }

@@ -2,12 +2,15 @@
 // encoder leaves padding uninitialised, src/encode.cu:325).
 #include "gfrs/format.h"
 
+#include <fcntl.h>
 #include <sys/stat.h>
+#include <unistd.h>
 
 #if defined(__x86_64__)
 #include <immintrin.h>
 #endif
 
+#include <cerrno>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -211,48 +214,116 @@ uint32_t crc32_combine(uint32_t crc_a, uint32_t crc_b, int64_t len_b) {
   return reg ^ crc_b;
 }
 
+namespace {
+
+// the metadata text of either form, built in memory (one atomic commit below)
+void matrix_lines(std::ostringstream& o, int p, int k, const std::vector<int>& e) {
+  for (int i = 0; i < k; ++i) {
+    for (int j = 0; j < k; ++j) o << (i == j ? "1 " : "0 ");
+    o << '\n';
+  }
+  for (int i = 0; i < p; ++i) {
+    for (int j = 0; j < k; ++j) o << e[size_t(i) * k + j] << ' ';
+    o << '\n';
+  }
+}
+
+void crc_line(std::ostringstream& o, const std::vector<uint32_t>& crc) {
+  if (crc.empty()) return;
+  o << "crc32";
+  char hex[16];
+  for (uint32_t c : crc) {
+    std::snprintf(hex, sizeof(hex), " %08x", c);
+    o << hex;
+  }
+  o << '\n';
+}
+
+[[noreturn]] void io_fail(const std::string& what, const std::string& path, int err) {
+  throw std::runtime_error(what + " " + path + ": " + std::strerror(err));
+}
+
+void write_all_fd(int fd, const uint8_t* src, int64_t len, const std::string& path) {
+  int64_t put = 0;
+  while (put < len) {
+    const ssize_t w = ::write(fd, src + put, size_t(std::min<int64_t>(len - put, int64_t(1) << 30)));
+    if (w < 0) {
+      if (errno == EINTR) continue;
+      io_fail("write failed:", path, errno);
+    }
+    put += w;
+  }
+}
+
+void fsync_dir_of(const std::string& path) {
+  const size_t s = path.find_last_of('/');
+  const std::string dir = s == std::string::npos ? "." : (s == 0 ? "/" : path.substr(0, s));
+  const int fd = ::open(dir.c_str(), O_RDONLY | O_DIRECTORY | O_CLOEXEC);
+  if (fd < 0) return;  // (a directory we cannot open cannot be synced; the rename itself succeeded)
+  ::fsync(fd);
+  ::close(fd);
+}
+
+}  // namespace
+
+void commit_file(const std::string& path, const std::vector<Piece>& pieces, bool durable) {
+  const std::string tmp = path + ".gfrs-tmp";
+  const int fd = ::open(tmp.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
+  if (fd < 0) io_fail("cannot create", tmp, errno);
+  try {
+    for (const Piece& pc : pieces) write_all_fd(fd, pc.data, pc.len, tmp);
+    if (durable && ::fsync(fd) != 0) io_fail("fsync failed:", tmp, errno);
+  } catch (...) {
+    ::close(fd);
+    ::unlink(tmp.c_str());
+    throw;
+  }
+  if (::close(fd) != 0) {
+    const int err = errno;
+    ::unlink(tmp.c_str());
+    io_fail("close failed:", tmp, err);
+  }
+  if (std::rename(tmp.c_str(), path.c_str()) != 0) {
+    const int err = errno;
+    ::unlink(tmp.c_str());
+    io_fail("cannot rename onto", path, err);
+  }
+  if (durable) fsync_dir_of(path);
+}
+
+void commit_file(const std::string& path, const uint8_t* data, int64_t len, bool durable) {
+  commit_file(path, std::vector<Piece>{{data, len}}, durable);
+}
+
+void remove_file(const std::string& path, bool durable) {
+  if (::unlink(path.c_str()) != 0) {
+    if (errno == ENOENT) return;
+    io_fail("cannot remove", path, errno);
+  }
+  if (durable) fsync_dir_of(path);
+}
+
 void write_metadata(const std::string& path, int64_t total_size, int p, int k, const Mat& e, bool with_matrix,
                     const std::vector<uint32_t>& crc) {
-  FILE* fp = std::fopen(path.c_str(), "wb");
-  if (!fp) throw std::runtime_error("cannot open metadata file " + path);
-  std::fprintf(fp, "%lld\n%d %d\n", static_cast<long long>(total_size), p, k);
+  std::ostringstream o;
+  o << static_cast<long long>(total_size) << '\n' << p << ' ' << k << '\n';
   if (with_matrix) {
-    for (int i = 0; i < k; ++i) {
-      for (int j = 0; j < k; ++j) std::fprintf(fp, "%d ", i == j ? 1 : 0);
-      std::fprintf(fp, "\n");
-    }
-    for (int i = 0; i < p; ++i) {
-      for (int j = 0; j < k; ++j) std::fprintf(fp, "%d ", int(e[size_t(i) * k + j]));
-      std::fprintf(fp, "\n");
-    }
-    if (!crc.empty()) {
-      std::fprintf(fp, "crc32");
-      for (uint32_t c : crc) std::fprintf(fp, " %08x", c);
-      std::fprintf(fp, "\n");
-    }
+    matrix_lines(o, p, k, std::vector<int>(e.begin(), e.end()));
+    crc_line(o, crc);
   }
-  std::fclose(fp);
+  const std::string s = o.str();
+  commit_file(path, reinterpret_cast<const uint8_t*>(s.data()), int64_t(s.size()));
 }
 
 void write_metadata16(const std::string& path, int64_t total_size, int p, int k, const gf16w::Mat& e,
                       const std::vector<uint32_t>& crc) {
-  FILE* fp = std::fopen(path.c_str(), "wb");
-  if (!fp) throw std::runtime_error("cannot open metadata file " + path);
-  std::fprintf(fp, "GFRS-METADATA %d 16\n%lld\n%d %d\n", kMetadataVersion, static_cast<long long>(total_size), p, k);
-  for (int i = 0; i < k; ++i) {
-    for (int j = 0; j < k; ++j) std::fprintf(fp, "%d ", i == j ? 1 : 0);
-    std::fprintf(fp, "\n");
-  }
-  for (int i = 0; i < p; ++i) {
-    for (int j = 0; j < k; ++j) std::fprintf(fp, "%d ", int(e[size_t(i) * k + j]));
-    std::fprintf(fp, "\n");
-  }
-  if (!crc.empty()) {
-    std::fprintf(fp, "crc32");
-    for (uint32_t c : crc) std::fprintf(fp, " %08x", c);
-    std::fprintf(fp, "\n");
-  }
-  std::fclose(fp);
+  std::ostringstream o;
+  o << "GFRS-METADATA " << kMetadataVersion << " 16\n" << static_cast<long long>(total_size) << '\n' << p << ' ' << k
+    << '\n';
+  matrix_lines(o, p, k, std::vector<int>(e.begin(), e.end()));
+  crc_line(o, crc);
+  const std::string s = o.str();
+  commit_file(path, reinterpret_cast<const uint8_t*>(s.data()), int64_t(s.size()));
 }
 
 namespace {
@@ -339,9 +410,9 @@ std::vector<std::string> read_conf(const std::string& path) {
 }
 
 void write_conf(const std::string& path, const std::vector<std::string>& names) {
-  std::ofstream out(path);
-  if (!out) throw std::runtime_error("cannot write configuration file " + path);
-  for (const auto& n : names) out << n << "\n";
+  std::string s;
+  for (const auto& n : names) s += n + "\n";
+  commit_file(path, reinterpret_cast<const uint8_t*>(s.data()), int64_t(s.size()), false);
 }
 
 int64_t file_size(const std::string& path) {
@@ -365,17 +436,18 @@ void read_into(const std::string& path, int64_t offset, uint8_t* dst, int64_t le
   if (got < len) std::memset(dst + got, 0, size_t(len - got));
 }
 
-void write_from(const std::string& path, const uint8_t* src, int64_t len) {
-  FILE* fp = std::fopen(path.c_str(), "wb");
-  if (!fp) throw std::runtime_error("cannot open output file " + path);
-  int64_t put = 0;
-  while (put < len) {
-    const size_t w = std::fwrite(src + put, 1, size_t(len - put), fp);
-    if (w == 0) break;
-    put += int64_t(w);
+void write_from(const std::string& path, const uint8_t* src, int64_t len, bool durable) {
+  const int fd = ::open(path.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
+  if (fd < 0) io_fail("cannot open output file", path, errno);
+  try {
+    write_all_fd(fd, src, len, path);
+    if (durable && ::fdatasync(fd) != 0) io_fail("fdatasync failed:", path, errno);
+  } catch (...) {
+    ::close(fd);
+    throw;
   }
-  std::fclose(fp);
-  if (put < len) throw std::runtime_error("short write to " + path);
+  // (a deferred write error, e.g. ENOSPC on an NFS flush, surfaces at close)
+  if (::close(fd) != 0) io_fail("close failed:", path, errno);
 }
 
 std::string resolve_chunk(const std::string& name, const std::string& anchor) {

@@ -89,15 +89,23 @@ int64_t pick_window(const StreamOptions& opt, int rows, int64_t C) {
   return std::max<int64_t>(1, std::min(w, C));
 }
 
-// Atomic checkpoint: write a temp file, fsync it, rename over the old one.
+// Atomic checkpoint: temp file, checked writes, fsync, rename over the old one (format.h).
 void write_progress(const std::string& path, const std::string& line, bool durable) {
-  const std::string tmp = path + ".tmp";
-  {
-    Fd f = open_or_throw(tmp, O_WRONLY | O_CREAT | O_TRUNC);
-    pwrite_full(f.fd, reinterpret_cast<const uint8_t*>(line.data()), int64_t(line.size()), 0);
-    if (durable) ::fsync(f.fd);
-  }
-  if (std::rename(tmp.c_str(), path.c_str()) != 0) throw std::runtime_error("cannot write checkpoint " + path);
+  commit_file(path, reinterpret_cast<const uint8_t*>(line.data()), int64_t(line.size()), durable);
+}
+
+// modification time (ns) of a file the output bytes depend on: part of a checkpoint's key, so a
+// checkpoint never resumes over an input that changed since it was written
+long long mtime_ns(const std::string& path) {
+  struct stat sb;
+  if (::stat(path.c_str(), &sb) != 0) return -1;
+  return static_cast<long long>(sb.st_mtim.tv_sec) * 1000000000LL + sb.st_mtim.tv_nsec;
+}
+
+// fsync every output (the windows were fdatasync'ed; the final size change was not)
+void sync_all(const std::vector<Fd>& fds, const std::string& what) {
+  for (const Fd& f : fds)
+    if (::fsync(f.fd) != 0) throw std::runtime_error("fsync failed on " + what + ": " + std::strerror(errno));
 }
 
 std::vector<std::string> read_progress(const std::string& path) {
@@ -191,6 +199,10 @@ int64_t stream_window(const StreamOptions& opt, int rows, int64_t C) { return pi
 
 std::string progress_path(const std::string& target) { return target + ".PROGRESS"; }
 
+std::string shard_progress_path(const std::string& target, int64_t lo, int64_t hi) {
+  return progress_path(target) + "." + std::to_string(lo) + "-" + std::to_string(hi);
+}
+
 namespace {
 
 // The column range [lo, hi) of a call (validated), the checkpoint path and the window.
@@ -207,8 +219,7 @@ Range column_range(const StreamOptions& opt, const std::string& target, int rows
   if (field_w == 16 && (r.lo % 2 || r.hi % 2)) throw std::invalid_argument("stream codec: GF(2^16) columns are whole symbols");
   r.W = pick_window(opt, rows, std::max<int64_t>(1, r.hi - r.lo));
   if (field_w == 16) r.W += r.W % 2;  // whole 16-bit symbols per window
-  r.prog = progress_path(target);
-  if (opt.shard) r.prog += "." + std::to_string(r.lo) + "-" + std::to_string(r.hi);
+  r.prog = opt.shard ? shard_progress_path(target, r.lo, r.hi) : progress_path(target);
   return r;
 }
 
@@ -262,7 +273,7 @@ StreamReport encode_file_stream(const std::string& file, int k, int p, MatrixKin
   // resume point (the key names everything the bytes depend on, the column range included)
   std::ostringstream key;
   key << "gfrs-progress 2 encode " << rep.total_size << ' ' << k << ' ' << p << ' ' << int(kind) << ' '
-      << int(cpu_meta) << ' ' << C << ' ' << fw << ' ' << rg.lo << ' ' << rg.hi;
+      << int(cpu_meta) << ' ' << C << ' ' << fw << ' ' << rg.lo << ' ' << rg.hi << ' ' << mtime_ns(file);
   int64_t start = rg.lo;
   std::vector<uint32_t> crc(size_t(n), 0);
   if (opt.resume) {
@@ -278,6 +289,8 @@ StreamReport encode_file_stream(const std::string& file, int k, int p, MatrixKin
     }
   }
   rep.resumed_from = start;
+  // an older METADATA goes before the first chunk byte changes (a shard's coordinator removes it)
+  if (!opt.shard) remove_file(metadata_path(file), opt.durable);
 
   Fd in = open_or_throw(file, O_RDONLY);
   std::vector<Fd> outs;
@@ -311,21 +324,25 @@ StreamReport encode_file_stream(const std::string& file, int k, int p, MatrixKin
 
   const int64_t done = start + int64_t(rep.windows) * W;
   if (done < rg.hi) return rep;  // stopped early (stop_after): the checkpoint says where to resume
-  if (opt.shard) {  // the coordinator combines the shards' CRCs and writes the METADATA
-    rep.crc = crc;
-    std::remove(rg.prog.c_str());
+  rep.crc = crc;
+  if (opt.shard) {
+    // The coordinator combines the shards' CRCs and commits the METADATA; this shard's checkpoint
+    // (offset = hi, its CRCs) stays until then, so a job that dies before the commit resumes every
+    // finished shard at its end instead of re-encoding it (the caller removes it afterwards).
     rep.complete = true;
     return rep;
   }
   if (rg.lo != 0 || rg.hi != C) throw std::invalid_argument("encode: a partial column range needs shard mode");
+  if (opt.stop_before_commit) return rep;  // (testing: a crash between the last window and the commit)
+  // commit: sized and synced chunks, then the METADATA (atomic), then the checkpoint goes
   for (int i = 0; i < n; ++i)
     if (::ftruncate(outs[size_t(i)].fd, C) != 0) throw std::runtime_error("cannot size chunk file");
+  if (opt.durable) sync_all(outs, "chunk file");
   if (fw == 16)
     write_metadata16(metadata_path(file), rep.total_size, p, k, e16, crc);
   else
     write_metadata(metadata_path(file), rep.total_size, p, k, e, !cpu_meta, cpu_meta ? std::vector<uint32_t>{} : crc);
-  rep.crc = crc;
-  std::remove(rg.prog.c_str());
+  remove_file(rg.prog, opt.durable);
   rep.complete = true;
   return rep;
 }
@@ -449,16 +466,21 @@ std::vector<int> choose_survivors(const std::string& file, const std::string& co
   return rows;
 }
 
-std::vector<ShardCrc> shard_crcs(const std::string& file, const std::string& conf, int64_t lo, int64_t hi) {
+std::vector<ShardCrc> shard_crcs(const std::string& file, const std::string& conf, int64_t lo, int64_t hi, int first,
+                                 int count) {
   const Metadata md = read_metadata(metadata_path(file));
   const Candidates cand = conf_candidates(file, conf, md);
   const int64_t C = stripe_chunk(md);
   lo = std::max<int64_t>(0, std::min(lo, C));
   hi = std::max<int64_t>(lo, std::min(hi, C));
+  const int ncand = int(cand.idx.size());
+  first = std::max(0, std::min(first, ncand));
+  const int end = count < 0 ? ncand : std::min(ncand, first + count);
   std::vector<ShardCrc> out(cand.idx.size());
-  parallel_indices(int(cand.idx.size()), verify_threads(), [&](int ci) {
+  for (int ci = 0; ci < ncand; ++ci) out[size_t(ci)].index = cand.idx[size_t(ci)];
+  parallel_indices(end - first, verify_threads(), [&](int i) {
+    const int ci = first + i;
     ShardCrc& r = out[size_t(ci)];
-    r.index = cand.idx[size_t(ci)];
     try {
       const std::string& path = cand.path[size_t(ci)];
       if (!file_at_least(path, md.total_size > 0 ? C : 0)) return;
@@ -545,7 +567,7 @@ StreamReport decode_file_stream(const std::string& file, const std::string& conf
 
   std::ostringstream key;
   key << "gfrs-progress 2 decode " << md.total_size << ' ' << k << ' ' << md.p << ' ' << C << ' ' << md.w << ' '
-      << rg.lo << ' ' << rg.hi;
+      << rg.lo << ' ' << rg.hi << ' ' << mtime_ns(metadata_path(file));
   for (int r : rows) key << ' ' << r;
   int64_t start = rg.lo;
   if (opt.resume) {
@@ -591,11 +613,15 @@ StreamReport decode_file_stream(const std::string& file, const std::string& conf
 
   const int64_t done = start + int64_t(rep.windows) * W;
   if (done < rg.hi) return rep;
-  if (!opt.shard) {
-    if (rg.lo != 0 || rg.hi != C) throw std::invalid_argument("decode: a partial column range needs shard mode");
-    if (::ftruncate(of.fd, md.total_size) != 0) throw std::runtime_error("cannot size output file " + dst);
+  if (opt.shard) {  // (the checkpoint stays until the coordinator's final barrier, as for encode)
+    rep.complete = true;
+    return rep;
   }
-  std::remove(rg.prog.c_str());
+  if (rg.lo != 0 || rg.hi != C) throw std::invalid_argument("decode: a partial column range needs shard mode");
+  if (opt.stop_before_commit) return rep;
+  if (::ftruncate(of.fd, md.total_size) != 0) throw std::runtime_error("cannot size output file " + dst);
+  if (opt.durable && ::fsync(of.fd) != 0) throw std::runtime_error("fsync failed on " + dst + ": " + std::strerror(errno));
+  remove_file(rg.prog, opt.durable);
   rep.complete = true;
   return rep;
 }

@@ -125,40 +125,50 @@ PYBIND11_MODULE(_cpu, m) {
   m.def(
       "encode_file_stream",
       [gemm_fn](const std::string& file, int k, int p, const std::string& matrix, bool cpu_meta,
-                const std::string& strategy, int threads, int64_t window, bool resume, bool durable, int stop_after,
+                const std::string& strategy, int threads, int64_t window, bool resume, bool durable, int stop_after, bool stop_before_commit,
                 int field_w, int64_t col_lo, int64_t col_hi, bool shard) {
         const GemmFn g = gemm_fn(strategy, threads);
         StreamReport r;
         {
           py::gil_scoped_release nogil;
-          r = encode_file_stream(file, k, p, parse_matrix_kind(matrix), g, default_host_alloc(),
-                                 stream_options(window, resume, durable, stop_after, field_w, col_lo, col_hi, shard),
-                                 cpu_meta);
+          StreamOptions so = stream_options(window, resume, durable, stop_after, field_w, col_lo, col_hi, shard);
+          so.stop_before_commit = stop_before_commit;
+          r = encode_file_stream(file, k, p, parse_matrix_kind(matrix), g, default_host_alloc(), so, cpu_meta);
         }
         return stream_report(r);
       },
       py::arg("file"), py::arg("k"), py::arg("p"), py::arg("matrix") = "vandermonde", py::arg("cpu_meta") = false,
       py::arg("strategy") = "simd", py::arg("threads") = 1, py::arg("window") = 0, py::arg("resume") = true,
-      py::arg("durable") = true, py::arg("stop_after") = -1, py::arg("field_w") = 8, py::arg("col_lo") = 0,
+      py::arg("durable") = true, py::arg("stop_after") = -1, py::arg("stop_before_commit") = false, py::arg("field_w") = 8, py::arg("col_lo") = 0,
       py::arg("col_hi") = -1, py::arg("shard") = false);
   m.def(
       "decode_file_stream",
       [gemm_fn](const std::string& file, const std::string& conf, const std::string& out, const std::string& strategy,
-                int threads, int64_t window, bool resume, bool durable, int stop_after, int64_t col_lo, int64_t col_hi,
+                int threads, int64_t window, bool resume, bool durable, int stop_after, bool stop_before_commit, int64_t col_lo, int64_t col_hi,
                 bool shard, const std::vector<int>& rows) {
         const GemmFn g = gemm_fn(strategy, threads);
         StreamReport r;
         {
           py::gil_scoped_release nogil;
-          r = decode_file_stream(file, conf, out, g, default_host_alloc(),
-                                 stream_options(window, resume, durable, stop_after, 8, col_lo, col_hi, shard, rows));
+          StreamOptions so = stream_options(window, resume, durable, stop_after, 8, col_lo, col_hi, shard, rows);
+          so.stop_before_commit = stop_before_commit;
+          r = decode_file_stream(file, conf, out, g, default_host_alloc(), so);
         }
         return stream_report(r);
       },
       py::arg("file"), py::arg("conf"), py::arg("out") = "", py::arg("strategy") = "simd", py::arg("threads") = 1,
-      py::arg("window") = 0, py::arg("resume") = true, py::arg("durable") = true, py::arg("stop_after") = -1,
+      py::arg("window") = 0, py::arg("resume") = true, py::arg("durable") = true, py::arg("stop_after") = -1, py::arg("stop_before_commit") = false,
       py::arg("col_lo") = 0, py::arg("col_hi") = -1, py::arg("shard") = false, py::arg("rows") = std::vector<int>{});
   m.def("progress_path", &progress_path);
+  m.def("shard_progress_path", &shard_progress_path, py::arg("target"), py::arg("lo"), py::arg("hi"));
+  m.def("commit_file", [](const std::string& path, const py::bytes& data, bool durable) {
+    const std::string s = data;
+    py::gil_scoped_release nogil;
+    commit_file(path, reinterpret_cast<const uint8_t*>(s.data()), int64_t(s.size()), durable);
+  }, py::arg("path"), py::arg("data"), py::arg("durable") = true,
+     "write `data` to path.gfrs-tmp, fsync, rename over `path`, fsync the directory (errors raise)");
+  m.def("remove_file", [](const std::string& path, bool durable) { remove_file(path, durable); }, py::arg("path"),
+        py::arg("durable") = true);
   m.def("choose_survivors", [](const std::string& file, const std::string& conf) {
     int rejected = 0;
     std::vector<int> rows;
@@ -175,19 +185,20 @@ PYBIND11_MODULE(_cpu, m) {
   m.def("crc32_combine", &crc32_combine);
   m.def(
       "shard_crcs",
-      [](const std::string& file, const std::string& conf, int64_t lo, int64_t hi) {
+      [](const std::string& file, const std::string& conf, int64_t lo, int64_t hi, int first, int count) {
         std::vector<ShardCrc> r;
         {
           py::gil_scoped_release nogil;
-          r = shard_crcs(file, conf, lo, hi);
+          r = shard_crcs(file, conf, lo, hi, first, count);
         }
         py::list out;
         for (const auto& x : r) out.append(py::make_tuple(x.index, x.present, x.crc));
         return out;
       },
-      py::arg("file"), py::arg("conf"), py::arg("lo"), py::arg("hi"),
+      py::arg("file"), py::arg("conf"), py::arg("lo"), py::arg("hi"), py::arg("first") = 0, py::arg("count") = -1,
       "One rank's part of a split survivor check: (chunk index, present, CRC-32 of bytes [lo, hi)) per conf "
-      "candidate");
+      "candidate; candidates [first, first + count) only (count < 0: to the end) are read, the others come back "
+      "as (index, False, 0)");
   m.def(
       "choose_survivors_given",
       [](const std::string& file, const std::string& conf, const std::vector<int>& intact) {

@@ -416,7 +416,7 @@ PYBIND11_MODULE(_hip, m) {
       "encode_file_stream",
       [gpu_gemm, take_prep](const std::string& file, int k, int p, const std::string& matrix, bool cpu_meta,
                             const std::vector<int>& devices, int streams, int64_t slice, int max_blocks,
-                            int64_t window, bool resume, bool durable, int stop_after, int field_w, int64_t col_lo,
+                            int64_t window, bool resume, bool durable, int stop_after, bool stop_before_commit, int field_w, int64_t col_lo,
                             int64_t col_hi, bool shard, bool zero_copy, py::object prep_handle) {
         StreamReport r;
         std::unique_ptr<AsyncPrepare> given = take_prep(prep_handle);
@@ -424,7 +424,8 @@ PYBIND11_MODULE(_hip, m) {
         {
           py::gil_scoped_release nogil;
           // device setup on a helper thread during the first window's reads, as bin/RS does
-          const StreamOptions so = stream_options(window, resume, durable, stop_after, field_w, col_lo, col_hi, shard);
+          StreamOptions so = stream_options(window, resume, durable, stop_after, field_w, col_lo, col_hi, shard);
+          so.stop_before_commit = stop_before_commit;
           PipelineOptions popt = pipeline_options(streams, slice, max_blocks);
           popt.field_w = field_w;
           popt.zero_copy = zero_copy;
@@ -437,13 +438,13 @@ PYBIND11_MODULE(_hip, m) {
       py::arg("file"), py::arg("k"), py::arg("p"), py::arg("matrix") = "vandermonde", py::arg("cpu_meta") = false,
       py::arg("devices") = std::vector<int>{0}, py::arg("streams") = 2, py::arg("slice") = 16 << 20,
       py::arg("max_blocks") = 0, py::arg("window") = 0, py::arg("resume") = true, py::arg("durable") = true,
-      py::arg("stop_after") = -1, py::arg("field_w") = 8, py::arg("col_lo") = 0, py::arg("col_hi") = -1,
+      py::arg("stop_after") = -1, py::arg("stop_before_commit") = false, py::arg("field_w") = 8, py::arg("col_lo") = 0, py::arg("col_hi") = -1,
       py::arg("shard") = false, py::arg("zero_copy") = false, py::arg("prep") = py::none());
   m.def(
       "decode_file_stream",
       [gpu_gemm, take_prep](const std::string& file, const std::string& conf, const std::string& out,
                             const std::vector<int>& devices, int streams, int64_t slice, int max_blocks,
-                            int64_t window, bool resume, bool durable, int stop_after, int64_t col_lo,
+                            int64_t window, bool resume, bool durable, int stop_after, bool stop_before_commit, int64_t col_lo,
                             int64_t col_hi, bool shard, const std::vector<int>& rows, bool zero_copy,
                             py::object prep_handle) {
         StreamReport r;
@@ -451,7 +452,8 @@ PYBIND11_MODULE(_hip, m) {
         const bool have = bool(given) || !prep_handle.is_none();
         {
           py::gil_scoped_release nogil;
-          const StreamOptions so = stream_options(window, resume, durable, stop_after, 8, col_lo, col_hi, shard, rows);
+          StreamOptions so = stream_options(window, resume, durable, stop_after, 8, col_lo, col_hi, shard, rows);
+          so.stop_before_commit = stop_before_commit;
           PipelineOptions popt = pipeline_options(streams, slice, max_blocks);
           popt.zero_copy = zero_copy;
           auto prep = have ? std::move(given) : prepare_for_decode(devices, popt, file, &so);
@@ -462,7 +464,7 @@ PYBIND11_MODULE(_hip, m) {
       },
       py::arg("file"), py::arg("conf"), py::arg("out") = "", py::arg("devices") = std::vector<int>{0},
       py::arg("streams") = 2, py::arg("slice") = 16 << 20, py::arg("max_blocks") = 0, py::arg("window") = 0,
-      py::arg("resume") = true, py::arg("durable") = true, py::arg("stop_after") = -1, py::arg("col_lo") = 0,
+      py::arg("resume") = true, py::arg("durable") = true, py::arg("stop_after") = -1, py::arg("stop_before_commit") = false, py::arg("col_lo") = 0,
       py::arg("col_hi") = -1, py::arg("shard") = false, py::arg("rows") = std::vector<int>{},
       py::arg("zero_copy") = false, py::arg("prep") = py::none());
 }

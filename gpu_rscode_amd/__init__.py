@@ -10,9 +10,14 @@ Capabilities of zvonkok/GPU-RSCode (the reference), re-designed for CDNA4:
 """
 from __future__ import annotations
 
-# (HSA_ENABLE_IPC_MODE_LEGACY=0 — dmabuf IPC, needed by RCCL peers on this driver — is set by the
-# launchers: bench.py, scripts, __graft_entry__; parallel.dist.init_distributed warns without it.)
-import torch  # noqa: F401  — load torch's HIP runtime before the native extension
+import os
+
+# dmabuf IPC, needed by RCCL peers on this driver: the HIP runtime reads this once when it
+# initialises, so it is set here, before this package imports torch (parallel.dist.ensure_ipc_env
+# refuses to build an RCCL group if HIP started without it).
+os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+
+import torch  # noqa: E402,F401  — load torch's HIP runtime before the native extension
 
 from . import gf  # noqa: E402
 from .gf import GF, SingularMatrixError

@@ -35,6 +35,27 @@ import torch.distributed as dist
 from ..models.rs import ReedSolomon, alloc_rows
 
 SHARD_ALIGN = 4096
+IPC_ENV = "HSA_ENABLE_IPC_MODE_LEGACY"
+
+
+def default_pg_timeout() -> float:
+    """Process-group timeout (s) of every entry point that does not pass its own: GFRS_PG_TIMEOUT_S,
+    else 300 (``bench.py`` passes a longer one that covers its budgets)."""
+    return float(os.environ.get("GFRS_PG_TIMEOUT_S", 300))
+
+
+def ensure_ipc_env(backend: str) -> None:
+    """RCCL peers on this driver need dmabuf IPC (``HSA_ENABLE_IPC_MODE_LEGACY=0``; without it
+    ``hipIpcGetMemHandle`` fails when the first peer buffer is shared). The HIP runtime reads the
+    variable once, when it initialises: set it here if HIP has not started yet, and refuse to build
+    an RCCL group if it has started without it (the package's ``__init__`` sets it before importing
+    torch, so every entry point through the package gets it in time)."""
+    if backend != "nccl" or os.environ.get(IPC_ENV) == "0":
+        return
+    if torch.cuda.is_initialized():
+        raise RuntimeError(f"{IPC_ENV}=0 must be set before HIP initialises (RCCL peers use dmabuf IPC on this "
+                           "driver); export it before the process starts")
+    os.environ[IPC_ENV] = "0"
 
 
 @dataclass
@@ -54,7 +75,7 @@ def init_distributed(backend: str | None = None, force_pg: bool | None = None,
                      timeout_s: float | None = None) -> DistContext:
     """Initialise from torchrun's environment (RANK, WORLD_SIZE, LOCAL_RANK, MASTER_*).
 
-    The process group gets a bounded timeout (``timeout_s``, default ``GFRS_PG_TIMEOUT_S`` or 600 s):
+    The process group gets a bounded timeout (``timeout_s``, default :func:`default_pg_timeout`):
     a collective whose peer is gone raises (gloo) or is aborted by the RCCL watchdog after at most
     that long, instead of hanging the job.
 
@@ -64,6 +85,8 @@ def init_distributed(backend: str | None = None, force_pg: bool | None = None,
     is how the RCCL code paths execute on a single MI355X (tests, ``bench.py --force-pg``).
     """
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if (world > 1 or force_pg) and backend in (None, "nccl"):
+        ensure_ipc_env("nccl")  # (before torch.cuda.set_device initialises HIP below)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if force_pg is None:
@@ -75,17 +98,14 @@ def init_distributed(backend: str | None = None, force_pg: bool | None = None,
     else:
         device = torch.device("cpu")
     backend = backend or ("nccl" if use_gpu else "gloo")
-    if backend == "nccl" and world > 1 and os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY") != "0":
-        import warnings
-
-        warnings.warn("RCCL peers need dmabuf IPC on this driver: export HSA_ENABLE_IPC_MODE_LEGACY=0 before "
-                      "the process starts (hipIpcGetMemHandle fails without it)", RuntimeWarning, stacklevel=2)
+    if world > 1 or force_pg:
+        ensure_ipc_env(backend)
     if (world > 1 or force_pg) and not dist.is_initialized():
         kw = {"device_id": device} if device.type == "cuda" else {}
         if world == 1 and "MASTER_PORT" not in os.environ:
             kw.update(init_method=f"tcp://127.0.0.1:{free_port()}", rank=0, world_size=1)
         if timeout_s is None:
-            timeout_s = float(os.environ.get("GFRS_PG_TIMEOUT_S", 600))
+            timeout_s = default_pg_timeout()
         dist.init_process_group(backend, timeout=datetime.timedelta(seconds=timeout_s), **kw)
     return DistContext(rank, world, local, device, backend)
 
@@ -119,17 +139,28 @@ def shard_range(ncols: int, world: int, rank: int, align: int = SHARD_ALIGN) -> 
     return a, b
 
 
-def broadcast_matrix(mat: np.ndarray | None, device: torch.device, src: int = 0) -> np.ndarray:
-    """Broadcast a small uint8 matrix (E, or a decode inverse) from ``src`` to every rank."""
+_BCAST_DTYPES = {np.dtype(np.uint8): torch.uint8, np.dtype(np.int32): torch.int32}
+
+
+def broadcast_matrix(mat: np.ndarray | None, device: torch.device, src: int = 0, dtype=np.uint8) -> np.ndarray:
+    """Broadcast a small matrix from ``src`` to every rank: E or a decode inverse (``dtype`` uint8:
+    GF(2^8) symbols), GF(2^16) symbols or chunk ids (``int32``: values up to 65535 survive, which a
+    byte broadcast would truncate past 255). Returns ``dtype``."""
+    dt = np.dtype(dtype)
+    if dt not in _BCAST_DTYPES:
+        raise ValueError(f"broadcast_matrix: dtype {dt} (uint8 or int32)")
     if not dist.is_initialized():
-        return np.asarray(mat, dtype=np.uint8)
+        return np.asarray(mat).astype(dt)
     shape = torch.zeros(2, dtype=torch.int64, device=device)
     if _rank() == src:
-        m = np.ascontiguousarray(mat, dtype=np.uint8)
+        m = np.asarray(mat)
+        if m.size and (m.min() < np.iinfo(dt).min or m.max() > np.iinfo(dt).max):
+            raise ValueError(f"broadcast_matrix: values outside {dt}")
+        m = np.ascontiguousarray(m.astype(dt))
         shape[0], shape[1] = m.shape
     dist.broadcast(shape, src)
     rows, cols = int(shape[0]), int(shape[1])
-    buf = torch.empty((rows, cols), dtype=torch.uint8, device=device)
+    buf = torch.empty((rows, cols), dtype=_BCAST_DTYPES[dt], device=device)
     if _rank() == src:
         buf.copy_(torch.from_numpy(m))
     dist.broadcast(buf, src)
@@ -244,13 +275,20 @@ class DistributedRS:
 
     Rank 0 owns the coding matrix and broadcasts it, so every rank encodes with bit-identical
     tables even if ranks were configured differently (the reference regenerates E per device).
+    ``field`` as :class:`~gpu_rscode_amd.models.ReedSolomon`: ``"gf256"`` (the reference's bytes),
+    ``"gf65536"`` (16-bit symbols, n <= 65535, ``src/galoisfield.cu:22-32``; shards then hold whole
+    symbols — the 4 KiB shard alignment is even) or ``"gf16"``. Matrices and survivor ids travel as
+    int32 for every field wider than a byte.
     """
 
-    def __init__(self, k: int, n: int, ctx: DistContext, matrix: str = "vandermonde"):
+    def __init__(self, k: int, n: int, ctx: DistContext, matrix: str = "vandermonde", field: str = "gf256"):
         self.ctx = ctx
-        self.rs = ReedSolomon(k, n, matrix=matrix)
-        self.rs.E = broadcast_matrix(self.rs.E if ctx.is_root else None, ctx.device)
-        self.rs.G = np.vstack([np.eye(k, dtype=np.uint8), self.rs.E])
+        self.rs = ReedSolomon(k, n, matrix=matrix, field=field)
+        self.field = field
+        dt = self.rs.E.dtype
+        wire = np.int32 if dt.itemsize > 1 else np.uint8
+        self.rs.E = broadcast_matrix(self.rs.E if ctx.is_root else None, ctx.device, dtype=wire).astype(dt)
+        self.rs.G = np.vstack([np.eye(k, dtype=dt), self.rs.E])
         self.k, self.n, self.p = k, n, n - k
 
     def encode_local(self, data_shard, parity_shard=None):
@@ -270,8 +308,8 @@ class DistributedRS:
 
     def decode_global(self, survivors: torch.Tensor | None, rows, ncols: int) -> torch.Tensor | None:
         """Rank 0's k survivor rows (chunk ids ``rows``) -> natives [k, C] on rank 0."""
-        rows = [int(r) for r in broadcast_matrix(np.asarray([rows], dtype=np.uint8) if self.ctx.is_root else None,
-                                                 self.ctx.device)[0]]
+        rows = [int(r) for r in broadcast_matrix(np.asarray([rows]) if self.ctx.is_root else None,
+                                                 self.ctx.device, dtype=np.int32)[0]]
         shard = scatter_columns(survivors, self.k, ncols, self.ctx.device)
         out = self.decode_local(shard, rows)
         if self.ctx.device.type == "cuda":

@@ -45,8 +45,9 @@ def _parser() -> argparse.ArgumentParser:
     ap.add_argument("--threads", type=int, default=1, help="CPU backend threads")
     ap.add_argument("--mul", default="simd", help="CPU multiply strategy (row: the scalar product-row form)")
     ap.add_argument("--dist", action="store_true", help="torch.distributed multi-GPU mode (torchrun)")
-    ap.add_argument("--pg-timeout", type=float, default=float(os.environ.get("GFRS_PG_TIMEOUT_S", 300)),
-                    help="--dist: process-group timeout in seconds (a lost peer ends the job after at most this)")
+    ap.add_argument("--pg-timeout", type=float, default=None,
+                    help="--dist: process-group timeout in seconds (a lost peer ends the job after at most this; "
+                         "default GFRS_PG_TIMEOUT_S or 300, parallel.dist.default_pg_timeout)")
     ap.add_argument("--window", type=int, default=None,
                     help="bounded-memory streaming codec: column windows of this many bytes per chunk "
                          "(0 = auto), checkpointed to <target>.PROGRESS and resumable")
@@ -54,6 +55,9 @@ def _parser() -> argparse.ArgumentParser:
     ap.add_argument("--no-sync", action="store_true", help="with --window: no fdatasync before checkpoints")
     ap.add_argument("-q", action="store_true", dest="quiet")
     ap.add_argument("--json", action="store_true", help="--dist: rank 0 prints a JSON line of the job's codec time")
+    # testing: a shard stops after this many windows (a simulated crash; the job fails and a re-run resumes)
+    ap.add_argument("--stop-after", type=int, default=-1, help=argparse.SUPPRESS)
+    ap.add_argument("--stop-rank", type=int, default=-1, help=argparse.SUPPRESS)
     return ap
 
 
@@ -116,14 +120,50 @@ def main(argv=None) -> int:
 
 
 # ---- distributed mode -------------------------------------------------------------------------
-def _create(path: str, size: int) -> None:
-    """Create (or truncate) ``path`` and size it: shards then write their columns in place, so no
-    stale bytes of an older, longer file survive."""
-    fd = os.open(path, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644)
+def _size_file(path: str, size: int) -> None:
+    """Create ``path`` if missing and set its size to exactly ``size`` (shards then write their
+    columns in place; an older, longer file loses its stale tail). Never truncated to zero first:
+    the columns a resumed shard checkpointed before a crash are still in it, and every column no
+    checkpoint covers is rewritten by its shard."""
+    fd = os.open(path, os.O_WRONLY | os.O_CREAT, 0o644)
     try:
         os.ftruncate(fd, size)
     finally:
         os.close(fd)
+
+
+def _shard_checkpoints(target: str, C: int, world: int) -> list[str]:
+    from .._native import cpu
+    from ..parallel.dist import shard_range
+
+    return [cpu().shard_progress_path(target, *shard_range(C, world, r)) for r in range(world)]
+
+
+def _prune_checkpoints(target: str, keep: list[str]) -> None:
+    """Rank 0, before any shard starts: remove every ``<target>.PROGRESS.*`` that is not one of this
+    job's shard checkpoints (another world size or chunk size, an interrupted temp file), so no stale
+    checkpoint can ever be matched later."""
+    from .._native import cpu
+
+    prefix = os.path.basename(cpu().progress_path(target)) + "."
+    d = os.path.dirname(os.path.abspath(target))
+    keep_names = {os.path.basename(x) for x in keep}
+    for name in os.listdir(d):
+        if name.startswith(prefix) and name not in keep_names:
+            try:
+                os.unlink(os.path.join(d, name))
+            except FileNotFoundError:
+                pass
+
+
+def _interrupted(a, rank: int, r: dict) -> None:
+    if not r["complete"]:
+        raise RuntimeError(f"shard stopped after {r['windows']} window(s) (--stop-after {a.stop_after}); "
+                           "its checkpoint resumes it")
+
+
+def _stop_after(a, rank: int) -> int:
+    return a.stop_after if a.stop_after >= 0 and a.stop_rank in (-1, rank) else -1
 
 
 def _main_dist(a) -> int:
@@ -146,9 +186,9 @@ def _main_dist(a) -> int:
     fails (gloo) or is aborted by the process group's bounded timeout (``--pg-timeout``), and torchrun
     ends the job."""
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # (before the first HIP call: RCCL peers)
-    from ..parallel.dist import init_distributed
+    from ..parallel.dist import default_pg_timeout, init_distributed
 
-    ctx = init_distributed(timeout_s=a.pg_timeout)
+    ctx = init_distributed(timeout_s=default_pg_timeout() if a.pg_timeout is None else a.pg_timeout)
     try:
         rc = _dist_run(a, ctx)
     except Exception as ex:  # noqa: BLE001 — this rank stops here, without another collective
@@ -194,19 +234,28 @@ def _dist_run(a, ctx) -> int:
         # under the output creation, the barrier and the first window's reads (as bin/RS overlaps it)
         prep = (hip().prepare_encode_async(path, k, p, [ctx.local_rank], a.streams, a.slice, a.grid, a.field_w,
                                            a.zero_copy, a.window or 0) if on_gpu else None)
+        # Commit protocol (a crash anywhere leaves either no METADATA or a complete stripe, and a
+        # re-run resumes): rank 0 removes an older METADATA, keeps this layout's shard checkpoints
+        # (unless --no-resume) and sizes the chunks without truncating them; every shard resumes from
+        # its own checkpoint; rank 0 commits the METADATA atomically; only then do the shards drop
+        # their checkpoints.
+        ckpts = _shard_checkpoints(path, C, world)
         if ctx.is_root:
+            ff.remove_file(ff.metadata_path(path))
+            _prune_checkpoints(path, [] if a.no_resume else ckpts)
             for i in range(n):
-                _create(ff.chunk_path(path, i), C)
+                _size_file(ff.chunk_path(path, i), C)
         barrier()
         if fault is not None and int(fault) == rank:
             raise RuntimeError("injected fault (GFRS_DIST_FAULT_RANK)")
         lo, hi = shard_range(C, world, rank)
-        kw = dict(st, field_w=a.field_w, col_lo=lo, col_hi=hi, shard=True)
+        kw = dict(st, field_w=a.field_w, col_lo=lo, col_hi=hi, shard=True, stop_after=_stop_after(a, rank))
         if on_gpu:
             r = hip().encode_file_stream(path, k, p, a.matrix, a.cpu_meta, [ctx.local_rank], a.streams, a.slice,
                                          a.grid, zero_copy=a.zero_copy, prep=prep, **kw)
         else:
             r = cpu().encode_file_stream(path, k, p, a.matrix, a.cpu_meta, a.mul, a.threads, **kw)
+        _interrupted(a, rank, r)
         # every rank's shard CRCs (and width) to rank 0, combined in column order
         mine = torch.tensor([hi - lo] + list(r["crc"]), dtype=torch.int64, device=ctx.device)
         parts = [torch.zeros_like(mine) for _ in range(world)] if world > 1 else [mine]
@@ -221,6 +270,7 @@ def _dist_run(a, ctx) -> int:
             ff.write_metadata(ff.metadata_path(path), total, p, k, e, with_matrix=not a.cpu_meta,
                               crc=None if a.cpu_meta else crc, w=a.field_w)
         barrier()
+        ff.remove_file(ckpts[rank], durable=not a.no_sync)  # (the METADATA is committed)
         _say(a, f"[rank {rank}] encoded columns [{lo}, {hi}) of {C} in {r['windows']} window(s) of {r['window']} B "
                 f"in {1e3 * (time.perf_counter() - t0):.1f}ms (read {r['ms_read']:.1f}, GEMM {r['ms_compute']:.1f}, "
                 f"write {r['ms_write']:.1f} ms, overlapped)")
@@ -235,39 +285,51 @@ def _dist_run(a, ctx) -> int:
     prep = (hip().prepare_decode_async(a.in_file, [ctx.local_rank], a.streams, a.slice, a.grid, a.zero_copy,
                                        a.window or 0) if on_gpu else None)
     lo, hi = shard_range(C, world, rank)
-    # the survivor check, split over the ranks: each reads and CRCs only its column shard of every
-    # conf candidate; rank 0 combines the CRCs in column order, compares them with the METADATA and
-    # picks (one rank: the whole check in-process)
-    shard = None
-    if world > 1:
-        n = md.k + md.p
-        rows_h = [[1, 0, 0]] + [[0, 0, 0]] * n  # row 0: status, candidate count, shard width
-        try:
-            got = cpu().shard_crcs(a.in_file, a.conf, lo, hi)
-            rows_h[0] = [0, len(got), hi - lo]
-            for i, (idx, present, crc) in enumerate(got[:n]):
-                rows_h[1 + i] = [idx, int(present), crc]
-        except Exception:  # noqa: BLE001 — rank 0 reports (it hits the same conf / METADATA)
-            rows_h[0][0] = 1
-        shard = torch.tensor(rows_h, dtype=torch.int64).to(ctx.device)
-        parts = [torch.zeros_like(shard) for _ in range(world)]
-        dist.all_gather(parts, shard)
-    # rank 0 picks the survivors; status first: a failure there stops every rank
+    # The survivor check, split over the ranks: each reads and CRCs only its column shard of the
+    # conf candidates; rank 0 combines the CRCs in column order, compares them with the METADATA and
+    # picks (one rank: the whole check in-process). Round 1 reads the first k candidates only (all
+    # a clean decode needs, as the single-process check); a round 2 over the rest runs only when
+    # rank 0 finds those short of a recoverable set. pick[0]: 0 = chosen, 1 = failed, 2 = read more.
+    ckpts = _shard_checkpoints(dst, C, world)
     pick = torch.zeros(md.k + 1, dtype=torch.int64, device=ctx.device)
-    if ctx.is_root:
-        try:
-            if shard is None:
-                rows, _ = cpu().choose_survivors(a.in_file, a.conf)
-            else:
-                rows = cpu().choose_survivors_given(a.in_file, a.conf, _combine_shard_crcs(parts, md))
-            pick[1:] = torch.tensor(rows, dtype=torch.int64)
-        except Exception as ex:  # noqa: BLE001 — told to every rank through the broadcast
-            pick[0] = 1
-            err = ex
-        if not int(pick[0].item()):
-            _create(dst, md.total_size)
-    if world > 1:
-        dist.broadcast(pick, 0)
+    err = None
+    verdicts = None
+    for first, count in ((0, md.k), (md.k, -1)):
+        parts = None
+        if world > 1:
+            n = md.k + md.p
+            rows_h = [[1, 0, 0]] + [[0, 0, 0]] * n  # row 0: status, candidate count, shard width
+            try:
+                got = cpu().shard_crcs(a.in_file, a.conf, lo, hi, first, count)
+                rows_h[0] = [0, len(got), hi - lo]
+                for i, (idx, present, crc) in enumerate(got[:n]):
+                    rows_h[1 + i] = [idx, int(present), crc]
+            except Exception:  # noqa: BLE001 — rank 0 reports (it hits the same conf / METADATA)
+                rows_h[0][0] = 1
+            shard = torch.tensor(rows_h, dtype=torch.int64).to(ctx.device)
+            parts = [torch.zeros_like(shard) for _ in range(world)]
+            dist.all_gather(parts, shard)
+        if ctx.is_root:
+            pick.zero_()
+            try:
+                if parts is None:
+                    rows, _ = cpu().choose_survivors(a.in_file, a.conf)
+                else:
+                    got_v = _combine_shard_crcs(parts, md)
+                    verdicts = got_v if verdicts is None else [x | y for x, y in zip(verdicts, got_v)]
+                    rows = cpu().choose_survivors_given(a.in_file, a.conf, verdicts)
+                pick[1:] = torch.tensor(rows, dtype=torch.int64)
+            except Exception as ex:  # noqa: BLE001 — told to every rank through the broadcast
+                more = parts is not None and first == 0 and verdicts is not None and len(verdicts) > md.k
+                pick[0] = 2 if more else 1
+                err = ex
+            if not int(pick[0].item()):
+                _prune_checkpoints(dst, [] if a.no_resume else ckpts)
+                _size_file(dst, md.total_size)
+        if world > 1:
+            dist.broadcast(pick, 0)
+        if int(pick[0].item()) != 2:
+            break
     if int(pick[0].item()):
         if ctx.is_root:
             raise err
@@ -276,13 +338,15 @@ def _dist_run(a, ctx) -> int:
     barrier()
     if fault is not None and int(fault) == rank:
         raise RuntimeError("injected fault (GFRS_DIST_FAULT_RANK)")
-    kw = dict(st, col_lo=lo, col_hi=hi, shard=True, rows=rows)
+    kw = dict(st, col_lo=lo, col_hi=hi, shard=True, rows=rows, stop_after=_stop_after(a, rank))
     if on_gpu:
         r = hip().decode_file_stream(a.in_file, a.conf, dst, [ctx.local_rank], a.streams, a.slice, a.grid,
                                      zero_copy=a.zero_copy, prep=prep, **kw)
     else:
         r = cpu().decode_file_stream(a.in_file, a.conf, dst, a.mul, a.threads, **kw)
+    _interrupted(a, rank, r)
     barrier()
+    ff.remove_file(ckpts[rank], durable=not a.no_sync)  # (every shard of the output is written)
     _say(a, f"[rank {rank}] decoded columns [{lo}, {hi}) of {C} ({r['erased']} erased native(s)) in "
             f"{r['windows']} window(s) of {r['window']} B in {1e3 * (time.perf_counter() - t0):.1f}ms")
     _dist_summary(a, ctx, "decode", md.total_size, t0)

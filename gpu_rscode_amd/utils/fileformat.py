@@ -80,8 +80,50 @@ def write_metadata(path: str, total_size: int, p: int, k: int, e: np.ndarray | N
             lines.append("".join(f"{int(v)} " for v in np.asarray(e)[i]) + "\n")
         if crc:
             lines.append("crc32" + "".join(f" {int(c):08x}" for c in crc) + "\n")
-    with open(path, "w") as f:
-        f.writelines(lines)
+    commit_file(path, "".join(lines).encode())
+
+
+def _fsync_dir(path: str) -> None:
+    try:
+        fd = os.open(os.path.dirname(os.path.abspath(path)), os.O_RDONLY | os.O_DIRECTORY)
+    except OSError:
+        return
+    try:
+        os.fsync(fd)
+    finally:
+        os.close(fd)
+
+
+def commit_file(path: str, data: bytes, durable: bool = True) -> None:
+    """Durable, atomic replacement of a small file (the C++ ``gfrs::commit_file``): ``path.gfrs-tmp``
+    written and fsync'ed, renamed over ``path``, the directory fsync'ed. A failed write (ENOSPC,
+    EFBIG) raises and leaves ``path`` as it was — a METADATA exists only once complete."""
+    tmp = path + ".gfrs-tmp"
+    fd = os.open(tmp, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644)
+    try:
+        view = memoryview(data)
+        while view:
+            view = view[os.write(fd, view):]
+        if durable:
+            os.fsync(fd)
+    except BaseException:
+        os.close(fd)
+        os.unlink(tmp)
+        raise
+    os.close(fd)
+    os.replace(tmp, path)
+    if durable:
+        _fsync_dir(path)
+
+
+def remove_file(path: str, durable: bool = True) -> None:
+    """Unlink ``path`` (missing is fine) and, durable, fsync its directory."""
+    try:
+        os.unlink(path)
+    except FileNotFoundError:
+        return
+    if durable:
+        _fsync_dir(path)
 
 
 def read_metadata(path: str) -> Metadata:
@@ -121,8 +163,7 @@ def read_conf(path: str) -> list[str]:
 
 
 def write_conf(path: str, names) -> None:
-    with open(path, "w") as f:
-        f.writelines(f"{n}\n" for n in names)
+    commit_file(path, "".join(f"{n}\n" for n in names).encode(), durable=False)
 
 
 def worst_case_conf(file: str, n: int, k: int) -> list[str]:

@@ -185,3 +185,103 @@ def test_torchrun_dist_cli_rank_failure_exits_in_bounded_time(tmp_path):
     t0 = time.monotonic()
     r = subprocess.run(dcmd, cwd=tmp_path, capture_output=True, text=True, timeout=240, env=env)
     assert r.returncode != 0 and "injected fault" in r.stderr and time.monotonic() - t0 < 120, r.stderr[-3000:]
+
+
+@pytest.mark.parametrize("stop_rank", [0, 1])
+def test_torchrun_dist_cli_resumes_after_a_shard_crash(tmp_path, stop_rank):
+    """A --dist job whose rank `stop_rank` stops after one window (--stop-after: a simulated crash)
+    fails without a METADATA; the re-run keeps the chunk files (no truncation), resumes the stopped
+    shard from its checkpoint and every finished shard at its end, and the stripe comes out
+    byte-exact, with every checkpoint gone. The same for a decode into an output file. (Round 5's
+    rank 0 re-created the outputs zero-filled, so the columns a shard had checkpointed became zeros.)"""
+    payload = os.urandom(4 * 4096 * 10 + 999)
+    d1, d2 = tmp_path / "dist", tmp_path / "single"
+    d1.mkdir()
+    d2.mkdir()
+    (d1 / "f.bin").write_bytes(payload)
+    (d2 / "f.bin").write_bytes(payload)
+    env = dict(os.environ, PYTHONPATH=ROOT, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+
+    def job(args):
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+               "--master-addr=127.0.0.1", f"--master-port={_port()}", "-m", "gpu_rscode_amd", "--dist",
+               "--window", "4096", "--pg-timeout", "60", *args]
+        return subprocess.run(cmd, cwd=d1, capture_output=True, text=True, timeout=300, env=env)
+
+    enc = ["-k", "10", "-n", "14", "-e", "f.bin"]
+    r = job(enc + ["--stop-after", "1", "--stop-rank", str(stop_rank)])
+    assert r.returncode != 0 and "--stop-after" in r.stderr, r.stderr[-3000:]
+    assert not (d1 / "f.bin.METADATA").exists()
+    assert any(x.startswith("f.bin.PROGRESS.") for x in os.listdir(d1))
+    r = job(enc)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert _py(enc + ["--backend", "cpu"], d2).returncode == 0
+    for name in [f"_{i}_f.bin" for i in range(14)] + ["f.bin.METADATA"]:
+        assert (d1 / name).read_bytes() == (d2 / name).read_bytes(), name
+    assert not [x for x in os.listdir(d1) if ".PROGRESS" in x]
+
+    ff.write_conf(str(d1 / "conf"), [f"_{i}_f.bin" for i in (0, 2, 3, 4, 6, 7, 10, 11, 12, 13)])
+    dec = ["-d", "-i", "f.bin", "-c", "conf", "-o", "o.bin"]
+    r = job(dec + ["--stop-after", "1", "--stop-rank", str(stop_rank)])
+    assert r.returncode != 0, r.stderr[-3000:]
+    r = job(dec)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert (d1 / "o.bin").read_bytes() == payload
+    assert not [x for x in os.listdir(d1) if ".PROGRESS" in x]
+
+
+def test_dist_ipc_env_is_set_before_torch_distributed(tmp_path):
+    """`python -m gpu_rscode_amd --dist` reaches torch.distributed with HSA_ENABLE_IPC_MODE_LEGACY=0
+    already in the environment (the HIP runtime reads it once, at initialisation), even when the
+    caller's environment lacks it: the package sets it before its own `import torch`."""
+    probe = ("import os, sys\n"
+             "import torch.distributed as d\n"
+             "seen = []\n"
+             "orig = d.init_process_group\n"
+             "def spy(*a, **k):\n"
+             "    seen.append(os.environ.get('HSA_ENABLE_IPC_MODE_LEGACY'))\n"
+             "    raise SystemExit(7 if seen[0] == '0' else 8)\n"
+             "d.init_process_group = spy\n"
+             "from gpu_rscode_amd.utils.cli import main\n"
+             "main(['--dist', '-k', '2', '-n', '3', '-e', 'f.bin'])\n")
+    env = {k: v for k, v in os.environ.items() if k != "HSA_ENABLE_IPC_MODE_LEGACY"}
+    env.update(PYTHONPATH=ROOT, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+               MASTER_PORT=str(_port()), CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    (tmp_path / "f.bin").write_bytes(b"x" * 100)
+    r = subprocess.run([sys.executable, "-c", probe], cwd=tmp_path, capture_output=True, text=True, timeout=120,
+                       env=env)
+    assert r.returncode == 7, (r.returncode, r.stderr[-2000:])
+    # the package sets it before ITS first `import torch` (torch's HIP runtime may initialise from then on)
+    order = ("import builtins, os, sys\n"
+             "real = builtins.__import__\n"
+             "seen = []\n"
+             "def imp(name, *a, **k):\n"
+             "    if name == 'torch' and not seen:\n"
+             "        seen.append(os.environ.get('HSA_ENABLE_IPC_MODE_LEGACY'))\n"
+             "    return real(name, *a, **k)\n"
+             "builtins.__import__ = imp\n"
+             "import gpu_rscode_amd\n"
+             "sys.exit(0 if seen == ['0'] else 9)\n")
+    r = subprocess.run([sys.executable, "-c", order], cwd=tmp_path, capture_output=True, text=True, timeout=120,
+                       env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    # and a process whose HIP is already up without it is refused an RCCL group (not a late failure)
+    from gpu_rscode_amd.parallel import dist as pdist
+
+    saved = os.environ.pop("HSA_ENABLE_IPC_MODE_LEGACY", None)
+    try:
+        import torch
+
+        orig = torch.cuda.is_initialized
+        torch.cuda.is_initialized = lambda: True
+        try:
+            with pytest.raises(RuntimeError, match="HSA_ENABLE_IPC_MODE_LEGACY"):
+                pdist.ensure_ipc_env("nccl")
+        finally:
+            torch.cuda.is_initialized = orig
+        pdist.ensure_ipc_env("gloo")  # (gloo needs no IPC)
+        pdist.ensure_ipc_env("nccl")  # HIP not up: set in time
+        assert os.environ["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+    finally:
+        if saved is not None:
+            os.environ["HSA_ENABLE_IPC_MODE_LEGACY"] = saved

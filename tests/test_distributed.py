@@ -81,6 +81,33 @@ def _case_distributed_codec(ctx):
         assert torch.equal(out, data)
 
 
+def _case_distributed_codec16(ctx):
+    """GF(2^16) over the process group: E broadcast as int32 (16-bit symbols), survivor ids > 255
+    broadcast as int32 (a byte broadcast would wrap 256..269 to 0..13 and decode garbage), shards of
+    whole symbols; bit-exact against the single-process codec."""
+    from gpu_rscode_amd.models import ReedSolomon
+
+    k, n, C = 250, 270, 3 * 4096 + 78  # C even: whole 16-bit symbols
+    drs = pdist.DistributedRS(k, n, ctx, field="gf65536")
+    ref = ReedSolomon(k, n, field="gf65536")
+    assert drs.rs.E.dtype == np.uint16 and np.array_equal(drs.rs.E, ref.E)
+    data = torch.from_numpy(np.random.default_rng(1).integers(0, 256, size=(k, C), dtype=np.uint8))
+    parity = drs.encode_global(data if ctx.rank == 0 else None, C)
+    if ctx.rank == 0:
+        want = torch.zeros((n - k, C), dtype=torch.uint8)
+        ref.encode(data, want)
+        assert torch.equal(parity, want)
+        stripe = torch.cat([data, parity])
+        rows = list(range(20, k)) + list(range(k, n))  # natives 0..19 erased: parity ids 250..269 used
+        assert max(rows) > 255
+        surv = stripe[rows]
+    else:
+        rows, surv = None, None
+    out = drs.decode_global(surv, rows, C)
+    if ctx.rank == 0:
+        assert torch.equal(out, data)
+
+
 def _case_parity_exchange(ctx):
     """ParityExchange delivers exactly the senders' bytes: owners = piece `rank` of every rank's
     block, in source order; root = every peer's whole block on rank 0. Two alternating slots, each
@@ -180,6 +207,20 @@ def test_distributed_world2(case):
 
 def test_distributed_codec_world3():
     _run("_case_distributed_codec", 3)
+
+
+def test_distributed_codec_gf65536_world3():
+    _run("_case_distributed_codec16", 3)
+
+
+def _case_broadcast_wide(ctx):
+    ids = np.array([[0, 255, 256, 4095, 65534]]) if ctx.rank == 0 else None
+    got = pdist.broadcast_matrix(ids, ctx.device, dtype=np.int32)
+    assert got.dtype == np.int32 and got.tolist() == [[0, 255, 256, 4095, 65534]]
+
+
+def test_broadcast_int32_world2():
+    _run("_case_broadcast_wide", 2)
 
 
 def test_parity_exchange_world3():
