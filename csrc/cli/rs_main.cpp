@@ -14,6 +14,7 @@
 #include <string>
 
 #include "cli_common.h"
+#include "gfrs/tune.h"
 #include "gfrs/async_prepare.h"
 #include "gfrs/codec_file.h"
 #include "gfrs/format.h"
@@ -88,9 +89,9 @@ int main(int argc, char** argv) {
     opt.field_w = enc ? a.field_w : 8;  // (decode: the field comes from the METADATA)
     std::unique_ptr<AsyncPrepare> prep = enc ? prepare_for_encode(devices, opt, a.in_file, a.k, a.n - a.k, sop)
                                              : prepare_for_decode(devices, opt, a.in_file, sop);
-    // GFRS_SETUP=serial (measurement aid): finish the device setup before the host buffers are
+    // GFRS_TUNE=setup=serial (measurement aid): finish the device setup before the host buffers are
     // allocated and the file is read, so each phase's uncontended cost shows
-    if (prep && std::getenv("GFRS_SETUP") && std::string(std::getenv("GFRS_SETUP")) == "serial") {
+    if (prep && gfrs::tune_str("setup") == "serial") {
       const double ms = prep->wait();
       if (!a.quiet) {
         std::printf("GPU pipeline setup (serial): %fms\n", ms);

@@ -7,6 +7,7 @@
 // thread and guarded by a mutex. Lookups after the first are a map probe under an uncontended lock.
 #pragma once
 
+#include "gfrs/tune.h"
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -52,16 +53,13 @@ inline int device_cu_count() {
 
 // Chunk slots of a persistent FP4 grid (blocks = slots x groups). With several M-groups a slot's
 // blocks must share an XCD, so slots are a multiple of 8. With one group every block owns its chunk
-// stream outright and the slot count is free: the grid then leaves GFRS_FP4_FREE_CUS compute units
+// stream outright and the slot count is free: the grid then leaves GFRS_TUNE=fp4_free_cus=N compute units
 // (default 0) without a block, so a one-workgroup side kernel — the decode-system solve of the next
 // step — finds an empty CU instead of holding one of the GEMM's blocks back (a persistent GEMM with
 // one block per CU ends when its last block does: a 50 us solve in front of one block delays the
 // whole kernel by 50 us).
 inline int64_t persistent_slots(int occ, int groups, int64_t nchunks) {
-  static const int free_cus = [] {
-    const char* e = std::getenv("GFRS_FP4_FREE_CUS");
-    return e ? std::max(0, std::atoi(e)) : 0;
-  }();
+  static const int free_cus = int(std::max<int64_t>(0, tune_int("fp4_free_cus", 0)));
   const int64_t full = int64_t(device_cu_count()) * occ / groups;
   if (groups == 1 && free_cus > 0) {
     const int64_t s = std::max<int64_t>(1, full - free_cus);

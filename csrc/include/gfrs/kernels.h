@@ -105,6 +105,9 @@ size_t mfma_bitmat_bytes(int k, int m);
 hipError_t launch_gf_gemm_fp4(const void* bitmat, const void* desc, int k, int m, int64_t col0,
                               int64_t ncols, int mg_cap, int64_t in_stride, bool copies, hipStream_t stream);
 size_t fp4_bitmat_bytes(int k, int m, int mg_cap);
+// the form launch_gf_gemm_fp4 runs for (k, m, copies): "v1", "ar" or "tm" (fp4_route,
+// gf_mfma_fp4.hip, documents each choice with its measurement)
+const char* fp4_route_name(int k, int m, bool copies, int mg_cap);
 // Batched form (small-object serving): `batch` stripes of identical shape whose rows sit at fixed
 // strides — stripe b's input rows are stripe 0's + b * in_bstride, its output and copy rows stripe
 // 0's + b * out_bstride (desc built with desc_layout(k, m_pad, batch); the kernel reads stripe 0's
@@ -139,19 +142,6 @@ hipError_t launch_gf_gemm16_fp4_batched(const void* bitmat, const void* desc, in
 size_t fp16_bitmat_bytes(int k, int m, int mg_cap);
 // coefficient (o, i) = coeff[row(o) * ld + i] (uint16, device), row(o) = sel ? sel[o] : o
 hipError_t launch_fp16_bitmat(const uint16_t* coeff, int ld, const int* sel, int m, int k, void* bitmat, int mg_cap,
-                              hipStream_t stream);
-
-// ---- GF(2^8) on the FP4 matrix cores, register-streamed (csrc/kernels/gf_mfma8r.hip) -----------
-// desc: a desc_layout descriptor; bitmat from launch_fp4r_bitmat with the same (k, m). Rows 2-byte
-// aligned, col0 even; ragged tails on the matrix cores too. copies: fused survivor copy (decode);
-// in_stride as launch_gf_gemm_fp4.
-// mg: M-tiles per block (1..4), fixed per plan (the bit-matrix layout depends on it).
-hipError_t launch_gf_gemm_fp4r(const void* bitmat, const void* desc, int k, int m, int64_t col0, int64_t ncols,
-                               int mg, int64_t in_stride, bool copies, hipStream_t stream);
-int fp4r_choose_mg(int k, int m);  // GFRS_FP4R_MG, else the widest grouping without padded tiles
-size_t fp4r_bitmat_bytes(int k, int m, int mg);
-// coefficient (o, i) = coeff[row(o) * ld + i] (device bytes), row(o) = sel ? sel[o] : o
-hipError_t launch_fp4r_bitmat(const uint8_t* coeff, int ld, const int* sel, int m, int k, void* bitmat, int mg,
                               hipStream_t stream);
 
 // FP4 kernels: the bit-matrix allocation ends with a write-only sink of kFp4SinkSlots 1-KiB slots;

@@ -1,6 +1,7 @@
 // File formats (see gfrs/format.h). 64-bit sizes throughout; tails zero-padded (the reference's GPU
 // encoder leaves padding uninitialised, src/encode.cu:325).
 #include "gfrs/format.h"
+#include "gfrs/tune.h"
 
 #include <fcntl.h>
 #include <sys/stat.h>
@@ -146,8 +147,7 @@ GFRS_CLMUL uint32_t crc32_clmul(const uint8_t* buf, int64_t len, uint32_t state)
 
 bool have_clmul() {
   static const bool v = [] {
-    if (const char* e = std::getenv("GFRS_CRC_SCALAR"))  // (tests: the table path on the same machine)
-      if (std::atoi(e) == 1) return false;
+    if (tune_str("crc") == "scalar") return false;  // (tests: the table path on the same machine)
     __builtin_cpu_init();
     return __builtin_cpu_supports("pclmul") && __builtin_cpu_supports("sse4.1");
   }();

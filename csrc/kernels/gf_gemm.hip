@@ -30,6 +30,7 @@
 
 #include "gfrs/desc.h"
 #include "gfrs/kernels.h"
+#include "gfrs/tune.h"
 #include "gfrs/perm_device.h"
 
 namespace gfrs {
@@ -563,39 +564,30 @@ struct Cfg {
 // the rows kernel: 2^22 groups = 64 MiB of every row. Measured (profiles/serving/r07_serve):
 // every serving batch up to 256 x 1 MiB objects encodes 15-30 % faster with it (256 x 64 KiB
 // 20.6 vs 28.0 us, 256 x 1 MiB 67 vs 96 us); the 1 GiB headline stripe (6.7 M groups) keeps the
-// throughput form for its two-lane overlap. GFRS_ROWS_LAT_GROUPS overrides (0 = never).
+// throughput form for its two-lane overlap. GFRS_TUNE=rows_lat_groups=N overrides (0 = never).
 int64_t rows_lat_groups() {
-  static const int64_t v = [] {
-    const char* e = std::getenv("GFRS_ROWS_LAT_GROUPS");
-    return e ? std::max<int64_t>(0, std::atoll(e)) : int64_t(1) << 22;
-  }();
+  static const int64_t v = std::max<int64_t>(0, tune_int("rows_lat_groups", int64_t(1) << 22));
   return v;
 }
 
 // Lane target of a wide-code launch (output tile of 8+ rows) that the k-split kernel does not
-// take, before its tile is narrowed; GFRS_SHORT_LANES sets it (default 0 = never narrow: the
-// k-split kernel beat every narrowed tile on the short-row points, profiles/serving/r07_wide).
+// take, before its tile is narrowed; GFRS_TUNE=short_lanes=N sets it (default 0 = never narrow:
+// the k-split kernel beat every narrowed tile on the short-row points, profiles/serving/r07_wide).
 int64_t short_lanes() {
-  static const int64_t v = [] {
-    const char* e = std::getenv("GFRS_SHORT_LANES");
-    return e ? std::max<int64_t>(0, std::atoll(e)) : int64_t(0);
-  }();
+  static const int64_t v = std::max<int64_t>(0, tune_int("short_lanes", 0));
   return v;
 }
 
 // Launches whose lanes (16-byte groups x stripes x output tiles at the widest tile) number fewer
 // than this take the k-split kernel when 32 <= k <= 256 (its LDS holds 256 rows of tables);
-// GFRS_KSPLIT_LANES overrides (0 = never).
+// GFRS_TUNE=ksplit_lanes=N overrides (0 = never).
 // Measured with scripts/serve_bench.py --code (profiles/serving/r07_wide/xcd): the k-split kernel
 // wins every point up to 65 K lanes (RS(128,160) 16 x 64 KiB encode 294 -> 23 us, 16 x 1 MiB
 // 263 -> 51 us; RS(64,80) 16 x 4 MiB 141 -> 88 us; RS(32,40) 16 x 1 MiB 33 -> 18 us) and the vec
 // kernel every point from 131 K (RS(128,160) 256 x 1 MiB 432 vs 738 us; RS(32,40) 256 x 256 KiB
 // 41 vs 51 us).
 int64_t ksplit_lanes() {
-  static const int64_t v = [] {
-    const char* e = std::getenv("GFRS_KSPLIT_LANES");
-    return e ? std::max<int64_t>(0, std::atoll(e)) : int64_t(1) << 17;
-  }();
+  static const int64_t v = std::max<int64_t>(0, tune_int("ksplit_lanes", int64_t(1) << 17));
   return v;
 }
 
@@ -697,21 +689,21 @@ hipError_t launch_vec(const DescView& d, int k, int m_pad, int batch, int64_t co
 // (profiles/r01_kbench/kbench.json): non-temporal streaming with two rows in flight wins on every
 // HBM-bound shape (k=10 encode 5.6 TB/s, 4-erasure decode 5.8 TB/s); the VALU-bound wide tile
 // (MT = 16) prefers two 16-byte groups per lane to amortise the per-row table moves.
-// GFRS_VEC_CFG="V,PF,NT" (e.g. "1,4,1") replaces the default for every vector-kernel launch
+// GFRS_TUNE=vec_cfg=V:PF:NT (e.g. 1:4:1) replaces the default for every vector-kernel launch
 // without an explicit variant (in the k=10 step: the decode; A/B measurements)
 Cfg default_cfg(int mt) {
   static const int env[3] = {[] {
-    const char* e = std::getenv("GFRS_VEC_CFG");
-    return e ? std::atoi(e) : 0;
+    const std::string v = tune_str("vec_cfg");
+    return v.empty() ? 0 : std::atoi(v.c_str());
   }(), [] {
-    const char* e = std::getenv("GFRS_VEC_CFG");
-    const char* c = e ? std::strchr(e, ',') : nullptr;
-    return c ? std::atoi(c + 1) : 0;
+    const std::string v = tune_str("vec_cfg");
+    const size_t c = v.find(':');
+    return c == std::string::npos ? 0 : std::atoi(v.c_str() + c + 1);
   }(), [] {
-    const char* e = std::getenv("GFRS_VEC_CFG");
-    const char* c = e ? std::strchr(e, ',') : nullptr;
-    c = c ? std::strchr(c + 1, ',') : nullptr;
-    return c ? std::atoi(c + 1) : 1;
+    const std::string v = tune_str("vec_cfg");
+    const size_t c = v.find(':');
+    const size_t d = c == std::string::npos ? c : v.find(':', c + 1);
+    return d == std::string::npos ? 1 : std::atoi(v.c_str() + d + 1);
   }()};
   Cfg c;
   c.vec = mt >= 16 ? 2 : 1;

@@ -28,6 +28,7 @@
 
 #include "gfrs/desc.h"
 #include "gfrs/kernels.h"
+#include "gfrs/tune.h"
 #include "gfrs/perm_device.h"
 
 namespace gfrs {
@@ -237,13 +238,10 @@ inline Grid make_grid(int64_t items, int ntiles, int max_blocks) {
   return g;
 }
 
-// 16-byte groups per lane of the vector kernel where it may take two (GFRS_GF16_VEC_G=1: always one,
-// for A/B measurements)
+// 16-byte groups per lane of the vector kernel where it may take two (GFRS_TUNE=gf16_vec_g=1: always
+// one, for A/B measurements)
 int vec_groups() {
-  static const int v = [] {
-    const char* e = std::getenv("GFRS_GF16_VEC_G");
-    return e && std::atoi(e) == 1 ? 1 : 2;
-  }();
+  static const int v = tune_int("gf16_vec_g", 2) == 1 ? 1 : 2;
   return v;
 }
 
@@ -275,14 +273,11 @@ hipError_t launch_gf_gemm16_batched(const void* desc, int k, int m_pad, int batc
   // Short rows: one output per tile. The kernel parallelises over columns and output tiles only,
   // so a row of a few KiB is a handful of blocks each walking all k rows for 8 outputs (k = 300,
   // m = 40, 3.4 KiB: 5 blocks). One output per tile puts m times as many blocks on the chip; the
-  // inputs they re-read are small enough to stay in L2. GFRS_GF16_SHORT_GROUPS sets the cut
+  // inputs they re-read are small enough to stay in L2. GFRS_TUNE=gf16_short_groups=N sets the cut
   // (16-byte groups per row, default 32768 = 512 KiB; 0 = never). Measured (profiles/gf65536/
   // r07_short): k = 300 m = 40, 3.4 KiB rows 1.05 -> 0.24 ms, 218 KiB rows 1.11 -> 0.64 ms;
   // k = 64 m = 16, 256 KiB rows 0.145 -> 0.055 ms; at 1 MiB rows one output per tile loses.
-  static const int64_t short_groups = [] {
-    const char* e = std::getenv("GFRS_GF16_SHORT_GROUPS");
-    return e ? std::max<int64_t>(0, std::atoll(e)) : int64_t(32768);
-  }();
+  static const int64_t short_groups = std::max<int64_t>(0, tune_int("gf16_short_groups", 32768));
   // (a batch fills the chip with its own grid rows: the cut counts the groups of every stripe)
   const int mt_cap = (ncols / 16 * batch < short_groups && !one_tile) ? 1 : 8;
   return dispatch16(m_pad, mt_cap, [&](auto mt) -> hipError_t {

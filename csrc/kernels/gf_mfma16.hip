@@ -40,6 +40,7 @@
 #include "gfrs/desc.h"
 #include "gfrs/device_cache.h"
 #include "gfrs/kernels.h"
+#include "gfrs/tune.h"
 
 namespace gfrs {
 namespace {
@@ -448,12 +449,9 @@ Geo16 geometry16(int k, int m, int mg_cap, bool copy) {
   Geo16 g{};
   g.ksteps = (k + 7) / 8;
   g.mtiles = (m + 3) / 4;
-  // MG in {2, 1} (<= mg_cap): the fewest padded M-tiles, then the wider (GFRS_FP16_MG forces one).
+  // MG in {2, 1} (<= mg_cap): the fewest padded M-tiles, then the wider (GFRS_TUNE=fp16_mg=N forces one).
   // (MG = 4 — 256 accumulator registers beside the unrolled input ring — spilled ~2 KiB per lane.)
-  static const int forced = [] {
-    const char* e = std::getenv("GFRS_FP16_MG");
-    return e ? std::atoi(e) : 0;
-  }();
+  static const int forced = int(tune_int("fp16_mg", 0));
   g.mg = 1;
   for (int cand : {2, 1}) {
     if (cand > mg_cap || (forced && cand != forced)) continue;

@@ -30,6 +30,7 @@
 #include "gfrs/desc.h"
 #include "gfrs/device_cache.h"
 #include "gfrs/kernels.h"
+#include "gfrs/tune.h"
 
 namespace gfrs {
 namespace {
@@ -134,10 +135,11 @@ constexpr int kSlotBytes = 1024;
 // and fused copies with no destination are stored there, so neither the epilogue nor the K loop
 // branches — one basic block the scheduler can interleave (MFMAs and conditional stores in
 // separate blocks serialise). Nothing reads the sink. One 1-KiB slot per wave, spread over
-// kFp4SinkSlots (kernels.h): GFRS_FP4_SINK=1 restores the single shared slot (A/B measurements).
+// kFp4SinkSlots (kernels.h): a single shared slot serialised every CU on its lines (1100 vs 880 us
+// at m = 24, profiles/wide_stripe/r02_fp4_ablate).
 constexpr int kSinkBytes = 1024 * kFp4SinkSlots;
-__device__ __forceinline__ uint64_t sink_slot(uint64_t base, int spread) {
-  const unsigned slot = spread ? (blockIdx.x * 4u + (threadIdx.x >> 6)) % unsigned(kFp4SinkSlots) : 0u;
+__device__ __forceinline__ uint64_t sink_slot(uint64_t base) {
+  const unsigned slot = (blockIdx.x * 4u + (threadIdx.x >> 6)) % unsigned(kFp4SinkSlots);
   return base + uint64_t(slot) * 1024u + 16u * (threadIdx.x & 63u);
 }
 // LDS the launcher tries to leave free next to a persistent block, so a side-stream kernel (the
@@ -177,7 +179,7 @@ template <int MG, bool UNI, bool COPY, int kRing, int KS>
 __global__ __launch_bounds__(256, 1) void gf_gemm_fp4_kernel(cptr<uint64_t> in, cptr<uint64_t> out, cptr<uint64_t> copy,
                                                              const i32x4* __restrict__ bitmat, int k, int m,
                                                              int ksteps, int groups, int64_t col0, int64_t nchunks,
-                                                             int64_t chunk_slots, int64_t in_stride, int sink_spread) {
+                                                             int64_t chunk_slots, int64_t in_stride) {
   constexpr int NTW = kNTW;              // N-tiles (32 columns each) per wave
   constexpr int kWaves = 4, kThreads = 256;
   constexpr int kCW = 32 * NTW;          // columns per wave
@@ -206,7 +208,7 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4_kernel(cptr<uint64_t> in, 
   uint64_t* outptr = rowptr + 256;  // this group's 4*MG output rows
   const i32x4* src = bitmat + size_t(g) * MG * ksteps * 64;
   // this lane's 16 bytes of the sink past the bit-matrix (kSinkBytes)
-  const uint64_t sink = sink_slot(uint64_t(bitmat + size_t(groups) * MG * ksteps * 64), sink_spread);
+  const uint64_t sink = sink_slot(uint64_t(bitmat + size_t(groups) * MG * ksteps * 64));
   for (int i = threadIdx.x; i < MG * ksteps * 64; i += kThreads) afrag[i] = src[i];
   if (!UNI)
     for (int i = threadIdx.x; i < k; i += kThreads) rowptr[i] = in[i];
@@ -518,501 +520,6 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4_kernel(cptr<uint64_t> in, 
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA (dummy or not) outlives the wave
 }
 
-// ---- the tile-staggered form ("sk", k in (112, 128]) -------------------------------------------
-// The kernel above idles its matrix pipe through every chunk epilogue: its 256 accumulators fill
-// the AGPRs, so a chunk cannot start before the 256 accumulator reads, 224 bit-field inserts and
-// 16 bias MFMAs of the previous one are done (65 % MFMA-pipe utilisation at k=128, p=32,
-// profiles/wide_stripe/r02_pmc_fp4). Here the M-tiles run their K loops STAGGERED by one K-step each: at step
-// j of a chunk, M-tile mt works on K-step (j - mt) mod NS (of the previous chunk while mt > j).
-// Tile j therefore finishes its chunk at step j-1 and is packed, stored and re-biased during step
-// j — one tile's epilogue per step over the first MG steps of every chunk, interleaved with the 14
-// MFMAs of the other tiles instead of serialised after all of them. Same registers (one
-// accumulator per tile), same operands: the B operand of K-step s is kept for MG steps in a
-// window bw[s mod MG] (tile MG-1 uses it last), A fragments are read per (tile, K-step).
-// The last real chunk is drained by one phantom chunk (dummy DMAs, results discarded): its first
-// MG steps pack the real chunk's tiles. Every ring position, DMA target and counted wait is a
-// compile-time constant (KS slots per chunk, a multiple of the ring depth R).
-__host__ __device__ constexpr int sk_mod(int a, int n) { return ((a % n) + n) % n; }
-// ushort epilogue stores (2 per packed tile) in chunk-relative steps [s0, s1)
-__host__ __device__ constexpr int sk_stores_in(int s0, int s1, int mg, int ns) {
-  int n = 0;
-  for (int s = s0; s < s1; ++s) n += sk_mod(s, ns) < mg ? 2 : 0;
-  return n;
-}
-// DMA(t) (ring slot t % R) is issued in the second K-step of slot t-R, right after that slot's data
-// has been consumed. vm ops younger than DMA(sp+1) when it is awaited (first step of slot sp): R-2
-// DMAs, the copy stores of slots sp+1-R .. sp-1 (issued at the end of their second step) and the
-// epilogue stores of steps [2 (sp+1-R) + 1, 2 sp) (exact: the prologue issues the stores of the
-// virtual slots before chunk 0 as dummies in the same order)
-__host__ __device__ constexpr int sk_wait_count(int sp, int mg, int ks, int r, bool copy) {
-  const int n = (r - 2) + (copy ? r - 1 : 0) + sk_stores_in(2 * (sp + 1 - r) + 1, 2 * sp, mg, 2 * ks);
-  return n < 63 ? n : 63;
-}
-
-template <typename F, int... I>
-__device__ __forceinline__ void static_for_impl(F& f, std::integer_sequence<int, I...>) {
-  (f(std::integral_constant<int, I>{}), ...);
-}
-template <int N, typename F>
-__device__ __forceinline__ void static_for(F&& f) {
-  static_for_impl(f, std::make_integer_sequence<int, N>{});
-}
-
-// ABL (ablation builds for measurements only, GFRS_FP4_ABL; 0 = the product kernel): bit 0 skips
-// the epilogue's accumulator reads and inserts (stores a constant), bit 1 skips the B expansion
-// masks (raw gathered words as the B operand), bit 2 points every DMA at the block's first chunk
-// (L2-resident input: no HBM latency or bandwidth). Results are wrong for ABL != 0.
-template <int MG, bool UNI, bool COPY, int R, int KS, int ABL = 0>
-__global__ __launch_bounds__(256, 1) void gf_gemm_fp4sk_kernel(cptr<uint64_t> in, cptr<uint64_t> out,
-                                                               cptr<uint64_t> copy, const i32x4* __restrict__ bitmat,
-                                                               int k, int m, int groups, int64_t col0, int64_t nchunks,
-                                                               int64_t chunk_slots, int64_t in_stride, int sink_spread) {
-  constexpr int NTW = kNTW;              // N-tiles (32 columns each) per wave
-  constexpr int kWaves = 4, kThreads = 256;
-  constexpr int kCW = 32 * NTW;          // columns per wave (64)
-  constexpr int kRS = kSlotBytes / kCW;  // input rows per ring slot (16)
-  constexpr int kSPS = kRS / 8;          // K-steps per ring slot (2)
-  constexpr int kLPR = kCW / 16;         // DMA lanes per row (4)
-  constexpr int NS = KS * kSPS;          // K-steps per chunk
-  static_assert(kSPS == 2, "the wait / read pattern below assumes two K-steps per slot");
-  static_assert(KS % R == 0 && NS % MG == 0 && R >= 3, "ring depth must divide the chunk; MG must divide NS");
-  extern __shared__ __attribute__((aligned(16))) i32x4 afrag[];
-  const int bid = blockIdx.x;
-  const int xcd = bid & 7;
-  const int local = bid >> 3;
-  const int g = local % groups;
-  const int64_t slot0 = int64_t(local / groups) * 8 + xcd;
-  if (slot0 >= chunk_slots) return;
-
-  // LDS: A [NS][MG][64] x 16 B | row pointers [256] | out pointers [32] | (COPY) copy pointers
-  // [256] | rings [kWaves][R][1 KiB] | one spare slot shared by the waves' dummy DMAs
-  const size_t a_bytes = size_t(MG) * NS * 1024;
-  uint64_t* rowptr = reinterpret_cast<uint64_t*>(reinterpret_cast<uint8_t*>(afrag) + a_bytes);
-  uint64_t* outptr = rowptr + 256;
-  uint64_t* copyptr = rowptr + 256 + 32;
-  const i32x4* src = bitmat + size_t(g) * MG * NS * 64;
-  const uint64_t sink = sink_slot(uint64_t(bitmat + size_t(groups) * MG * NS * 64), sink_spread);
-  for (int i = threadIdx.x; i < MG * NS * 64; i += kThreads) afrag[i] = src[i];
-  if (!UNI)
-    for (int i = threadIdx.x; i < k; i += kThreads) rowptr[i] = in[i];
-  for (int i = threadIdx.x; i < 4 * MG; i += kThreads) {
-    const int row = 4 * g * MG + i;
-    outptr[i] = row < m ? out[row] : 0;
-  }
-  if (COPY)
-    for (int i = threadIdx.x; i < k; i += kThreads) copyptr[i] = g == 0 ? copy[i] : 0;  // group 0 copies
-  __syncthreads();
-
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 31, h = lane >> 5;
-  const uint32_t lds0 = uint32_t(reinterpret_cast<uintptr_t>((lds_u8*)afrag));
-  const uint32_t a_addr = lds0 + 16u * lane;
-  const uint32_t a_addr_hi = a_addr + 65536u;  // (A offsets past 64 KiB: second base, immediates)
-  const uint32_t optr_addr = lds0 + uint32_t(a_bytes) + 2048u + 16u * h;  // outptr[4e + 2h + u]: + 32e + 8u
-  lds_u8* rings = (lds_u8*)(reinterpret_cast<uint8_t*>(afrag) + a_bytes + 2304 + (COPY ? 2048 : 0));
-  lds_u8* ring = rings + size_t(wave) * R * kSlotBytes;
-  lds_u8* spare = rings + size_t(kWaves) * R * kSlotBytes;
-  const uint32_t ring_x = uint32_t(reinterpret_cast<uintptr_t>(ring)) + uint32_t(4 * h * kCW + NTW * c);
-  const uint32_t ring_lane = uint32_t(reinterpret_cast<uintptr_t>(ring)) + 16u * lane;
-  const int scale = 0x7F7F7F7F;  // E8M0 1.0 for every block of 32
-  const int bias_scale = bias_scale_of_lane(lane);
-  const i32x8 one_k0 = {h == 0 ? 0x2 : 0, 0, 0, 0, 0, 0, 0, 0};  // 1.0 at K index 0 (A and B)
-  const int my_chunks = int((nchunks - slot0 + chunk_slots - 1) / chunk_slots);
-  if (my_chunks <= 0) return;
-  const uint64_t in0 = UNI ? in[0] : 0;
-  const int drow = lane / kLPR;  // this lane's row within a DMA'd slot
-  const int dcol = wave * kCW + 16 * (lane % kLPR);
-  // this lane's DMA row of slot-of-chunk p (rows >= k meet zero bit-matrix columns)
-  auto dma_row = [&](int p) __attribute__((always_inline)) { return kRS * p + drow < k ? kRS * p + drow : k - 1; };
-  const uint32_t rowptr_addr = lds0 + uint32_t(a_bytes);
-  const uint32_t cptr_addr = rowptr_addr + 2304u;
-  // scattered inputs: the row pointer of the next DMA, read from LDS one slot ahead (a register
-  // per slot of the chunk would cost 16 VGPRs)
-  uint64_t pn = UNI ? 0 : rowptr[dma_row(R % KS)];
-
-  // DMA of slot T (chunk-relative, T may reach past the chunk) of chunk ci: past the last chunk
-  // it lands in the spare slot (valid source), so the number in flight stays the same
-  auto dma_issue = [&](int ci, auto t_tag, uint64_t rowp) __attribute__((always_inline)) {
-    constexpr int T = decltype(t_tag)::value;
-    constexpr int p = T % KS, ring_slot = T % R;
-    const int chunk = ci + T / KS;
-    const bool live = chunk < my_chunks;
-    const int64_t col = col0 + (slot0 + int64_t(live && !(ABL & 4) ? chunk : 0) * chunk_slots) * kBlockCols + dcol;
-    uint64_t sa;
-    if constexpr (UNI)
-      sa = in0 + uint64_t(int64_t(dma_row(p)) * in_stride + col);
-    else
-      sa = rowp + uint64_t(col);
-    __builtin_amdgcn_global_load_lds((gptr<const void>)sa, live ? ring + ring_slot * kSlotBytes : spare, 16, 0, 0);
-  };
-  // rows 4h+i of K-step half HS of ring slot SL, this lane's column pair (2c, 2c+1)
-  auto read_x = [&](uint32_t (&x)[4], auto sl_tag, auto hs_tag) __attribute__((always_inline)) {
-    constexpr int off = decltype(sl_tag)::value * kSlotBytes + decltype(hs_tag)::value * 8 * kCW;
-    const uint32_t addr = ring_x;
-    uint32_t x0, x1, x2, x3;  // (locals: clang does not capture asm operands in generic lambdas)
-    asm volatile(
-        "ds_read_u16 %0, %4 offset:%5\n\t"
-        "ds_read_u16 %1, %4 offset:%6\n\t"
-        "ds_read_u16 %2, %4 offset:%7\n\t"
-        "ds_read_u16 %3, %4 offset:%8"
-        : "=&v"(x0), "=&v"(x1), "=&v"(x2), "=&v"(x3)
-        : "v"(addr), "n"(off), "n"(off + 64), "n"(off + 128), "n"(off + 192)
-        : "memory");
-    x[0] = x0;
-    x[1] = x1;
-    x[2] = x2;
-    x[3] = x3;
-  };
-  // A fragment of (K-step S, tile MT)
-  auto read_a1 = [&](i32x4& a, auto s_tag, auto mt_tag) __attribute__((always_inline)) {
-    constexpr int off = (decltype(s_tag)::value * MG + decltype(mt_tag)::value) * 1024;
-    const uint32_t base = off >= 65536 ? a_addr_hi : a_addr;
-    i32x4 v;
-    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=&v"(v) : "v"(base), "n"(off % 65536) : "memory");
-    a = v;
-  };
-  constexpr int kExpandValu = 14;
-  auto expand = [&](i32x4 (&bo)[NTW], const uint32_t (&x)[4]) __attribute__((always_inline)) {
-    const uint32_t p01 = x[0] | (x[1] << 16), p23 = x[2] | (x[3] << 16);
-    const uint32_t w[2] = {__builtin_amdgcn_perm(p23, p01, 0x06040200u), __builtin_amdgcn_perm(p23, p01, 0x07050301u)};
-    if constexpr ((ABL & 2) != 0) {
-#pragma unroll
-      for (int t = 0; t < NTW; ++t) bo[t] = i32x4{int(w[t]), int(w[t]), int(w[t]), int(w[t])};
-      return;
-    }
-#pragma unroll
-    for (int t = 0; t < NTW; ++t) {
-      bo[t][0] = int(w[t] & 0x11111111u);
-      bo[t][1] = int(w[t] & 0x22222222u);
-      bo[t][2] = int(w[t] & 0x44444444u);
-      bo[t][3] = int((w[t] >> 1) & 0x44444444u);
-    }
-  };
-
-  f32x16 acc[MG][NTW];
-  auto bias_init = [&](auto mt_tag) __attribute__((always_inline)) {
-    constexpr int MT = decltype(mt_tag)::value;
-#pragma unroll
-    for (int t = 0; t < NTW; ++t) {
-      int bs = bias_scale;  // (opaque: keeps these identical MFMAs from being hoisted or merged)
-      asm volatile("" : "+v"(bs));
-      acc[MT][t] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(one_k0, one_k0, (f32x16)(0.0f), 4, 4, 0, bs, 0,
-                                                                    scale);
-    }
-  };
-
-  // prologue: R slots in flight; around each DMA the stores its steady-state position has (the
-  // issuing virtual slot's second-step epilogue stores and copy store after it, the next virtual
-  // slot's first-step epilogue stores before the next DMA) as dummies to the sink
-  static_for<R>([&](auto t) {
-    constexpr int T = decltype(t)::value;
-    dma_issue(0, t, UNI ? 0 : rowptr[dma_row(T % KS)]);
-    constexpr int v = KS + T - R;  // the virtual slot of chunk -1 issuing it
-    constexpr int n_epi = sk_stores_in(2 * v + 1, 2 * v + 2, MG, NS) +
-                          (T + 1 < R ? sk_stores_in(2 * v + 2, 2 * v + 3, MG, NS) : 0);
-    const uint64_t sk = sink;
-    if constexpr (COPY) {
-      const u32x4 zero = {0u, 0u, 0u, 0u};
-      asm volatile("global_store_dwordx4 %0, %1, off nt" ::"v"(sk), "v"(zero) : "memory");
-    }
-#pragma unroll
-    for (int i = 0; i < n_epi; ++i) asm volatile("global_store_short %0, %1, off" ::"v"(sk), "v"(0) : "memory");
-  });
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(R - 1) : "memory");
-  using I0 = std::integral_constant<int, 0>;
-  using I1 = std::integral_constant<int, 1>;
-  uint32_t x0[4], x1[4], x2[4];  // raw bytes: x1 = step s+1 (in registers), x2 = step s+2 (in flight)
-  i32x4 ac[MG], an[MG];          // A fragments of the current / next step, per tile
-  i32x4 bw[MG][NTW];             // B operands of the last MG K-steps (bw[s % MG])
-  read_x(x0, I0{}, I0{});
-  read_x(x1, I0{}, I1{});
-  static_for<MG>([&](auto mt) { read_a1(ac[decltype(mt)::value], std::integral_constant<int, sk_mod(-decltype(mt)::value, NS)>{}, mt); });
-  lgkm_wait();
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    tie(x0[i]);
-    tie(x1[i]);
-  }
-#pragma unroll
-  for (int mt = 0; mt < MG; ++mt) tie(ac[mt]);
-#pragma unroll
-  for (int s = 1; s < MG; ++s)
-#pragma unroll
-    for (int t = 0; t < NTW; ++t) bw[s][t] = i32x4{0, 0, 0, 0};  // K-steps of "chunk -1": discarded
-  expand(bw[0], x0);
-  static_for<MG>([&](auto mt) { bias_init(mt); });
-
-  // output row pointers of the tile packed at the next step, read one step ahead
-  uint64_t opc[2] = {0, 0};
-  {
-    const uint32_t addr = optr_addr;
-    uint64_t o0, o1;
-    asm volatile("ds_read_b64 %0, %2\n\tds_read_b64 %1, %2 offset:8" : "=&v"(o0), "=&v"(o1) : "v"(addr) : "memory");
-    lgkm_wait();
-    tie(o0);
-    tie(o1);
-    opc[0] = o0;
-    opc[1] = o1;
-  }
-
-  // One chunk (ci == my_chunks: the phantom that drains the last real chunk). Step layout, so the
-  // matrix pipe never waits on a step boundary: [2 MFMAs] [this slot's counted wait, the LDS reads
-  // of the next step, the DMA of the slot R-1 ahead] [the remaining MFMAs, with the B expansion
-  // and the packed tile's epilogue as VALU between them] [its two stores] [lgkmcnt(0)].
-  auto chunk_body = [&](int ci) __attribute__((always_inline)) {
-    const bool live = ci < my_chunks;
-    const int64_t cbase = col0 + (slot0 + int64_t(ci) * chunk_slots) * kBlockCols;
-    const bool plive = ci > 0;  // packs of "chunk -1" (steps < MG of chunk 0) go to the sink
-    const int64_t pcolw = cbase - chunk_slots * kBlockCols + wave * kCW + NTW * c;
-    [[maybe_unused]] u32x4 cdat;
-    [[maybe_unused]] uint64_t cp = 0;
-    static_for<KS>([&](auto sp_tag) {
-      constexpr int SP = decltype(sp_tag)::value;
-      constexpr int RS = SP % R, RS1 = (SP + 1) % R;
-      [[maybe_unused]] const int crow = kRS * SP + drow;
-      static_for<kSPS>([&](auto jj_tag) {
-        constexpr int JJ = decltype(jj_tag)::value;
-        constexpr int J = SP * kSPS + JJ;                          // K-step of the chunk
-        constexpr int EP = J < MG ? J : -1;                        // tile packed and restarted
-        constexpr int EN = (J + 1) % NS < MG ? (J + 1) % NS : -1;  // tile packed at the next step
-        constexpr int EE = (J + 1) % NS < MG ? (J + 1) % NS : -1;  // tile finishing its chunk now
-        auto mfma_tile = [&](auto mt) __attribute__((always_inline)) {
-          constexpr int MT = decltype(mt)::value;
-          constexpr int B = sk_mod(J - MT, MG);
-          const i32x8 a = {ac[MT][0], ac[MT][1], ac[MT][2], ac[MT][3], 0, 0, 0, 0};
-#pragma unroll
-          for (int t = 0; t < NTW; ++t) {
-            const i32x8 bb = {bw[B][t][0], bw[B][t][1], bw[B][t][2], bw[B][t][3], 0, 0, 0, 0};
-            acc[MT][t] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, bb, acc[MT][t], 4, 4, 0, scale, 0, scale);
-          }
-        };
-        // MFMA order: the finishing tile first (complete when packed next step), then the others,
-        // then the packed tile's bias and its first K-step of the new chunk
-        constexpr int kFirst = EE >= 0 && EE != EP ? EE : (EP == 0 ? 1 : 0);
-        __builtin_amdgcn_sched_barrier(0);
-        mfma_tile(std::integral_constant<int, kFirst>{});
-        __builtin_amdgcn_sched_barrier(0);
-        if constexpr (JJ == 0)  // slot SP+1 has landed: exact count of the younger ops
-          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(sk_wait_count(SP, MG, KS, R, COPY)) : "memory");
-        read_x(x2, std::integral_constant<int, RS1>{}, jj_tag);
-        static_for<MG>([&](auto mt) {
-          constexpr int MT = decltype(mt)::value;
-          read_a1(an[MT], std::integral_constant<int, sk_mod(J + 1 - MT, NS)>{}, mt);
-        });
-        [[maybe_unused]] uint64_t opn[2];
-        if constexpr (EN >= 0) {
-          const uint32_t addr = optr_addr;
-          uint64_t o0, o1;
-          asm volatile("ds_read_b64 %0, %2 offset:%3\n\tds_read_b64 %1, %2 offset:%4"
-                       : "=&v"(o0), "=&v"(o1)
-                       : "v"(addr), "n"(32 * (EN >= 0 ? EN : 0)), "n"(32 * (EN >= 0 ? EN : 0) + 8)
-                       : "memory");
-          opn[0] = o0;
-          opn[1] = o1;
-        }
-        if constexpr (JJ == 1) {  // this slot's data is consumed: refill its ring slot R ahead
-          dma_issue(ci, std::integral_constant<int, SP + R>{}, pn);
-          if constexpr (!UNI) {  // the next slot's DMA row pointer
-            const uint32_t addr = rowptr_addr + 8u * uint32_t(dma_row((SP + 1 + R) % KS));
-            uint64_t v;
-            asm volatile("ds_read_b64 %0, %1" : "=&v"(v) : "v"(addr) : "memory");
-            pn = v;
-          }
-        }
-        if constexpr (JJ == 0) {
-          if constexpr (COPY) {  // this lane's 16 B of the current slot and its row's copy pointer
-            const uint32_t addr = ring_lane + uint32_t(RS * kSlotBytes);
-            const uint32_t caddr = cptr_addr + 8u * uint32_t(crow < k ? crow : k - 1);
-            u32x4 v;
-            uint64_t cv;
-            asm volatile("ds_read_b128 %0, %1" : "=&v"(v) : "v"(addr) : "memory");
-            asm volatile("ds_read_b64 %0, %1" : "=&v"(cv) : "v"(caddr) : "memory");
-            cdat = v;
-            cp = cv;
-          }
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        // (descending: tile MG-1 reads the oldest window slot, which the expansion below refills)
-        static_for<MG>([&](auto mt) {
-          constexpr int MT = MG - 1 - decltype(mt)::value;
-          if constexpr (MT != kFirst && MT != EP) mfma_tile(std::integral_constant<int, MT>{});
-        });
-        [[maybe_unused]] uint32_t w[2];
-        if constexpr (EP >= 0) {
-          constexpr int E = EP >= 0 ? EP : 0;
-          // output bytes of tile E (rows 2h, 2h+1; columns 2c, 2c+1): 7 v_bfi per byte over the
-          // biased accumulators (the parity of bit b's count sits at bit b). The empty asm makes
-          // the accumulators a new value here, so their reads stay in this segment (between the
-          // MFMAs) instead of being hoisted to the head of the step.
-#pragma unroll
-          for (int t = 0; t < NTW; ++t) asm volatile("" : "+a"(acc[E][t]));
-          uint32_t y[NTW][2];
-          if constexpr ((ABL & 1) != 0) {
-            w[0] = w[1] = uint32_t(lane);
-          } else {
-#pragma unroll
-            for (int b = 0; b < 8; ++b)
-#pragma unroll
-              for (int t = 0; t < NTW; ++t)
-#pragma unroll
-                for (int u = 0; u < 2; ++u) {
-                  const uint32_t v = __float_as_uint(acc[E][t][8 * u + b]);
-                  y[t][u] = b == 0 ? v : bfi(1u << b, v, y[t][u]);
-                }
-#pragma unroll
-            for (int u = 0; u < 2; ++u) w[u] = __builtin_amdgcn_perm(y[1][u], y[0][u], 0x0c0c0400u);
-          }
-          bias_init(std::integral_constant<int, E>{});
-          if constexpr (E != kFirst) mfma_tile(std::integral_constant<int, E>{});
-        }
-        // B of the next K-step (into the window slot whose last reader is this step's tile MG-1)
-        expand(bw[(J + 1) % MG], x1);
-        constexpr int kMfma = MG * NTW + (EP >= 0 ? NTW : 0) - NTW;
-        constexpr int kValu = kExpandValu + (EP >= 0 ? 2 * NTW * 16 + NTW * 2 * 7 + 2 : 0);
-#pragma unroll
-        for (int i = 0; i < kMfma; ++i) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                            // MFMA
-          __builtin_amdgcn_sched_group_barrier(0x002, (kValu + kMfma - 1) / kMfma, 0);  // VALU
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        if constexpr (EP >= 0) {
-#pragma unroll
-          for (int u = 0; u < 2; ++u) {
-            const uint64_t o = opc[u];
-            *(gptr<uint16_t>)(plive && o ? o + uint64_t(pcolw) : sink) = uint16_t(w[u]);
-          }
-        }
-        if constexpr (COPY && JJ == 1) {  // (cdat / cp retired by step 0's lgkmcnt(0))
-          __builtin_nontemporal_store(cdat, (gptr<u32x4>)(live && crow < k && cp ? cp + uint64_t(cbase + dcol) : sink));
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        lgkm_wait();
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          tie(x2[i]);
-          x1[i] = x2[i];
-        }
-#pragma unroll
-        for (int mt = 0; mt < MG; ++mt) {
-          tie(an[mt]);
-          ac[mt] = an[mt];
-        }
-        if constexpr (EN >= 0) {
-          uint64_t o0 = opn[0], o1 = opn[1];
-          tie(o0);
-          tie(o1);
-          opc[0] = o0;
-          opc[1] = o1;
-        }
-        if constexpr (JJ == 1 && !UNI) {
-          uint64_t v = pn;
-          tie(v);
-          pn = v;
-        }
-        if constexpr (JJ == 0) {
-          if constexpr (COPY) {
-            u32x4 d = cdat;
-            uint64_t cv = cp;
-            tie(d);
-            tie(cv);
-            cdat = d;
-            cp = cv;
-          }
-        }
-      });
-    });
-  };
-
-  for (int ci = 0; ci <= my_chunks; ++ci) chunk_body(ci);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA (dummy or not) outlives the wave
-}
-
-// Survivor copy beside the matrix-core decode GEMM (the "split" form of the fused copy): the wide
-// FP4 GEMM is matrix-core bound and reads HBM at ~1.3 TB/s, so a copy kernel that fits in the
-// registers the persistent GEMM leaves free (the sk kernel allocates 448 of a SIMD's 512; this
-// kernel stays at <= 32 VGPRs, no LDS) streams the survivors through the idle HBM bandwidth on a
-// side stream. copy[j] != 0: bytes [col0, col0 + ncols) of input row j go to copy[j]. 16-byte
-// loads four deep per lane, non-temporal stores; rows whose two addresses are not 16-byte aligned
-// alike take a byte loop (never the case for pitched alloc_rows buffers).
-__global__ __launch_bounds__(256) void copy_rows_kernel(cptr<uint64_t> in, cptr<uint64_t> copy, int k, int64_t col0,
-                                                        int64_t ncols) {
-  const int64_t nthr = int64_t(gridDim.x) * blockDim.x;
-  const int64_t t = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-  for (int j = 0; j < k; ++j) {
-    const uint64_t dst = copy[j];
-    if (!dst) continue;
-    gptr<const uint8_t> s = (gptr<const uint8_t>)(in[j] + uint64_t(col0));
-    gptr<uint8_t> d = (gptr<uint8_t>)(dst + uint64_t(col0));
-    int64_t done = 0;
-    if ((((in[j] + uint64_t(col0)) | (dst + uint64_t(col0))) & 15) == 0 && ncols < (int64_t(1) << 32)) {
-      // wave-uniform row bases (SGPRs) + 32-bit lane byte offsets: saddr + voffset addressing, so
-      // four loads in flight cost 16 data VGPRs and one offset
-      const int64_t n16 = ncols >> 4;
-      const uint32_t step = uint32_t(nthr) * 16;
-      const uint32_t end = uint32_t(n16) * 16;
-      uint32_t o = uint32_t(t) * 16;
-      for (; uint64_t(o) + 3ull * step < end; o += 4 * step) {
-        const u32x4 v0 = *(gptr<const u32x4>)(s + o);
-        const u32x4 v1 = *(gptr<const u32x4>)(s + (o + step));
-        const u32x4 v2 = *(gptr<const u32x4>)(s + (o + 2 * step));
-        const u32x4 v3 = *(gptr<const u32x4>)(s + (o + 3 * step));
-        __builtin_nontemporal_store(v0, (gptr<u32x4>)(d + o));
-        __builtin_nontemporal_store(v1, (gptr<u32x4>)(d + (o + step)));
-        __builtin_nontemporal_store(v2, (gptr<u32x4>)(d + (o + 2 * step)));
-        __builtin_nontemporal_store(v3, (gptr<u32x4>)(d + (o + 3 * step)));
-      }
-      for (; o < end; o += step) __builtin_nontemporal_store(*(gptr<const u32x4>)(s + o), (gptr<u32x4>)(d + o));
-      done = n16 << 4;
-    }
-    for (int64_t b = done + t; b < ncols; b += nthr) d[b] = s[b];
-  }
-}
-
-// side stream + fork/join events per (device, launch stream): the split copy runs beside the GEMM
-// and the launch stream waits for both (capturable into a hipGraph: event fork/join)
-struct SideCtx {
-  hipStream_t side = nullptr;
-  hipEvent_t fork = nullptr, join = nullptr;
-};
-
-hipError_t side_ctx(hipStream_t stream, SideCtx* out) {
-  static std::mutex mu;
-  static std::map<std::pair<int, hipStream_t>, SideCtx>* ctxs = new std::map<std::pair<int, hipStream_t>, SideCtx>();
-  const std::pair<int, hipStream_t> key{current_device(), stream};
-  std::lock_guard<std::mutex> g(mu);
-  auto it = ctxs->find(key);
-  if (it != ctxs->end()) {
-    *out = it->second;
-    return hipSuccess;
-  }
-  SideCtx c;
-  hipError_t e = hipStreamCreateWithFlags(&c.side, hipStreamNonBlocking);
-  if (e == hipSuccess) e = hipEventCreateWithFlags(&c.fork, hipEventDisableTiming);
-  if (e == hipSuccess) e = hipEventCreateWithFlags(&c.join, hipEventDisableTiming);
-  if (e != hipSuccess) return e;
-  (*ctxs)[key] = c;
-  *out = c;
-  return hipSuccess;
-}
-
-hipError_t launch_copy_rows(cptr<uint64_t> in, cptr<uint64_t> copy, int k, int64_t col0, int64_t ncols,
-                            hipStream_t stream) {
-  const unsigned blocks = unsigned(2 * device_cu_count());  // two waves per SIMD beside the GEMM's one
-  copy_rows_kernel<<<blocks, 256, 0, stream>>>(in, copy, k, col0, ncols);
-  return hipGetLastError();
-}
-
-// GFRS_FP4_COPY: fused (default) = copy inside the GEMM kernel; split = staggered GEMM, then the
-// side-stream copy; split_first = the copy launched first. Measured on k=128, 26 rebuilt rows +
-// 102 copies, 1 GiB (profiles/wide_stripe/r02_split): fused 1019 us, split 1034, split_first 1081 (medians;
-// the plain GEMM alone 762, the copy alone 334) — the co-running copy costs the GEMM more than it
-// saves: re-reading the survivors adds 0.8 GB of HBM traffic, the chip holds a lower clock, and
-// the copy waves take issue slots on the GEMM's SIMDs. Kept as the measured alternative.
-int split_copy_mode() {
-  const char* env = std::getenv("GFRS_FP4_COPY");
-  if (!env || std::strcmp(env, "split") != 0) return env && std::strcmp(env, "split_first") == 0 ? 2 : 0;
-  return 1;
-}
-
 struct Fp4Geometry {
   int ksteps, mtiles, mg, groups;
   size_t fixed;  // LDS bytes before the rings: A slice + row/out pointers
@@ -1033,16 +540,10 @@ Fp4Geometry geometry(int k, int m, int mg_cap, bool copy = false) {
   while (g.mg < g.mtiles && g.mg < mg_cap) g.mg <<= 1;
   // (the copy-pointer block is always budgeted, so the bitmat layout does not depend on `copy`)
   while (g.mg > 1 && g.mg * g.ksteps > kMaxLdsKiB - 2) g.mg >>= 1;
-  // the static wide-stripe chunk (k in (112, 128], the instantiated MG = 5..7 kernels): exactly
-  // mtiles M-tiles instead of a padded 8 — a decode rebuilding 20..28 natives skips 1..3 tiles of
-  // MFMAs that would only compute padding rows (12.5-37.5 % of the matrix-core work)
-  // (GFRS_FP4_EXACT_MG=0: the padded 8, for A/B measurements; read once per process so a plan's
-  // bit-matrix and its launches always agree)
-  static const bool exact = [] {
-    const char* env = std::getenv("GFRS_FP4_EXACT_MG");
-    return !(env && std::strcmp(env, "0") == 0);
-  }();
-  if (exact && g.ksteps == 16 && ((g.mg == 8 && g.mtiles > 4 && g.mtiles < 8) || (g.mg == 4 && g.mtiles == 3)))
+  // the static wide-stripe chunk (k in (112, 128]): exactly mtiles M-tiles instead of a padded 8 or
+  // 4 — a decode rebuilding 20..28 natives skips 1..3 tiles of MFMAs that would only compute padding
+  // rows (12.5-37.5 % of the matrix-core work; profiles/wide_stripe/r02_exact_mg)
+  if (g.ksteps == 16 && ((g.mg == 8 && g.mtiles > 4 && g.mtiles < 8) || (g.mg == 4 && g.mtiles == 3)))
     g.mg = g.mtiles;
   g.groups = (g.mtiles + g.mg - 1) / g.mg;
   g.fixed = size_t(g.mg) * g.ksteps * 64 * 16 + 2304 + (copy ? 2048 : 0);
@@ -1069,15 +570,6 @@ int fp4_occupancy(size_t fixed) {
   return occ;
 }
 
-// GFRS_FP4_SINK=1: every wave's sink stores share one 1-KiB slot (the round-2 layout, A/B only)
-int fp4_sink_spread() {
-  static const int v = [] {
-    const char* e = std::getenv("GFRS_FP4_SINK");
-    return (e && std::atoi(e) == 1) ? 0 : 1;
-  }();
-  return v;
-}
-
 struct Fp4Args {
   cptr<uint64_t> in, out, copy;
   const void* bitmat;
@@ -1095,7 +587,7 @@ hipError_t launch_fp4(const Fp4Geometry& geo, int occ, const Fp4Args& a, hipStre
   const unsigned blocks = unsigned(slots * geo.groups);
   gf_gemm_fp4_kernel<MG, UNI, COPY, R, KS><<<blocks, 256, lds, stream>>>(
       a.in, a.out, a.copy, static_cast<const i32x4*>(a.bitmat), a.k, a.m, geo.ksteps, geo.groups, a.col0, a.nchunks,
-      slots, a.in_stride, fp4_sink_spread());
+      slots, a.in_stride);
   return hipGetLastError();
 }
 
@@ -1113,12 +605,6 @@ hipError_t launch_fp4_ring(const Fp4Geometry& geo, const Fp4Args& a, hipStream_t
   const std::pair<int, int> ch = choice.get_or(geo.fixed / 1024, [&] {
     const int occs[kN] = {fp4_occupancy<MG, UNI, COPY, Rs, KS>(geo.fixed)...};
     auto reserve_ok = [&](int i) { return geo.fixed + ring_lds(rings[i]) + kSideReserve <= 160 * 1024; };
-    static const int forced = [] {  // GFRS_FP4_RING=R: that depth when it fits (A/B measurements)
-      const char* env = std::getenv("GFRS_FP4_RING");
-      return env ? std::atoi(env) : 0;
-    }();
-    for (int i = 0; i < kN; ++i)
-      if (forced && rings[i] == forced && occs[i] > 0) return std::pair<int, int>{i + 1, occs[i]};
     int best = -1;
     for (int i = 0; i < kN; ++i) {
       if (occs[i] <= 0) continue;
@@ -1154,9 +640,10 @@ hipError_t launch_fp4_any(const Fp4Geometry& geo, const Fp4Args& a, hipStream_t 
                      : launch_fp4_var<MG, false, false>(geo, a, stream);
 }
 
-// MG = 3, 5..7 exist for the static 8-slot chunk only (geometry() picks them there), ring depth 4:
-// the depth-8 forms fit the LDS but need ~90 more VGPRs (256 with spills into AGPRs) and ran
-// 0-19 % slower at every shape (profiles/wide_stripe/r02_exact_mg: k=128, m=28 + 100 copies 885 vs 1050 us)
+// MG = 3 and 6 exist for the static 8-slot chunk only (geometry() picks them there; fp4_route sends
+// 5 and 7 tiles to the tile-major kernel), ring depth 4: the depth-8 forms fit the LDS but need ~90
+// more VGPRs (256 with spills into AGPRs) and ran 0-19 % slower at every shape
+// (profiles/wide_stripe/r02_exact_mg: k=128, m=28 + 100 copies 885 vs 1050 us)
 template <int MG>
 hipError_t launch_fp4_static_any(const Fp4Geometry& geo, const Fp4Args& a, hipStream_t stream) {
   if (geo.ksteps != 16) return hipErrorInvalidConfiguration;
@@ -1165,102 +652,55 @@ hipError_t launch_fp4_static_any(const Fp4Geometry& geo, const Fp4Args& a, hipSt
                      : launch_fp4_ring<MG, false, false, 8, 4>(geo, a, stream);
 }
 
-// sk kernel (k in (112, 128]: 8 ring slots per chunk): ring depth 8 or 4, deepest that fits the LDS
-// with the side reserve, else without it
-template <int MG, bool UNI, bool COPY, int R, int ABL = 0>
-hipError_t launch_fp4sk(const Fp4Geometry& geo, const Fp4Args& a, hipStream_t stream) {
-  constexpr int KS = 8;
-  const void* f = reinterpret_cast<const void*>(&gf_gemm_fp4sk_kernel<MG, UNI, COPY, R, KS, ABL>);
-  const size_t lds = size_t(MG) * KS * 2 * 1024 + 2304 + (COPY ? 2048 : 0) + ring_lds(R);
-  if (lds > 160 * 1024) return hipErrorInvalidConfiguration;
-  hipError_t e = ensure_lds_optin(f);
-  if (e != hipSuccess) return e;
-  static DeviceMemo<size_t, int> occ_memo;
-  const int occ = occ_memo.get_or(lds, [&] {
-    int o = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, f, 256, lds) != hipSuccess) o = 0;
-    return o;
-  });
-  if (occ <= 0) return hipErrorInvalidConfiguration;
-  const int64_t slots = persistent_slots(occ, geo.groups, a.nchunks);
-  const unsigned blocks = unsigned(slots * geo.groups);
-  gf_gemm_fp4sk_kernel<MG, UNI, COPY, R, KS, ABL><<<blocks, 256, lds, stream>>>(
-      a.in, a.out, a.copy, static_cast<const i32x4*>(a.bitmat), a.k, a.m, geo.groups, a.col0, a.nchunks, slots,
-      a.in_stride, fp4_sink_spread());
-  return hipGetLastError();
-}
+// ---- the one routing decision of the GF(2^8) FP4 engine ------------------------------------------
+// Forms: v1 (the LDS-ring kernel above: any k, any M-tile count, groups of M-tiles), ar (A-resident,
+// gf_mfma_fp4ar.hip: bit-matrix in AGPRs, k in (112, 128], one group of <= 8 tiles, also the batched
+// launch) and tm (tile-major, gf_mfma_fp4tm.hip: B in AGPRs, tiles in pairs, 5..7 tiles). Every
+// branch is a measured win (k = 128, 1 GiB, medians, two interleaved rounds each):
+//   * 1..3 tiles: v1 — memory-bound shapes; ar loses there (profiles/wide_stripe/r02_fp4_ablate);
+//   * 4 tiles: ar, plain and with fused copies (m = 16: 490 vs 530 us plain, 659 vs 722 with 112
+//     copies; r02_fp4_ablate);
+//   * 5 tiles: tm, plain and copies (m = 20: 595-611 vs 625-631 us plain, 750-766 vs 776-784 with
+//     108 copies; profiles/wide_stripe/r09_route);
+//   * 6 tiles: tm plain (m = 22/24: 644-673 vs 696-719 on v1, 668-677 on ar; r09_route, r08_tm); with
+//     copies v1 (830-836 us; the tm copy build spills 16 VGPRs and runs 1300 us, r09_route);
+//   * 7 tiles: tm, plain and copies (m = 26: 729-767 vs 795-798 plain, 877-884 vs 935-940 with 102
+//     copies; r09_route);
+//   * 8 tiles: ar plain (the p = 32 encode: 809 vs 842 us; r02_fp4_ablate), v1 with copies (ar's two
+//     row halves lose with copies: 1060-1360 vs 760-970 us);
+//   * more than one group (m > 32) or k outside (112, 128]: v1.
+// GFRS_TUNE=fp4=v1|ar|tm forces that form wherever it is built for the shape (A/B measurements).
+enum class Fp4Form { kV1, kAResident, kTileMajor };
 
-template <int MG, bool UNI, bool COPY>
-hipError_t launch_fp4sk_ring(const Fp4Geometry& geo, const Fp4Args& a, hipStream_t stream) {
-  const size_t base = size_t(MG) * 16 * 1024 + 2304 + (COPY ? 2048 : 0);
-  if (base + ring_lds(8) + kSideReserve <= 160 * 1024) return launch_fp4sk<MG, UNI, COPY, 8>(geo, a, stream);
-  if constexpr (MG == 8 && UNI && !COPY) {  // ablation builds (measurements only, see the kernel)
-    static const int abl = [] {
-      const char* env = std::getenv("GFRS_FP4_ABL");
-      return env ? std::atoi(env) : 0;
-    }();
-    switch (abl) {
-      case 1: return launch_fp4sk<MG, UNI, COPY, 4, 1>(geo, a, stream);
-      case 2: return launch_fp4sk<MG, UNI, COPY, 4, 2>(geo, a, stream);
-      case 3: return launch_fp4sk<MG, UNI, COPY, 4, 3>(geo, a, stream);
-      case 4: return launch_fp4sk<MG, UNI, COPY, 4, 4>(geo, a, stream);
-      case 7: return launch_fp4sk<MG, UNI, COPY, 4, 7>(geo, a, stream);
-      default: break;
-    }
+bool form_built(Fp4Form f, const Fp4Geometry& geo, int k, bool copies) {
+  switch (f) {
+    case Fp4Form::kAResident: return geo.groups == 1 && fp4ar_supported(k, geo.mg);
+    case Fp4Form::kTileMajor: return geo.groups == 1 && fp4tm_supported(k, geo.mg, copies);
+    default: return geo.ksteps != 16 || geo.mg == 1 || geo.mg == 2 || geo.mg == 3 || geo.mg == 4 || geo.mg == 6 ||
+                    geo.mg == 8;
   }
-  return launch_fp4sk<MG, UNI, COPY, 4>(geo, a, stream);
 }
 
-template <int MG>
-hipError_t launch_fp4sk_any(const Fp4Geometry& geo, const Fp4Args& a, hipStream_t stream) {
-  if (a.copy) return launch_fp4sk_ring<MG, false, true>(geo, a, stream);
-  return a.in_stride ? launch_fp4sk_ring<MG, true, false>(geo, a, stream)
-                     : launch_fp4sk_ring<MG, false, false>(geo, a, stream);
-}
-
-// the staggered kernel covers the static 8-slot chunk (k in (112, 128]) with 4 or 8 M-tiles per
-// group; GFRS_FP4_KERNEL=v1 selects the single-schedule kernel (A/B measurements)
-bool use_sk(const Fp4Geometry& geo, bool copies) {
-  const char* env = std::getenv("GFRS_FP4_KERNEL");
-  if (env && std::strcmp(env, "v1") == 0) return false;
-  if (env && std::strcmp(env, "sk") == 0) copies = false;  // (force it for the fused-copy form too)
-  // GFRS_FP4_COPY_KERNEL=sk: the staggered form for fused-copy GEMMs only (the encode keeps its
-  // kernel); with GFRS_FP4_EXACT_MG=0 a 5..7-tile decode then runs as 8 staggered tiles (A/B)
-  static const bool copy_sk = [] {
-    const char* e = std::getenv("GFRS_FP4_COPY_KERNEL");
-    return e && std::strcmp(e, "sk") == 0;
+Fp4Form fp4_route(const Fp4Geometry& geo, int k, bool copies) {
+  // (read per call: the form does not change the bit-matrix layout, so an A/B run may switch it
+  // between launches of one plan)
+  const int forced = [] {
+    const std::string e = tune_str("fp4");
+    if (e == "v1") return int(Fp4Form::kV1);
+    if (e == "ar") return int(Fp4Form::kAResident);
+    if (e == "tm") return int(Fp4Form::kTileMajor);
+    return -1;
   }();
-  if (copies && copy_sk) copies = false;
-  // measured (profiles/wide_stripe/r02_fp4): 6 % faster than v1 for plain GEMMs, 1 % slower with fused copies
-  return !copies && geo.ksteps == 16 && (geo.mg == 4 || geo.mg == 8);
-}
-
-// The A-resident kernel (gf_mfma_fp4ar.hip; k in (112, 128], all M-tiles in one group) where it
-// measured faster (profiles/wide_stripe/r02_fp4_ablate, k=128, 1 GiB, medians of alternating runs): plain
-// GEMMs with 6 or 8 M-tiles (two row halves of 3 / 4, no padding tile: m=24 670 vs 714 us, m=32
-// 809 vs 842 — the p=32 encode) and 4 M-tiles with or without fused copies (one wave per column
-// group: m=16 490 vs 530 us plain, 659 vs 722 with 112 copies). It loses with padding tiles
-// (5, 7 M-tiles), at 1-3 M-tiles (memory-bound shapes), and with fused copies at two row halves
-// (1060-1360 vs 760-970 us). GFRS_FP4_KERNEL=ar forces it wherever supported; =sk / =v1 never.
-bool use_ar(const Fp4Geometry& geo, int k, bool copies) {
-  if (geo.groups != 1 || !fp4ar_supported(k, geo.mg)) return false;
-  const char* env = std::getenv("GFRS_FP4_KERNEL");
-  if (env && std::strcmp(env, "ar") == 0) return true;
-  if (env && (std::strcmp(env, "sk") == 0 || std::strcmp(env, "v1") == 0)) return false;
-  return geo.mg == 4 || (!copies && (geo.mg == 6 || geo.mg == 8));
-}
-
-// The tile-major kernel (gf_mfma_fp4tm.hip) for one group of 5..7 M-tiles at k in (112, 128], where
-// it measured faster (profiles/wide_stripe/r08_tm, k = 128, 1 GiB, medians): plain GEMMs at 5..7
-// tiles (m = 26: 728-744 vs 784-790 us on v1; m = 24: 646-648 vs 668-677 on the A-resident kernel;
-// m = 20: 569-608 vs 625) and the 7-tile GEMM with fused copies (the k = 128 decode: 888-904 vs
-// 902-908). With copies at 5 or 6 tiles it trails v1 (819-824 vs 773-780, 849-866 vs 831-832 us).
-// GFRS_FP4_KERNEL=tm forces it wherever supported; =v1 / =sk / =ar never.
-bool use_tm(const Fp4Geometry& geo, int k, bool copies) {
-  if (geo.groups != 1 || !fp4tm_supported(k, geo.mg, copies)) return false;
-  const char* env = std::getenv("GFRS_FP4_KERNEL");
-  if (env && *env) return std::strcmp(env, "tm") == 0;
-  return !copies || geo.mg == 7;
+  if (forced >= 0 && form_built(Fp4Form(forced), geo, k, copies)) return Fp4Form(forced);
+  if (geo.groups != 1 || k <= 112 || k > 128) return Fp4Form::kV1;
+  switch (geo.mg) {
+    case 4: return Fp4Form::kAResident;
+    case 5:
+    case 7: return Fp4Form::kTileMajor;
+    case 6: return copies ? Fp4Form::kV1 : Fp4Form::kTileMajor;
+    case 8: return copies ? Fp4Form::kV1 : Fp4Form::kAResident;
+    default: return Fp4Form::kV1;
+  }
 }
 
 }  // namespace
@@ -1292,7 +732,8 @@ hipError_t launch_gf_gemm_fp4(const void* bitmat, const void* desc, int k, int m
   const DescLayout l = desc_layout(k, m_pad);
   const char* b = static_cast<const char*>(desc);
   const Fp4Geometry geo = geometry(k, m, mg_cap, copies);
-  if (use_tm(geo, k, copies) && !(copies && split_copy_mode())) {  // the tile-major form (gf_mfma_fp4tm.hip)
+  const Fp4Form form = fp4_route(geo, k, copies);
+  if (form != Fp4Form::kV1) {  // the AGPR-resident forms (launch record of gfrs/kernels.h)
     Fp4ArLaunch a{};
     a.in = reinterpret_cast<const uint64_t*>(b + l.in_off);
     a.out = reinterpret_cast<const uint64_t*>(b + l.out_off);
@@ -1305,81 +746,49 @@ hipError_t launch_gf_gemm_fp4(const void* bitmat, const void* desc, int k, int m
     a.ncols = ncols;
     a.in_stride = copies ? 0 : in_stride;
     int64_t done = 0;
-    const hipError_t e = launch_gf_gemm_fp4tm(a, &done, stream);
+    const hipError_t e = form == Fp4Form::kTileMajor ? launch_gf_gemm_fp4tm(a, &done, stream)
+                                                     : launch_gf_gemm_fp4ar(a, &done, stream);
     if (e != hipSuccess) return e;
     if (done < ncols) return launch_gf_gemm(desc, k, m_pad, col0 + done, ncols - done, false, 0, stream);
     return hipSuccess;
   }
-  // split copy (GFRS_FP4_COPY=split, measured and not the default: split_copy_mode)
-  if (use_ar(geo, k, copies) && !(copies && split_copy_mode())) {  // the A-resident form (gf_mfma_fp4ar.hip)
-    Fp4ArLaunch a{};
-    a.in = reinterpret_cast<const uint64_t*>(b + l.in_off);
-    a.out = reinterpret_cast<const uint64_t*>(b + l.out_off);
-    a.copy = copies ? reinterpret_cast<const uint64_t*>(b + l.copy_off) : nullptr;
-    a.bitmat = bitmat;
-    a.k = k;
-    a.m = m;
-    a.mg = geo.mg;
-    a.col0 = col0;
-    a.ncols = ncols;
-    a.in_stride = copies ? 0 : in_stride;
-    int64_t done = 0;
-    const hipError_t e = launch_gf_gemm_fp4ar(a, &done, stream);
-    if (e != hipSuccess) return e;
-    if (done < ncols) return launch_gf_gemm(desc, k, m_pad, col0 + done, ncols - done, false, 0, stream);
-    return hipSuccess;
-  }
-  const int split = copies && use_sk(geo, false) ? split_copy_mode() : 0;
-  const bool fused = copies && !split;
-  const bool sk = use_sk(geo, fused);
   const int64_t chunk_cols = kBlockCols;
   const int64_t nchunks = ncols / chunk_cols;
   if (nchunks > 0) {
     Fp4Args a{};
     a.in = (cptr<uint64_t>)(b + l.in_off);
     a.out = (cptr<uint64_t>)(b + l.out_off);
-    a.copy = fused ? (cptr<uint64_t>)(b + l.copy_off) : nullptr;
+    a.copy = copies ? (cptr<uint64_t>)(b + l.copy_off) : nullptr;
     a.bitmat = bitmat;
     a.k = k;
     a.m = m;
     a.col0 = col0;
     a.nchunks = nchunks;
     a.in_stride = copies ? 0 : in_stride;  // the copy variant reads row pointers from the table
-    SideCtx side{};
-    if (split) {
-      hipError_t e = side_ctx(stream, &side);
-      if (e == hipSuccess) e = hipEventRecord(side.fork, stream);
-      if (e == hipSuccess) e = hipStreamWaitEvent(side.side, side.fork, 0);
-      if (e == hipSuccess && split == 2)
-        e = launch_copy_rows(a.in, (cptr<uint64_t>)(b + l.copy_off), k, col0, nchunks * chunk_cols, side.side);
-      if (e != hipSuccess) return e;
-    }
     hipError_t e;
-    if (split) {
-      e = geo.mg == 8 ? launch_fp4sk_any<8>(geo, a, stream) : launch_fp4sk_any<4>(geo, a, stream);
-      if (e == hipSuccess && split == 1)
-        e = launch_copy_rows(a.in, (cptr<uint64_t>)(b + l.copy_off), k, col0, nchunks * chunk_cols, side.side);
-      if (e == hipSuccess) e = hipEventRecord(side.join, side.side);
-      if (e == hipSuccess) e = hipStreamWaitEvent(stream, side.join, 0);
-    } else if (sk) {
-      e = geo.mg == 8 ? launch_fp4sk_any<8>(geo, a, stream) : launch_fp4sk_any<4>(geo, a, stream);
-    } else {
-      switch (geo.mg) {
-        case 8: e = launch_fp4_any<8>(geo, a, stream); break;
-        case 7: e = launch_fp4_static_any<7>(geo, a, stream); break;
-        case 6: e = launch_fp4_static_any<6>(geo, a, stream); break;
-        case 5: e = launch_fp4_static_any<5>(geo, a, stream); break;
-        case 4: e = launch_fp4_any<4>(geo, a, stream); break;
-        case 3: e = launch_fp4_static_any<3>(geo, a, stream); break;
-        case 2: e = launch_fp4_any<2>(geo, a, stream); break;
-        default: e = launch_fp4_any<1>(geo, a, stream); break;
-      }
+    switch (geo.mg) {
+      case 8: e = launch_fp4_any<8>(geo, a, stream); break;
+      case 6: e = launch_fp4_static_any<6>(geo, a, stream); break;
+      case 4: e = launch_fp4_any<4>(geo, a, stream); break;
+      case 3: e = launch_fp4_static_any<3>(geo, a, stream); break;
+      case 2: e = launch_fp4_any<2>(geo, a, stream); break;
+      case 1: e = launch_fp4_any<1>(geo, a, stream); break;
+      default: e = hipErrorInvalidConfiguration; break;  // (5, 7 tiles: tile-major only, fp4_route)
     }
     if (e != hipSuccess) return e;
   }
   const int64_t done = nchunks * chunk_cols;
   if (done < ncols) return launch_gf_gemm(desc, k, m_pad, col0 + done, ncols - done, false, 0, stream);
   return hipSuccess;
+}
+
+const char* fp4_route_name(int k, int m, bool copies, int mg_cap) {
+  if (k <= 0 || m <= 0 || mg_cap < 1) return "invalid";
+  switch (fp4_route(geometry(k, m, mg_cap, copies), k, copies)) {
+    case Fp4Form::kAResident: return "ar";
+    case Fp4Form::kTileMajor: return "tm";
+    default: return "v1";
+  }
 }
 
 hipError_t launch_gf_gemm_fp4_batched(const void* bitmat, const void* desc, int k, int m, int batch, int64_t col0,

@@ -109,7 +109,7 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4ar_kernel(cptr<uint64_t> in
                                                                cptr<uint64_t> copy, const i32x4* __restrict__ bitmat,
                                                                int k, int m, int mg, int64_t col0, int64_t nchunks,
                                                                int64_t chunk_slots, int64_t in_stride,
-                                                               int sink_spread, int64_t cps, int64_t in_bstride,
+                                                               int64_t cps, int64_t in_bstride,
                                                                int64_t out_bstride) {
   constexpr int CG = 4 / WPG;               // column groups per block
   constexpr int kBC = CG * kCW;             // block columns per chunk
@@ -152,7 +152,7 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4ar_kernel(cptr<uint64_t> in
   const uint32_t rowptr_addr = lds0;
   const uint32_t cptr_addr = lds0 + 8u * (256u + 32u);
   // this wave's 1-KiB slot of the sink past the bit-matrix (kFp4SinkSlots, kernels.h)
-  const unsigned sslot = sink_spread ? (blockIdx.x * 4u + unsigned(wave)) % unsigned(kFp4SinkSlots) : 0u;
+  const unsigned sslot = (blockIdx.x * 4u + unsigned(wave)) % unsigned(kFp4SinkSlots);
   const uint64_t sink = uint64_t(bitmat + size_t(mg) * kNS * 64) + uint64_t(sslot) * 1024u + 16 * lane;
   const int scale = 0x7F7F7F7F;  // E8M0 1.0 for every block of 32
   const uint64_t in0 = UNI ? in[0] : 0;
@@ -469,14 +469,10 @@ hipError_t launch_ar(const Fp4ArLaunch& a, int64_t* done, hipStream_t stream) {
   *done = cps * kBC;
   if (nchunks == 0) return hipSuccess;
   if (BATCH && nchunks >= (int64_t(1) << 31)) return hipErrorInvalidValue;
-  static const int sink_spread = [] {  // GFRS_FP4_SINK=1: one shared sink slot (A/B only)
-    const char* e = std::getenv("GFRS_FP4_SINK");
-    return (e && std::atoi(e) == 1) ? 0 : 1;
-  }();
   const int64_t slots = persistent_slots(occ, 1, nchunks);
   gf_gemm_fp4ar_kernel<MGW, WPG, UNI, COPY, R, BATCH><<<unsigned(slots), 256, lds, stream>>>(
       (cptr<uint64_t>)a.in, (cptr<uint64_t>)a.out, (cptr<uint64_t>)a.copy, static_cast<const i32x4*>(a.bitmat), a.k,
-      a.m, a.mg, a.col0, nchunks, slots, a.in_stride, sink_spread, cps, a.in_bstride, a.out_bstride);
+      a.m, a.mg, a.col0, nchunks, slots, a.in_stride, cps, a.in_bstride, a.out_bstride);
   return hipGetLastError();
 }
 

@@ -89,8 +89,7 @@ template <int MG, bool UNI, bool COPY>
 __global__ __launch_bounds__(256, 1) void gf_gemm_fp4tm_kernel(cptr<uint64_t> in, cptr<uint64_t> out,
                                                                cptr<uint64_t> copy, const i32x4* __restrict__ bitmat,
                                                                int k, int m, int64_t col0, int64_t nchunks,
-                                                               int64_t chunk_slots, int64_t in_stride,
-                                                               int sink_spread) {
+                                                               int64_t chunk_slots, int64_t in_stride) {
   static_assert(MG >= 5 && MG <= 7, "three tile groups at least: DMAs in group 0, the wait in group NG-2");
   constexpr size_t kA = size_t(MG) * kNS * 1024;  // LDS A slice [kstep][tile][lane] x 16 B
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -125,7 +124,7 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4tm_kernel(cptr<uint64_t> in
                          uint32_t(((lane & 15) >> 2) * kKS * kSlotBytes + wrow * kCW + 16 * (lane & 3));
   const uint32_t a_lo = lds0 + 16u * lane, a_hi = a_lo + 65536u;
   const uint32_t optr_addr = lds0 + uint32_t(kA) + 2048u + 16u * h;  // outptr[4t + 2h + u]: + 32t + 8u
-  const unsigned sslot = sink_spread ? (blockIdx.x * 4u + unsigned(wave)) % unsigned(kFp4SinkSlots) : 0u;
+  const unsigned sslot = (blockIdx.x * 4u + unsigned(wave)) % unsigned(kFp4SinkSlots);
   const uint64_t sink = uint64_t(bitmat + size_t(MG) * kNS * 64) + uint64_t(sslot) * 1024u + 16 * lane;
   const int scale = 0x7F7F7F7F;  // E8M0 1.0 for every block of 32
   const uint64_t in0 = UNI ? in[0] : 0;
@@ -498,16 +497,10 @@ hipError_t launch_tm(const Fp4ArLaunch& a, int64_t* done, hipStream_t stream) {
   const int64_t nchunks = a.ncols / kBlockCols;
   *done = nchunks * kBlockCols;
   if (nchunks == 0) return hipSuccess;
-  // GFRS_FP4_SINK=1: one shared sink slot (A/B only). (The copy-to-sink ablation of
-  // profiles/wide_stripe/r08_tm was a temporary flag here; it made the copies wrong and is gone.)
-  static const int sink_spread = [] {
-    const char* env = std::getenv("GFRS_FP4_SINK");
-    return (env && std::atoi(env) == 1) ? 0 : 1;
-  }();
   const int64_t slots = persistent_slots(occ, 1, nchunks);
   gf_gemm_fp4tm_kernel<MG, UNI, COPY><<<unsigned(slots), 256, lds, stream>>>(
       (cptr<uint64_t>)a.in, (cptr<uint64_t>)a.out, (cptr<uint64_t>)a.copy, static_cast<const i32x4*>(a.bitmat), a.k,
-      a.m, a.col0, nchunks, slots, a.in_stride, sink_spread);
+      a.m, a.col0, nchunks, slots, a.in_stride);
   return hipGetLastError();
 }
 

@@ -184,20 +184,9 @@ PYBIND11_MODULE(_hip, m) {
                              ncols, mg_cap, in_stride, copies, as_stream(stream)),
           "gf_gemm_fp4");
   });
-  m.def("gemm_fp4r", [](uint64_t bitmat, uint64_t desc, int k, int mm, int64_t col0, int64_t ncols, int mg,
-                        int64_t in_stride, bool copies, uint64_t stream) {
-    check(launch_gf_gemm_fp4r(reinterpret_cast<const void*>(bitmat), reinterpret_cast<const void*>(desc), k, mm, col0,
-                              ncols, mg, in_stride, copies, as_stream(stream)),
-          "gf_gemm_fp4r");
-  });
-  m.def("fp4r_choose_mg", [](int k, int mm) { return fp4r_choose_mg(k, mm); });
-  m.def("fp4r_bitmat_bytes", [](int k, int mm, int mg) { return fp4r_bitmat_bytes(k, mm, mg); });
-  m.def("fp4r_bitmat", [](uint64_t coeff, int ld, uint64_t sel, int mm, int k, uint64_t bitmat, int mg,
-                          uint64_t stream) {
-    check(launch_fp4r_bitmat(reinterpret_cast<const uint8_t*>(coeff), ld, reinterpret_cast<const int*>(sel), mm, k,
-                             reinterpret_cast<void*>(bitmat), mg, as_stream(stream)),
-          "fp4r_bitmat");
-  });
+  m.def("fp4_route", [](int k, int mm, bool copies, int mg_cap) { return std::string(fp4_route_name(k, mm, copies, mg_cap)); },
+        py::arg("k"), py::arg("m"), py::arg("copies") = false, py::arg("mg_cap") = 8,
+        "the FP4 kernel form (v1 / ar / tm) launch_gf_gemm_fp4 runs for this shape");
   m.def("gemm_fp4_batched", [](uint64_t bitmat, uint64_t desc, int k, int mm, int batch, int64_t col0, int64_t ncols,
                                int mg_cap, int64_t in_stride, int64_t in_bstride, int64_t out_bstride, bool copies,
                                uint64_t stream) {

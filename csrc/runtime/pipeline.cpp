@@ -1,5 +1,6 @@
 // Host<->device streaming pipeline. See gfrs/pipeline.h for the design notes.
 #include "gfrs/pipeline.h"
+#include "gfrs/tune.h"
 #include "gfrs/trace.h"
 
 #include <algorithm>
@@ -175,16 +176,13 @@ struct Run {
 
 // Largest host row pitch a 2-D copy is given. hipMemcpy2DAsync's pitches are size_t, but the DMA
 // engines' pitch fields are narrower than that; beyond 2^31 - 1 (a non-streamed bin/RS run of a big
-// file with small k: C of several GiB) rows are copied one by one. GFRS_MAX_RECT_PITCH lowers the
-// cap (tests exercise the fallback with small rows).
+// file with small k: C of several GiB) rows are copied one by one. GFRS_TUNE=max_rect_pitch=N
+// lowers the cap (tests exercise the fallback with small rows).
 int64_t max_rect_pitch() {
   static const int64_t cap = [] {
-    int64_t c = (int64_t(1) << 31) - 1;
-    if (const char* e = std::getenv("GFRS_MAX_RECT_PITCH")) {
-      const long long v = std::atoll(e);
-      if (v > 0 && v < c) c = v;
-    }
-    return c;
+    const int64_t c = (int64_t(1) << 31) - 1;
+    const int64_t v = tune_int("max_rect_pitch", c);
+    return v > 0 && v < c ? v : c;
   }();
   return cap;
 }
@@ -272,12 +270,9 @@ bool zc_one_tile(int m, int field_w) { return pad_m(m) <= (field_w == 16 ? 8 : k
 // 8-25 ms on first use (the first stream even more), and the null stream is the one queue the
 // synchronous descriptor upload uses anyway (scripts/setup_probe.cpp, profiles/host_pipeline/r07_zc2:
 // a dedicated stream put 21-23 ms of stream creation plus 8 ms of null-stream bring-up into the
-// setup; the null stream alone costs ~26 ms once). GFRS_ZC_STREAM=own restores a stream of its own.
+// setup; the null stream alone costs ~26 ms once). GFRS_TUNE=zc_stream=own restores a stream of its own.
 bool zc_null_stream() {
-  static const bool v = [] {
-    const char* e = std::getenv("GFRS_ZC_STREAM");
-    return !(e && std::string(e) == "own");
-  }();
+  static const bool v = tune_str("zc_stream") != "own";
   return v;
 }
 

@@ -46,11 +46,9 @@ def flat_rows(t: torch.Tensor) -> torch.Tensor:
 
 
 def _row_align() -> int:
-    import os
-    try:
-        a = int(os.environ.get("GFRS_ROW_ALIGN", str(2 << 20)))
-    except ValueError:
-        a = 0
+    from ..utils.tune import tune_int
+
+    a = tune_int("row_align", 2 << 20)
     # a power of two of at least 256 (rows stay 16-byte aligned), else the default
     return a if a >= PITCH and (a & (a - 1)) == 0 else 2 << 20
 
@@ -62,7 +60,7 @@ def row_pitch(ncols: int, device="cuda") -> int:
     ``profiles/headline/r07_pitch``): the k=10 encode pattern (10 rows in, 4 out) streams at
     6.26 TB/s with 2 MiB-aligned rows against 5.93 at 256-byte pitch, the decode pattern (10 in,
     10 out) at 5.77 against 5.33 — the rows' placement in HBM's channel interleave, not the kernel.
-    ``GFRS_ROW_ALIGN`` (bytes, power of two, 256 = the old layout) overrides the large-row
+    ``GFRS_TUNE=row_align=N`` (bytes, power of two, 256 = the old layout) overrides the large-row
     alignment."""
     p = max(PITCH, (ncols + PITCH - 1) // PITCH * PITCH)
     if torch.device(device).type == "cuda" and ncols >= (8 << 20):

@@ -16,6 +16,7 @@ import torch
 
 from .. import gf
 from .._native import hip
+from ..utils.tune import tune_int, tune_str
 
 MAX_TILE = 16
 
@@ -256,11 +257,10 @@ class GemmPlan:
             stride = ptrs[1] - ptrs[0] if self.k > 1 else 1
             uniform = stride != 0 and all(p - ptrs[0] == j * stride for j, p in enumerate(ptrs))
             self.in_stride = stride if uniform else 0
-            # FP4 kernel family: "lds" (gf_mfma_fp4.hip / gf_mfma_fp4ar.hip: LDS-DMA input rings, one
-            # wave per SIMD) or "r" (gf_mfma8r.hip: register-streamed input, two waves per SIMD);
-            # each has its own bit-matrix layout
-            self.fp4_form = _fp4_form(self.k, self.m, self.batch, self.copies is not None) if engine == "mfma" else None
-            self.fp4r_mg = hip().fp4r_choose_mg(self.k, self.m) if self.fp4_form == "r" else 0
+            # the FP4 kernel form the native router runs for this shape (v1 / ar / tm:
+            # fp4_route in csrc/kernels/gf_mfma_fp4.hip; one bit-matrix layout serves all three)
+            self.fp4_form = (hip().fp4_route(self.k, self.m, self.copies is not None, mfma_mg)
+                             if engine == "mfma" and self.batch == 1 else None)
             if coeff is not None:
                 self._build_bitmat(coeff)
             else:  # filled on device later (set_device_coeff / invert_into_plan)
@@ -277,8 +277,6 @@ class GemmPlan:
         self._mark_ready()
 
     def _bitmat_bytes(self) -> int:
-        if self.engine == "mfma" and self.fp4_form == "r":
-            return hip().fp4r_bitmat_bytes(self.k, self.m, self.fp4r_mg)
         if self.engine == "mfma":
             return hip().fp4_bitmat_bytes(self.k, self.m, self.mfma_mg)
         return hip().mfma_bitmat_bytes(self.k, self.m)
@@ -289,11 +287,7 @@ class GemmPlan:
         c = c.to(self.device)
         h = hip()
         st = torch.cuda.current_stream(self.device).cuda_stream
-        if self.engine == "mfma" and self.fp4_form == "r":
-            if self.bitmat is None:
-                self.bitmat = torch.empty(self._bitmat_bytes(), dtype=torch.uint8, device=self.device)
-            h.fp4r_bitmat(c.data_ptr(), self.k, 0, self.m, self.k, self.bitmat.data_ptr(), self.fp4r_mg, st)
-        elif self.engine == "mfma":
+        if self.engine == "mfma":
             if self.bitmat is None:
                 self.bitmat = torch.empty(h.fp4_bitmat_bytes(self.k, self.m, self.mfma_mg), dtype=torch.uint8,
                                           device=self.device)
@@ -321,12 +315,8 @@ class GemmPlan:
             sel = rows.data_ptr()
         elif coeff.shape[0] < self.m:
             raise ValueError("coeff needs m rows")
-        if self.fp4_form == "r":
-            hip().fp4r_bitmat(coeff.data_ptr(), coeff.stride(0), sel, self.m, self.k, self.bitmat.data_ptr(),
-                              self.fp4r_mg, st.cuda_stream)
-        else:
-            hip().fp4_bitmat_sel(coeff.data_ptr(), coeff.stride(0), sel, self.m, self.k, self.bitmat.data_ptr(),
-                                 self.mfma_mg, st.cuda_stream)
+        hip().fp4_bitmat_sel(coeff.data_ptr(), coeff.stride(0), sel, self.m, self.k, self.bitmat.data_ptr(),
+                             self.mfma_mg, st.cuda_stream)
         if not torch.cuda.is_current_stream_capturing():
             coeff.record_stream(st)
 
@@ -383,9 +373,6 @@ class GemmPlan:
                 raise ValueError("kernel variants are not selectable on batched plans")
             h.gemm_batched(int(self.desc.data_ptr()), self.k, self.m_pad, self.batch, col0, ncols, self.bytewise, s,
                            self.has_copies)
-        elif self.engine == "mfma" and vec is None and col0 % 2 == 0 and self.fp4_form == "r":
-            h.gemm_fp4r(int(self.bitmat.data_ptr()), int(self.desc.data_ptr()), self.k, self.m, col0, ncols,
-                        self.fp4r_mg, self.in_stride, self.has_copies, s)
         elif self.engine == "mfma" and vec is None and col0 % 2 == 0:
             h.gemm_fp4(int(self.bitmat.data_ptr()), int(self.desc.data_ptr()), self.k, self.m, col0, ncols,
                        self.mfma_mg, self.in_stride, self.has_copies, s)
@@ -399,22 +386,6 @@ class GemmPlan:
             h.gemm(int(self.desc.data_ptr()), self.k, self.m_pad, col0, ncols, False, max_blocks, s, self.has_copies)
         else:
             h.gemm_variant(int(self.desc.data_ptr()), self.k, self.m_pad, col0, ncols, vec, pf, nt, max_blocks, s)
-
-
-def _fp4_form(k: int, m: int, batch: int, copies: bool) -> str:
-    """Which FP4 kernel family a single-stripe ``engine="mfma"`` plan runs: ``GFRS_FP4_FORM=r|lds``
-    forces one; batched plans always take the LDS family's batched kernel. The LDS ring is the
-    default everywhere: the register-streamed form lost at every measured GF(2^8) shape
-    (k = 128: 906-918 vs 794-804 us plain, 1331-1366 vs 911-993 with copies;
-    profiles/wide_stripe/r08_fp4r), unlike its GF(2^16) sibling."""
-    import os
-
-    forced = os.environ.get("GFRS_FP4_FORM")
-    if batch > 1:
-        return "lds"
-    if forced in ("r", "lds"):
-        return forced
-    return "lds"
 
 
 # wide stripes go to the FP4 matrix-core kernel: measured on MI355X (profiles/archive/r01_kbench5) it wins
@@ -437,8 +408,8 @@ _SHORT_ROW, _MID_ROW = 512 << 10, 4 << 20
 # us, 256 x 1 MiB 419 -> 221 us; decode rebuilding 26 natives (+ 102 fused copies) 256 x 1 MiB
 # 451 -> 256 us; rebuilding 8: 16 x 1 MiB 32.3 -> 28.1 but 256 x 1 MiB 150 -> 166 (v_perm kept);
 # rebuilding 4 (memory-bound beside 124 copies) stays on the v_perm kernels. (scripts/serve_bench.py --code 128:160;
-# GFRS_FP4_BATCH_MIN_COLS overrides, e.g. a huge value keeps every batch on the v_perm kernels.)
-_FP4_BATCH_MIN_COLS = int(__import__("os").environ.get("GFRS_FP4_BATCH_MIN_COLS", 256))
+# GFRS_TUNE=fp4_batch_min_cols=N overrides, e.g. a huge value keeps every batch on the v_perm kernels.)
+_FP4_BATCH_MIN_COLS = 256
 _FP4_BATCH_MID_COLS = 1 << 20
 
 
@@ -447,7 +418,7 @@ def _auto_engine(k: int, m: int, gf256: bool, bytewise: bool, batch: int, ncols:
     if not gf256 or bytewise:
         return "valu"
     if batch != 1:  # (a narrow decode — few rebuilt rows beside many fused copies — is memory-bound)
-        if not batch_fp4 or ncols is None or ncols < _FP4_BATCH_MIN_COLS:
+        if not batch_fp4 or ncols is None or ncols < tune_int("fp4_batch_min_cols", _FP4_BATCH_MIN_COLS):
             return "valu"
         return "mfma" if (m >= 16 or (m >= 8 and ncols * batch <= _FP4_BATCH_MID_COLS)) else "valu"
     if k >= _MFMA_MIN_K and m >= _MFMA_MIN_M:
@@ -485,16 +456,14 @@ def _batch_strides(stripes_in, stripes_out, stripes_copy=None) -> tuple[int, int
 # w = 16 kernel, 1 GiB stripes (profiles/gf65536/r08_mfma16): encodes win from k = 16 at any m
 # (k=16, m=4: 0.30 vs 0.40 ms; k=300, m=40: 1.98 vs 4.49), k = 10 loses (0.55 vs 0.48). Decodes,
 # which also copy the survivors, lose at m = 4 (k=16: 0.51 vs 0.43) and win from m = 8 on wider
-# codes (k=64, m=8: 0.62 vs 0.73; k=300, m=40: 2.43 vs 4.52). (GFRS_GF16_MFMA=0 / 1: never /
+# codes (k=64, m=8: 0.62 vs 0.73; k=300, m=40: 2.43 vs 4.52). (GFRS_TUNE=gf16_mfma=0 / 1: never /
 # always where supported.)
 _GF16_MFMA_MIN_K = 16
 _GF16_MFMA_COPY_MIN_M, _GF16_MFMA_COPY_MIN_KM = 8, 256
 
 
 def _auto_engine16(k: int, m: int, symwise: bool, copies: bool = False) -> bool:
-    import os
-
-    forced = os.environ.get("GFRS_GF16_MFMA")
+    forced = tune_str("gf16_mfma")
     if symwise or k > 65535:
         return False
     if forced is not None:

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Median kernel time of wide FP4 GEMM shapes (k=128; m rebuilt rows; optional fused copies), one
-JSON line. Run once per environment setting to A/B kernel choices (e.g. GFRS_FP4_EXACT_MG=0)."""
+JSON line, with the form the router ran. Run once per GFRS_TUNE=fp4=... setting (v1 / ar / tm) to A/B
+the FP4 kernel forms."""
 from __future__ import annotations
 
 import json
@@ -22,7 +23,7 @@ def main():
     data = alloc_rows(k, C, "cuda")
     fill_random_(flat_rows(data), seed=3)
     dst = alloc_rows(k, C, "cuda")
-    res = {"env": {x: os.environ.get(x) for x in ("GFRS_FP4_EXACT_MG", "GFRS_FP4_KERNEL", "GFRS_FP4_COPY", "GFRS_FP4_SINK")}}
+    res = {"env": {"GFRS_TUNE": os.environ.get("GFRS_TUNE")}}
     rng = np.random.default_rng(5)
     ms = [int(x) for x in sys.argv[1].split(",")] if len(sys.argv) > 1 else [20, 24, 28, 32]
     if "--scattered" in sys.argv:  # inputs as separate allocations (the row-pointer-table kernels)
@@ -51,8 +52,9 @@ def main():
             ok = np.array_equal(out[:, :cols].cpu().numpy(), gf.GF256.gemm(coeff, src.cpu().numpy()))
             if ncopy:
                 ok = ok and all(torch.equal(dst[j], data[j]) for j in range(ncopy))
+            from gpu_rscode_amd._native import hip
             res[f"m{m}_copies{ncopy}"] = {"median_us": round(float(np.median(ts)), 1), "min_us": round(min(ts), 1),
-                                          "ok": bool(ok)}
+                                          "ok": bool(ok), "form": hip().fp4_route(k, m, bool(ncopy), 8)}
     print(json.dumps(res), flush=True)
 
 

@@ -84,7 +84,7 @@ r_setup() {  # bin/RS device + host setup breakdown, 1 GiB encode + decode (THP-
   step setup_dec2 120 bin/RS -d -i $F -c /tmp/rs_conf -o /tmp/rs_out.bin -s 2 &&
   step setup_enc_hhm 120 env GFRS_HOST_ALLOC=hipHostMalloc bin/RS -k 10 -n 14 -e $F -s 2 &&
   step setup_dec_hhm 120 env GFRS_HOST_ALLOC=hipHostMalloc bin/RS -d -i $F -c /tmp/rs_conf -o /tmp/rs_out.bin -s 2 &&
-  step setup_enc_serial 120 env GFRS_SETUP=serial bin/RS -k 10 -n 14 -e $F -s 2 &&
+  step setup_enc_serial 120 env GFRS_TUNE=setup=serial bin/RS -k 10 -n 14 -e $F -s 2 &&
   step setup_stream_enc 120 bin/RS -k 10 -n 14 -e $F --window 0 --no-sync -s 4 &&
   step setup_stream_dec 120 bin/RS -d -i $F -c /tmp/rs_conf -o /tmp/rs_out2.bin --window 0 --no-sync -s 4 &&
   step setup_cmp2 60 cmp $F /tmp/rs_out2.bin
@@ -130,9 +130,9 @@ r_wide() {  # wide-stripe FP4 kernel shapes (k=128, m rebuilt rows, with / witho
   local i
   for i in 1 2; do
     step wide_default_$i 300 $PY scripts/fp4_shapes.py ${WIDE_MS:-20,24,26,28,32} &&
-    step wide_default_sink1_$i 300 env GFRS_FP4_SINK=1 $PY scripts/fp4_shapes.py ${WIDE_MS:-20,24,26,28,32} &&
-    step wide_ar_$i 300 env GFRS_FP4_KERNEL=ar $PY scripts/fp4_shapes.py ${WIDE_MS:-20,24,26,28,32} &&
-    step wide_ar_sink1_$i 300 env GFRS_FP4_KERNEL=ar GFRS_FP4_SINK=1 $PY scripts/fp4_shapes.py ${WIDE_MS:-20,24,26,28,32} || return 1
+    step wide_v1_$i 300 env GFRS_TUNE=fp4=v1 $PY scripts/fp4_shapes.py ${WIDE_MS:-20,24,26,28,32} &&
+    step wide_ar_$i 300 env GFRS_TUNE=fp4=ar $PY scripts/fp4_shapes.py ${WIDE_MS:-20,24,26,28,32} &&
+    step wide_tm_$i 300 env GFRS_TUNE=fp4=tm $PY scripts/fp4_shapes.py ${WIDE_MS:-20,24,26,28,32} || return 1
   done
 }
 r_e2efull() {  # host pipeline, the reference's decode shape (k=10 in, all 10 natives out) and the encode shape

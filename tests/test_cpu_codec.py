@@ -326,14 +326,14 @@ def test_plan_cache_is_lru():
 def test_row_pitch_layout(monkeypatch):
     """alloc_rows / row_pitch: every pitch a multiple of 256 (16-byte aligned rows for odd C);
     device rows of >= 8 MiB rounded to 2 MiB (measured HBM placement win), host rows never;
-    GFRS_ROW_ALIGN overrides the large-row alignment."""
+    GFRS_TUNE=row_align overrides the large-row alignment."""
     from gpu_rscode_amd.models.rs import alloc_rows, row_pitch
     C = 107374183  # the headline chunk (1 GiB / 10, odd)
     assert row_pitch(C, "cpu") == 107374336
     assert row_pitch(C, "cuda") % (2 << 20) == 0 and row_pitch(C, "cuda") >= C
     assert row_pitch(1000, "cuda") == 1024 and row_pitch(1, "cuda") == 256
     assert row_pitch((8 << 20) - 1, "cuda") == 8 << 20
-    monkeypatch.setenv("GFRS_ROW_ALIGN", "256")
+    monkeypatch.setenv("GFRS_TUNE", "row_align=256")
     assert row_pitch(C, "cuda") == 107374336
     t = alloc_rows(3, 1001, "cpu", fill=7)
     assert t.shape == (3, 1001) and t.stride() == (1024, 1) and int(t.sum()) == 7 * 3 * 1001

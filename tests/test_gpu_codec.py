@@ -472,7 +472,7 @@ print("DRS-RCCL-OK")
 
 def test_host_pipeline_rows_beyond_the_2d_pitch_cap_copy_row_by_row():
     """Equally spaced host rows whose pitch exceeds the 2-D copy cap (2^31 - 1; lowered here with
-    GFRS_MAX_RECT_PITCH) move as per-row copies and still encode exactly."""
+    GFRS_TUNE=max_rect_pitch) move as per-row copies and still encode exactly."""
     code = r'''
 import numpy as np, torch
 from gpu_rscode_amd._native import hip
@@ -486,7 +486,7 @@ hip().gemm_host([0], [host[j].data_ptr() for j in range(k)], [par[i].data_ptr() 
 assert np.array_equal(par.numpy(), GF256.gemm(e, host.numpy()))
 print("PITCH-CAP-OK")
 '''
-    env = dict(os.environ, GFRS_MAX_RECT_PITCH="4096")
+    env = dict(os.environ, GFRS_TUNE="max_rect_pitch=4096")
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     r = subprocess.run(["python", "-c", code], capture_output=True, text=True, timeout=180, env=env, cwd=root)
     assert r.returncode == 0 and "PITCH-CAP-OK" in r.stdout, (r.stdout[-2000:], r.stderr[-3000:])

@@ -280,7 +280,7 @@ def test_batched_w16_encode_decode(k, n, C, B, engine_env, monkeypatch):
     """GF(2^16) batched launches (ReedSolomon.encode_batch / decode_batch): B stripes in one call,
     on the matrix cores (stripes at fixed strides; every stripe's ragged rest on the batched v_perm
     kernel) and on the batched v_perm kernel alone; decode copies the survivors in the same pass."""
-    monkeypatch.setenv("GFRS_GF16_MFMA", engine_env)
+    monkeypatch.setenv("GFRS_TUNE", f"gf16_mfma={engine_env}")
     rs = ReedSolomon(k, n, field="gf65536", matrix="cauchy")
     data = torch.stack([_rand(k, C, 100 + b) for b in range(B)]).cuda()
     par = rs.encode_batch(data)

@@ -8,6 +8,7 @@ from gpu_rscode_amd.gf import GF256
 from gpu_rscode_amd.models import alloc_rows
 from gpu_rscode_amd.ops import GemmPlan, fill_random_, gen_matrix_device, gf_invert, invert_into_plan
 from gpu_rscode_amd.ops.gemm import perm_tables_from_coeff
+from gpu_rscode_amd.utils.tune import with_tune
 
 pytestmark = pytest.mark.gpu
 
@@ -349,13 +350,13 @@ def test_fp4_fused_copy_decode_shape(m):
 @pytest.mark.parametrize("variant", ["uniform", "scattered", "copy"])
 @pytest.mark.parametrize("nblk", [256 * 3 + 5, 256 * 2, 40])
 def test_fp4_tile_major_kernel_matches_oracle(k, m, variant, nblk, monkeypatch):
-    """The tile-major FP4 kernel (gf_gemm_fp4tm_kernel, GFRS_FP4_KERNEL=tm: the chunk's B resident
+    """The tile-major FP4 kernel (gf_gemm_fp4tm_kernel, GFRS_TUNE=fp4=tm: the chunk's B resident
     in AGPRs, tiles in turn, 5..7 M-tiles). Column counts give the persistent blocks an odd or an
     even number of chunks (the phantom chunk and the drain after the loop) or a single one, plus a
     v_perm remainder. The fused copy covers the first inputs only (the decode layout). Bit-exact
     against the oracle, and nothing is written outside the outputs' and copies' columns."""
     _native_loaded()
-    monkeypatch.setenv("GFRS_FP4_KERNEL", "tm")
+    monkeypatch.setenv("GFRS_TUNE", "fp4=tm")
     ncols = 256 * nblk + 77
     rng = np.random.default_rng(k * 131 + m * 7 + nblk)
     coeff = rng.integers(0, 256, size=(m, k), dtype=np.uint8)
@@ -452,50 +453,69 @@ def test_decode_system_matches_host_decode_matrix(k, n, matrix):
     assert checked > 0
 
 
-@pytest.mark.parametrize("k,m", [(128, 32), (128, 16), (120, 24), (113, 17), (100, 17), (40, 32)])
-@pytest.mark.parametrize("variant", ["uniform", "scattered", "copy"])
-def test_fp4_staggered_kernel_matches_v1_and_oracle(k, m, variant, monkeypatch):
-    """The tile-staggered FP4 kernel (gf_gemm_fp4sk_kernel, k in (112, 128]: M-tile mt runs K-step
-    (j - mt) of its chunk, one tile's epilogue per step, a phantom chunk draining the last one)
-    with 4 or 8 M-tiles, padding output rows, uniform / scattered / fused-copy inputs and a column
-    count giving the persistent blocks several chunks plus a v_perm remainder — bit-exact against
-    the oracle and against the single-schedule kernel (GFRS_FP4_KERNEL=v1). Other k run v1 both
-    times (a control)."""
+# every form the FP4 router (fp4_route, csrc/kernels/gf_mfma_fp4.hip) returns, with its shapes
+_ROUTE_CASES = [(128, 8, False, "v1"), (128, 12, True, "v1"), (128, 16, False, "ar"), (128, 16, True, "ar"),
+                (128, 20, False, "tm"), (128, 20, True, "tm"), (128, 24, False, "tm"), (128, 24, True, "v1"),
+                (128, 26, True, "tm"), (128, 28, False, "tm"), (128, 32, False, "ar"), (128, 32, True, "v1"),
+                (128, 40, False, "v1"), (100, 17, True, "v1"), (40, 32, False, "v1")]
+
+
+@pytest.mark.parametrize("k,m,copy,form", _ROUTE_CASES)
+@pytest.mark.parametrize("scattered", [False, True])
+def test_fp4_router_every_form_matches_oracle(k, m, copy, form, scattered):
+    """Every form the router can return (v1 LDS ring, A-resident, tile-major) on the shapes it is
+    routed to, uniform or scattered inputs, fused copies: the plan reports the form, and outputs and
+    copies are bit-exact against the oracle, with several chunks per persistent block and a v_perm
+    remainder; nothing is written outside the outputs and the copy rows."""
     _native_loaded()
     ncols = 256 * (256 * 3 + 5) + 77
-    rng = np.random.default_rng(k * 31 + m)
+    rng = np.random.default_rng(k * 31 + m + 7 * copy)
     coeff = rng.integers(0, 256, size=(m, k), dtype=np.uint8)
     host, dev = _rand_rows(k, ncols, k + m)
     inputs, want_in = dev, host
-    copies = None
-    if variant in ("scattered", "copy"):
+    if scattered or copy:
         perm = rng.permutation(k)
         inputs = [dev[j].clone() for j in perm]
         want_in = host[perm]
-    if variant == "copy":
+    copies = None
+    if copy:
         cdst = alloc_rows(k, ncols, "cuda", fill=0x44)
         copies = [cdst[j] if j % 4 else None for j in range(k)]
-    results = []
-    for kernel in ("sk", "v1", "ar") + (("split",) if variant == "copy" else ()):
-        if kernel == "split":  # the plain kernel + the side-stream copy kernel (GFRS_FP4_COPY=split)
-            monkeypatch.delenv("GFRS_FP4_KERNEL", raising=False)
-            monkeypatch.setenv("GFRS_FP4_COPY", "split")
-        else:
-            monkeypatch.setenv("GFRS_FP4_KERNEL", kernel)  # "sk" also forces the fused-copy form onto it
-        out = alloc_rows(m, ncols, "cuda", fill=0x5A)
-        if copies is not None:
-            cdst.fill_(0x44)
+    out = alloc_rows(m, ncols, "cuda", fill=0x5A)
+    plan = GemmPlan(inputs, out, coeff, copies=copies, engine="mfma")
+    assert plan.fp4_form == form
+    plan.run()
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), GF256.gemm(coeff, want_in)), form
+    if copies is not None:
+        c = cdst.cpu().numpy()
+        for j in range(k):
+            assert np.array_equal(c[j], want_in[j] if j % 4 else np.full(ncols, 0x44, np.uint8)), (form, j)
+
+
+@pytest.mark.parametrize("k,m,copy", [(128, 26, True), (128, 24, False), (128, 16, True)])
+def test_fp4_forced_forms_agree(k, m, copy, monkeypatch):
+    """GFRS_TUNE=fp4=v1 / ar / tm (the A/B override) on a shape each of them is built for: the
+    three forms give identical bytes."""
+    _native_loaded()
+    ncols = 256 * 600 + 33
+    rng = np.random.default_rng(k + m)
+    coeff = rng.integers(0, 256, size=(m, k), dtype=np.uint8)
+    host, dev = _rand_rows(k, ncols, 5 * m)
+    inputs = [dev[j].clone() for j in range(k)]
+    cdst = alloc_rows(k, ncols, "cuda", fill=0) if copy else None
+    copies = [cdst[j] if j < k - m else None for j in range(k)] if copy else None
+    got = {}
+    for kernel in ("v1", "ar", "tm"):
+        monkeypatch.setenv("GFRS_TUNE", f"fp4={kernel}")
+        out = alloc_rows(m, ncols, "cuda", fill=0)
         plan = GemmPlan(inputs, out, coeff, copies=copies, engine="mfma")
         plan.run()
         torch.cuda.synchronize()
-        got = out.cpu().numpy()
-        assert np.array_equal(got, GF256.gemm(coeff, want_in)), kernel
-        if copies is not None:
-            c = cdst.cpu().numpy()
-            for j in range(k):
-                assert np.array_equal(c[j], want_in[j] if j % 4 else np.full(ncols, 0x44, np.uint8)), (kernel, j)
-        results.append(got)
-    assert all(np.array_equal(results[0], r) for r in results[1:])
+        got[kernel] = out.cpu().numpy()
+        assert np.array_equal(got[kernel], GF256.gemm(coeff, host)), kernel
+        if copy:
+            assert np.array_equal(cdst.cpu().numpy()[: k - m], host[: k - m])
 
 
 @pytest.mark.parametrize("k,m", [(128, 32), (128, 28), (128, 24), (128, 20), (127, 13), (120, 8), (113, 4), (128, 1)])
@@ -520,7 +540,7 @@ def test_fp4_a_resident_kernel_matches_oracle(k, m, variant, monkeypatch):
     if variant == "copy":
         cdst = alloc_rows(k, ncols, "cuda", fill=0x44)
         copies = [cdst[j] if j % 3 else None for j in range(k)]
-    monkeypatch.setenv("GFRS_FP4_KERNEL", "ar")
+    monkeypatch.setenv("GFRS_TUNE", "fp4=ar")
     out = alloc_rows(m, ncols, "cuda", fill=0x5A)
     plan = GemmPlan(inputs, out, coeff, copies=copies, engine="mfma")
     plan.run()
@@ -596,7 +616,7 @@ print("FORMS-OK")
 
 @pytest.mark.parametrize("lat_groups", ["0", "1000000000"])
 def test_rows_kernel_forms_match_oracle(lat_groups):
-    """Both forms of the rows-in-flight kernel on the same shapes: GFRS_ROWS_LAT_GROUPS=0 forces the
+    """Both forms of the rows-in-flight kernel on the same shapes: GFRS_TUNE=rows_lat_groups=0 forces the
     throughput form (the 1 GiB headline's; small test launches otherwise take the latency form),
     10^9 the latency form (also for fused-copy decodes). Subprocess: the threshold is read once."""
     import os
@@ -604,7 +624,7 @@ def test_rows_kernel_forms_match_oracle(lat_groups):
     import sys
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, GFRS_ROWS_LAT_GROUPS=lat_groups)
+    env = with_tune(rows_lat_groups=lat_groups)
     r = subprocess.run([sys.executable, "-c", _FORMS_SNIPPET % root], capture_output=True, text=True, timeout=300,
                        env=env)
     assert r.returncode == 0 and "FORMS-OK" in r.stdout, (r.stdout[-2000:], r.stderr[-3000:])
@@ -643,15 +663,15 @@ print("WIDE-OK")
 @pytest.mark.parametrize("knobs", [("0", "0"), ("0", "1000000000000"), ("1000000000000", "0")])
 def test_batched_wide_kernels_match_oracle(knobs):
     """Batched wide-code launches on every kernel that can take them: the vec kernel at its widest
-    tile (both knobs 0), with the tile narrowed for short rows (GFRS_SHORT_LANES), and the k-split
-    kernel (GFRS_KSPLIT_LANES, LDS reduction over row slices; ragged columns and fused copies
+    tile (both knobs 0), with the tile narrowed for short rows (GFRS_TUNE short_lanes), and the k-split
+    kernel (GFRS_TUNE ksplit_lanes, LDS reduction over row slices; ragged columns and fused copies
     included). Subprocess: the thresholds are read once."""
     import os
     import subprocess
     import sys
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, GFRS_KSPLIT_LANES=knobs[0], GFRS_SHORT_LANES=knobs[1])
+    env = with_tune(ksplit_lanes=knobs[0], short_lanes=knobs[1])
     r = subprocess.run([sys.executable, "-c", _WIDE_BATCH_SNIPPET % root], capture_output=True, text=True,
                        timeout=300, env=env)
     assert r.returncode == 0 and "WIDE-OK" in r.stdout, (r.stdout[-2000:], r.stderr[-3000:])

@@ -17,7 +17,7 @@ HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 
 
 @pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
-@pytest.mark.parametrize("name", ["gf_mfma16", "gf_mfma8r", "gf_mfma_fp4", "gf_mfma_fp4ar", "gf_mfma_fp4tm"])
+@pytest.mark.parametrize("name", ["gf_mfma16", "gf_mfma_fp4", "gf_mfma_fp4ar", "gf_mfma_fp4tm"])
 def test_no_unguarded_accumulator_reads(name, tmp_path):
     asm = tmp_path / f"{name}.s"
     # (compiled as csrc/Makefile does: the A-resident and tile-major kernels in MFMA VGPR form)

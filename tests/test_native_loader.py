@@ -52,3 +52,28 @@ def test_file_lock_serialises_processes():
         assert p.exitcode == 0
     ev = sorted((q.get(timeout=5) for _ in range(6)), key=lambda x: x[1])
     assert [e[0] for e in ev] == ["in", "out"] * 3  # no two holders at once
+
+
+def test_fp4_router_table():
+    """The FP4 engine's one routing function (fp4_route, csrc/kernels/gf_mfma_fp4.hip) and its
+    override (GFRS_TUNE=fp4=..., parsed among other keys): k = 128 wide-stripe shapes by M-tile count, plain and with fused copies."""
+    import os
+
+    from gpu_rscode_amd._native import hip
+
+    h = hip()
+    want = {(8, False): "v1", (12, True): "v1", (16, False): "ar", (16, True): "ar", (20, False): "tm",
+            (20, True): "tm", (24, False): "tm", (24, True): "v1", (28, True): "tm", (28, False): "tm",
+            (32, False): "ar", (32, True): "v1", (40, False): "v1"}
+    for (m, copy), form in want.items():
+        assert h.fp4_route(128, m, copy, 8) == form, (m, copy)
+    assert h.fp4_route(100, 17, False, 8) == "v1"  # k outside (112, 128]
+    os.environ["GFRS_TUNE"] = "fp4=v1"
+    try:
+        assert h.fp4_route(128, 28, True, 8) == "tm"  # (no v1 build for 7 tiles: the routed form)
+        assert h.fp4_route(128, 16, True, 8) == "v1"
+        os.environ["GFRS_TUNE"] = "ksplit_lanes=5,fp4=tm"
+        assert h.fp4_route(128, 24, True, 8) == "tm"
+        assert h.fp4_route(128, 16, False, 8) == "ar"  # (not built for 4 tiles: the routed form)
+    finally:
+        del os.environ["GFRS_TUNE"]

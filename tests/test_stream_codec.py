@@ -155,7 +155,7 @@ def test_crc32_combine_matches_zlib():
 def test_crc32_fast_path_matches_zlib_and_the_table_path():
     """The carry-less-multiply CRC-32 (64-byte folds, then 16-byte folds, then the table for the
     tail) equals zlib for every length around its block sizes, unaligned starts and chained seeds;
-    the slicing-by-8 table path (GFRS_CRC_SCALAR=1, a fresh process) gives the same values."""
+    the slicing-by-8 table path (GFRS_TUNE=crc=scalar, a fresh process) gives the same values."""
     import zlib
 
     buf = os.urandom(1 << 18)
@@ -165,7 +165,7 @@ def test_crc32_fast_path_matches_zlib_and_the_table_path():
     assert [cpu().crc32(buf[off:off + n], seed) for n, off, seed in cases] == want
     code = ("import sys, zlib, os; sys.path.insert(0, sys.argv[1]); from gpu_rscode_amd._native import cpu; "
             "b = os.urandom(70_001); assert cpu().crc32(b, 7) == zlib.crc32(b, 7); print('ok')")
-    r = subprocess.run([sys.executable, "-c", code, ROOT], env=dict(os.environ, GFRS_CRC_SCALAR="1"),
+    r = subprocess.run([sys.executable, "-c", code, ROOT], env=dict(os.environ, GFRS_TUNE="crc=scalar"),
                        capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]
 
