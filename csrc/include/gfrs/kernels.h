@@ -70,12 +70,18 @@ hipError_t launch_gf_invert(const uint8_t* a, uint8_t* a_inv, int n, int batch, 
 // natives, ascending, derived from rows. Writes X (e x k uint16) to dm (optional), status (0 ok,
 // 1 singular, 2 invalid survivor list) and, into a desc_layout16 descriptor (k inputs, m_pad >= e
 // outputs), the four v_perm records per coefficient; with ptrs = {chunk row 0..n-1, output row
-// 0..k-1} also the descriptor's row pointers. One workgroup, the system in LDS:
-// decode_system16_supported says whether (n, k, e) fits (e <= 256, ~ 8 e (e + k) + 4 n + 4 k bytes).
+// 0..k-1} also the descriptor's row pointers. Systems that fit one workgroup's LDS
+// (decode_system16_supported: e <= 256, ~ 8 e (e + k) + 4 n + 4 k bytes) are solved there in one
+// launch; larger ones (e.g. k = 2000, e = 100, or any e > 256) by the blocked multi-workgroup solve
+// (panels of pivot columns, row pivoting, rank-P updates over the chip), which needs a device
+// `workspace` of decode_system16_workspace(n, k, e) bytes (-1: too large even for it: e past
+// ~19 K). force_blocked takes the blocked solve for any size (tests).
 bool decode_system16_supported(int n, int k, int e);
+int64_t decode_system16_workspace(int n, int k, int e);
 hipError_t launch_gf_decode_system16(const uint16_t* g, int n, int k, const int* rows, int* erased, int e,
                                      uint16_t* dm, int* status, void* desc, int m_pad, hipStream_t stream,
-                                     const uint64_t* ptrs = nullptr);
+                                     const uint64_t* ptrs = nullptr, void* workspace = nullptr,
+                                     bool force_blocked = false);
 
 // ---- matrix utilities (csrc/kernels/gf_matrix.hip) -------------------------------------------
 // kind: 0 = reference Vandermonde, 1 = Cauchy. Writes the p x k block.

@@ -30,6 +30,8 @@
 #include "gfrs/kernels.h"
 #include "gfrs/perm_device.h"
 
+#include <algorithm>
+
 namespace gfrs {
 namespace {
 
@@ -284,18 +286,415 @@ __global__ __launch_bounds__(kThreads) void gf_decode_system16_kernel(
 
 constexpr size_t kMaxLds16 = 160 * 1024;
 
+// ---- blocked multi-workgroup solve (systems past one workgroup's LDS, or e > 256) --------------
+//
+// The reference's blocked Gauss-Jordan (decode-gj.cu, GPUGausSeidel :1059-1201 with its panel
+// kernels :347-904) is a 4x4-block LU without pivoting on floats that never built; here the same
+// e x (e + k) systematic system as above is reduced in HBM (L2-resident for the sizes that get here)
+// panel by panel, with row pivoting and singular detection:
+//   prep (1 WG)      pattern check and derivation (as above, counts in the workspace: n <= 65535)
+//   gather (grid)    [M | B'] into the workspace, e rows of W = e + k symbols
+//   for each panel of P pivot columns [c0, c0 + P):
+//     panel (1 WG)   the e x P panel in LDS: Gauss-Jordan with row pivoting among the rows not yet
+//                    pivots picks the P pivot rows pi (singular: status 1, every later kernel returns
+//                    at once); snapshots the panel A and writes A[pi]^-1 (P x P, Gauss-Jordan again)
+//     y (grid)       Y = A[pi]^-1 . M[pi] over columns [c0, W)
+//     update (grid)  M[pi_j] = Y_j; every other row r: M_r += A_r . Y  (the rank-P update; columns
+//                    before c0 are already reduced and Y is zero there)
+//   finish (grid)    X[b] = M[piv(b)][e:] (pivot rows end normalised: no scaling), dm / tables /
+//                    row pointers as the one-workgroup kernel writes them
+// Work e^2 (e + k) GF(2^16) products over the panels (e = 500, k = 4000: ~1.1 G), spread over the
+// chip instead of one CU; 3 launches per panel, all on `stream` (graph-capturable).
+struct Ws16 {
+  int* flags;     // [0] bad, [1] parity survivors, [2] singular
+  int* cnt;       // [n]
+  int* erased;    // [e]
+  int* prow;      // [e]
+  int* rows;      // [k]
+  int* used;      // [e] pivot column + 1 of a row that is a pivot, 0 = not yet
+  int* piv;       // [e] pivot row of column c
+  uint16_t* ainv; // [P x P]
+  uint16_t* asn;  // [e x P] panel snapshot
+  uint16_t* y;    // [P x W]
+  uint16_t* m;    // [e x ld]
+  int ld;         // row stride of m (symbols)
+};
+
+constexpr int kPanelMax = 32;
+
+__host__ __device__ constexpr size_t al256(size_t x) { return (x + 255) / 256 * 256; }
+
+struct Ws16Layout {
+  size_t off[11];
+  size_t bytes;
+  int ld;
+};
+
+__host__ __device__ inline Ws16Layout ws16_layout(int n, int k, int e, int P) {
+  Ws16Layout L{};
+  const int W = e + k;
+  L.ld = (W + 7) / 8 * 8;
+  const size_t sz[11] = {32, 4 * size_t(n), 4 * size_t(e), 4 * size_t(e), 4 * size_t(k), 4 * size_t(e),
+                         4 * size_t(e), 2 * size_t(P) * P, 2 * size_t(e) * P, 2 * size_t(P) * W,
+                         2 * size_t(e) * L.ld};
+  size_t o = 0;
+  for (int i = 0; i < 11; ++i) {
+    L.off[i] = o;
+    o += al256(sz[i]);
+  }
+  L.bytes = o;
+  return L;
+}
+
+__host__ __device__ inline Ws16 ws16_of(void* base, int n, int k, int e, int P) {
+  const Ws16Layout L = ws16_layout(n, k, e, P);
+  char* b = static_cast<char*>(base);
+  Ws16 w;
+  w.flags = reinterpret_cast<int*>(b + L.off[0]);
+  w.cnt = reinterpret_cast<int*>(b + L.off[1]);
+  w.erased = reinterpret_cast<int*>(b + L.off[2]);
+  w.prow = reinterpret_cast<int*>(b + L.off[3]);
+  w.rows = reinterpret_cast<int*>(b + L.off[4]);
+  w.used = reinterpret_cast<int*>(b + L.off[5]);
+  w.piv = reinterpret_cast<int*>(b + L.off[6]);
+  w.ainv = reinterpret_cast<uint16_t*>(b + L.off[7]);
+  w.asn = reinterpret_cast<uint16_t*>(b + L.off[8]);
+  w.y = reinterpret_cast<uint16_t*>(b + L.off[9]);
+  w.m = reinterpret_cast<uint16_t*>(b + L.off[10]);
+  w.ld = L.ld;
+  return w;
+}
+
+// LDS of the panel kernel: panel [e][P] | used [e] | factors [e] | misc | pivots | [A[pi] | I]
+__host__ __device__ inline size_t panel_lds(int e, int P) {
+  return al256(size_t(e) * P * 2) + size_t(e) * 4 + size_t((e + 1) & ~1) * 2 + 16 + 4 * kPanelMax +
+         size_t(kPanelMax) * 2 * kPanelMax * 2;
+}
+
+// panel width: the widest power of two <= 32 whose panel kernel fits the LDS
+__host__ __device__ inline int panel_of(int e) {
+  int P = kPanelMax;
+  while (P > 4 && panel_lds(e, P) > kMaxLds16) P >>= 1;
+  return P;
+}
+
+__device__ __forceinline__ bool ws_failed(const Ws16& w) {
+  return *reinterpret_cast<volatile int*>(&w.flags[0]) || *reinterpret_cast<volatile int*>(&w.flags[2]);
+}
+
+__global__ __launch_bounds__(kThreads) void ds16_prep_kernel(const int* __restrict__ rows, int n, int k, int e,
+                                                             Ws16 w, int* __restrict__ erased_out) {
+  const int tid = threadIdx.x;
+  constexpr int B = kThreads;
+  __shared__ int bad_s, pcount_s;
+  for (int i = tid; i < n; i += B) w.cnt[i] = 0;
+  for (int i = tid; i < e; i += B) w.used[i] = 0;
+  if (tid == 0) {
+    bad_s = 0;
+    pcount_s = 0;
+  }
+  __syncthreads();  // (the block's own global writes: visible to it after the barrier)
+  for (int i = tid; i < k; i += B) {
+    const int r = rows[i];
+    const bool ok = r >= 0 && r < n;
+    w.rows[i] = ok ? r : 0;
+    if (ok) atomicAdd(&w.cnt[r], 1);
+    else bad_s = 1;
+  }
+  __syncthreads();
+  for (int i = tid; i < n; i += B)
+    if (w.cnt[i] > 1) bad_s = 1;  // a chunk listed twice
+  if (tid < 64) {  // erased natives (ascending) and parity survivors (survivor order)
+    int base = 0;
+    for (int i0 = 0; i0 < k; i0 += 64) {
+      const int i = i0 + tid;
+      const bool miss = i < k && w.cnt[i] == 0;
+      const unsigned long long bal = __ballot(miss);
+      const int a = base + __popcll(bal & ((1ull << tid) - 1ull));
+      if (miss && a < e) w.erased[a] = i;
+      base += __popcll(bal);
+    }
+    if (tid == 0 && base != e) bad_s = 1;
+    int pbase = 0;
+    for (int j0 = 0; j0 < k; j0 += 64) {
+      const int j = j0 + tid;
+      const bool is_par = j < k && w.rows[j] >= k;
+      const unsigned long long bal = __ballot(is_par);
+      const int a = pbase + __popcll(bal & ((1ull << tid) - 1ull));
+      if (is_par && a < e) w.prow[a] = w.rows[j];
+      pbase += __popcll(bal);
+    }
+    if (tid == 0) pcount_s = pbase;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    w.flags[0] = bad_s;
+    w.flags[1] = pcount_s;
+    w.flags[2] = (bad_s || pcount_s != e) ? 1 : 0;
+  }
+  if (!bad_s)
+    for (int i = tid; i < e; i += B) erased_out[i] = w.erased[i];
+}
+
+__global__ __launch_bounds__(kThreads) void ds16_gather_kernel(const uint16_t* __restrict__ g, int k, int e, Ws16 w) {
+  if (ws_failed(w)) return;
+  const int W = e + k;
+  const int64_t total = int64_t(e) * W;
+  for (int64_t i = int64_t(blockIdx.x) * kThreads + threadIdx.x; i < total; i += int64_t(gridDim.x) * kThreads) {
+    const int a = int(i / W), col = int(i - int64_t(a) * W);
+    const size_t grow = size_t(w.prow[a]) * k;
+    uint16_t v;
+    if (col < e) {
+      v = g[grow + w.erased[col]];
+    } else {
+      const int r = w.rows[col - e];
+      v = r < k ? g[grow + r] : uint16_t(r == w.prow[a]);
+    }
+    w.m[size_t(a) * w.ld + col] = v;
+  }
+}
+
+// One panel [c0, c0 + P): pivot rows by Gauss-Jordan on the panel in LDS, A[pi]^-1, snapshot.
+__global__ __launch_bounds__(kThreads) void ds16_panel_kernel(int e, int c0, int P, Ws16 w) {
+  if (ws_failed(w)) return;
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  constexpr int B = kThreads;
+  const int tid = threadIdx.x;
+  uint16_t* pan = reinterpret_cast<uint16_t*>(smem);                       // [e][P]
+  int* used = reinterpret_cast<int*>(smem + al256(size_t(e) * P * 2));     // [e]
+  uint16_t* fcol = reinterpret_cast<uint16_t*>(used + e);                  // [e] (elimination factors)
+  int* misc = reinterpret_cast<int*>(fcol + ((e + 1) & ~1));               // [0] bid, [1] fail, [2] inverse
+  int* lpiv = misc + 4;                                                     // [P]
+  uint16_t* aug = reinterpret_cast<uint16_t*>(lpiv + kPanelMax);           // [P][2P]
+  const int Pc = min(P, e - c0);
+  for (int i = tid; i < e * P; i += B) {
+    const int r = i / P, t = i - r * P;
+    const uint16_t v = t < Pc ? w.m[size_t(r) * w.ld + c0 + t] : uint16_t(0);
+    pan[i] = v;
+    w.asn[i] = v;
+  }
+  for (int i = tid; i < e; i += B) used[i] = w.used[i];
+  if (tid == 0) misc[1] = 0;
+  __syncthreads();
+  for (int j = 0; j < Pc; ++j) {
+    if (tid == 0) misc[0] = e;
+    __syncthreads();
+    for (int r = tid; r < e; r += B)
+      if (!used[r] && pan[r * P + j]) atomicMin(&misc[0], r);
+    __syncthreads();
+    const int p = misc[0];
+    if (p >= e) {  // no pivot in this column among the unused rows: singular (uniform)
+      if (tid == 0) w.flags[2] = 1;
+      return;
+    }
+    for (int r = tid; r < e; r += B) fcol[r] = pan[r * P + j];
+    if (tid == 0) {
+      used[p] = 1 + (c0 + j);
+      lpiv[j] = p;
+      misc[2] = int(inv16(pan[p * P + j]));
+    }
+    __syncthreads();
+    const uint32_t iv = uint32_t(misc[2]);
+    for (int t = tid; t < P; t += B) pan[p * P + t] = uint16_t(mul16(pan[p * P + t], iv));
+    __syncthreads();
+    for (int i = tid; i < e * P; i += B) {
+      const int r = i / P, t = i - r * P;
+      const uint32_t f = fcol[r];
+      if (r != p && f) pan[i] = uint16_t(pan[i] ^ mul16(f, pan[p * P + t]));
+    }
+    __syncthreads();
+  }
+  // A[pi]^-1: Gauss-Jordan on [A[pi] | I] (Pc x 2Pc, row pivoting among the Pc rows; A[pi] is
+  // nonsingular because every pivot above was found)
+  const int P2 = 2 * Pc;
+  for (int i = tid; i < Pc * P2; i += B) {
+    const int a = i / P2, t = i - a * P2;
+    aug[i] = t < Pc ? w.asn[size_t(lpiv[a]) * P + t] : uint16_t(t - Pc == a);
+  }
+  __syncthreads();
+  for (int j = 0; j < Pc; ++j) {
+    if (tid == 0) {
+      int q = j;
+      while (q < Pc && !aug[q * P2 + j]) ++q;
+      if (q < Pc && q != j)
+        for (int t = 0; t < P2; ++t) {
+          const uint16_t x = aug[j * P2 + t];
+          aug[j * P2 + t] = aug[q * P2 + t];
+          aug[q * P2 + t] = x;
+        }
+      misc[2] = q < Pc ? int(inv16(aug[j * P2 + j])) : 0;
+      if (q >= Pc) misc[1] = 1;
+    }
+    __syncthreads();
+    if (misc[1]) {
+      if (tid == 0) w.flags[2] = 1;
+      return;
+    }
+    const uint32_t iv = uint32_t(misc[2]);
+    for (int t = tid; t < P2; t += B) aug[j * P2 + t] = uint16_t(mul16(aug[j * P2 + t], iv));
+    __syncthreads();
+    for (int a = tid; a < Pc; a += B) fcol[a] = aug[a * P2 + j];
+    __syncthreads();
+    for (int i = tid; i < Pc * P2; i += B) {
+      const int a = i / P2, t = i - a * P2;
+      const uint32_t f = fcol[a];
+      if (a != j && f) aug[i] = uint16_t(aug[i] ^ mul16(f, aug[j * P2 + t]));
+    }
+    __syncthreads();
+  }
+  for (int i = tid; i < P * P; i += B) {
+    const int a = i / P, t = i - a * P;
+    w.ainv[i] = (a < Pc && t < Pc) ? aug[a * P2 + Pc + t] : uint16_t(0);
+  }
+  for (int j = tid; j < Pc; j += B) w.piv[c0 + j] = lpiv[j];
+  for (int r = tid; r < e; r += B) w.used[r] = used[r];
+}
+
+// Y[j][col] = sum_i A[pi]^-1[j][i] M[pi_i][col], columns [c0, W)
+template <int P>
+__global__ __launch_bounds__(kThreads) void ds16_y_kernel(int k, int e, int c0, Ws16 w) {
+  if (ws_failed(w)) return;
+  __shared__ uint16_t ainv[P * P];
+  __shared__ int pv[P];
+  const int Pc = min(P, e - c0);
+  for (int i = threadIdx.x; i < P * P; i += kThreads) ainv[i] = w.ainv[i];
+  for (int i = threadIdx.x; i < Pc; i += kThreads) pv[i] = w.piv[c0 + i];
+  __syncthreads();
+  const int W = e + k;
+  const int col = c0 + int(blockIdx.x) * kThreads + int(threadIdx.x);
+  if (col >= W) return;
+  uint16_t x[P];
+#pragma unroll
+  for (int i = 0; i < P; ++i) x[i] = i < Pc ? w.m[size_t(pv[i]) * w.ld + col] : uint16_t(0);
+  for (int j = 0; j < Pc; ++j) {
+    uint32_t acc = 0;
+#pragma unroll
+    for (int i = 0; i < P; ++i) {
+      const uint32_t a = ainv[j * P + i];
+      if (a && x[i]) acc ^= mul16(a, x[i]);
+    }
+    w.y[size_t(j) * W + col] = uint16_t(acc);
+  }
+}
+
+// rank-P update of rows [r0, r0 + kRowsPerBlock) over columns [c0, W)
+constexpr int kRowsPerBlock = 8;
+template <int P>
+__global__ __launch_bounds__(kThreads) void ds16_update_kernel(int k, int e, int c0, Ws16 w) {
+  if (ws_failed(w)) return;
+  const int W = e + k;
+  const int Pc = min(P, e - c0);
+  const int col = c0 + int(blockIdx.x) * kThreads + int(threadIdx.x);
+  if (col >= W) return;
+  uint16_t y[P];
+#pragma unroll
+  for (int j = 0; j < P; ++j) y[j] = j < Pc ? w.y[size_t(j) * W + col] : uint16_t(0);
+  const int r0 = int(blockIdx.y) * kRowsPerBlock;
+  for (int r = r0; r < min(e, r0 + kRowsPerBlock); ++r) {
+    const int u = w.used[r] - 1;  // pivot column of row r, if any
+    uint16_t* dst = w.m + size_t(r) * w.ld + col;
+    if (u >= c0 && u < c0 + Pc) {
+      *dst = y[u - c0];
+      continue;
+    }
+    uint32_t acc = *dst;
+    const uint16_t* a = w.asn + size_t(r) * P;
+#pragma unroll
+    for (int j = 0; j < P; ++j) {
+      const uint32_t f = a[j];
+      if (f && y[j]) acc ^= mul16(f, y[j]);
+    }
+    *dst = uint16_t(acc);
+  }
+}
+
+// X[b] = M[piv[b]][e:], then dm / tables / row pointers (as gf_decode_system16_kernel's epilogue)
+__global__ __launch_bounds__(kThreads) void ds16_finish_kernel(int n, int k, int e, Ws16 w, uint16_t* __restrict__ dm,
+                                                               int* __restrict__ status, uint32_t* __restrict__ tab,
+                                                               int m_pad, const uint64_t* __restrict__ ptrs,
+                                                               uint64_t* __restrict__ dptr) {
+  const int bad = w.flags[0];
+  const int singular = bad || w.flags[2];
+  const int64_t tid = int64_t(blockIdx.x) * kThreads + threadIdx.x;
+  const int64_t nthr = int64_t(gridDim.x) * kThreads;
+  if (tid == 0 && status) *status = bad ? 2 : singular;
+  if (dptr) {
+    const uint64_t* outp = ptrs + n;
+    for (int64_t j = tid; j < k; j += nthr) {
+      const int rr = w.rows[j];
+      dptr[j] = ptrs[rr];
+      dptr[k + j] = (!singular && rr < k) ? outp[rr] : 0;
+    }
+    for (int64_t i = tid; i < m_pad; i += nthr) dptr[2 * k + i] = (!singular && i < e) ? outp[w.erased[i]] : 0;
+  }
+  auto x_at = [&](int b, int j) -> uint32_t { return w.m[size_t(w.piv[b]) * w.ld + e + j]; };
+  if (dm)
+    for (int64_t i = tid; i < int64_t(e) * k; i += nthr) {
+      const int b = int(i / k), j = int(i - int64_t(b) * k);
+      dm[i] = singular ? uint16_t(0) : uint16_t(x_at(b, j));
+    }
+  if (tab && !singular)
+    for (int64_t idx = tid; idx < int64_t(k) * e; idx += nthr) {
+      const int j = int(idx / e), b = int(idx - int64_t(j) * e);
+      uint32_t q[4][5];
+      quad_of(x_at(b, j), q);
+      uint32_t* dst = tab + (size_t(j) * m_pad + b) * 4 * kPermStride;
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) {
+#pragma unroll
+        for (int v = 0; v < 5; ++v) dst[qq * kPermStride + v] = q[qq][v];
+        dst[qq * kPermStride + 5] = dst[qq * kPermStride + 6] = dst[qq * kPermStride + 7] = 0;
+      }
+    }
+}
+
+template <int P>
+hipError_t launch_blocked16(const uint16_t* g, int n, int k, const int* rows, int* erased, int e, uint16_t* dm,
+                            int* status, uint32_t* tab, int m_pad, const uint64_t* ptrs, uint64_t* dptr, void* ws,
+                            hipStream_t stream) {
+  const Ws16 w = ws16_of(ws, n, k, e, P);
+  const int W = e + k;
+  ds16_prep_kernel<<<1, kThreads, 0, stream>>>(rows, n, k, e, w, erased);
+  const int64_t cells = int64_t(e) * W;
+  const unsigned gblocks = unsigned(std::min<int64_t>((cells + kThreads - 1) / kThreads, 8 * 256));
+  ds16_gather_kernel<<<gblocks, kThreads, 0, stream>>>(g, k, e, w);
+  const size_t plds = panel_lds(e, P);
+  if (plds > 65536) {
+    const hipError_t err = ensure_lds_optin(reinterpret_cast<const void*>(&ds16_panel_kernel));
+    if (err != hipSuccess) return err;
+  }
+  for (int c0 = 0; c0 < e; c0 += P) {
+    ds16_panel_kernel<<<1, kThreads, plds, stream>>>(e, c0, P, w);
+    const unsigned cb = unsigned((W - c0 + kThreads - 1) / kThreads);
+    ds16_y_kernel<P><<<cb, kThreads, 0, stream>>>(k, e, c0, w);
+    ds16_update_kernel<P><<<dim3(cb, unsigned((e + kRowsPerBlock - 1) / kRowsPerBlock)), kThreads, 0, stream>>>(
+        k, e, c0, w);
+  }
+  const int64_t fin = std::max<int64_t>(int64_t(k) * e, std::max(k, m_pad));
+  const unsigned fblocks = unsigned(std::min<int64_t>((fin + kThreads - 1) / kThreads, 4 * 256));
+  ds16_finish_kernel<<<fblocks, kThreads, 0, stream>>>(n, k, e, w, dm, status, tab, m_pad, ptrs, dptr);
+  return hipGetLastError();
+}
+
+bool blocked16_fits(int n, int k, int e) {
+  return k >= 1 && e >= 1 && e <= k && n >= k + e && n <= 65535 && panel_lds(e, panel_of(e)) <= kMaxLds16;
+}
+
 }  // namespace
 
 bool decode_system16_supported(int n, int k, int e) {
   return k >= 1 && e >= 1 && e <= k && e <= kThreads && n >= k + e && lds16(n, k, e) <= kMaxLds16;
 }
 
+int64_t decode_system16_workspace(int n, int k, int e) {
+  if (!blocked16_fits(n, k, e)) return -1;
+  return int64_t(ws16_layout(n, k, e, panel_of(e)).bytes);
+}
+
 hipError_t launch_gf_decode_system16(const uint16_t* g, int n, int k, const int* rows, int* erased, int e,
                                      uint16_t* dm, int* status, void* desc, int m_pad, hipStream_t stream,
-                                     const uint64_t* ptrs) {
-  if (!decode_system16_supported(n, k, e) || !erased || (desc && e > m_pad) || (ptrs && !desc))
-    return hipErrorInvalidValue;
-  const size_t lds = lds16(n, k, e);
+                                     const uint64_t* ptrs, void* workspace, bool force_blocked) {
+  if (!erased || (desc && e > m_pad) || (ptrs && !desc)) return hipErrorInvalidValue;
   uint32_t* tab = nullptr;
   uint64_t* dptr = nullptr;
   if (desc) {
@@ -303,6 +702,16 @@ hipError_t launch_gf_decode_system16(const uint16_t* g, int n, int k, const int*
     tab = reinterpret_cast<uint32_t*>(static_cast<char*>(desc) + l.tab_off);
     if (ptrs) dptr = reinterpret_cast<uint64_t*>(static_cast<char*>(desc) + l.in_off);
   }
+  if (force_blocked || !decode_system16_supported(n, k, e)) {  // the blocked multi-workgroup solve
+    if (!workspace || !blocked16_fits(n, k, e)) return hipErrorInvalidValue;
+    switch (panel_of(e)) {
+      case 32: return launch_blocked16<32>(g, n, k, rows, erased, e, dm, status, tab, m_pad, ptrs, dptr, workspace, stream);
+      case 16: return launch_blocked16<16>(g, n, k, rows, erased, e, dm, status, tab, m_pad, ptrs, dptr, workspace, stream);
+      case 8: return launch_blocked16<8>(g, n, k, rows, erased, e, dm, status, tab, m_pad, ptrs, dptr, workspace, stream);
+      default: return launch_blocked16<4>(g, n, k, rows, erased, e, dm, status, tab, m_pad, ptrs, dptr, workspace, stream);
+    }
+  }
+  const size_t lds = lds16(n, k, e);
   if (lds > 65536) {
     const hipError_t err = ensure_lds_optin(reinterpret_cast<const void*>(&gf_decode_system16_kernel));
     if (err != hipSuccess) return err;

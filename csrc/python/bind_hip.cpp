@@ -162,16 +162,20 @@ PYBIND11_MODULE(_hip, m) {
   m.def(
       "decode_system16",
       [](uint64_t g, int n, int k, uint64_t rows, uint64_t erased, int e, uint64_t dm, uint64_t status, uint64_t desc,
-         int m_pad, uint64_t stream, uint64_t ptrs) {
+         int m_pad, uint64_t stream, uint64_t ptrs, uint64_t workspace, bool force_blocked) {
         check(launch_gf_decode_system16(reinterpret_cast<const uint16_t*>(g), n, k, reinterpret_cast<const int*>(rows),
                                         reinterpret_cast<int*>(erased), e, reinterpret_cast<uint16_t*>(dm),
                                         reinterpret_cast<int*>(status), reinterpret_cast<void*>(desc), m_pad,
-                                        as_stream(stream), reinterpret_cast<const uint64_t*>(ptrs)),
+                                        as_stream(stream), reinterpret_cast<const uint64_t*>(ptrs),
+                                        reinterpret_cast<void*>(workspace), force_blocked),
               "decode_system16");
       },
       py::arg("g"), py::arg("n"), py::arg("k"), py::arg("rows"), py::arg("erased"), py::arg("e"), py::arg("dm"),
-      py::arg("status"), py::arg("desc"), py::arg("m_pad"), py::arg("stream"), py::arg("ptrs") = 0);
+      py::arg("status"), py::arg("desc"), py::arg("m_pad"), py::arg("stream"), py::arg("ptrs") = 0,
+      py::arg("workspace") = 0, py::arg("force_blocked") = false);
   m.def("decode_system16_supported", &decode_system16_supported);
+  m.def("decode_system16_workspace", &decode_system16_workspace,
+        "device workspace bytes of the blocked GF(2^16) decode solve (-1: too large)");
   m.def("fp4_bitmat_sel",[](uint64_t coeff, int ld, uint64_t sel, int mm, int k, uint64_t bitmat, int mg_cap,
                              uint64_t stream) {
     check(launch_fp4_bitmat_sel(reinterpret_cast<const uint8_t*>(coeff), ld, reinterpret_cast<const int*>(sel), mm, k,

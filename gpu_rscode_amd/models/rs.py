@@ -21,7 +21,7 @@ import torch
 from .. import gf
 from .._native import cpu, hip
 from ..ops.gemm import Gemm16Plan, GemmPlan, _rows
-from ..ops.inverse import decode_system16_into_plan, decode_system_into_plan
+from ..ops.inverse import decode16_device_supported, decode_system16_into_plan, decode_system_into_plan
 from ..ops.matrix import decode_matrix, encoding_matrix
 
 PITCH = 256
@@ -476,7 +476,7 @@ class ReedSolomon:
             # systematic decode solved on device: e x (e+k) Gauss-Jordan, tables written in place
             decode_system_into_plan(g_dev, plan.rows_dev, plan.erased_dev, plan, status=plan.status, stream=stream)
             self.last_status = plan.status
-        elif device_invert and self.wide and hip().decode_system16_supported(self.n, self.k, len(erased)):
+        elif device_invert and self.wide and decode16_device_supported(self.n, self.k, len(erased)):
             plan = self._plans.get(key)
             if plan is None:
                 plan = Gemm16Plan(ins, [outs[i] for i in erased], copies=copies, device_tables=True,

@@ -118,14 +118,23 @@ def _is_w16(g: torch.Tensor) -> bool:
     return g.dtype in (torch.int16, torch.uint16)
 
 
+def decode16_device_supported(n: int, k: int, e: int) -> bool:
+    """Whether the device builds GF(2^16) decode plans for (n, k, e): one workgroup's LDS, else the
+    blocked multi-workgroup solve (any e up to ~19 K)."""
+    return hip().decode_system16_supported(n, k, e) or hip().decode_system16_workspace(n, k, e) >= 0
+
+
 def decode_system16_into_plan(g: torch.Tensor, rows: torch.Tensor, erased: torch.Tensor, plan: Gemm16Plan, *,
                               status: torch.Tensor | None = None, stream: torch.cuda.Stream | None = None,
-                              ptrs: torch.Tensor | None = None, dm: torch.Tensor | None = None) -> torch.Tensor:
+                              ptrs: torch.Tensor | None = None, dm: torch.Tensor | None = None,
+                              force_blocked: bool = False) -> torch.Tensor:
     """GF(2^16) form of :func:`decode_system_into_plan` (``csrc/kernels/gf_decode16.hip``): ``g`` is
     the (n, k) generator as a 16-bit device tensor; ``erased`` (device int32 [e]) is always written
     by the kernel (derived from ``rows``); ``dm`` (optional, int16 [e, k]) receives the decode rows.
     Writes the plan's four-record tables (and with ``ptrs`` its row pointers). Graph-capturable.
-    Returns the device status word (0 ok, 1 singular, 2 invalid survivor list)."""
+    Systems past one workgroup's LDS (e.g. k = 2000, e = 100; any e > 256) take the blocked
+    multi-workgroup solve with a device workspace cached on the plan (``force_blocked``: for any
+    size, tests). Returns the device status word (0 ok, 1 singular, 2 invalid survivor list)."""
     n, k = g.shape
     e = erased.numel()
     if plan.k != k or plan.m != e or rows.numel() != k:
@@ -133,8 +142,15 @@ def decode_system16_into_plan(g: torch.Tensor, rows: torch.Tensor, erased: torch
     for t in (rows, erased):
         if t.dtype != torch.int32 or t.device != g.device:
             raise ValueError("rows / erased must be int32 tensors on the generator's device")
-    if not hip().decode_system16_supported(n, k, e):
-        raise ValueError(f"GF(2^16) device decode system (n={n}, k={k}, e={e}) does not fit one workgroup's LDS")
+    blocked = force_blocked or not hip().decode_system16_supported(n, k, e)
+    ws_bytes = hip().decode_system16_workspace(n, k, e) if blocked else 0
+    if ws_bytes < 0:
+        raise ValueError(f"GF(2^16) device decode system (n={n}, k={k}, e={e}) is too large for the device solve")
+    ws = None
+    if blocked:
+        ws = getattr(plan, "_solve_ws", None)
+        if ws is None or ws.numel() < ws_bytes or ws.device != g.device:
+            ws = plan._solve_ws = torch.empty(ws_bytes, dtype=torch.uint8, device=g.device)
     if status is None:
         status = torch.zeros(1, dtype=torch.int32, device=g.device)
     if ptrs is not None and (ptrs.dtype != torch.int64 or ptrs.device != g.device or ptrs.numel() != n + k):
@@ -149,7 +165,10 @@ def decode_system16_into_plan(g: torch.Tensor, rows: torch.Tensor, erased: torch
         dm = plan._dm_buf
     hip().decode_system16(g.data_ptr(), n, k, rows.data_ptr(), erased.data_ptr(), e,
                           0 if dm is None else dm.data_ptr(), status.data_ptr(), plan.desc.data_ptr(), plan.m_pad,
-                          st.cuda_stream, 0 if ptrs is None else ptrs.data_ptr())
+                          st.cuda_stream, 0 if ptrs is None else ptrs.data_ptr(), 0 if ws is None else ws.data_ptr(),
+                          force_blocked)
+    if ws is not None and not torch.cuda.is_current_stream_capturing():
+        ws.record_stream(st)
     if plan.engine == "mfma":
         plan.set_device_coeff(dm, stream=st)
     return status
@@ -191,8 +210,8 @@ class PatternDecoder:
         self.wide = _is_w16(g)
         # placeholders until the first solve: inputs = the natives, outputs = the first e output rows
         if self.wide:
-            if not hip().decode_system16_supported(n, k, e):
-                raise ValueError(f"GF(2^16) device decode system (n={n}, k={k}, e={e}) does not fit one workgroup")
+            if not decode16_device_supported(n, k, e):
+                raise ValueError(f"GF(2^16) device decode system (n={n}, k={k}, e={e}) is too large for the device solve")
             self.plan = Gemm16Plan(chunks[:k], out[:e], copies=out, device_tables=True,
                                    engine="auto" if engine == "auto" else ("mfma" if engine == "mfma" else "valu16"))
         else:

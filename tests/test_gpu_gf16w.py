@@ -315,3 +315,91 @@ def test_batched_w16_scattered_stripes_fall_back_to_vperm():
     for b in range(B):
         x = torch.stack(ins[b]).cpu().numpy()
         assert np.array_equal(torch.stack(outs[b]).cpu().numpy().view("<u2"), _oracle(coeff, x))
+
+
+def _w16_setup(k, n, matrix="cauchy"):
+    rs = ReedSolomon(k, n, field="gf65536", matrix=matrix)
+    g = torch.from_numpy(np.ascontiguousarray(rs.G, dtype="<u2").view(np.int16)).cuda()
+    return rs, g
+
+
+def _solve16(g, rows, e, k, force_blocked):
+    from gpu_rscode_amd.ops.gemm import Gemm16Plan
+    from gpu_rscode_amd.ops.inverse import decode_system16_into_plan
+
+    ins = alloc_rows(k, 64, "cuda")
+    outs = alloc_rows(e, 64, "cuda")
+    plan = Gemm16Plan(ins, outs, device_tables=True, engine="valu16")
+    erased = torch.zeros(e, dtype=torch.int32, device="cuda")
+    dm = torch.zeros((e, k), dtype=torch.int16, device="cuda")
+    st = decode_system16_into_plan(g, torch.tensor(rows, dtype=torch.int32, device="cuda"), erased, plan, dm=dm,
+                                   force_blocked=force_blocked)
+    torch.cuda.synchronize()
+    return int(st.item()), erased.tolist(), dm.cpu().numpy().view(np.uint16)
+
+
+@pytest.mark.parametrize("k,n,e", [(10, 14, 4), (64, 100, 33), (300, 340, 40), (40, 120, 37)])
+def test_blocked_w16_solve_equals_one_workgroup_solve(k, n, e):
+    """The blocked multi-workgroup GF(2^16) solve (panels of pivot columns, rank-P updates over the
+    chip) forced on systems the one-workgroup kernel also solves: identical decode rows, erased
+    natives and status, for several random patterns (panels of 32: one, two and a ragged last)."""
+    rs, g = _w16_setup(k, n)
+    rng = np.random.default_rng(k * 7 + e)
+    for _ in range(3):
+        erased = sorted(rng.choice(k, size=e, replace=False).tolist())
+        par = sorted(rng.choice(range(k, n), size=e, replace=False).tolist())
+        rows = [r for r in range(k) if r not in erased] + par
+        rng.shuffle(rows)
+        one = _solve16(g, rows, e, k, False)
+        blk = _solve16(g, rows, e, k, True)
+        assert one[0] == blk[0] == 0
+        assert one[1] == blk[1] == erased
+        assert np.array_equal(one[2], blk[2])
+        assert np.array_equal(blk[2], rs._erased_rows(rows, erased))
+
+
+def test_blocked_w16_solve_flags_singular_and_invalid_patterns():
+    k, n, e = 20, 30, 6
+    rs, _ = _w16_setup(k, n)
+    G = np.array(rs.G)
+    G[k + 3] = G[k + 1]  # two equal parity rows: any pattern using both is singular
+    g = torch.from_numpy(np.ascontiguousarray(G, dtype="<u2").view(np.int16)).cuda()
+    rows = list(range(e, k)) + [k + 1, k + 3, k + 4, k + 5, k + 6, k + 7]
+    assert _solve16(g, rows, e, k, True)[0] == 1
+    bad = list(range(k - 1)) + [0]  # a chunk listed twice
+    assert _solve16(g, bad, 1, k, True)[0] == 2
+
+
+@pytest.mark.parametrize("k,n,e", [(2000, 2100, 100), (600, 1000, 300)])
+def test_blocked_w16_decode_large_systems_end_to_end(k, n, e):
+    """Systems past one workgroup: k = 2000 with e = 100 (the e x (e + k) system is 420 KB) and
+    e = 300 > 256. PatternDecoder builds the plan on the device (blocked solve) and the decode
+    rebuilds every erased native bit-exactly; the decode rows equal the host solve's
+    (gfrs::gf16w::decode_rows)."""
+    from gpu_rscode_amd.ops import PatternDecoder
+
+    C = 2 * 1024 + 32
+    rs, g = _w16_setup(k, n, "cauchy")
+    assert not __import__("gpu_rscode_amd")._native.hip().decode_system16_supported(n, k, e)
+    data = alloc_rows(k, C, "cuda")
+    data.copy_(_rand(k, C, 3 + e))
+    par = rs.encode(data)
+    out = alloc_rows(k, C, "cuda")
+    dec = PatternDecoder(g, [data[i] for i in range(k)] + [par[i] for i in range(n - k)], [out[i] for i in range(k)], e)
+    rng = np.random.default_rng(k + e)
+    erased = sorted(rng.choice(k, size=e, replace=False).tolist())
+    rows = [r for r in range(k) if r not in erased] + sorted(rng.choice(range(k, n), size=e, replace=False).tolist())
+    rng.shuffle(rows)
+    dec.rows.copy_(torch.tensor(rows, dtype=torch.int32))
+    dec.solve()
+    dec.run()
+    torch.cuda.synchronize()
+    assert int(dec.status.item()) == 0
+    assert dec.erased.tolist() == erased
+    assert torch.equal(out, data)
+    dm = torch.zeros((e, k), dtype=torch.int16, device="cuda")
+    from gpu_rscode_amd.ops.inverse import decode_system16_into_plan
+    decode_system16_into_plan(g, torch.tensor(rows, dtype=torch.int32, device="cuda"), dec.erased, dec.plan,
+                              ptrs=dec.ptrs, dm=dm)
+    torch.cuda.synchronize()
+    assert np.array_equal(dm.cpu().numpy().view(np.uint16), rs._erased_rows(rows, erased))
