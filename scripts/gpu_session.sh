@@ -21,6 +21,7 @@
 #   wide       FP4 wide-stripe shapes: default kernels vs A-resident, spread vs single sink slot
 #   e2efull    host pipeline sweep (streams x slice) for the full-decode and encode shapes
 #   serve      small-object serving throughput: batched vs per-object launches vs hipGraph
+#   decsys16   GF(2^16) decode-plan solve, host vs device (one workgroup / blocked), wide codes
 #   ad hoc:    CMD="..." scripts/gpu_session.sh NAME cmd   (one step, 600 s)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -91,7 +92,11 @@ r_setup() {  # bin/RS device + host setup breakdown, 1 GiB encode + decode (THP-
 }
 r_prof() {
   step prof_k10 300 $PROF -d $O/prof_k10 -- python3 bench.py --steps 20 --no-e2e &&
-  step prof_k128 300 $PROF -d $O/prof_k128 -- python3 bench.py --preset k128n160 --steps 20 --no-e2e
+  step prof_k128 300 $PROF -d $O/prof_k128 -- python3 bench.py --preset k128n160 --steps 20 --no-e2e &&
+  step prof_k16 300 $PROF -d $O/prof_k16 -- python3 bench.py --preset k16n20_8g --steps 10 --no-e2e
+}
+r_decsys16() {  # GF(2^16) decode-plan solve: host vs device (one workgroup / blocked)
+  step decsys16 300 $PY scripts/decsys16_bench.py
 }
 r_rcclprof() {  # kernel timelines: RCCL kernels on their own stream beside the GEMMs (one-rank group)
   local m

@@ -76,13 +76,11 @@ def main():
     res["copy_roofline_TBps"] = round(2 * a.bytes / us / 1e6, 3)
     del src, dst
 
-    cases = [make_case("enc_k10_p4", 10, 4, 0, a.bytes), make_case("dec_k10_e4_copy6", 10, 4, 6, a.bytes),
-             make_case("enc_k4_p2", 4, 2, 0, a.bytes), make_case("enc_k16_p4", 16, 4, 0, a.bytes),
-             make_case("enc_k128_p32", 128, 32, 0, a.bytes), make_case("dec_k10_e1_copy9", 10, 1, 9, a.bytes),
-             make_case("dec_k128_e32_copy96", 128, 32, 96, a.bytes)]
-    if a.cases:
-        keep = set(a.cases.split(","))
-        cases = [c for c in cases if c["name"] in keep]
+    specs = [("enc_k10_p4", 10, 4, 0), ("dec_k10_e4_copy6", 10, 4, 6), ("enc_k4_p2", 4, 2, 0), ("enc_k16_p4", 16, 4, 0),
+             ("enc_k128_p32", 128, 32, 0), ("dec_k10_e1_copy9", 10, 1, 9), ("dec_k128_e32_copy96", 128, 32, 96),
+             ("dec_k16_e4_copy12", 16, 4, 12)]
+    keep = set(a.cases.split(",")) if a.cases else None
+    cases = (make_case(nm, k, m, nc, a.bytes) for nm, k, m, nc in specs if keep is None or nm in keep)
     variants = VARIANTS
     if a.variants:
         variants = []

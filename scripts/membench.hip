@@ -6,6 +6,7 @@
 // Run:   build/membench [REPS]     (prints one JSON object)
 //        build/membench sdma [ROWS WIDTH]   (copy engines vs blit copies, one JSON line per case)
 //        build/membench pitch [REPS]        (enc / dec patterns at different row pitches)
+//        build/membench k16 [REPS]          (config #4's k = 16 patterns at 512 MiB rows)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -153,6 +154,61 @@ int pattern_main(int argc, char** argv) {
            v[0], bytes / (v[v.size() / 2] * 1e-6) / 1e12, i + 1 < cases.size() ? "," : "");
   }
   printf("}\n");
+  return 0;
+}
+
+// ---- config #4's pattern: `membench k16 [REPS]` ----------------------------------------------
+// The k16n20_8g step's access patterns with no math, at its row size (8 GiB / 16 = 512 MiB rows,
+// 2 MiB pitch as alloc_rows lays them out): encode 16 rows in / 4 out, decode 16 in / 16 out (the
+// rebuilt natives plus the fused survivor copies), one span per wave (grid) and persistent. One
+// JSON line per case: the ceiling the k = 16 kernels are priced against.
+int k16_main(int argc, char** argv) {
+  const int64_t C = int64_t(512) << 20;
+  const int64_t pitch = C;  // (already a multiple of 2 MiB)
+  const int reps = argc > 1 ? atoi(argv[1]) : 5;
+  int cus = 0;
+  CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+  uint8_t *in, *out;
+  CHECK(hipMalloc(&in, 16 * pitch));
+  CHECK(hipMalloc(&out, 16 * pitch));
+  CHECK(hipMemset(in, 0x5a, 16 * pitch));
+  CHECK(hipMemset(out, 0, 16 * pitch));
+  std::vector<Case> cases = {mk<16, 4, 1, true, false, 256>("enc"), mk<16, 4, 1, true, true, 256>("enc"),
+                             mk<16, 4, 2, true, true, 256>("enc"), mk<16, 16, 1, true, false, 256>("dec"),
+                             mk<16, 16, 1, true, true, 256>("dec")};
+  hipEvent_t e0, e1;
+  CHECK(hipEventCreate(&e0));
+  CHECK(hipEventCreate(&e1));
+  std::vector<std::vector<float>> t(cases.size());
+  for (int round = 0; round < 3; ++round)
+    for (size_t i = 0; i < cases.size(); ++i) {
+      const Case& c = cases[i];
+      const int64_t nspans = (C / 16) / (64 * c.V);
+      int64_t blocks = (nspans + 3) / 4;
+      if (c.persist) {
+        int occ = 0;
+        CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void*>(c.fn), c.BS, 0));
+        blocks = std::min<int64_t>(blocks, int64_t(cus) * occ);
+      }
+      hipLaunchKernelGGL(c.fn, dim3(unsigned(blocks)), dim3(c.BS), 0, 0, in, out, pitch, nspans);
+      CHECK(hipEventRecord(e0));
+      for (int r = 0; r < reps; ++r)
+        hipLaunchKernelGGL(c.fn, dim3(unsigned(blocks)), dim3(c.BS), 0, 0, in, out, pitch, nspans);
+      CHECK(hipEventRecord(e1));
+      CHECK(hipEventSynchronize(e1));
+      CHECK(hipGetLastError());
+      float ms = 0;
+      CHECK(hipEventElapsedTime(&ms, e0, e1));
+      t[i].push_back(ms / reps * 1e3f);
+    }
+  for (size_t i = 0; i < cases.size(); ++i) {
+    std::vector<float> v = t[i];
+    std::sort(v.begin(), v.end());
+    const Case& c = cases[i];
+    const double bytes = double(c.R + c.W) * C;
+    printf("{\"case\": \"%s\", \"us_median\": %.1f, \"us_min\": %.1f, \"TBps\": %.3f}\n", c.name.c_str(),
+           v[v.size() / 2], v[0], bytes / (v[v.size() / 2] * 1e-6) / 1e12);
+  }
   return 0;
 }
 
@@ -361,5 +417,6 @@ int pitch_main(int argc, char** argv) {
 int main(int argc, char** argv) {
   if (argc > 1 && std::string(argv[1]) == "sdma") return sdma_main(argc - 1, argv + 1);
   if (argc > 1 && std::string(argv[1]) == "pitch") return pitch_main(argc - 1, argv + 1);
+  if (argc > 1 && std::string(argv[1]) == "k16") return k16_main(argc - 1, argv + 1);
   return pattern_main(argc, argv);
 }
