@@ -120,16 +120,23 @@ def main(argv=None) -> int:
 
 
 # ---- distributed mode -------------------------------------------------------------------------
-def _size_file(path: str, size: int) -> None:
+def _size_file(path: str, size: int) -> bool:
     """Create ``path`` if missing and set its size to exactly ``size`` (shards then write their
     columns in place; an older, longer file loses its stale tail). Never truncated to zero first:
     the columns a resumed shard checkpointed before a crash are still in it, and every column no
-    checkpoint covers is rewritten by its shard."""
+    checkpoint covers is rewritten by its shard. Returns whether the file was already there at
+    exactly that size — when one was not, no checkpoint may be trusted (a re-created file is zeros
+    where a checkpoint says columns were written)."""
+    try:
+        intact = os.stat(path).st_size == size
+    except FileNotFoundError:
+        intact = False
     fd = os.open(path, os.O_WRONLY | os.O_CREAT, 0o644)
     try:
         os.ftruncate(fd, size)
     finally:
         os.close(fd)
+    return intact
 
 
 def _shard_checkpoints(target: str, C: int, world: int) -> list[str]:
@@ -242,9 +249,8 @@ def _dist_run(a, ctx) -> int:
         ckpts = _shard_checkpoints(path, C, world)
         if ctx.is_root:
             ff.remove_file(ff.metadata_path(path))
-            _prune_checkpoints(path, [] if a.no_resume else ckpts)
-            for i in range(n):
-                _size_file(ff.chunk_path(path, i), C)
+            intact = all([_size_file(ff.chunk_path(path, i), C) for i in range(n)])
+            _prune_checkpoints(path, ckpts if intact and not a.no_resume else [])
         barrier()
         if fault is not None and int(fault) == rank:
             raise RuntimeError("injected fault (GFRS_DIST_FAULT_RANK)")
@@ -324,8 +330,8 @@ def _dist_run(a, ctx) -> int:
                 pick[0] = 2 if more else 1
                 err = ex
             if not int(pick[0].item()):
-                _prune_checkpoints(dst, [] if a.no_resume else ckpts)
-                _size_file(dst, md.total_size)
+                intact = _size_file(dst, md.total_size)
+                _prune_checkpoints(dst, ckpts if intact and not a.no_resume else [])
         if world > 1:
             dist.broadcast(pick, 0)
         if int(pick[0].item()) != 2:

@@ -220,6 +220,15 @@ def test_torchrun_dist_cli_resumes_after_a_shard_crash(tmp_path, stop_rank):
         assert (d1 / name).read_bytes() == (d2 / name).read_bytes(), name
     assert not [x for x in os.listdir(d1) if ".PROGRESS" in x]
 
+    # a chunk lost between the crash and the re-run: it is re-created, so no checkpoint is trusted
+    r = job(enc + ["--stop-after", "1", "--stop-rank", str(stop_rank)])
+    assert r.returncode != 0
+    os.remove(d1 / "_12_f.bin")
+    r = job(enc)
+    assert r.returncode == 0, r.stderr[-3000:]
+    for name in [f"_{i}_f.bin" for i in range(14)] + ["f.bin.METADATA"]:
+        assert (d1 / name).read_bytes() == (d2 / name).read_bytes(), name
+
     ff.write_conf(str(d1 / "conf"), [f"_{i}_f.bin" for i in (0, 2, 3, 4, 6, 7, 10, 11, 12, 13)])
     dec = ["-d", "-i", "f.bin", "-c", "conf", "-o", "o.bin"]
     r = job(dec + ["--stop-after", "1", "--stop-rank", str(stop_rank)])
