@@ -6,7 +6,7 @@
 // Run:   build/membench [REPS]     (prints one JSON object)
 //        build/membench sdma [ROWS WIDTH]   (copy engines vs blit copies, one JSON line per case)
 //        build/membench pitch [REPS]        (enc / dec patterns at different row pitches)
-//        build/membench k16 [REPS]          (config #4's k = 16 patterns at 512 MiB rows)
+//        build/membench k16 [REPS [PITCH_MiB...]]   (config #4's k = 16 patterns at 512 MiB rows)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -164,51 +164,67 @@ int pattern_main(int argc, char** argv) {
 // JSON line per case: the ceiling the k = 16 kernels are priced against.
 int k16_main(int argc, char** argv) {
   const int64_t C = int64_t(512) << 20;
-  const int64_t pitch = C;  // (already a multiple of 2 MiB)
   const int reps = argc > 1 ? atoi(argv[1]) : 5;
+  // row pitches to compare (MiB, >= 512): alloc_rows gives 512 (a power of two: row j's byte x sits
+  // at j * 2^29 + x, the same offset inside every large power-of-two block); default: only that
+  std::vector<int64_t> pitches;
+  for (int i = 2; i < argc; ++i) pitches.push_back(int64_t(atoi(argv[i])) << 20);
+  if (pitches.empty()) pitches.push_back(C);
+  int64_t maxp = 0;
+  for (int64_t p : pitches) {
+    if (p < C) {
+      fprintf(stderr, "pitch below 512 MiB\n");
+      return 2;
+    }
+    maxp = std::max(maxp, p);
+  }
   int cus = 0;
   CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
   uint8_t *in, *out;
-  CHECK(hipMalloc(&in, 16 * pitch));
-  CHECK(hipMalloc(&out, 16 * pitch));
-  CHECK(hipMemset(in, 0x5a, 16 * pitch));
-  CHECK(hipMemset(out, 0, 16 * pitch));
-  std::vector<Case> cases = {mk<16, 4, 1, true, false, 256>("enc"), mk<16, 4, 1, true, true, 256>("enc"),
-                             mk<16, 4, 2, true, true, 256>("enc"), mk<16, 16, 1, true, false, 256>("dec"),
+  CHECK(hipMalloc(&in, 16 * maxp + (2 << 20)));
+  CHECK(hipMalloc(&out, 16 * maxp + (2 << 20)));
+  CHECK(hipMemset(in, 0x5a, 16 * maxp));
+  CHECK(hipMemset(out, 0, 16 * maxp));
+  uint8_t* in0 = reinterpret_cast<uint8_t*>((reinterpret_cast<uintptr_t>(in) + (2 << 20) - 1) & ~uintptr_t((2 << 20) - 1));
+  uint8_t* out0 = reinterpret_cast<uint8_t*>((reinterpret_cast<uintptr_t>(out) + (2 << 20) - 1) & ~uintptr_t((2 << 20) - 1));
+  std::vector<Case> cases = {mk<16, 4, 1, true, false, 256>("enc"), mk<16, 16, 1, true, false, 256>("dec"),
                              mk<16, 16, 1, true, true, 256>("dec")};
   hipEvent_t e0, e1;
   CHECK(hipEventCreate(&e0));
   CHECK(hipEventCreate(&e1));
-  std::vector<std::vector<float>> t(cases.size());
+  std::vector<std::vector<float>> t(cases.size() * pitches.size());
   for (int round = 0; round < 3; ++round)
-    for (size_t i = 0; i < cases.size(); ++i) {
-      const Case& c = cases[i];
-      const int64_t nspans = (C / 16) / (64 * c.V);
-      int64_t blocks = (nspans + 3) / 4;
-      if (c.persist) {
-        int occ = 0;
-        CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void*>(c.fn), c.BS, 0));
-        blocks = std::min<int64_t>(blocks, int64_t(cus) * occ);
+    for (size_t pi = 0; pi < pitches.size(); ++pi)
+      for (size_t i = 0; i < cases.size(); ++i) {
+        const Case& c = cases[i];
+        const int64_t nspans = (C / 16) / (64 * c.V);
+        int64_t blocks = (nspans + 3) / 4;
+        if (c.persist) {
+          int occ = 0;
+          CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void*>(c.fn), c.BS, 0));
+          blocks = std::min<int64_t>(blocks, int64_t(cus) * occ);
+        }
+        hipLaunchKernelGGL(c.fn, dim3(unsigned(blocks)), dim3(c.BS), 0, 0, in0, out0, pitches[pi], nspans);
+        CHECK(hipEventRecord(e0));
+        for (int r = 0; r < reps; ++r)
+          hipLaunchKernelGGL(c.fn, dim3(unsigned(blocks)), dim3(c.BS), 0, 0, in0, out0, pitches[pi], nspans);
+        CHECK(hipEventRecord(e1));
+        CHECK(hipEventSynchronize(e1));
+        CHECK(hipGetLastError());
+        float ms = 0;
+        CHECK(hipEventElapsedTime(&ms, e0, e1));
+        t[pi * cases.size() + i].push_back(ms / reps * 1e3f);
       }
-      hipLaunchKernelGGL(c.fn, dim3(unsigned(blocks)), dim3(c.BS), 0, 0, in, out, pitch, nspans);
-      CHECK(hipEventRecord(e0));
-      for (int r = 0; r < reps; ++r)
-        hipLaunchKernelGGL(c.fn, dim3(unsigned(blocks)), dim3(c.BS), 0, 0, in, out, pitch, nspans);
-      CHECK(hipEventRecord(e1));
-      CHECK(hipEventSynchronize(e1));
-      CHECK(hipGetLastError());
-      float ms = 0;
-      CHECK(hipEventElapsedTime(&ms, e0, e1));
-      t[i].push_back(ms / reps * 1e3f);
+  for (size_t pi = 0; pi < pitches.size(); ++pi)
+    for (size_t i = 0; i < cases.size(); ++i) {
+      std::vector<float> v = t[pi * cases.size() + i];
+      std::sort(v.begin(), v.end());
+      const Case& c = cases[i];
+      const double bytes = double(c.R + c.W) * C;
+      printf("{\"case\": \"%s\", \"pitch_mib\": %lld, \"us_median\": %.1f, \"us_min\": %.1f, \"TBps\": %.3f}\n",
+             c.name.c_str(), (long long)(pitches[pi] >> 20), v[v.size() / 2], v[0],
+             bytes / (v[v.size() / 2] * 1e-6) / 1e12);
     }
-  for (size_t i = 0; i < cases.size(); ++i) {
-    std::vector<float> v = t[i];
-    std::sort(v.begin(), v.end());
-    const Case& c = cases[i];
-    const double bytes = double(c.R + c.W) * C;
-    printf("{\"case\": \"%s\", \"us_median\": %.1f, \"us_min\": %.1f, \"TBps\": %.3f}\n", c.name.c_str(),
-           v[v.size() / 2], v[0], bytes / (v[v.size() / 2] * 1e-6) / 1e12);
-  }
   return 0;
 }
 
