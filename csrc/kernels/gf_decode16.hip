@@ -297,14 +297,15 @@ constexpr size_t kMaxLds16 = 160 * 1024;
 //   for each panel of P pivot columns [c0, c0 + P):
 //     panel (1 WG)   the e x P panel in LDS: Gauss-Jordan with row pivoting among the rows not yet
 //                    pivots picks the P pivot rows pi (singular: status 1, every later kernel returns
-//                    at once); snapshots the panel A and writes A[pi]^-1 (P x P, Gauss-Jordan again)
+//                    at once) and snapshots the panel A
+//     ainv (1 WG)    A[pi]^-1 (P x P, Gauss-Jordan on [A[pi] | I] from the snapshot)
 //     y (grid)       Y = A[pi]^-1 . M[pi] over columns [c0, W)
 //     update (grid)  M[pi_j] = Y_j; every other row r: M_r += A_r . Y  (the rank-P update; columns
 //                    before c0 are already reduced and Y is zero there)
 //   finish (grid)    X[b] = M[piv(b)][e:] (pivot rows end normalised: no scaling), dm / tables /
 //                    row pointers as the one-workgroup kernel writes them
 // Work e^2 (e + k) GF(2^16) products over the panels (e = 500, k = 4000: ~1.1 G), spread over the
-// chip instead of one CU; 3 launches per panel, all on `stream` (graph-capturable).
+// chip instead of one CU; 4 launches per panel, all on `stream` (graph-capturable).
 struct Ws16 {
   int* flags;     // [0] bad, [1] parity survivors, [2] singular
   int* cnt;       // [n]
@@ -365,10 +366,9 @@ __host__ __device__ inline Ws16 ws16_of(void* base, int n, int k, int e, int P) 
   return w;
 }
 
-// LDS of the panel kernel: panel [e][P] | used [e] | factors [e] | misc | pivots | [A[pi] | I]
+// LDS of the panel kernel: panel [e][P] | used [e] | factors [e] | misc | pivots
 __host__ __device__ inline size_t panel_lds(int e, int P) {
-  return al256(size_t(e) * P * 2) + size_t(e) * 4 + size_t((e + 1) & ~1) * 2 + 16 + 4 * kPanelMax +
-         size_t(kPanelMax) * 2 * kPanelMax * 2;
+  return al256(size_t(e) * P * 2) + size_t(e) * 4 + size_t((e + 1) & ~1) * 2 + 16 + 4 * kPanelMax;
 }
 
 // panel width: the widest power of two <= 32 whose panel kernel fits the LDS
@@ -393,7 +393,8 @@ __global__ __launch_bounds__(kThreads) void ds16_prep_kernel(const int* __restri
     bad_s = 0;
     pcount_s = 0;
   }
-  __syncthreads();  // (the block's own global writes: visible to it after the barrier)
+  __threadfence();  // (the zeroed counts reach L2 before any wave's atomics add to them)
+  __syncthreads();
   for (int i = tid; i < k; i += B) {
     const int r = rows[i];
     const bool ok = r >= 0 && r < n;
@@ -401,14 +402,17 @@ __global__ __launch_bounds__(kThreads) void ds16_prep_kernel(const int* __restri
     if (ok) atomicAdd(&w.cnt[r], 1);
     else bad_s = 1;
   }
+  __threadfence();  // (rows and counts visible past every wave's L1 before the ballots read them)
   __syncthreads();
+  // (the counts were built by device-scope atomics in L2: read them past this CU's L1)
+  auto count = [&](int i) { return __hip_atomic_load(&w.cnt[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
   for (int i = tid; i < n; i += B)
-    if (w.cnt[i] > 1) bad_s = 1;  // a chunk listed twice
+    if (count(i) > 1) bad_s = 1;  // a chunk listed twice
   if (tid < 64) {  // erased natives (ascending) and parity survivors (survivor order)
     int base = 0;
     for (int i0 = 0; i0 < k; i0 += 64) {
       const int i = i0 + tid;
-      const bool miss = i < k && w.cnt[i] == 0;
+      const bool miss = i < k && count(i) == 0;
       const unsigned long long bal = __ballot(miss);
       const int a = base + __popcll(bal & ((1ull << tid) - 1ull));
       if (miss && a < e) w.erased[a] = i;
@@ -418,10 +422,10 @@ __global__ __launch_bounds__(kThreads) void ds16_prep_kernel(const int* __restri
     int pbase = 0;
     for (int j0 = 0; j0 < k; j0 += 64) {
       const int j = j0 + tid;
-      const bool is_par = j < k && w.rows[j] >= k;
+      const bool is_par = j < k && __hip_atomic_load(&w.rows[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= k;
       const unsigned long long bal = __ballot(is_par);
       const int a = pbase + __popcll(bal & ((1ull << tid) - 1ull));
-      if (is_par && a < e) w.prow[a] = w.rows[j];
+      if (is_par && a < e) w.prow[a] = __hip_atomic_load(&w.rows[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       pbase += __popcll(bal);
     }
     if (tid == 0) pcount_s = pbase;
@@ -454,7 +458,7 @@ __global__ __launch_bounds__(kThreads) void ds16_gather_kernel(const uint16_t* _
   }
 }
 
-// One panel [c0, c0 + P): pivot rows by Gauss-Jordan on the panel in LDS, A[pi]^-1, snapshot.
+// One panel [c0, c0 + P): pivot rows by Gauss-Jordan on the panel in LDS, and its snapshot.
 __global__ __launch_bounds__(kThreads) void ds16_panel_kernel(int e, int c0, int P, Ws16 w) {
   if (ws_failed(w)) return;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -465,7 +469,6 @@ __global__ __launch_bounds__(kThreads) void ds16_panel_kernel(int e, int c0, int
   uint16_t* fcol = reinterpret_cast<uint16_t*>(used + e);                  // [e] (elimination factors)
   int* misc = reinterpret_cast<int*>(fcol + ((e + 1) & ~1));               // [0] bid, [1] fail, [2] inverse
   int* lpiv = misc + 4;                                                     // [P]
-  uint16_t* aug = reinterpret_cast<uint16_t*>(lpiv + kPanelMax);           // [P][2P]
   const int Pc = min(P, e - c0);
   for (int i = tid; i < e * P; i += B) {
     const int r = i / P, t = i - r * P;
@@ -504,13 +507,27 @@ __global__ __launch_bounds__(kThreads) void ds16_panel_kernel(int e, int c0, int
     }
     __syncthreads();
   }
-  // A[pi]^-1: Gauss-Jordan on [A[pi] | I] (Pc x 2Pc, row pivoting among the Pc rows; A[pi] is
-  // nonsingular because every pivot above was found)
+  for (int j = tid; j < Pc; j += B) w.piv[c0 + j] = lpiv[j];
+  for (int r = tid; r < e; r += B) w.used[r] = used[r];
+}
+
+// A[pi]^-1 of the panel just factored: Gauss-Jordan on [A[pi] | I] (Pc x 2Pc, row pivoting among the
+// Pc rows; A[pi] is nonsingular because every pivot was found). Its own launch: it reads the panel
+// snapshot the panel kernel wrote, which another wave of that kernel's block could see stale in L1.
+__global__ __launch_bounds__(kThreads) void ds16_ainv_kernel(int e, int c0, int P, Ws16 w) {
+  if (ws_failed(w)) return;
+  constexpr int B = kThreads;
+  const int tid = threadIdx.x;
+  __shared__ uint16_t aug[kPanelMax * 2 * kPanelMax];
+  __shared__ uint16_t fcol[kPanelMax];
+  __shared__ int misc[4];
+  const int Pc = min(P, e - c0);
   const int P2 = 2 * Pc;
   for (int i = tid; i < Pc * P2; i += B) {
     const int a = i / P2, t = i - a * P2;
-    aug[i] = t < Pc ? w.asn[size_t(lpiv[a]) * P + t] : uint16_t(t - Pc == a);
+    aug[i] = t < Pc ? w.asn[size_t(w.piv[c0 + a]) * P + t] : uint16_t(t - Pc == a);
   }
+  if (tid == 0) misc[1] = 0;
   __syncthreads();
   for (int j = 0; j < Pc; ++j) {
     if (tid == 0) {
@@ -546,8 +563,6 @@ __global__ __launch_bounds__(kThreads) void ds16_panel_kernel(int e, int c0, int
     const int a = i / P, t = i - a * P;
     w.ainv[i] = (a < Pc && t < Pc) ? aug[a * P2 + Pc + t] : uint16_t(0);
   }
-  for (int j = tid; j < Pc; j += B) w.piv[c0 + j] = lpiv[j];
-  for (int r = tid; r < e; r += B) w.used[r] = used[r];
 }
 
 // Y[j][col] = sum_i A[pi]^-1[j][i] M[pi_i][col], columns [c0, W)
@@ -665,6 +680,7 @@ hipError_t launch_blocked16(const uint16_t* g, int n, int k, const int* rows, in
   }
   for (int c0 = 0; c0 < e; c0 += P) {
     ds16_panel_kernel<<<1, kThreads, plds, stream>>>(e, c0, P, w);
+    ds16_ainv_kernel<<<1, kThreads, 0, stream>>>(e, c0, P, w);
     const unsigned cb = unsigned((W - c0 + kThreads - 1) / kThreads);
     ds16_y_kernel<P><<<cb, kThreads, 0, stream>>>(k, e, c0, w);
     ds16_update_kernel<P><<<dim3(cb, unsigned((e + kRowsPerBlock - 1) / kRowsPerBlock)), kThreads, 0, stream>>>(

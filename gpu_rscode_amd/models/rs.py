@@ -66,7 +66,19 @@ def row_pitch(ncols: int, device="cuda") -> int:
     if torch.device(device).type == "cuda" and ncols >= (8 << 20):
         a = max(PITCH, _row_align())
         p = (ncols + a - 1) // a * a
+        p += _row_skew(p)
     return p
+
+
+def _row_skew(p: int) -> int:
+    """Extra pitch for rows whose aligned pitch is a multiple of 64 MiB (GFRS_TUNE=row_skew=BYTES,
+    a multiple of 2 MiB; default 0)."""
+    from ..utils.tune import tune_int
+
+    skew = tune_int("row_skew", 0)
+    if skew <= 0 or skew % (2 << 20) or p % (64 << 20):
+        return 0
+    return skew
 
 
 class UnrecoverableError(gf.SingularMatrixError):

@@ -6,7 +6,7 @@
 // Run:   build/membench [REPS]     (prints one JSON object)
 //        build/membench sdma [ROWS WIDTH]   (copy engines vs blit copies, one JSON line per case)
 //        build/membench pitch [REPS]        (enc / dec patterns at different row pitches)
-//        build/membench k16 [REPS [PITCH_MiB...]]   (config #4's k = 16 patterns at 512 MiB rows)
+//        build/membench k16 [REPS [ROW_MiB [PITCH_MiB...]]]   (config #4's k = 16 patterns, 512 MiB rows)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -163,17 +163,18 @@ int pattern_main(int argc, char** argv) {
 // rebuilt natives plus the fused survivor copies), one span per wave (grid) and persistent. One
 // JSON line per case: the ceiling the k = 16 kernels are priced against.
 int k16_main(int argc, char** argv) {
-  const int64_t C = int64_t(512) << 20;
   const int reps = argc > 1 ? atoi(argv[1]) : 5;
-  // row pitches to compare (MiB, >= 512): alloc_rows gives 512 (a power of two: row j's byte x sits
-  // at j * 2^29 + x, the same offset inside every large power-of-two block); default: only that
+  // row length (MiB, default 512 = config #4's 8 GiB / 16) and the row pitches to compare (MiB,
+  // >= the row): a power-of-two pitch puts row j's byte x at j * 2^29 + x, the same offset inside
+  // every large power-of-two block; default: only the row length itself
+  const int64_t C = (argc > 2 ? int64_t(atoi(argv[2])) : 512) << 20;
   std::vector<int64_t> pitches;
-  for (int i = 2; i < argc; ++i) pitches.push_back(int64_t(atoi(argv[i])) << 20);
+  for (int i = 3; i < argc; ++i) pitches.push_back(int64_t(atoi(argv[i])) << 20);
   if (pitches.empty()) pitches.push_back(C);
   int64_t maxp = 0;
   for (int64_t p : pitches) {
     if (p < C) {
-      fprintf(stderr, "pitch below 512 MiB\n");
+      fprintf(stderr, "pitch below the row length\n");
       return 2;
     }
     maxp = std::max(maxp, p);
@@ -193,7 +194,7 @@ int k16_main(int argc, char** argv) {
   CHECK(hipEventCreate(&e0));
   CHECK(hipEventCreate(&e1));
   std::vector<std::vector<float>> t(cases.size() * pitches.size());
-  for (int round = 0; round < 3; ++round)
+  for (int round = 0; round < 5; ++round)
     for (size_t pi = 0; pi < pitches.size(); ++pi)
       for (size_t i = 0; i < cases.size(); ++i) {
         const Case& c = cases[i];
@@ -221,8 +222,9 @@ int k16_main(int argc, char** argv) {
       std::sort(v.begin(), v.end());
       const Case& c = cases[i];
       const double bytes = double(c.R + c.W) * C;
-      printf("{\"case\": \"%s\", \"pitch_mib\": %lld, \"us_median\": %.1f, \"us_min\": %.1f, \"TBps\": %.3f}\n",
-             c.name.c_str(), (long long)(pitches[pi] >> 20), v[v.size() / 2], v[0],
+      printf("{\"case\": \"%s\", \"row_mib\": %lld, \"pitch_mib\": %lld, \"us_median\": %.1f, \"us_min\": %.1f, "
+             "\"TBps\": %.3f}\n",
+             c.name.c_str(), (long long)(C >> 20), (long long)(pitches[pi] >> 20), v[v.size() / 2], v[0],
              bytes / (v[v.size() / 2] * 1e-6) / 1e12);
     }
   return 0;
