@@ -71,14 +71,23 @@ def row_pitch(ncols: int, device="cuda") -> int:
 
 
 def _row_skew(p: int) -> int:
-    """Extra pitch for rows whose aligned pitch is a multiple of 64 MiB (GFRS_TUNE=row_skew=BYTES,
-    a multiple of 2 MiB; default 0)."""
+    """Extra pitch for large rows whose 2 MiB-aligned pitch is a multiple of 64 MiB: a quarter of the
+    pitch (rounded to 2 MiB). At such a pitch every row's byte x sits at the same offset of a large
+    power-of-two block, and the k rows of a stripe stream into the same HBM channels together.
+    Measured on MI355X (scripts/membench.hip k16, profiles/headline/r09_k16): 16 rows of 512 MiB
+    stream the decode pattern (16 in, 16 out) at 5.35 TB/s with a 512 MiB pitch and 6.41 with 640,
+    the encode pattern (16 in, 4 out) at 5.38 / 5.54; 128 MiB rows 4.87 -> 5.36 (decode) at 160, 1 GiB
+    rows 4.98 -> 6.15 at 1280. The k16n20_8g step: 5.01-5.02 -> 4.68-4.70 ms (8 MiB: 4.89, 64 MiB:
+    4.78-4.80). Rows of the other BASELINE configs (104 MiB, 262 MiB, 8 MiB pitches) are not
+    multiples of 64 MiB and keep their pitch. GFRS_TUNE=row_skew=BYTES fixes the skew (0: none)."""
     from ..utils.tune import tune_int
 
-    skew = tune_int("row_skew", 0)
-    if skew <= 0 or skew % (2 << 20) or p % (64 << 20):
+    if p % (64 << 20):
         return 0
-    return skew
+    skew = tune_int("row_skew", -1)
+    if skew < 0:
+        return (p // 4) // (2 << 20) * (2 << 20)
+    return skew if skew % (2 << 20) == 0 else 0
 
 
 class UnrecoverableError(gf.SingularMatrixError):

@@ -325,14 +325,22 @@ def test_plan_cache_is_lru():
 
 def test_row_pitch_layout(monkeypatch):
     """alloc_rows / row_pitch: every pitch a multiple of 256 (16-byte aligned rows for odd C);
-    device rows of >= 8 MiB rounded to 2 MiB (measured HBM placement win), host rows never;
-    GFRS_TUNE=row_align overrides the large-row alignment."""
+    device rows of >= 8 MiB rounded to 2 MiB (measured HBM placement win), host rows never; pitches
+    that are multiples of 64 MiB skewed by a quarter; GFRS_TUNE=row_align / row_skew override."""
     from gpu_rscode_amd.models.rs import alloc_rows, row_pitch
     C = 107374183  # the headline chunk (1 GiB / 10, odd)
     assert row_pitch(C, "cpu") == 107374336
     assert row_pitch(C, "cuda") % (2 << 20) == 0 and row_pitch(C, "cuda") >= C
     assert row_pitch(1000, "cuda") == 1024 and row_pitch(1, "cuda") == 256
     assert row_pitch((8 << 20) - 1, "cuda") == 8 << 20
+    # a pitch that is a multiple of 64 MiB gets a quarter more (HBM channel placement of large rows)
+    assert row_pitch(512 << 20, "cuda") == 640 << 20 and row_pitch(128 << 20, "cuda") == 160 << 20
+    assert row_pitch((512 << 20) - 5, "cuda") == 640 << 20 and row_pitch(C, "cuda") == 104 << 20
+    assert row_pitch(512 << 20, "cpu") == 512 << 20
+    monkeypatch.setenv("GFRS_TUNE", "row_skew=8388608")
+    assert row_pitch(512 << 20, "cuda") == 520 << 20
+    monkeypatch.setenv("GFRS_TUNE", "row_skew=0")
+    assert row_pitch(512 << 20, "cuda") == 512 << 20
     monkeypatch.setenv("GFRS_TUNE", "row_align=256")
     assert row_pitch(C, "cuda") == 107374336
     t = alloc_rows(3, 1001, "cpu", fill=7)
