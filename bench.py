@@ -111,9 +111,10 @@ CONFIG_PRESETS = ("k128n160", "k16n20_8g", "k4n6", "k10n14_w16", "k4n6_cpu")
 # BASELINE.json configs. Weak presets are per GPU; strong presets are the whole job's bytes.
 PRESETS = {
     "k10n14": dict(k=10, n=14, bytes=1 << 30, erasures=4),
-    # one lane: with 512 MiB rows the two lanes' streams only contend for HBM (5.00-5.01 vs 5.06-5.10
-    # ms/step, three alternating rounds, profiles/headline/r09_k16)
-    "k16n20_8g": dict(k=16, n=20, bytes=8 << 30, erasures=4, lanes=1),
+    # (two lanes, the default: with alloc_rows' skewed 640 MiB pitch 4.72-4.77 ms/step against
+    # 4.94-4.96 with one lane; at the old 512 MiB pitch one lane had won, 5.00 vs 5.06-5.10:
+    # profiles/headline/r09_k16)
+    "k16n20_8g": dict(k=16, n=20, bytes=8 << 30, erasures=4),
     # config #4 as one stripe: 64 GiB column-sharded over the ranks (8 GiB each at N = 8), parity and
     # decoded natives gathered into rank 0 once after the timed loop (timed on its own)
     "k16n20_64g": dict(k=16, n=20, bytes=64 << 30, erasures=4, scaling="strong", gather="end", lanes=1),
