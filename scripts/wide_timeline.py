@@ -40,12 +40,12 @@ def load(path: str) -> list[dict]:
 def kind(name: str) -> str | None:
     if "gf_decode_system_kernel" in name:
         return "solve"
-    m = re.search(r"gf_gemm_fp4(?:ar|sk)?_kernel<([^>]*)>", name)
+    m = re.search(r"gf_gemm_fp4(ar|tm)?_kernel<([^>]*)>", name)
     if not m:
         return None
-    args = [a.strip() for a in m.group(1).split(",")]
-    # fp4ar<MGW, WPG, UNI, COPY, R>; fp4<MG, UNI, COPY, R, KS>; fp4sk<MG, UNI, COPY, R, KS, ABL>
-    copy = args[3] if "fp4ar" in name else args[2]
+    args = [a.strip() for a in m.group(2).split(",")]
+    # fp4ar<MGW, WPG, UNI, COPY, R, ...>; fp4<MG, UNI, COPY, R, KS>; fp4tm<MG, UNI, COPY>
+    copy = args[3] if m.group(1) == "ar" else args[2]
     return "decode" if copy == "true" else "encode"
 
 
