@@ -641,7 +641,7 @@ hipError_t launch_fp4_any(const Fp4Geometry& geo, const Fp4Args& a, hipStream_t 
 }
 
 // MG = 3 and 6 exist for the static 8-slot chunk only (geometry() picks them there; fp4_route sends
-// 5 and 7 tiles to the tile-major kernel), ring depth 4: the depth-8 forms fit the LDS but need ~90
+// 5 to 7 tiles to the tile-major kernel, so MG = 6 runs here only under GFRS_TUNE=fp4=v1), ring depth 4: the depth-8 forms fit the LDS but need ~90
 // more VGPRs (256 with spills into AGPRs) and ran 0-19 % slower at every shape
 // (profiles/wide_stripe/r02_exact_mg: k=128, m=28 + 100 copies 885 vs 1050 us)
 template <int MG>
@@ -662,8 +662,10 @@ hipError_t launch_fp4_static_any(const Fp4Geometry& geo, const Fp4Args& a, hipSt
 //     copies; r02_fp4_ablate);
 //   * 5 tiles: tm, plain and copies (m = 20: 595-611 vs 625-631 us plain, 750-766 vs 776-784 with
 //     108 copies; profiles/wide_stripe/r09_route);
-//   * 6 tiles: tm plain (m = 22/24: 644-673 vs 696-719 on v1, 668-677 on ar; r09_route, r08_tm); with
-//     copies v1 (830-836 us; the tm copy build spills 16 VGPRs and runs 1300 us, r09_route);
+//   * 6 tiles: tm, plain (m = 22/24: 644-673 vs 696-719 on v1, 668-677 on ar; r09_route, r08_tm)
+//     and with copies (818-842 vs 833-842 us; k128n160 1.405-1.416 vs 1.414-1.420 ms/step,
+//     profiles/wide_stripe/r09_tm6 — before its row indices were laundered, the tm copy build
+//     spilled 16 VGPRs to scratch and ran 1300 us);
 //   * 7 tiles: tm, plain and copies (m = 26: 729-767 vs 795-798 plain, 877-884 vs 935-940 with 102
 //     copies; r09_route);
 //   * 8 tiles: ar plain (the p = 32 encode: 809 vs 842 us; r02_fp4_ablate), v1 with copies (ar's two
@@ -697,7 +699,7 @@ Fp4Form fp4_route(const Fp4Geometry& geo, int k, bool copies) {
     case 4: return Fp4Form::kAResident;
     case 5:
     case 7: return Fp4Form::kTileMajor;
-    case 6: return copies ? Fp4Form::kV1 : Fp4Form::kTileMajor;
+    case 6: return Fp4Form::kTileMajor;
     case 8: return copies ? Fp4Form::kV1 : Fp4Form::kAResident;
     default: return Fp4Form::kV1;
   }

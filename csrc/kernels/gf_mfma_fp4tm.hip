@@ -132,7 +132,17 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4tm_kernel(cptr<uint64_t> in
   const int dcol = wave * kCW + 16 * (lane & 3);   // and its 16 columns (block-relative)
   const uint32_t rowptr_addr = lds0 + uint32_t(kA);
   const uint32_t cptr_addr = rowptr_addr + 8u * (256u + 32u);
-  auto slot_row = [&](int p) __attribute__((always_inline)) { return kRS * p + drow < k ? kRS * p + drow : k - 1; };
+  // (row indices pass through an empty asm at each use: hoisted out of the chunk loop, the 8 + 8
+  // per-slot LDS addresses they feed were spilled to scratch at MG = 6 with copies, and every
+  // reload made the compiler wait for the LDS-DMAs in flight)
+  auto opaque = [](int v) __attribute__((always_inline)) {
+    asm volatile("" : "+v"(v));
+    return v;
+  };
+  auto slot_row = [&](int p) __attribute__((always_inline)) {
+    const int r = kRS * p + opaque(drow);
+    return r < k ? r : k - 1;
+  };
   auto cbase = [&](int ci) __attribute__((always_inline)) {
     return col0 + (slot0 + int64_t(ci) * chunk_slots) * kBlockCols;
   };
@@ -148,7 +158,10 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4tm_kernel(cptr<uint64_t> in
     const bool live = cn < my_chunks && kRS * p + wrow < k && cp;
     __builtin_nontemporal_store(v, (gptr<u32x4>)(live ? cp + uint64_t(cbase(cn) + wcol) : sink));
   };
-  auto copy_row = [&](int p) __attribute__((always_inline)) { return kRS * p + wrow < k ? kRS * p + wrow : k - 1; };
+  auto copy_row = [&](int p) __attribute__((always_inline)) {
+    const int r = kRS * p + opaque(wrow);
+    return r < k ? r : k - 1;
+  };
   auto read_ptr = [&](uint64_t& v, uint32_t addr) __attribute__((always_inline)) {
     uint64_t r;
     asm volatile("ds_read_b64 %0, %1" : "=&v"(r) : "v"(addr) : "memory");

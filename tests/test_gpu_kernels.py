@@ -455,9 +455,10 @@ def test_decode_system_matches_host_decode_matrix(k, n, matrix):
 
 # every form the FP4 router (fp4_route, csrc/kernels/gf_mfma_fp4.hip) returns, with its shapes
 _ROUTE_CASES = [(128, 8, False, "v1"), (128, 12, True, "v1"), (128, 16, False, "ar"), (128, 16, True, "ar"),
-                (128, 20, False, "tm"), (128, 20, True, "tm"), (128, 24, False, "tm"), (128, 24, True, "v1"),
+                (128, 20, False, "tm"), (128, 20, True, "tm"), (128, 24, False, "tm"), (128, 24, True, "tm"),
                 (128, 26, True, "tm"), (128, 28, False, "tm"), (128, 32, False, "ar"), (128, 32, True, "v1"),
-                (128, 40, False, "v1"), (100, 17, True, "v1"), (40, 32, False, "v1")]
+                (128, 40, False, "v1"), (100, 17, True, "v1"), (40, 32, False, "v1"),
+                (128, 22, True, "tm"), (128, 12, False, "v1")]
 
 
 @pytest.mark.parametrize("k,m,copy,form", _ROUTE_CASES)
