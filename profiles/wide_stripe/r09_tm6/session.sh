@@ -9,9 +9,9 @@ export TMPDIR=/tmp HSA_ENABLE_IPC_MODE_LEGACY=0 GPURS_NO_BUILD=1
 O=gpurun_out/${1:-r6k}; mkdir -p $O
 R=${2:-2}
 st() { local n=$1 s=$2; shift 2; echo "[$(date +%T)] $n"; timeout -k 10 $s "$@" > $O/$n.log 2>&1; local rc=$?; echo "[$(date +%T)] $n rc=$rc"; return $rc; }
-st check_tm 240 env GFRS_TUNE=fp4=tm python3 -u scripts/tm6_check.py || exit 1
-st check_tm_early 240 env GFRS_TUNE=fp4=tm,tm_early=1 python3 -u scripts/tm6_check.py || exit 1
-st check_def 240 python3 -u scripts/tm6_check.py || exit 1
+st check_tm 240 env GFRS_TUNE=fp4=tm python3 -u scripts/fp4_check.py || exit 1
+st check_tm_early 240 env GFRS_TUNE=fp4=tm,tm_early=1 python3 -u scripts/fp4_check.py || exit 1
+st check_def 240 python3 -u scripts/fp4_check.py || exit 1
 for r in $(seq 1 $R); do
   st shapes_v1_$r 200 env GFRS_TUNE=fp4=v1 python3 -u scripts/fp4_shapes.py 20,22,24,26 || exit 1
   st shapes_tm_$r 200 env GFRS_TUNE=fp4=tm python3 -u scripts/fp4_shapes.py 20,22,24,26 || exit 1
