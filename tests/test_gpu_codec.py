@@ -470,6 +470,42 @@ print("DRS-RCCL-OK")
     assert r.returncode == 0 and "DRS-RCCL-OK" in r.stdout, (r.stdout[-2000:], r.stderr[-3000:])
 
 
+def test_distributed_rs_gf65536_on_a_one_rank_rccl_group():
+    """DistributedRS(field="gf65536") on a forced one-rank RCCL group: E and the survivor ids (here
+    up to 269, past a byte) travel as int32 RCCL broadcasts, the stripe through the RCCL scatter and
+    gather, the codec on the GPU's GF(2^16) kernels; bit-exact against the single-process codec."""
+    code = r'''
+import numpy as np, torch, torch.distributed as dist
+from gpu_rscode_amd.parallel import dist as pdist
+from gpu_rscode_amd.models import ReedSolomon
+ctx = pdist.init_distributed(force_pg=True)
+assert dist.get_backend() == "nccl" and dist.get_world_size() == 1
+k, n, C = 250, 270, 3 * 4096 + 78
+drs = pdist.DistributedRS(k, n, ctx, field="gf65536")
+ref = ReedSolomon(k, n, field="gf65536")
+host = np.random.default_rng(5).integers(0, 256, size=(k, C), dtype=np.uint8)
+data = torch.from_numpy(host).cuda()
+parity = drs.encode_global(data, C)
+torch.cuda.synchronize()
+want = torch.zeros((n - k, C), dtype=torch.uint8)
+ref.encode(torch.from_numpy(host), want)
+assert torch.equal(parity.cpu(), want)
+stripe = torch.cat([data, parity.contiguous()])
+rows = list(range(20, k)) + list(range(k, n))
+out = drs.decode_global(stripe[rows].contiguous(), rows, C)
+torch.cuda.synchronize()
+assert np.array_equal(out.cpu().numpy(), host)
+dist.destroy_process_group()
+print("DRS16-RCCL-OK")
+'''
+    env = dict(os.environ)
+    for v in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(v, None)
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run(["python", "-c", code], capture_output=True, text=True, timeout=180, env=env, cwd=root)
+    assert r.returncode == 0 and "DRS16-RCCL-OK" in r.stdout, (r.stdout[-2000:], r.stderr[-3000:])
+
+
 def test_host_pipeline_rows_beyond_the_2d_pitch_cap_copy_row_by_row():
     """Equally spaced host rows whose pitch exceeds the 2-D copy cap (2^31 - 1; lowered here with
     GFRS_TUNE=max_rect_pitch) move as per-row copies and still encode exactly."""
