@@ -160,17 +160,25 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4ar_kernel(cptr<uint64_t> in
   const int dcol = cg * kCW + 16 * (lane & 3);    // and its 16 columns (block-relative)
   auto dma_row = [&](int p) __attribute__((always_inline)) { return kRS * p + drow < k ? kRS * p + drow : k - 1; };
 
-  // A of this wave's tiles, resident in AGPRs for the whole kernel (tiles past mg: zero)
+  // A of this wave's tiles, resident in AGPRs for the whole kernel. All 64 loads are unconditional
+  // and issued before the first register tie: a conditional load (tiles past mg read zero) tied
+  // right after it made every load wait for the one before — 64 serialised L2 round trips per block
+  // (batched RS(128,160) encode of 16 x 64 KiB 18.0 -> 12.5-13.1 us, profiles/wide_stripe/r09_select).
+  // A padding tile (past mg) now reads the last real tile's A: its rows have no output pointer, so
+  // whatever it accumulates goes to the sink.
   i32x4 A[MGW][kNS];
   static_for<MGW>([&](auto t_tag) {
     constexpr int T = decltype(t_tag)::value;
-    const int mt = mh * MGW + T;
+    const int mt = min(mh * MGW + T, mg - 1);
     static_for<kNS>([&](auto s_tag) {
       constexpr int S = decltype(s_tag)::value;
-      A[T][S] = mt < mg ? bitmat[(size_t(S) * mg + mt) * 64 + lane] : i32x4{0, 0, 0, 0};
-      asm volatile("" : "+a"(A[T][S]));
+      A[T][S] = bitmat[(size_t(S) * mg + mt) * 64 + lane];
     });
   });
+#pragma unroll
+  for (int t = 0; t < MGW; ++t)
+#pragma unroll
+    for (int q = 0; q < kNS; ++q) asm volatile("" : "+a"(A[t][q]));
   // accumulator start value: 2^(23 - b) on output bit b = accumulator register & 7
   f32x16 bias;
 #pragma unroll
@@ -496,8 +504,8 @@ bool fp4ar_supported(int k, int mg) { return k > 112 && k <= 128 && mg >= 1 && m
 hipError_t launch_gf_gemm_fp4ar(const Fp4ArLaunch& a, int64_t* done, hipStream_t stream) {
   *done = 0;
   if (!fp4ar_supported(a.k, a.mg) || a.m > 4 * a.mg || a.ncols < 0 || (a.col0 & 1)) return hipErrorInvalidValue;
-  // rows split in two halves of at most 4 tiles when more than 4 tiles (padding tiles read zero A
-  // and store to the sink), else one wave covers every tile and the block 4 column groups
+  // rows split in two halves of at most 4 tiles when more than 4 tiles (padding tiles reuse the last
+  // tile's A and store to the sink), else one wave covers every tile and the block 4 column groups
   switch (a.mg) {
     case 1: return launch_ar_b<1, 1>(a, done, stream);
     case 2: return launch_ar_b<2, 1>(a, done, stream);

@@ -155,8 +155,15 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4tm_kernel(cptr<uint64_t> in
   };
   // fused copy of ring slot p (chunk cn's bytes), block-wide (wrow, wcol); cp: the row's copy pointer
   auto copy_store = [&](int cn, int p, uint64_t cp, u32x4 v) __attribute__((always_inline)) {
-    const bool live = cn < my_chunks && kRS * p + wrow < k && cp;
-    __builtin_nontemporal_store(v, (gptr<u32x4>)(live ? cp + uint64_t(cbase(cn) + wcol) : sink));
+    // (the address is a select, not a branch: as a divergent branch it split the last tile group into
+    // basic blocks, and the compiler then moved that group's MFMAs away from the B expansion they
+    // were scheduled to hide — 4x less VALU/MFMA co-execution; k128n160 1.472-1.480 -> 1.443-1.445
+    // ms/step on one box, profiles/wide_stripe/r09_select)
+    const uint64_t live = uint64_t(cn < my_chunks) & uint64_t(kRS * p + wrow < k) & uint64_t(cp != 0);
+    const uint64_t m = 0 - live;
+    uint64_t addr = ((cp + uint64_t(cbase(cn) + wcol)) & m) | (sink & ~m);
+    asm volatile("" : "+v"(addr));  // (kept a select: see above)
+    __builtin_nontemporal_store(v, (gptr<u32x4>)addr);
   };
   auto copy_row = [&](int p) __attribute__((always_inline)) {
     const int r = kRS * p + opaque(wrow);
