@@ -33,9 +33,11 @@ def test_tools_parse_arguments_on_a_host(script):
 
 
 @pytest.mark.skipif(not os.path.exists("/opt/rocm/bin/hipcc"), reason="hipcc not available")
-@pytest.mark.parametrize("src", ["scripts/membench.hip", "scripts/fp4_pattern_probe.hip"])
+@pytest.mark.parametrize("src", ["scripts/membench.hip", "scripts/fp4_pattern_probe.hip",
+                                 "scripts/bperm_probe.hip"])
 def test_hip_probes_compile_for_gfx950(src, tmp_path):
-    """The standalone HIP probes behind profiles/ (memory ceilings, the wide decode's access pattern)
+    """The standalone HIP probes behind profiles/ (memory ceilings, the wide decode's access pattern,
+    the GF(2^16) lookup rates)
     still build for gfx950 (cross-compiled on the host; they run only on the GPU box)."""
     r = subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-o",
                         str(tmp_path / "probe"), os.path.join(ROOT, src)], capture_output=True, text=True,
