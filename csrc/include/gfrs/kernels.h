@@ -175,7 +175,7 @@ struct Fp4ArLaunch {
 bool fp4ar_supported(int k, int mg);
 hipError_t launch_gf_gemm_fp4ar(const Fp4ArLaunch& a, int64_t* done, hipStream_t stream);
 // Tile-major form (csrc/kernels/gf_mfma_fp4tm.hip): same launch record (batch must be 1), k in
-// (112, 128] with one group of 5..7 M-tiles; the chunk's B operand resident
+// (112, 128] with one group of 5..8 M-tiles; the chunk's B operand resident
 // in AGPRs, tiles in pairs.
 bool fp4tm_supported(int k, int mg, bool copies);
 hipError_t launch_gf_gemm_fp4tm(const Fp4ArLaunch& a, int64_t* done, hipStream_t stream);

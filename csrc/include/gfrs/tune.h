@@ -6,7 +6,7 @@
 //   GFRS_TUNE=fp4=tm,ksplit_lanes=0 python bench.py --preset k128n160
 //
 // Keys (docs/API.md lists them with their defaults): fp4 (v1 | ar | tm: force a GF(2^8) FP4 kernel
-// form where it is built), rows_lat_groups, ksplit_lanes, short_lanes, vec_cfg (V:PF:NT), gf16_vec_g,
+// form where it is built), tm8, rows_lat_groups, ksplit_lanes, short_lanes, vec_cfg (V:PF:NT), gf16_vec_g,
 // gf16_short_groups, fp16_mg, fp4_free_cus, max_rect_pitch, zc_stream (own), setup (serial), crc
 // (scalar). Unknown keys are ignored. Besides GFRS_TUNE the native code reads only GFRS_HOST_ALLOC
 // and GFRS_VERIFY_THREADS (operational choices, not tuning).

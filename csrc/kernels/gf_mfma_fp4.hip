@@ -668,8 +668,10 @@ hipError_t launch_fp4_static_any(const Fp4Geometry& geo, const Fp4Args& a, hipSt
 //     spilled 16 VGPRs to scratch and ran 1300 us);
 //   * 7 tiles: tm, plain and copies (m = 26: 729-767 vs 795-798 plain, 877-884 vs 935-940 with 102
 //     copies; r09_route);
-//   * 8 tiles: ar plain (the p = 32 encode: 809 vs 842 us; r02_fp4_ablate), v1 with copies (ar's two
-//     row halves lose with copies: 1060-1360 vs 760-970 us);
+//   * 8 tiles: ar plain (the p = 32 encode: 809 vs 842 us on v1, r02_fp4_ablate; 798-827 vs 809-835
+//     on tm, profiles/wide_stripe/r10_tm8), tm with copies (tile 7's A in registers: m = 29 / 30 / 32
+//     + 99 / 98 / 96 copies 931-950 vs 979-1007 us on v1 and 997-1018 on ar; k128n160 1.418 vs
+//     1.426 ms/step over 100 steps, r10_tm8);
 //   * more than one group (m > 32) or k outside (112, 128]: v1.
 // GFRS_TUNE=fp4=v1|ar|tm forces that form wherever it is built for the shape (A/B measurements).
 enum class Fp4Form { kV1, kAResident, kTileMajor };
@@ -700,7 +702,8 @@ Fp4Form fp4_route(const Fp4Geometry& geo, int k, bool copies) {
     case 5:
     case 7: return Fp4Form::kTileMajor;
     case 6: return Fp4Form::kTileMajor;
-    case 8: return copies ? Fp4Form::kV1 : Fp4Form::kAResident;
+    case 8:  // (GFRS_TUNE=tm8=0: copies back on v1, for A/B runs)
+      return copies ? (tune_int("tm8", 1) ? Fp4Form::kTileMajor : Fp4Form::kV1) : Fp4Form::kAResident;
     default: return Fp4Form::kV1;
   }
 }

@@ -21,6 +21,9 @@
 //     the memory system takes at 1.7x the rate of one wave's 16 rows x 64 B.
 // With an odd tile count the last group is one tile: the next chunk's B expansion fills its stalls.
 // Per 256-column chunk at 7 tiles: 224 MFMAs and ~680 VALU (v1: 238 MFMAs, ~840 VALU).
+// At 8 tiles the A slice (128 KiB) plus the rings (32 KiB) and pointer tables would not fit the
+// 160 KiB LDS, so tile 7's 16 A fragments stay in registers (64 AGPRs beside the 128 of B) and
+// only tiles 0..6 are staged in LDS (112 KiB).
 //
 // Accumulator sets alternate by global group number; with an odd group count the chunk loop is
 // unrolled by two so the set a group writes is never the one still waiting to be packed. An odd
@@ -90,8 +93,9 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4tm_kernel(cptr<uint64_t> in
                                                                cptr<uint64_t> copy, const i32x4* __restrict__ bitmat,
                                                                int k, int m, int64_t col0, int64_t nchunks,
                                                                int64_t chunk_slots, int64_t in_stride) {
-  static_assert(MG >= 5 && MG <= 7, "three tile groups at least: DMAs in group 0, the wait in group NG-2");
-  constexpr size_t kA = size_t(MG) * kNS * 1024;  // LDS A slice [kstep][tile][lane] x 16 B
+  static_assert(MG >= 5 && MG <= 8, "three tile groups at least: DMAs in group 0, the wait in group NG-2");
+  constexpr int kLT = MG < 8 ? MG : 7;             // tiles whose A is staged in LDS (tile 7: registers)
+  constexpr size_t kA = size_t(kLT) * kNS * 1024;  // LDS A slice [kstep][tile < kLT][lane] x 16 B
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   i32x4* afrag = reinterpret_cast<i32x4*>(smem);
   uint64_t* rowptr = reinterpret_cast<uint64_t*>(smem + kA);
@@ -103,7 +107,8 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4tm_kernel(cptr<uint64_t> in
   const int my_chunks = int((nchunks - slot0 + chunk_slots - 1) / chunk_slots);
   if (my_chunks <= 0) return;
 
-  for (int i = threadIdx.x; i < MG * kNS * 64; i += 256) afrag[i] = bitmat[i];
+  for (int i = threadIdx.x; i < kLT * kNS * 64; i += 256)  // bitmat: [kstep][tile < MG][lane]
+    afrag[i] = bitmat[(i / (kLT * 64)) * (MG * 64) + i % (kLT * 64)];
   if (!UNI)
     for (int i = threadIdx.x; i < k; i += 256) rowptr[i] = in[i];
   for (int i = threadIdx.x; i < 32; i += 256) outptr[i] = i < m ? out[i] : 0;
@@ -193,9 +198,10 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4tm_kernel(cptr<uint64_t> in
     x[2] = x2;
     x[3] = x3;
   };
-  // A fragment of (tile T, K-step S)
+  // A fragment of (tile T < kLT, K-step S) from LDS
   auto read_a = [&](i32x4& a, auto t_tag, auto s_tag) __attribute__((always_inline)) {
-    constexpr int off = (decltype(s_tag)::value * MG + decltype(t_tag)::value) * 1024;
+    static_assert(decltype(t_tag)::value < kLT, "tile 7 of 8 is register-resident");
+    constexpr int off = (decltype(s_tag)::value * kLT + decltype(t_tag)::value) * 1024;
     const uint32_t base = off >= 65536 ? a_hi : a_lo;
     i32x4 v;
     asm volatile("ds_read_b128 %0, %1 offset:%2" : "=&v"(v) : "v"(base), "n"(off % 65536) : "memory");
@@ -249,6 +255,16 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4tm_kernel(cptr<uint64_t> in
   };
 
   i32x4 Bc[kNS][2];     // B of the chunk being multiplied, resident in AGPRs
+  // tile 7's A at MG = 8 (every K-step), loaded once and kept in AGPRs: its group reads it in place
+  [[maybe_unused]] i32x4 A7[kNS];
+  if constexpr (MG == 8) {
+#pragma unroll
+    for (int q = 0; q < kNS; ++q) A7[q] = bitmat[(size_t(q) * MG + 7) * 64 + lane];
+#pragma unroll
+    for (int q = 0; q < kNS; ++q) asm volatile("" : "+a"(A7[q]));
+  }
+  // whether tile T's A is register-resident (read in place, never through Acur)
+  constexpr auto kRegA = [](int T) { return MG == 8 && T == 7; };
   f32x16 acc[2][2][2];  // [set][tile of the group][N-tile]
   f32x16 bias;          // start value 2^(23 - b) on output bit b = accumulator register & 7
 #pragma unroll
@@ -340,7 +356,7 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4tm_kernel(cptr<uint64_t> in
         static_for<kQ>([&](auto j) {
           constexpr int J = decltype(j)::value;
           read_a(An[0][J], std::integral_constant<int, NT0>{}, std::integral_constant<int, kQ * NQ + J>{});
-          if constexpr (NGS == 2)
+          if constexpr (NGS == 2 && !kRegA(NT0 + 1))
             read_a(An[1][J], std::integral_constant<int, NT0 + 1>{}, std::integral_constant<int, kQ * NQ + J>{});
         });
         constexpr bool kLastG = G == NG - 1;
@@ -380,7 +396,8 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4tm_kernel(cptr<uint64_t> in
           constexpr int S = kQ * Q + J;
 #pragma unroll
           for (int e = 0; e < GS; ++e) {
-            const i32x8 a = {Acur[e][J][0], Acur[e][J][1], Acur[e][J][2], Acur[e][J][3], 0, 0, 0, 0};
+            const i32x4& af = kRegA(T0 + e) ? A7[S] : Acur[e][J];
+            const i32x8 a = {af[0], af[1], af[2], af[3], 0, 0, 0, 0};
 #pragma unroll
             for (int n = 0; n < 2; ++n) {
               const i32x8 bb = {Bc[S][n][0], Bc[S][n][1], Bc[S][n][2], Bc[S][n][3], 0, 0, 0, 0};
@@ -432,7 +449,7 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4tm_kernel(cptr<uint64_t> in
         for (int j = 0; j < kQ; ++j) {
           tie(An[0][j]);
           Acur[0][j] = An[0][j];
-          if constexpr (NGS == 2) {
+          if constexpr (NGS == 2 && !kRegA(NT0 + 1)) {
             tie(An[1][j]);
             Acur[1][j] = An[1][j];
           }
@@ -503,7 +520,7 @@ __global__ __launch_bounds__(256, 1) void gf_gemm_fp4tm_kernel(cptr<uint64_t> in
 template <int MG, bool UNI, bool COPY>
 hipError_t launch_tm(const Fp4ArLaunch& a, int64_t* done, hipStream_t stream) {
   const void* f = reinterpret_cast<const void*>(&gf_gemm_fp4tm_kernel<MG, UNI, COPY>);
-  const size_t lds = size_t(MG) * kNS * 1024 + kPtrBytes + size_t(4) * kKS * kSlotBytes;
+  const size_t lds = size_t(MG < 8 ? MG : 7) * kNS * 1024 + kPtrBytes + size_t(4) * kKS * kSlotBytes;
   if (lds > 160 * 1024) return hipErrorInvalidConfiguration;
   hipError_t e = ensure_lds_optin(f, int(lds));
   if (e != hipSuccess) return e;
@@ -534,7 +551,7 @@ hipError_t launch_tm_var(const Fp4ArLaunch& a, int64_t* done, hipStream_t stream
 
 bool fp4tm_supported(int k, int mg, bool copies) {
   (void)copies;
-  return k > 112 && k <= 128 && mg >= 5 && mg <= 7;
+  return k > 112 && k <= 128 && mg >= 5 && mg <= 8;
 }
 
 hipError_t launch_gf_gemm_fp4tm(const Fp4ArLaunch& a, int64_t* done, hipStream_t stream) {
@@ -545,7 +562,8 @@ hipError_t launch_gf_gemm_fp4tm(const Fp4ArLaunch& a, int64_t* done, hipStream_t
   switch (a.mg) {
     case 5: return launch_tm_var<5>(a, done, stream);
     case 6: return launch_tm_var<6>(a, done, stream);
-    default: return launch_tm_var<7>(a, done, stream);
+    case 7: return launch_tm_var<7>(a, done, stream);
+    default: return launch_tm_var<8>(a, done, stream);
   }
 }
 

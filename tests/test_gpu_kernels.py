@@ -346,12 +346,13 @@ def test_fp4_fused_copy_decode_shape(m):
     assert (got[ncopy:] == 0x44).all()
 
 
-@pytest.mark.parametrize("k,m", [(128, 26), (128, 20), (128, 24), (120, 21), (113, 17)])
+@pytest.mark.parametrize("k,m", [(128, 26), (128, 20), (128, 24), (120, 21), (113, 17), (128, 32), (128, 29),
+                                 (116, 30)])
 @pytest.mark.parametrize("variant", ["uniform", "scattered", "copy"])
 @pytest.mark.parametrize("nblk", [256 * 3 + 5, 256 * 2, 40])
 def test_fp4_tile_major_kernel_matches_oracle(k, m, variant, nblk, monkeypatch):
     """The tile-major FP4 kernel (gf_gemm_fp4tm_kernel, GFRS_TUNE=fp4=tm: the chunk's B resident
-    in AGPRs, tiles in turn, 5..7 M-tiles). Column counts give the persistent blocks an odd or an
+    in AGPRs, tiles in turn, 5..8 M-tiles; at 8 tiles tile 7's A is register-resident). Column counts give the persistent blocks an odd or an
     even number of chunks (the phantom chunk and the drain after the loop) or a single one, plus a
     v_perm remainder. The fused copy covers the first inputs only (the decode layout). Bit-exact
     against the oracle, and nothing is written outside the outputs' and copies' columns."""
@@ -382,7 +383,7 @@ def test_fp4_tile_major_kernel_matches_oracle(k, m, variant, nblk, monkeypatch):
         assert (c[ncopy:] == 0x44).all()
 
 
-@pytest.mark.parametrize("m,copy", [(26, True), (26, False), (20, False)])
+@pytest.mark.parametrize("m,copy", [(26, True), (26, False), (20, False), (30, True)])
 def test_fp4_tile_major_column_windows(m, copy):
     """Windowed launches on the tile-major kernel (its default shapes): three column windows with
     ragged starts and lengths, as the windowed codecs issue them, fill exactly their columns.
@@ -456,7 +457,7 @@ def test_decode_system_matches_host_decode_matrix(k, n, matrix):
 # every form the FP4 router (fp4_route, csrc/kernels/gf_mfma_fp4.hip) returns, with its shapes
 _ROUTE_CASES = [(128, 8, False, "v1"), (128, 12, True, "v1"), (128, 16, False, "ar"), (128, 16, True, "ar"),
                 (128, 20, False, "tm"), (128, 20, True, "tm"), (128, 24, False, "tm"), (128, 24, True, "tm"),
-                (128, 26, True, "tm"), (128, 28, False, "tm"), (128, 32, False, "ar"), (128, 32, True, "v1"),
+                (128, 26, True, "tm"), (128, 28, False, "tm"), (128, 32, False, "ar"), (128, 32, True, "tm"),
                 (128, 40, False, "v1"), (100, 17, True, "v1"), (40, 32, False, "v1"),
                 (128, 22, True, "tm"), (128, 12, False, "v1")]
 
@@ -494,7 +495,7 @@ def test_fp4_router_every_form_matches_oracle(k, m, copy, form, scattered):
             assert np.array_equal(c[j], want_in[j] if j % 4 else np.full(ncols, 0x44, np.uint8)), (form, j)
 
 
-@pytest.mark.parametrize("k,m,copy", [(128, 26, True), (128, 24, False), (128, 16, True)])
+@pytest.mark.parametrize("k,m,copy", [(128, 26, True), (128, 24, False), (128, 16, True), (128, 30, True)])
 def test_fp4_forced_forms_agree(k, m, copy, monkeypatch):
     """GFRS_TUNE=fp4=v1 / ar / tm (the A/B override) on a shape each of them is built for: the
     three forms give identical bytes."""

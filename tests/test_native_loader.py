@@ -64,7 +64,7 @@ def test_fp4_router_table():
     h = hip()
     want = {(8, False): "v1", (12, True): "v1", (16, False): "ar", (16, True): "ar", (20, False): "tm",
             (20, True): "tm", (24, False): "tm", (24, True): "tm", (28, True): "tm", (28, False): "tm",
-            (32, False): "ar", (32, True): "v1", (40, False): "v1"}
+            (32, False): "ar", (32, True): "tm", (40, False): "v1"}
     for (m, copy), form in want.items():
         assert h.fp4_route(128, m, copy, 8) == form, (m, copy)
     assert h.fp4_route(100, 17, False, 8) == "v1"  # k outside (112, 128]
@@ -73,6 +73,10 @@ def test_fp4_router_table():
         assert h.fp4_route(128, 28, True, 8) == "tm"  # (no v1 build for 7 tiles: the routed form)
         assert h.fp4_route(128, 16, True, 8) == "v1"
         assert h.fp4_route(128, 24, True, 8) == "v1"
+        assert h.fp4_route(128, 32, True, 8) == "v1"
+        os.environ["GFRS_TUNE"] = "tm8=0"
+        assert h.fp4_route(128, 32, True, 8) == "v1"
+        assert h.fp4_route(128, 32, False, 8) == "ar"
         os.environ["GFRS_TUNE"] = "ksplit_lanes=5,fp4=tm"
         assert h.fp4_route(128, 24, True, 8) == "tm"
         assert h.fp4_route(128, 12, True, 8) == "v1"  # (not built for 3 tiles: the routed form)
