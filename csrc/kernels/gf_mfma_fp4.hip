@@ -655,7 +655,7 @@ hipError_t launch_fp4_static_any(const Fp4Geometry& geo, const Fp4Args& a, hipSt
 // ---- the one routing decision of the GF(2^8) FP4 engine ------------------------------------------
 // Forms: v1 (the LDS-ring kernel above: any k, any M-tile count, groups of M-tiles), ar (A-resident,
 // gf_mfma_fp4ar.hip: bit-matrix in AGPRs, k in (112, 128], one group of <= 8 tiles, also the batched
-// launch) and tm (tile-major, gf_mfma_fp4tm.hip: B in AGPRs, tiles in pairs, 5..7 tiles). Every
+// launch) and tm (tile-major, gf_mfma_fp4tm.hip: B in AGPRs, tiles in pairs, 5..8 tiles). Every
 // branch is a measured win (k = 128, 1 GiB, medians, two interleaved rounds each):
 //   * 1..3 tiles: v1 — memory-bound shapes; ar loses there (profiles/wide_stripe/r02_fp4_ablate);
 //   * 4 tiles: ar, plain and with fused copies (m = 16: 490 vs 530 us plain, 659 vs 722 with 112
