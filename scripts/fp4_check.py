@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Bit-exact check of the FP4 GEMM on k = 128 shapes under whatever GFRS_TUNE the caller sets (e.g.
-fp4=tm to force the tile-major form): 5-7 tiles with fused copies, and 5-8 tiles plain with
+fp4=tm to force the tile-major form): 5-8 tiles with fused copies, and 5-8 tiles plain with
 uniform-stride and with scattered input rows; several chunk counts per persistent block (odd and
 even) and a ragged column tail. Prints one line per case, exits non-zero on the first mismatch."""
 import os
@@ -17,7 +17,7 @@ from gpu_rscode_amd.ops import GemmPlan
 
 def main() -> int:
     k = 128
-    cases = [(m, "copies") for m in (20, 21, 22, 24, 26, 28)]
+    cases = [(m, "copies") for m in (20, 21, 22, 24, 26, 28, 29, 32)]
     cases += [(m, kind) for m in (20, 24, 28, 29, 32) for kind in ("uniform", "scattered")]
     for m, kind in cases:
         for ncols in (256 * 256 * 3 + 77, 256 * 256 * 6 + 2, 256 * 1000 + 130):
