@@ -170,7 +170,7 @@ def parse(argv=None):
                     help="BASELINE.json config: k10n14 (headline, #2/#3), k16n20_8g (#4 per GPU), k16n20_64g "
                          "(#4 as one 64 GiB stripe), k128n160 (#5), k4n6 (the reference's published shape)")
     ap.add_argument("--engine", default="auto", choices=["auto", "valu", "mfma"],
-                    help="encode GEMM engine (auto: FP4 matrix cores for wide stripes, v_perm otherwise)")
+                    help="encode GEMM engine, GF(2^8) and GF(2^16) (auto: FP4 matrix cores for wide stripes, v_perm otherwise)")
     ap.add_argument("--graph", action="store_true", help="replay each step from a captured hipGraph (N = 1)")
     ap.add_argument("--pg-backend", default=None, choices=["nccl", "gloo"],
                     help="process-group backend (default: nccl = RCCL on cuda, gloo on cpu). gloo on cuda "
@@ -297,8 +297,8 @@ class GpuWorkload:
         # erased natives per pool pattern (known on the host: it picks the plan shape, the pattern
         # itself only ever travels on the device)
         self.e_of = [k - sum(1 for r in rows if r < k) for rows in pool_dev.tolist()]
-        self.enc = [Gemm16Plan(self.data, par, e_mat) if self.wide else GemmPlan(self.data, par, e_mat, engine=a.engine)
-                    for par in self.parity]
+        self.enc = [Gemm16Plan(self.data, par, e_mat, engine=a.engine) if self.wide
+                    else GemmPlan(self.data, par, e_mat, engine=a.engine) for par in self.parity]
         # one device-built decode plan per (slot, number of erased natives)
         self.dec = [{e: PatternDecoder(self.g_dev, [self.data[i] for i in range(k)] + [par[i] for i in range(self.p)],
                                        [self.outs[s % self.lanes][i] for i in range(k)], e)
