@@ -61,14 +61,54 @@ __device__ uint32_t mul16(uint32_t a, uint32_t b) {
   return r;
 }
 
-// a^(2^16 - 2) = a^-1 for a != 0: r = prod_{i=1..15} a^(2^i)
-__device__ uint32_t inv16(uint32_t a) {
-  uint32_t r = 1, s = a;
-  for (int i = 1; i < 16; ++i) {
-    s = mul16(s, s);
-    r = mul16(r, s);
+// a^2: squaring is GF(2)-linear — spread bit i to bit 2i, then reduce the 31-bit result with
+// x^16 = x^12 + x^3 + x + 1 (four folds: each halves what is left above bit 15)
+__device__ __forceinline__ uint32_t sq16(uint32_t a) {
+  uint32_t x = a & 0xFFFFu;
+  x = (x | (x << 8)) & 0x00FF00FFu;
+  x = (x | (x << 4)) & 0x0F0F0F0Fu;
+  x = (x | (x << 2)) & 0x33333333u;
+  x = (x | (x << 1)) & 0x55555555u;
+#pragma unroll
+  for (int f = 0; f < 4; ++f) {
+    const uint32_t hi = x >> 16;
+    x = (x & 0xFFFFu) ^ (hi << 12) ^ (hi << 3) ^ (hi << 1) ^ hi;
   }
-  return r;
+  return x;
+}
+__device__ __forceinline__ uint32_t sqn16(uint32_t a, int n) {
+  for (int i = 0; i < n; ++i) a = sq16(a);
+  return a;
+}
+
+// a^-1 = (a^(2^15 - 1))^2 for a != 0, by the Itoh-Tsujii chain b_k = a^(2^k - 1):
+// b2 = b1^2 b1, b3 = b2^2 a, b6 = b3^(2^3) b3, b7 = b6^2 a, b14 = b7^(2^7) b7, b15 = b14^2 a —
+// 15 squarings and 6 multiplies instead of 15 + 15 (the pivot inverses run on one lane)
+__device__ uint32_t inv16(uint32_t a) {
+  const uint32_t b2 = mul16(sq16(a), a);
+  const uint32_t b3 = mul16(sq16(b2), a);
+  const uint32_t b6 = mul16(sqn16(b3, 3), b3);
+  const uint32_t b7 = mul16(sq16(b6), a);
+  const uint32_t b14 = mul16(sqn16(b7, 7), b7);
+  const uint32_t b15 = mul16(sq16(b14), a);
+  return sq16(b15);
+}
+
+// nibble-product table of c: tab[q * 16 + v] (stride `stride` words) = c * (v << 4q)
+template <typename T>
+__device__ __forceinline__ void nib_table(uint32_t c, T* tab, int stride, int q) {
+  uint32_t b0 = c;
+  for (int s = 0; s < 4 * q; ++s) b0 = xtime16(b0);
+  const uint32_t b1 = xtime16(b0), b2 = xtime16(b1), b3 = xtime16(b2);
+#pragma unroll
+  for (int v = 0; v < 16; ++v)
+    tab[(q * 16 + v) * stride] = T(((v & 1) ? b0 : 0u) ^ ((v & 2) ? b1 : 0u) ^ ((v & 4) ? b2 : 0u) ^ ((v & 8) ? b3 : 0u));
+}
+// c * x from c's nibble table (stride words apart)
+template <typename T>
+__device__ __forceinline__ uint32_t nib_mul(const T* tab, int stride, uint32_t x) {
+  return uint32_t(tab[(x & 15u) * stride]) ^ uint32_t(tab[(16 + ((x >> 4) & 15u)) * stride]) ^
+         uint32_t(tab[(32 + ((x >> 8) & 15u)) * stride]) ^ uint32_t(tab[(48 + (x >> 12)) * stride]);
 }
 
 // v_perm record of the byte map with basis images b[0..7] (layout of gfrs::perm_from_basis)
@@ -366,9 +406,12 @@ __host__ __device__ inline Ws16 ws16_of(void* base, int n, int k, int e, int P) 
   return w;
 }
 
-// LDS of the panel kernel: panel [e][P] | used [e] | factors [e] | misc | pivots
+// LDS of the panel kernel: product tables [4][16][P] u32 | panel [e][P] | used [e] | factors [e] |
+// misc | pivots
+__host__ __device__ inline size_t panel_tab_bytes(int P) { return size_t(4) * 16 * P * 4; }
 __host__ __device__ inline size_t panel_lds(int e, int P) {
-  return al256(size_t(e) * P * 2) + size_t(e) * 4 + size_t((e + 1) & ~1) * 2 + 16 + 4 * kPanelMax;
+  return panel_tab_bytes(P) + al256(size_t(e) * P * 2) + size_t(e) * 4 + size_t((e + 1) & ~1) * 2 + 16 +
+         4 * kPanelMax;
 }
 
 // panel width: the widest power of two <= 32 whose panel kernel fits the LDS
@@ -459,22 +502,29 @@ __global__ __launch_bounds__(kThreads) void ds16_gather_kernel(const uint16_t* _
 }
 
 // One panel [c0, c0 + P): pivot rows by Gauss-Jordan on the panel in LDS, and its snapshot.
-__global__ __launch_bounds__(kThreads) void ds16_panel_kernel(int e, int c0, int P, Ws16 w) {
+template <int P>
+__global__ __launch_bounds__(kThreads) void ds16_panel_kernel(int e, int c0, Ws16 w) {
   if (ws_failed(w)) return;
+  static_assert(kThreads % P == 0, "whole rows per pass");
+  constexpr int kRP = kThreads / P;  // rows per pass: lane tid works on column t = tid % P
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   constexpr int B = kThreads;
   const int tid = threadIdx.x;
-  uint16_t* pan = reinterpret_cast<uint16_t*>(smem);                       // [e][P]
-  int* used = reinterpret_cast<int*>(smem + al256(size_t(e) * P * 2));     // [e]
+  // ptab[(q * 16 + v) * P + t] = (pivot row value t) * (v << 4q): a product by a factor f is then
+  // four nibble lookups (t fastest: the lanes of a row step hit spread banks)
+  uint32_t* ptab = reinterpret_cast<uint32_t*>(smem);
+  uint8_t* body = smem + panel_tab_bytes(P);
+  uint16_t* pan = reinterpret_cast<uint16_t*>(body);                       // [e][P]
+  int* used = reinterpret_cast<int*>(body + al256(size_t(e) * P * 2));     // [e]
   uint16_t* fcol = reinterpret_cast<uint16_t*>(used + e);                  // [e] (elimination factors)
   int* misc = reinterpret_cast<int*>(fcol + ((e + 1) & ~1));               // [0] bid, [1] fail, [2] inverse
   int* lpiv = misc + 4;                                                     // [P]
   const int Pc = min(P, e - c0);
-  for (int i = tid; i < e * P; i += B) {
-    const int r = i / P, t = i - r * P;
-    const uint16_t v = t < Pc ? w.m[size_t(r) * w.ld + c0 + t] : uint16_t(0);
-    pan[i] = v;
-    w.asn[i] = v;
+  const int tl = tid % P, rl = tid / P;
+  for (int r = rl; r < e; r += kRP) {
+    const uint16_t v = tl < Pc ? w.m[size_t(r) * w.ld + c0 + tl] : uint16_t(0);
+    pan[r * P + tl] = v;
+    w.asn[size_t(r) * P + tl] = v;
   }
   for (int i = tid; i < e; i += B) used[i] = w.used[i];
   if (tid == 0) misc[1] = 0;
@@ -500,10 +550,12 @@ __global__ __launch_bounds__(kThreads) void ds16_panel_kernel(int e, int c0, int
     const uint32_t iv = uint32_t(misc[2]);
     for (int t = tid; t < P; t += B) pan[p * P + t] = uint16_t(mul16(pan[p * P + t], iv));
     __syncthreads();
-    for (int i = tid; i < e * P; i += B) {
-      const int r = i / P, t = i - r * P;
+    // the scaled pivot row's nibble-product tables: one (t, q) pair per thread, 16 entries
+    for (int tq = tid; tq < 4 * P; tq += B) nib_table(pan[p * P + tq % P], ptab + tq % P, P, tq / P);
+    __syncthreads();
+    for (int r = rl; r < e; r += kRP) {
       const uint32_t f = fcol[r];
-      if (r != p && f) pan[i] = uint16_t(pan[i] ^ mul16(f, pan[p * P + t]));
+      if (r != p && f) pan[r * P + tl] = uint16_t(pan[r * P + tl] ^ nib_mul(ptab + tl, P, f));
     }
     __syncthreads();
   }
@@ -565,47 +617,54 @@ __global__ __launch_bounds__(kThreads) void ds16_ainv_kernel(int e, int c0, int 
   }
 }
 
-// Y[j][col] = sum_i A[pi]^-1[j][i] M[pi_i][col], columns [c0, W)
+// Y[j][col] = sum_i A[pi]^-1[j][i] M[pi_i][col], columns [c0, W); block (column block, j): the P
+// coefficients of row j as nibble-product tables in LDS, so a product is four lookups
 template <int P>
 __global__ __launch_bounds__(kThreads) void ds16_y_kernel(int k, int e, int c0, Ws16 w) {
   if (ws_failed(w)) return;
-  __shared__ uint16_t ainv[P * P];
-  __shared__ int pv[P];
+  const int j = int(blockIdx.y);
   const int Pc = min(P, e - c0);
-  for (int i = threadIdx.x; i < P * P; i += kThreads) ainv[i] = w.ainv[i];
+  if (j >= Pc) return;  // (uniform per block)
+  __shared__ uint32_t tab[64 * P];  // [q * 16 + v][i]
+  __shared__ int pv[P];
+  for (int iq = threadIdx.x; iq < 4 * P; iq += kThreads) nib_table(w.ainv[j * P + iq % P], tab + iq % P, P, iq / P);
   for (int i = threadIdx.x; i < Pc; i += kThreads) pv[i] = w.piv[c0 + i];
   __syncthreads();
   const int W = e + k;
   const int col = c0 + int(blockIdx.x) * kThreads + int(threadIdx.x);
   if (col >= W) return;
-  uint16_t x[P];
-#pragma unroll
-  for (int i = 0; i < P; ++i) x[i] = i < Pc ? w.m[size_t(pv[i]) * w.ld + col] : uint16_t(0);
-  for (int j = 0; j < Pc; ++j) {
-    uint32_t acc = 0;
-#pragma unroll
-    for (int i = 0; i < P; ++i) {
-      const uint32_t a = ainv[j * P + i];
-      if (a && x[i]) acc ^= mul16(a, x[i]);
-    }
-    w.y[size_t(j) * W + col] = uint16_t(acc);
+  uint32_t acc = 0;
+  for (int i = 0; i < Pc; ++i) {
+    const uint32_t x = w.m[size_t(pv[i]) * w.ld + col];
+    acc ^= nib_mul(tab + i, P, x);
   }
+  w.y[size_t(j) * W + col] = uint16_t(acc);
 }
 
-// rank-P update of rows [r0, r0 + kRowsPerBlock) over columns [c0, W)
+// rank-P update of rows [r0, r0 + kRowsPerBlock) over columns [c0, W): the block's rows' panel
+// coefficients as nibble-product tables in LDS (kRowsPerBlock x P tables of 64 words)
 constexpr int kRowsPerBlock = 8;
 template <int P>
 __global__ __launch_bounds__(kThreads) void ds16_update_kernel(int k, int e, int c0, Ws16 w) {
   if (ws_failed(w)) return;
   const int W = e + k;
   const int Pc = min(P, e - c0);
+  const int r0 = int(blockIdx.y) * kRowsPerBlock;
+  const int nr = min(e - r0, kRowsPerBlock);
+  constexpr int kT = kRowsPerBlock * P;  // tables, interleaved: [q * 16 + v][row * P + j]
+  __shared__ uint16_t tab[64 * kT];       // (32 KiB at P = 32)
+  for (int iq = threadIdx.x; iq < 4 * kT; iq += kThreads) {
+    const int t = iq % kT, rr = t / P, j = t - rr * P;
+    nib_table(rr < nr && j < Pc ? uint32_t(w.asn[size_t(r0 + rr) * P + j]) : 0u, tab + t, kT, iq / kT);
+  }
+  __syncthreads();
   const int col = c0 + int(blockIdx.x) * kThreads + int(threadIdx.x);
   if (col >= W) return;
   uint16_t y[P];
 #pragma unroll
   for (int j = 0; j < P; ++j) y[j] = j < Pc ? w.y[size_t(j) * W + col] : uint16_t(0);
-  const int r0 = int(blockIdx.y) * kRowsPerBlock;
-  for (int r = r0; r < min(e, r0 + kRowsPerBlock); ++r) {
+  for (int rr = 0; rr < nr; ++rr) {
+    const int r = r0 + rr;
     const int u = w.used[r] - 1;  // pivot column of row r, if any
     uint16_t* dst = w.m + size_t(r) * w.ld + col;
     if (u >= c0 && u < c0 + Pc) {
@@ -613,12 +672,9 @@ __global__ __launch_bounds__(kThreads) void ds16_update_kernel(int k, int e, int
       continue;
     }
     uint32_t acc = *dst;
-    const uint16_t* a = w.asn + size_t(r) * P;
 #pragma unroll
-    for (int j = 0; j < P; ++j) {
-      const uint32_t f = a[j];
-      if (f && y[j]) acc ^= mul16(f, y[j]);
-    }
+    for (int j = 0; j < P; ++j)
+      if (j < Pc) acc ^= nib_mul(tab + rr * P + j, kT, y[j]);
     *dst = uint16_t(acc);
   }
 }
@@ -675,14 +731,14 @@ hipError_t launch_blocked16(const uint16_t* g, int n, int k, const int* rows, in
   ds16_gather_kernel<<<gblocks, kThreads, 0, stream>>>(g, k, e, w);
   const size_t plds = panel_lds(e, P);
   if (plds > 65536) {
-    const hipError_t err = ensure_lds_optin(reinterpret_cast<const void*>(&ds16_panel_kernel));
+    const hipError_t err = ensure_lds_optin(reinterpret_cast<const void*>(&ds16_panel_kernel<P>));
     if (err != hipSuccess) return err;
   }
   for (int c0 = 0; c0 < e; c0 += P) {
-    ds16_panel_kernel<<<1, kThreads, plds, stream>>>(e, c0, P, w);
+    ds16_panel_kernel<P><<<1, kThreads, plds, stream>>>(e, c0, w);
     ds16_ainv_kernel<<<1, kThreads, 0, stream>>>(e, c0, P, w);
     const unsigned cb = unsigned((W - c0 + kThreads - 1) / kThreads);
-    ds16_y_kernel<P><<<cb, kThreads, 0, stream>>>(k, e, c0, w);
+    ds16_y_kernel<P><<<dim3(cb, unsigned(P)), kThreads, 0, stream>>>(k, e, c0, w);
     ds16_update_kernel<P><<<dim3(cb, unsigned((e + kRowsPerBlock - 1) / kRowsPerBlock)), kThreads, 0, stream>>>(
         k, e, c0, w);
   }
