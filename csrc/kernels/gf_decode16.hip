@@ -407,11 +407,11 @@ __host__ __device__ inline Ws16 ws16_of(void* base, int n, int k, int e, int P) 
 }
 
 // LDS of the panel kernel: product tables [4][16][P] u32 | panel [e][P] | used [e] | factors [e] |
-// misc | pivots
+// misc | pivots | pivot inverses
 __host__ __device__ inline size_t panel_tab_bytes(int P) { return size_t(4) * 16 * P * 4; }
 __host__ __device__ inline size_t panel_lds(int e, int P) {
   return panel_tab_bytes(P) + al256(size_t(e) * P * 2) + size_t(e) * 4 + size_t((e + 1) & ~1) * 2 + 16 +
-         4 * kPanelMax;
+         4 * kPanelMax + 2 * kPanelMax;
 }
 
 // panel width: the widest power of two <= 32 whose panel kernel fits the LDS
@@ -519,6 +519,7 @@ __global__ __launch_bounds__(kThreads) void ds16_panel_kernel(int e, int c0, Ws1
   uint16_t* fcol = reinterpret_cast<uint16_t*>(used + e);                  // [e] (elimination factors)
   int* misc = reinterpret_cast<int*>(fcol + ((e + 1) & ~1));               // [0] bid, [1] fail, [2] inverse
   int* lpiv = misc + 4;                                                     // [P]
+  uint16_t* linv = reinterpret_cast<uint16_t*>(lpiv + kPanelMax);        // [P] pivot inverses (ainv reuses)
   const int Pc = min(P, e - c0);
   const int tl = tid % P, rl = tid / P;
   for (int r = rl; r < e; r += kRP) {
@@ -532,8 +533,14 @@ __global__ __launch_bounds__(kThreads) void ds16_panel_kernel(int e, int c0, Ws1
   for (int j = 0; j < Pc; ++j) {
     if (tid == 0) misc[0] = e;
     __syncthreads();
-    for (int r = tid; r < e; r += B)
-      if (!used[r] && pan[r * P + j]) atomicMin(&misc[0], r);
+    {  // lowest unused row with a nonzero in column j: per lane, then per wave, one LDS atomic a wave
+      int cand = e;
+      for (int r = tid; r < e && cand == e; r += B)
+        if (!used[r] && pan[r * P + j]) cand = r;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) cand = min(cand, __shfl_xor(cand, o));
+      if ((tid & 63) == 0 && cand < e) atomicMin(&misc[0], cand);
+    }
     __syncthreads();
     const int p = misc[0];
     if (p >= e) {  // no pivot in this column among the unused rows: singular (uniform)
@@ -545,6 +552,7 @@ __global__ __launch_bounds__(kThreads) void ds16_panel_kernel(int e, int c0, Ws1
       used[p] = 1 + (c0 + j);
       lpiv[j] = p;
       misc[2] = int(inv16(pan[p * P + j]));
+      linv[j] = uint16_t(misc[2]);
     }
     __syncthreads();
     const uint32_t iv = uint32_t(misc[2]);
@@ -553,53 +561,53 @@ __global__ __launch_bounds__(kThreads) void ds16_panel_kernel(int e, int c0, Ws1
     // the scaled pivot row's nibble-product tables: one (t, q) pair per thread, 16 entries
     for (int tq = tid; tq < 4 * P; tq += B) nib_table(pan[p * P + tq % P], ptab + tq % P, P, tq / P);
     __syncthreads();
-    for (int r = rl; r < e; r += kRP) {
-      const uint32_t f = fcol[r];
-      if (r != p && f) pan[r * P + tl] = uint16_t(pan[r * P + tl] ^ nib_mul(ptab + tl, P, f));
+    // four rows per step, every LDS read of the step issued before its stores
+    for (int r0 = rl; r0 < e; r0 += 4 * kRP) {
+      uint32_t f[4], x[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int r = r0 + u * kRP;
+        f[u] = (r < e && r != p) ? uint32_t(fcol[r]) : 0u;
+        x[u] = r < e ? uint32_t(pan[r * P + tl]) : 0u;
+      }
+      uint32_t d[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) d[u] = f[u] ? nib_mul(ptab + tl, P, f[u]) : 0u;
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (f[u]) pan[(r0 + u * kRP) * P + tl] = uint16_t(x[u] ^ d[u]);
     }
     __syncthreads();
   }
-  for (int j = tid; j < Pc; j += B) w.piv[c0 + j] = lpiv[j];
+  for (int j = tid; j < Pc; j += B) {
+    w.piv[c0 + j] = lpiv[j];
+    w.ainv[j] = linv[j];  // (read by ds16_ainv_kernel before it writes A[pi]^-1 there)
+  }
   for (int r = tid; r < e; r += B) w.used[r] = used[r];
 }
 
-// A[pi]^-1 of the panel just factored: Gauss-Jordan on [A[pi] | I] (Pc x 2Pc, row pivoting among the
-// Pc rows; A[pi] is nonsingular because every pivot was found). Its own launch: it reads the panel
-// snapshot the panel kernel wrote, which another wave of that kernel's block could see stale in L1.
+// A[pi]^-1 of the panel just factored: Gauss-Jordan on [A[pi] | I] (Pc x 2Pc) with the rows in the
+// panel's pivot order. Restricted to the pivot rows, the panel kernel applied exactly these row
+// operations, so step j's pivot is the one it found and its inverse is the one it computed (left in
+// w.ainv[j]): no search, no swap, no inversion here. Its own launch: it reads the panel snapshot
+// the panel kernel wrote, which another wave of that kernel's block could see stale in L1.
 __global__ __launch_bounds__(kThreads) void ds16_ainv_kernel(int e, int c0, int P, Ws16 w) {
   if (ws_failed(w)) return;
   constexpr int B = kThreads;
   const int tid = threadIdx.x;
   __shared__ uint16_t aug[kPanelMax * 2 * kPanelMax];
   __shared__ uint16_t fcol[kPanelMax];
-  __shared__ int misc[4];
+  __shared__ uint16_t pinv[kPanelMax];
   const int Pc = min(P, e - c0);
   const int P2 = 2 * Pc;
   for (int i = tid; i < Pc * P2; i += B) {
     const int a = i / P2, t = i - a * P2;
     aug[i] = t < Pc ? w.asn[size_t(w.piv[c0 + a]) * P + t] : uint16_t(t - Pc == a);
   }
-  if (tid == 0) misc[1] = 0;
+  for (int j = tid; j < Pc; j += B) pinv[j] = w.ainv[j];
   __syncthreads();
   for (int j = 0; j < Pc; ++j) {
-    if (tid == 0) {
-      int q = j;
-      while (q < Pc && !aug[q * P2 + j]) ++q;
-      if (q < Pc && q != j)
-        for (int t = 0; t < P2; ++t) {
-          const uint16_t x = aug[j * P2 + t];
-          aug[j * P2 + t] = aug[q * P2 + t];
-          aug[q * P2 + t] = x;
-        }
-      misc[2] = q < Pc ? int(inv16(aug[j * P2 + j])) : 0;
-      if (q >= Pc) misc[1] = 1;
-    }
-    __syncthreads();
-    if (misc[1]) {
-      if (tid == 0) w.flags[2] = 1;
-      return;
-    }
-    const uint32_t iv = uint32_t(misc[2]);
+    const uint32_t iv = pinv[j];
     for (int t = tid; t < P2; t += B) aug[j * P2 + t] = uint16_t(mul16(aug[j * P2 + t], iv));
     __syncthreads();
     for (int a = tid; a < Pc; a += B) fcol[a] = aug[a * P2 + j];
