@@ -606,16 +606,18 @@ __global__ __launch_bounds__(kThreads) void ds16_ainv_kernel(int e, int c0, int 
   }
   for (int j = tid; j < Pc; j += B) pinv[j] = w.ainv[j];
   __syncthreads();
+  __shared__ uint16_t rtab[64 * 2 * kPanelMax];  // nibble tables of the scaled pivot row: [q * 16 + v][t]
   for (int j = 0; j < Pc; ++j) {
     const uint32_t iv = pinv[j];
     for (int t = tid; t < P2; t += B) aug[j * P2 + t] = uint16_t(mul16(aug[j * P2 + t], iv));
-    __syncthreads();
     for (int a = tid; a < Pc; a += B) fcol[a] = aug[a * P2 + j];
+    __syncthreads();
+    for (int tq = tid; tq < 4 * P2; tq += B) nib_table(aug[j * P2 + tq % P2], rtab + tq % P2, P2, tq / P2);
     __syncthreads();
     for (int i = tid; i < Pc * P2; i += B) {
       const int a = i / P2, t = i - a * P2;
       const uint32_t f = fcol[a];
-      if (a != j && f) aug[i] = uint16_t(aug[i] ^ mul16(f, aug[j * P2 + t]));
+      if (a != j && f) aug[i] = uint16_t(aug[i] ^ nib_mul(rtab + t, P2, f));
     }
     __syncthreads();
   }
