@@ -522,10 +522,21 @@ __global__ __launch_bounds__(kThreads) void ds16_panel_kernel(int e, int c0, Ws1
   uint16_t* linv = reinterpret_cast<uint16_t*>(lpiv + kPanelMax);        // [P] pivot inverses (ainv reuses)
   const int Pc = min(P, e - c0);
   const int tl = tid % P, rl = tid / P;
-  for (int r = rl; r < e; r += kRP) {
-    const uint16_t v = tl < Pc ? w.m[size_t(r) * w.ld + c0 + tl] : uint16_t(0);
-    pan[r * P + tl] = v;
-    w.asn[size_t(r) * P + tl] = v;
+  for (int r0 = rl; r0 < e; r0 += 8 * kRP) {  // eight rows' loads in flight before their stores
+    uint16_t v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int r = r0 + u * kRP;
+      v[u] = (r < e && tl < Pc) ? w.m[size_t(r) * w.ld + c0 + tl] : uint16_t(0);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int r = r0 + u * kRP;
+      if (r < e) {
+        pan[r * P + tl] = v[u];
+        w.asn[size_t(r) * P + tl] = v[u];
+      }
+    }
   }
   for (int i = tid; i < e; i += B) used[i] = w.used[i];
   if (tid == 0) misc[1] = 0;
