@@ -502,13 +502,16 @@ __global__ __launch_bounds__(kThreads) void ds16_gather_kernel(const uint16_t* _
 }
 
 // One panel [c0, c0 + P): pivot rows by Gauss-Jordan on the panel in LDS, and its snapshot.
+// (1024 threads: one workgroup holds the whole panel, and its column loop is LDS-latency bound —
+// 16 waves instead of 4 hide it: profiles/gf65536/r10_blocked_solve)
+constexpr int kPanelThreads = 1024;
 template <int P>
-__global__ __launch_bounds__(kThreads) void ds16_panel_kernel(int e, int c0, Ws16 w) {
+__global__ __launch_bounds__(kPanelThreads) void ds16_panel_kernel(int e, int c0, Ws16 w) {
   if (ws_failed(w)) return;
-  static_assert(kThreads % P == 0, "whole rows per pass");
-  constexpr int kRP = kThreads / P;  // rows per pass: lane tid works on column t = tid % P
+  static_assert(kPanelThreads % P == 0, "whole rows per pass");
+  constexpr int kRP = kPanelThreads / P;  // rows per pass: lane tid works on column t = tid % P
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  constexpr int B = kThreads;
+  constexpr int B = kPanelThreads;
   const int tid = threadIdx.x;
   // ptab[(q * 16 + v) * P + t] = (pivot row value t) * (v << 4q): a product by a factor f is then
   // four nibble lookups (t fastest: the lanes of a row step hit spread banks)
@@ -646,9 +649,10 @@ __global__ __launch_bounds__(kThreads) void ds16_y_kernel(int k, int e, int c0, 
   const int j = int(blockIdx.y);
   const int Pc = min(P, e - c0);
   if (j >= Pc) return;  // (uniform per block)
-  __shared__ uint32_t tab[64 * P];  // [q * 16 + v][i]
+  constexpr int kS = P + 1;  // (odd row stride: lanes with different nibbles read different banks)
+  __shared__ uint32_t tab[64 * kS];  // [q * 16 + v][i]
   __shared__ int pv[P];
-  for (int iq = threadIdx.x; iq < 4 * P; iq += kThreads) nib_table(w.ainv[j * P + iq % P], tab + iq % P, P, iq / P);
+  for (int iq = threadIdx.x; iq < 4 * P; iq += kThreads) nib_table(w.ainv[j * P + iq % P], tab + iq % P, kS, iq / P);
   for (int i = threadIdx.x; i < Pc; i += kThreads) pv[i] = w.piv[c0 + i];
   __syncthreads();
   const int W = e + k;
@@ -657,7 +661,7 @@ __global__ __launch_bounds__(kThreads) void ds16_y_kernel(int k, int e, int c0, 
   uint32_t acc = 0;
   for (int i = 0; i < Pc; ++i) {
     const uint32_t x = w.m[size_t(pv[i]) * w.ld + col];
-    acc ^= nib_mul(tab + i, P, x);
+    acc ^= nib_mul(tab + i, kS, x);
   }
   w.y[size_t(j) * W + col] = uint16_t(acc);
 }
@@ -673,10 +677,13 @@ __global__ __launch_bounds__(kThreads) void ds16_update_kernel(int k, int e, int
   const int r0 = int(blockIdx.y) * kRowsPerBlock;
   const int nr = min(e - r0, kRowsPerBlock);
   constexpr int kT = kRowsPerBlock * P;  // tables, interleaved: [q * 16 + v][row * P + j]
-  __shared__ uint16_t tab[64 * kT];       // (32 KiB at P = 32)
+  // (row stride kT + 2 halfwords = an odd number of banks: lanes with different nibbles v read
+  // different banks; at kT the 16 values of v all hit one bank)
+  constexpr int kTs = kT + 2;
+  __shared__ uint16_t tab[64 * kTs];      // (~32 KiB at P = 32)
   for (int iq = threadIdx.x; iq < 4 * kT; iq += kThreads) {
     const int t = iq % kT, rr = t / P, j = t - rr * P;
-    nib_table(rr < nr && j < Pc ? uint32_t(w.asn[size_t(r0 + rr) * P + j]) : 0u, tab + t, kT, iq / kT);
+    nib_table(rr < nr && j < Pc ? uint32_t(w.asn[size_t(r0 + rr) * P + j]) : 0u, tab + t, kTs, iq / kT);
   }
   __syncthreads();
   const int col = c0 + int(blockIdx.x) * kThreads + int(threadIdx.x);
@@ -695,7 +702,7 @@ __global__ __launch_bounds__(kThreads) void ds16_update_kernel(int k, int e, int
     uint32_t acc = *dst;
 #pragma unroll
     for (int j = 0; j < P; ++j)
-      if (j < Pc) acc ^= nib_mul(tab + rr * P + j, kT, y[j]);
+      if (j < Pc) acc ^= nib_mul(tab + rr * P + j, kTs, y[j]);
     *dst = uint16_t(acc);
   }
 }
@@ -756,7 +763,7 @@ hipError_t launch_blocked16(const uint16_t* g, int n, int k, const int* rows, in
     if (err != hipSuccess) return err;
   }
   for (int c0 = 0; c0 < e; c0 += P) {
-    ds16_panel_kernel<P><<<1, kThreads, plds, stream>>>(e, c0, w);
+    ds16_panel_kernel<P><<<1, kPanelThreads, plds, stream>>>(e, c0, w);
     ds16_ainv_kernel<<<1, kThreads, 0, stream>>>(e, c0, P, w);
     const unsigned cb = unsigned((W - c0 + kThreads - 1) / kThreads);
     ds16_y_kernel<P><<<dim3(cb, unsigned(P)), kThreads, 0, stream>>>(k, e, c0, w);
