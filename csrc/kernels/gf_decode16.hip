@@ -147,12 +147,15 @@ __host__ __device__ constexpr size_t lds16(int n, int k, int e) {
   return lds_fixed16(n, k, e) + 8 * size_t(e) * units_of(e + k);
 }
 
-__global__ __launch_bounds__(kThreads) void gf_decode_system16_kernel(
+// (1024 threads: four times the lanes per row for the column loop, which is LDS-latency bound in
+// one workgroup — as ds16_panel_kernel below)
+constexpr int kSysThreads = 1024;
+__global__ __launch_bounds__(kSysThreads) void gf_decode_system16_kernel(
     const uint16_t* __restrict__ g, int n, int k, const int* __restrict__ rows, int* __restrict__ erased, int e,
     uint16_t* __restrict__ dm, int* __restrict__ status, uint32_t* __restrict__ tab, int m_pad,
     const uint64_t* __restrict__ ptrs, uint64_t* __restrict__ dptr) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  constexpr int B = kThreads;
+  constexpr int B = kSysThreads;
   const int W = e + k;
   const int PU = units_of(W);
   int* misc = reinterpret_cast<int*>(smem);  // [0..2] pivot bids, [3] parity count, [4] bad
@@ -816,7 +819,7 @@ hipError_t launch_gf_decode_system16(const uint16_t* g, int n, int k, const int*
     const hipError_t err = ensure_lds_optin(reinterpret_cast<const void*>(&gf_decode_system16_kernel));
     if (err != hipSuccess) return err;
   }
-  gf_decode_system16_kernel<<<1, kThreads, lds, stream>>>(g, n, k, rows, erased, e, dm, status, tab, m_pad, ptrs, dptr);
+  gf_decode_system16_kernel<<<1, kSysThreads, lds, stream>>>(g, n, k, rows, erased, e, dm, status, tab, m_pad, ptrs, dptr);
   return hipGetLastError();
 }
 
